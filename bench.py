@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-job ResNet-50 synthetic training images/sec.
+
+Driver contract (one rank per GPU, launched by torch.distributed.run for
+N > 1):  W untimed warmup steps, then EXACTLY K timed steps bracketed by a
+barrier + device synchronize on both sides; the max elapsed over ranks is
+used; rank 0 prints ONE JSON line.
+
+Config (BASELINE.json): ResNet-50 v1 (with its final FC, 1001 classes),
+bf16 compute with fp32 master weights, 256 images per GPU (weak scaling),
+Nesterov momentum SGD, --variable_update=kungfu --kungfu_option=sync_sgd
+(bucketed RCCL all-reduce overlapped with backward), synthetic ImageNet-shaped
+data (224x224x3) and random-init weights.  Each timed step is a complete
+training step: forward, backward, gradient all-reduce and optimizer update.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+# Reference numbers (fork's ResNet-50, fp32, RTX 3090; 4/8-GPU
+# values are the linear extrapolation BASELINE.md derives from the 2-GPU run).
+BASELINE_IMG_PER_SEC = {1: 416.43, 2: 713.23, 4: 1412.0, 8: 2825.0}
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch_size", type=int, default=256, help="per GPU")
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--kernel_impl", default="hip")
+    ap.add_argument("--optimizer", default="momentum")
+    ap.add_argument("--bucket_size_mb", type=float, default=64.0)
+    ap.add_argument("--wire_dtype", default="fp32")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--verbose", action="store_true")
+    a = ap.parse_args(argv)
+
+    import torch
+    from kf_benchmarks_amd import params as P
+    from kf_benchmarks_amd.benchmark import BenchmarkCNN
+    from kf_benchmarks_amd.parallel import comm
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != a.gpus:
+        print("warning: --gpus=%d but WORLD_SIZE=%d" % (a.gpus, world_env), file=sys.stderr)
+    p = P.make_params(model=a.model, batch_size=a.batch_size, num_gpus=1,
+                      variable_update="kungfu", kungfu_option="sync_sgd",
+                      optimizer=a.optimizer, use_bf16=a.dtype == "bf16",
+                      use_fp16=a.dtype == "fp16", data_format="NHWC",
+                      kernel_impl=a.kernel_impl, bucket_size_mb=a.bucket_size_mb,
+                      gradient_wire_dtype=a.wire_dtype, display_every=10**9)
+    bench = BenchmarkCNN(p)
+    bench.build()
+    world = comm.get_world()
+    dev = bench.device
+    bench.strategy.broadcast_initial_model(bench.optimizer.slot_tensors().values())
+
+    t0 = time.time()
+    for i in range(a.warmup):
+        loss, _ = bench.train_step(need_loss=(i == a.warmup - 1))
+    torch.cuda.synchronize(dev)
+    warm_loss = float(loss) if a.warmup > 0 else float("nan")
+    if a.verbose and world.is_chief:
+        print("warmup done in %.1fs, loss %.4f" % (time.time() - t0, warm_loss),
+              file=sys.stderr)
+
+    world.barrier(dev)
+    torch.cuda.synchronize(dev)
+    start = time.perf_counter()
+    for _ in range(a.steps):
+        loss, _ = bench.train_step()
+    torch.cuda.synchronize(dev)
+    world.barrier(dev)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - start
+    final_loss = float(loss)
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    comm.all_reduce(t, op="max")
+    elapsed = float(t.item())
+    n = world.size
+    images = a.batch_size * n * a.steps
+    value = images / elapsed
+    if world.is_chief:
+        base = BASELINE_IMG_PER_SEC.get(n)
+        out = {
+            "metric": "images/sec (whole node) ResNet-50 synthetic at 1/2/4/8 MI355X",
+            "value": round(value, 2),
+            "unit": "images/sec",
+            "n_gpus": n,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000.0 * elapsed / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / base, 3) if base else None,
+            "dtype": a.dtype,
+            "data": "synthetic (224x224x3 ImageNet-shaped images, random-init weights)",
+            "config": {"model": a.model, "global_batch": a.batch_size * n, "seq_len": None,
+                       "per_gpu_batch": a.batch_size, "parallelism": "dp%d" % n,
+                       "variable_update": "kungfu/sync_sgd", "optimizer": a.optimizer,
+                       "kernel_impl": a.kernel_impl, "loss_first": warm_loss,
+                       "loss_last": final_loss},
+        }
+        print(json.dumps(out))
+        sys.stdout.flush()
+    world.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,615 @@
+"""BenchmarkCNN: the training / eval / forward-only benchmark engine.
+
+Role of tcb/benchmark_cnn.py (C6-C18 in SURVEY §2.1), re-designed for an
+eager PyTorch-ROCm process per GPU:
+
+  params -> dataset + model -> Network (variables) -> FlatParams (one flat
+  fp32 buffer + grads + bf16 shadow) -> Strategy (RCCL aggregation per
+  --variable_update) -> FusedOptimizer -> hot loop.
+
+The hot loop never synchronizes the host per step: each step records a HIP
+event and step times are read back at display steps (the reference's
+per-step ``sess.run`` wall time, tcb/benchmark_cnn.py:786-884, without the
+host round trip).  Log lines keep the reference's format verbatim
+(Appendix B of SURVEY.md); tests parse them.
+"""
+
+from __future__ import annotations
+
+import json
+import math
+import os
+import sys
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from . import cnn_util, datasets, flags, optim, params as params_lib
+from .constants import BenchmarkMode
+from .models import model_config
+from .models.model import Network
+from .ops import _native
+from .parallel import comm
+from .parallel.variable_mgr import make_strategy
+
+log_fn = cnn_util.log_fn
+
+_DEFAULT_NUM_BATCHES = 100
+LOSS_AND_ACCURACY_DIGITS_TO_SHOW = 3
+_NUM_STEPS_TO_PROFILE = 10
+
+IGNORED_TF_FLAGS = ("xla", "xla_compile", "winograd_nonfused", "batchnorm_persistent", "mkl",
+                    "enable_optimizations", "rewriter_config", "trt_mode", "use_unified_memory",
+                    "force_gpu_compatible", "allow_growth", "use_resource_vars",
+                    "freeze_when_forward_only", "debugger", "gpu_thread_mode")
+
+
+class CheckpointNotFoundException(Exception):
+    pass
+
+
+def get_mode_from_params(params):
+    if params.eval:
+        return BenchmarkMode.EVAL
+    if params.forward_only:
+        return BenchmarkMode.FORWARD_ONLY
+    if (params.eval_during_training_every_n_steps or params.eval_during_training_every_n_epochs
+            or params.eval_during_training_at_specified_steps
+            or params.eval_during_training_at_specified_epochs):
+        return BenchmarkMode.TRAIN_AND_EVAL
+    return BenchmarkMode.TRAIN
+
+
+def get_num_batches_and_epochs(params, batch_size, num_examples_per_epoch):
+    if params.num_batches and params.num_epochs:
+        raise ValueError("At most one of --num_batches and --num_epochs may be specified.")
+    if params.num_epochs:
+        num_batches = int(float(params.num_epochs) * num_examples_per_epoch / batch_size)
+    else:
+        num_batches = params.num_batches or _DEFAULT_NUM_BATCHES
+    num_epochs = num_batches * batch_size / float(num_examples_per_epoch)
+    return num_batches, num_epochs
+
+
+def get_perf_timing(batch_size, step_train_times, scale=1):
+    times = np.array(step_train_times)
+    speeds = batch_size / times
+    speed_mean = scale * batch_size / np.mean(times)
+    speed_uncertainty = np.std(speeds) / np.sqrt(float(len(speeds)))
+    speed_jitter = 1.4826 * np.median(np.abs(speeds - np.median(speeds)))
+    return speed_mean, speed_uncertainty, speed_jitter
+
+
+def get_perf_timing_str(speed_mean, speed_uncertainty, speed_jitter, scale=1):
+    if scale == 1:
+        return "images/sec: %.1f +/- %.1f (jitter = %.1f)" % (speed_mean, speed_uncertainty,
+                                                             speed_jitter)
+    return "images/sec: %.1f" % speed_mean
+
+
+def validate_params_combinations(params):
+    """Cross-flag checks of tcb/benchmark_cnn.py:1268-1352 (those meaningful
+    on this stack)."""
+    p = params
+    if p.device.lower() == "cpu" and p.data_format == "NCHW" and not p.mkl:
+        raise ValueError("device=cpu requires that data_format=NHWC")
+    if ((p.num_epochs_per_decay or p.learning_rate_decay_factor) and
+            not (p.init_learning_rate is not None and p.num_epochs_per_decay
+                 and p.learning_rate_decay_factor)):
+        raise ValueError("If one of num_epochs_per_decay or learning_rate_decay_factor is set, "
+                         "both must be set and learning_rate must be set")
+    if (p.minimum_learning_rate and
+            not (p.init_learning_rate is not None and p.num_epochs_per_decay
+                 and p.learning_rate_decay_factor)):
+        raise ValueError("minimum_learning_rate requires learning_rate, num_epochs_per_decay, "
+                         "and learning_rate_decay_factor to be set")
+    if p.use_fp16 and p.fp16_vars and "replicated" in p.variable_update \
+            and p.all_reduce_spec and "nccl" in p.all_reduce_spec:
+        raise ValueError("fp16 variables are not supported with NCCL")
+    if p.use_fp16 and p.fp16_vars and p.gradient_repacking:
+        raise ValueError("--fp16_vars cannot be used with --gradient_repacking")
+    if p.use_fp16 and p.use_bf16:
+        raise ValueError("At most one of --use_fp16 and --use_bf16 may be set")
+    if p.variable_update == "horovod" and p.num_gpus > 1:
+        raise ValueError("Horovod benchmarks require num_gpus=1 on each worker")
+    if p.variable_update == "horovod" and p.job_name:
+        raise ValueError("job_name should not be specified for Horovod.")
+    if p.variable_update == "kungfu" and p.num_gpus > 1:
+        raise ValueError("KungFu benchmarks require num_gpus=1 on each worker")
+    if p.variable_update == "kungfu" and p.job_name:
+        raise ValueError("job_name should not be specified for KungFu.")
+    if p.use_fp16 and p.fp16_enable_auto_loss_scale:
+        if p.all_reduce_spec and "nccl" in p.all_reduce_spec:
+            raise ValueError("Automatic loss scaling is not supported with NCCL.")
+        if p.variable_update not in ("parameter_server", "replicated", "independent"):
+            raise ValueError("Automatic loss scaling is not supported with variable_update=%s."
+                             % p.variable_update)
+        if p.staged_vars:
+            raise ValueError("Automatic loss scaling is not supported with staged_vars.")
+    if p.debugger is not None and p.debugger != "cli" and ":" not in p.debugger:
+        raise ValueError('--debugger must be "cli" or in the form host:port')
+    if p.hierarchical_copy and p.num_gpus <= 1:
+        raise ValueError("--hierarchical_copy requires --num_gpus to be greater than 1")
+    if p.save_model_secs and p.save_model_steps:
+        raise ValueError("At most one of --save_model_secs and --save_model_steps can be "
+                         "specified")
+    evf = [bool(p.eval_during_training_every_n_steps),
+           bool(p.eval_during_training_every_n_epochs),
+           bool(p.eval_during_training_at_specified_steps),
+           bool(p.eval_during_training_at_specified_epochs)]
+    if evf.count(True) > 1:
+        raise ValueError("At most one flag with --eval_during_training_* prefix must be "
+                         "specified.")
+    if any(evf):
+        if p.eval:
+            raise ValueError("At most one of --eval and --eval_during_training_* must be "
+                             "specified")
+        if p.forward_only:
+            raise ValueError("At most one of --forward_only and --eval_during_training_* must "
+                             "be specified")
+        if p.job_name:
+            raise ValueError("--eval_during_training_* is not yet supported in distributed "
+                             "mode.")
+        if p.staged_vars:
+            raise ValueError("--eval_during_training_* is not currently compatible with "
+                             "staged_vars")
+    if p.stop_at_top_1_accuracy and not any(evf):
+        raise ValueError("--stop_at_top_1_accuracy is only supported with "
+                         "--eval_during_training_*")
+    if p.forward_only and p.freeze_when_forward_only:
+        if p.train_dir is not None:
+            raise ValueError("In forward_only mode, when --freeze_when_forward_only is True, "
+                             "--train_dir should not be specified")
+    elif p.trt_mode:
+        raise ValueError("--trt_mode should not be specified if one of --forward_only and "
+                         "--freeze_when_forward_only is set to False")
+    if p.staged_vars and p.variable_update != "parameter_server":
+        raise ValueError("staged_vars for enqueue/dequeue only support variable update "
+                         "parameter_server")
+    if p.eval and p.forward_only:
+        raise ValueError("Only one of --eval and --forward_only may be specified")
+    if p.variable_consistency == "relaxed" and p.variable_update != "replicated":
+        raise ValueError("variable_consistency=relaxed requires variable_update=replicated")
+    if p.kernel_impl not in ("hip", "torch"):
+        raise ValueError("--kernel_impl must be hip or torch")
+
+
+class _EventTimer:
+    """Per-step device timing without a per-step host sync."""
+
+    def __init__(self, device):
+        self.cuda = device.type == "cuda"
+        self.device = device
+        self._last = None
+        self._pending: List = []
+
+    def mark(self):
+        if self.cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            if self._last is not None:
+                self._pending.append((self._last, ev))
+            self._last = ev
+        else:
+            now = time.perf_counter()
+            if self._last is not None:
+                self._pending.append((self._last, now))
+            self._last = now
+
+    def reset(self):
+        self._last = None
+        self._pending = []
+
+    def collect(self) -> List[float]:
+        """Seconds per step since the last collect (blocks on the device)."""
+        out = []
+        if self.cuda and self._pending:
+            self._pending[-1][1].synchronize()
+            out = [a.elapsed_time(b) / 1e3 for a, b in self._pending]
+        elif self._pending:
+            out = [b - a for a, b in self._pending]
+        self._pending = []
+        return out
+
+
+class BenchmarkCNN:
+    """Class for benchmarking a cnn network."""
+
+    def __init__(self, params, dataset=None, model=None):
+        self.params = params
+        validate_params_combinations(params)
+        self._doing_eval = params.eval
+        self.dataset = dataset or datasets.create_dataset(params.data_dir, params.data_name)
+        self.model = model or model_config.get_model_config(params.model, self.dataset, params)
+        autotune_threshold = params.autotune_threshold or 1
+        min_autotune_warmup = 5 * autotune_threshold * autotune_threshold
+        self.num_warmup_batches = (params.num_warmup_batches
+                                   if params.num_warmup_batches is not None
+                                   else max(10, min_autotune_warmup))
+        self.trace_filename = params.trace_file
+        self.num_gpus = params.num_gpus
+        if params.gpu_indices:
+            self.gpu_indices = [int(x) for x in params.gpu_indices.split(",")]
+        else:
+            self.gpu_indices = list(range(self.num_gpus))
+        if params.batch_size > 0:
+            self.model.set_batch_size(params.batch_size)
+        self.batch_size = self.model.get_batch_size() * self.num_gpus
+        self.batch_group_size = params.batch_group_size
+        self.enable_auto_loss_scale = params.use_fp16 and params.fp16_enable_auto_loss_scale
+        self.mode = get_mode_from_params(params)
+        self.job_name = params.job_name
+
+        # ---- world & devices (one process per GPU; in-process towers are
+        # created by parallel.towers when --num_gpus > 1).
+        self.device_type = "cuda" if params.device.lower() == "gpu" else "cpu"
+        if self.device_type == "cuda" and not torch.cuda.is_available():
+            raise RuntimeError("--device=gpu but no GPU is visible; use --device=cpu "
+                               "--data_format=NHWC for the plumbing config")
+        self.world = comm.init_world(self.device_type)
+        self.num_workers = self.world.size
+        self.task_index = self.world.rank
+        if self.device_type == "cuda":
+            local = self.world.local_rank if self.world.size > 1 else 0
+            dev_index = self.gpu_indices[0] + local if self.num_gpus == 1 else self.gpu_indices[0]
+            dev_index = dev_index % max(torch.cuda.device_count(), 1)
+            torch.cuda.set_device(dev_index)
+            self.device = torch.device("cuda", dev_index)
+            _native.load()  # fail loudly now if the kernels are missing
+        else:
+            self.device = torch.device("cpu")
+        if params.variable_update == "kungfu":
+            self.devices = ["kungfu/gpu:%d" % i for i in range(self.num_gpus)]
+        elif self.device_type == "cuda":
+            self.devices = ["/gpu:%d" % i for i in self.gpu_indices[:self.num_gpus]]
+        else:
+            self.devices = ["/cpu:0"]
+        if self.num_workers > 1 and params.all_reduce_spec == "nccl":
+            raise ValueError("--all_reduce_spec=nccl is invalid in a multi-worker job")
+        self.num_batches, self.num_epochs = get_num_batches_and_epochs(
+            params, self.batch_size * self.num_workers,
+            self.dataset.num_examples_per_epoch("train"))
+        if params.eval:
+            nb = params.num_eval_batches
+            ne = params.num_eval_epochs
+            self.num_batches, self.num_epochs = get_num_batches_and_epochs(
+                params_lib.Params(**{**params._asdict(), "num_batches": nb, "num_epochs": ne}),
+                self.batch_size * self.num_workers,
+                self.dataset.num_examples_per_epoch("validation"))
+        self.compute_dtype = self.model.data_type
+        self.loss_scale = None
+        if params.use_fp16:
+            self.loss_scale = (params.fp16_loss_scale if params.fp16_loss_scale is not None
+                               else self.model.get_fp16_loss_scale())
+        self.loss_scale_normal_steps = 0
+        self.benchmark_logger = None
+        if params.benchmark_log_dir:
+            from .utils.logger import BenchmarkFileLogger
+            self.benchmark_logger = BenchmarkFileLogger(params.benchmark_log_dir,
+                                                        params.benchmark_test_id)
+        self.ignored_flags = [f for f in IGNORED_TF_FLAGS
+                              if getattr(params, f) != flags.param_specs[f].default_value]
+        self._built = False
+        self.global_step = 0
+
+    # ------------------------------------------------------------------ info
+    def _get_params_info(self):
+        if self.params.variable_update == "kungfu":
+            return "kungfu/" + ",".join(self.devices)
+        return str(self.devices)
+
+    def print_info(self):
+        p = self.params
+        log_fn("Model:       %s" % self.model.get_model_name())
+        ds = str(self.dataset)
+        if self.dataset.use_synthetic_gpu_inputs():
+            ds += " (synthetic)"
+        log_fn("Dataset:     %s" % ds)
+        log_fn("Mode:        %s" % self.mode)
+        log_fn("SingleSess:  %s" % False)
+        log_fn("Batch size:  %s global" % (self.batch_size * self.num_workers))
+        log_fn("             %s per device" % (self.batch_size / len(self.devices)))
+        if self.batch_group_size > 1:
+            log_fn("             %d batches per prepocessing group" % self.batch_group_size)
+        log_fn("Num batches: %d" % self.num_batches)
+        log_fn("Num epochs:  %.2f" % self.num_epochs)
+        log_fn("Devices:     %s" % self.devices)
+        log_fn("NUMA bind:   %s" % False)
+        log_fn("Data format: %s" % p.data_format)
+        if self.device_type == "cuda":
+            log_fn("Compute:     %s on %s (NHWC, %s kernels)"
+                   % (str(self.compute_dtype).replace("torch.", ""),
+                      torch.cuda.get_device_name(self.device), p.kernel_impl))
+        log_fn("Optimizer:   %s" % p.optimizer)
+        log_fn("Variables:   %s" % p.variable_update)
+        if p.variable_update in ("replicated", "distributed_all_reduce",
+                                 "collective_all_reduce"):
+            log_fn("AllReduce:   %s" % p.all_reduce_spec)
+        if self.job_name:
+            log_fn("Sync:        %s" % p.cross_replica_sync)
+        if p.staged_vars:
+            log_fn("Staged vars: %s" % p.staged_vars)
+        if p.variable_update == "kungfu":
+            log_fn("KungFu option:  %s" % p.kungfu_option)
+        if self.ignored_flags:
+            log_fn("Ignored TF-only flags: %s" % ", ".join(self.ignored_flags))
+        log_fn("==========")
+
+    # ----------------------------------------------------------------- build
+    def build(self):
+        if self._built:
+            return
+        p = self.params
+        log_fn("Generating training model")
+        seed = p.tf_random_seed
+        torch.manual_seed(seed + self.task_index)
+        np.random.seed(4321 + self.task_index)
+        nclass = self.dataset.num_classes
+        self.net = Network(self.model, nclass, self.device, self.compute_dtype,
+                           kernel_impl=p.kernel_impl, seed=seed)
+        lp = self.compute_dtype if self.compute_dtype != torch.float32 else None
+        self.flat = optim.FlatParams(self.net, lp)
+        self.optimizer = optim.FusedOptimizer(
+            self.flat, p.optimizer, momentum=p.momentum, rmsprop_decay=p.rmsprop_decay,
+            rmsprop_momentum=p.rmsprop_momentum, rmsprop_epsilon=p.rmsprop_epsilon,
+            adam_beta1=p.adam_beta1, adam_beta2=p.adam_beta2, adam_epsilon=p.adam_epsilon)
+        self.strategy = make_strategy(p, self.world, self.flat)
+        self.input = self._make_input()
+        self._built = True
+
+    def _make_input(self):
+        from .data.input_pipeline import make_input_source
+        return make_input_source(self, subset="validation" if self._doing_eval else "train")
+
+    # ------------------------------------------------------------------ step
+    def l2_loss_value(self):
+        """sum(w^2)/2 over trainable variables (device scalar)."""
+        w = self.flat.flat
+        if w.is_cuda:
+            out = torch.zeros(1, dtype=torch.float32, device=w.device)
+            _native.call("kfb_half_sumsq", w.data_ptr(), w.numel(), out.data_ptr(),
+                         _native.stream(w.device))
+            return out[0]
+        return 0.5 * (w.double() ** 2).sum().float()
+
+    def learning_rate(self, step=None):
+        step = self.global_step if step is None else step
+        ex = self.dataset.num_examples_per_epoch("train")
+        return optim.get_learning_rate(self.params, step, ex, self.model,
+                                       self.batch_size * self.num_workers)
+
+    def forward_backward(self, images, labels, need_accuracy=False):
+        res = self.net(images, phase_train=True)
+        loss = self.model.loss_function((images, labels), res)
+        scaled = loss * self.loss_scale if self.loss_scale else loss
+        scaled.backward()
+        acc = None
+        if need_accuracy:
+            acc = self.model.accuracy_function((images, labels), res.logits.detach())
+        return loss.detach(), acc
+
+    def train_step(self, need_loss=False, need_accuracy=False):
+        """One full training step; returns (loss_tensor, accuracy_dict)."""
+        p = self.params
+        images, labels = self.input.next()
+        self.flat.zero_grad()
+        step = self.global_step
+        self.strategy.before_backward(step)
+        loss, acc = self.forward_backward(images, labels, need_accuracy)
+        self.strategy.after_backward(step)
+        grad_scale = self.strategy.grad_scale
+        if self.loss_scale:
+            grad_scale /= self.loss_scale
+        skip = False
+        if self.enable_auto_loss_scale:
+            skip = self._auto_loss_scale_check()
+        if not skip:
+            self.strategy.before_update(step)
+            wd = (p.weight_decay or 0.0) * len(self.devices)
+            self.optimizer.step(self.learning_rate(step), grad_scale=grad_scale,
+                                weight_decay=wd, clip=p.gradient_clip)
+            self.strategy.after_update(step)
+        self.global_step += 1
+        if need_loss and p.loss_type_to_report == "total_loss" and p.weight_decay:
+            loss = loss + len(self.devices) * p.weight_decay * self.l2_loss_value()
+        return loss, acc
+
+    def _auto_loss_scale_check(self) -> bool:
+        """Dynamic loss scaling (tcb/variable_mgr_util.py:51-139): halve the
+        scale and skip the update on inf/nan, double it after
+        fp16_inc_loss_scale_every_n finite steps."""
+        g = self.flat.grad
+        if g.is_cuda:
+            flag = torch.zeros(1, dtype=torch.int32, device=g.device)
+            _native.call("kfb_nonfinite", g.data_ptr(), g.numel(), flag.data_ptr(),
+                         _native.stream(g.device))
+            bad = bool(flag.item())
+        else:
+            bad = not bool(torch.isfinite(g).all())
+        if bad:
+            self.loss_scale = max(self.loss_scale / 2.0, 1.0)
+            self.loss_scale_normal_steps = 0
+            return True
+        self.loss_scale_normal_steps += 1
+        if self.loss_scale_normal_steps >= self.params.fp16_inc_loss_scale_every_n:
+            self.loss_scale *= 2.0
+            self.loss_scale_normal_steps = 0
+        return False
+
+    def forward_only_step(self):
+        images, labels = self.input.next()
+        with torch.no_grad():
+            res = self.net(images, phase_train=False)
+        return res
+
+    # ------------------------------------------------------------------- run
+    def run(self):
+        if self._doing_eval:
+            from .eval import run_eval
+            return run_eval(self)
+        return self._benchmark_train()
+
+    def _benchmark_train(self):
+        p = self.params
+        self.build()
+        log_fn("Initializing graph")
+        from .utils import checkpoint as ckpt_lib
+        self.saver = ckpt_lib.Saver(self, max_to_keep=p.max_ckpts_to_keep)
+        if p.train_dir and os.path.isdir(p.train_dir):
+            restored = self.saver.restore_latest(p.train_dir)
+            if restored is not None:
+                log_fn("Restored checkpoint at global step %d" % restored)
+        if p.backbone_model_path:
+            self.saver.restore_partial(p.backbone_model_path)
+        self.strategy.broadcast_initial_model(self.optimizer.slot_tensors().values())
+        init_global_step = self.global_step
+        eval_hook = None
+        if self.mode == BenchmarkMode.TRAIN_AND_EVAL:
+            from .eval import EvalDuringTraining
+            eval_hook = EvalDuringTraining(self)
+        from .utils.tracing import StepTracer
+        tracer = StepTracer(self)
+        timer = _EventTimer(self.device)
+        step_train_times: List[float] = []
+        forward_only = p.forward_only
+        num_warmup = self.num_warmup_batches
+        if self.batch_group_size > 1:
+            num_warmup = (num_warmup + self.batch_group_size - 1) // self.batch_group_size * \
+                self.batch_group_size
+        total_steps = self.num_batches - (init_global_step if init_global_step else 0)
+        if init_global_step and total_steps < 0:
+            total_steps = 0
+        log_fn("Running warm up")
+        local_step = -1 * num_warmup
+        done = False
+        last_loss = None
+        loop_start = None
+        last_ckpt_time = time.time()
+        header_printed = False
+        while not done:
+            if local_step == 0:
+                log_fn("Done warm up")
+                if not header_printed:
+                    header = "Step\tImg/sec\t" + p.loss_type_to_report.replace("_", " ")
+                    if p.print_training_accuracy:
+                        header += "\ttop_1_accuracy\ttop_5_accuracy"
+                    log_fn(header)
+                    header_printed = True
+                if self.device_type == "cuda":
+                    torch.cuda.synchronize(self.device)
+                self.world.barrier(self.device if self.device_type == "cuda" else None)
+                loop_start = time.perf_counter()
+                step_train_times = []
+                timer.reset()
+                timer.mark()
+            display = local_step >= 0 and (local_step == 0 or
+                                           (local_step + 1) % p.display_every == 0)
+            tracer.begin(local_step)
+            if forward_only:
+                self.forward_only_step()
+                loss, acc = None, None
+            else:
+                loss, acc = self.train_step(need_loss=display or local_step >= total_steps - 1,
+                                            need_accuracy=display and p.print_training_accuracy)
+            tracer.end(local_step)
+            if local_step >= 0:
+                timer.mark()
+            if display:
+                step_train_times.extend(timer.collect())
+                if step_train_times:
+                    lossval = float(loss) if loss is not None else 0.0
+                    last_loss = lossval
+                    self._log_step(local_step, step_train_times, lossval, acc)
+            if local_step >= 0 and not forward_only:
+                self._maybe_checkpoint(local_step, last_ckpt_time)
+                if p.save_model_secs and time.time() - last_ckpt_time >= p.save_model_secs:
+                    last_ckpt_time = time.time()
+            if eval_hook is not None and local_step >= 0:
+                if eval_hook.maybe_eval(self.global_step):
+                    done = True
+            local_step += 1
+            if local_step >= total_steps:
+                done = True
+        step_train_times.extend(timer.collect())
+        if self.device_type == "cuda":
+            torch.cuda.synchronize(self.device)
+        elapsed = time.perf_counter() - (loop_start or time.perf_counter())
+        num_steps = local_step
+        images_per_sec = (self.num_workers * num_steps * self.batch_size / elapsed
+                          if elapsed > 0 else 0.0)
+        log_fn("-" * 64)
+        log_fn("total images/sec: %.2f" % images_per_sec)
+        log_fn("-" * 64)
+        if self.benchmark_logger:
+            self.benchmark_logger.log_metric("average_examples_per_sec", images_per_sec,
+                                             global_step=num_steps)
+        if p.train_dir and self.world.is_chief and not forward_only:
+            self.saver.save(p.train_dir, self.global_step)
+        tracer.finish()
+        if p.variable_update == "kungfu" or p.sync_on_finish:
+            self.world.barrier(self.device if self.device_type == "cuda" else None)
+        if last_loss is None and loss is not None:
+            last_loss = float(loss)
+        stats = {"num_workers": self.num_workers, "num_steps": num_steps,
+                 "average_wall_time": elapsed / num_steps if num_steps > 0 else 0,
+                 "images_per_sec": images_per_sec}
+        if last_loss is not None:
+            stats["last_average_loss"] = last_loss
+        if eval_hook is not None:
+            stats.update(eval_hook.stats())
+        if p.print_json_result and self.world.is_chief:
+            print(json.dumps(stats))
+        return stats
+
+    def _log_step(self, local_step, step_train_times, lossval, acc):
+        p = self.params
+        speed_mean, speed_unc, speed_jit = get_perf_timing(self.batch_size, step_train_times)
+        log_str = "%i\t%s\t%.*f" % (local_step + 1,
+                                    get_perf_timing_str(speed_mean, speed_unc, speed_jit),
+                                    LOSS_AND_ACCURACY_DIGITS_TO_SHOW, lossval)
+        if acc is not None:
+            n = float(self.batch_size)
+            log_str += "\t%.*f\t%.*f" % (LOSS_AND_ACCURACY_DIGITS_TO_SHOW,
+                                         float(acc["top_1_accuracy"]) / n,
+                                         LOSS_AND_ACCURACY_DIGITS_TO_SHOW,
+                                         float(acc["top_5_accuracy"]) / n)
+        log_fn(log_str)
+        if self.benchmark_logger:
+            self.benchmark_logger.log_metric("current_examples_per_sec", speed_mean,
+                                             global_step=local_step + 1)
+
+    def _maybe_checkpoint(self, local_step, last_ckpt_time):
+        p = self.params
+        if not p.train_dir or not self.world.is_chief:
+            return
+        if p.save_model_steps and self.global_step % p.save_model_steps == 0:
+            self.saver.save(p.train_dir, self.global_step)
+        elif p.save_model_secs and time.time() - last_ckpt_time >= p.save_model_secs:
+            self.saver.save(p.train_dir, self.global_step)
+
+
+def setup(params):
+    """Process-level setup (tcb/benchmark_cnn.py:3356-3395): thread counts and
+    environment.  No session to create on this stack."""
+    if params.num_intra_threads:
+        torch.set_num_threads(params.num_intra_threads)
+    if params.num_inter_threads:
+        try:
+            torch.set_num_interop_threads(params.num_inter_threads)
+        except RuntimeError:
+            pass
+    if params.mkl:
+        os.environ["KMP_BLOCKTIME"] = str(params.kmp_blocktime)
+        os.environ["KMP_SETTINGS"] = str(params.kmp_settings)
+        os.environ["KMP_AFFINITY"] = params.kmp_affinity
+    return params
+
+
+def make_params(**kwargs):
+    return params_lib.make_params(**kwargs)
+
+
+def make_params_from_flags(argv=None):
+    return params_lib.make_params_from_flags(argv)

@@ -1,0 +1,414 @@
+// Fused batch-norm (+ residual add) (+ ReLU) forward and backward for NHWC
+// activations viewed as [rows, C].
+//
+// Replaces cuDNN's fused BN as used by tcb/convnet_builder.py:437-461 and the
+// ResNet block tail relu(shortcut + bn(conv)) (tcb/models/resnet_model_legacy.py:76-78).
+//
+// Structure (each phase is one launch, all HBM-streaming with 16-byte lanes):
+//   fwd : partial_stats  -> finalize (mean, invstd, running-stat update,
+//         per-channel scale/shift) -> apply (y = relu(x*scale+shift [+res]))
+//   bwd : partial_grad (sum dy', sum dy'*(x-mean), dy' = relu-masked dy)
+//         -> finalize (dgamma, dbeta, dx coefficients) -> apply
+//         (dx = dy'*A + x*B + Cc, dres = dy')
+// The partial kernels give every block a slab of rows and a window of channels
+// so a launch has >= 1024 workgroups on 256 CUs for the ResNet shapes.
+#include "common.h"
+
+namespace kfb {
+
+constexpr int BN_THREADS = 256;
+
+struct Geo {
+  int cw;    // channels per block window
+  int tpr;   // threads per row = cw / V
+  int rpi;   // rows per iteration = BN_THREADS / tpr
+  int nchunk;
+};
+
+template <int V>
+static Geo make_geo(int C) {
+  Geo g;
+  g.cw = C < BN_THREADS * V ? C : BN_THREADS * V;
+  g.tpr = g.cw / V;
+  g.rpi = BN_THREADS / g.tpr;
+  g.nchunk = ceil_div(C, g.cw);
+  return g;
+}
+
+// Sum of per-lane vectors over the rpi row-lanes of the block, via LDS.
+template <int V>
+__device__ __forceinline__ void block_row_reduce(float (&a)[V], float (&b)[V], float* lds, int t,
+                                                 int r, int tpr, int rpi) {
+  // lds layout: [rpi][tpr][V] for a then b.
+  const int stride = rpi * tpr * V;
+  if (r < rpi) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      lds[(r * tpr + t) * V + i] = a[i];
+      lds[stride + (r * tpr + t) * V + i] = b[i];
+    }
+  }
+  __syncthreads();
+  if (r == 0) {
+    for (int rr = 1; rr < rpi; ++rr) {
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        a[i] += lds[(rr * tpr + t) * V + i];
+        b[i] += lds[stride + (rr * tpr + t) * V + i];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- forward
+template <typename T, int V>
+__global__ void __launch_bounds__(BN_THREADS)
+bn_partial_stats_k(const T* __restrict__ x, long rows, int C, int cw, int tpr, int rpi,
+                   long slab_rows, float* __restrict__ psum, float* __restrict__ psq) {
+  extern __shared__ float lds[];
+  const int tid = threadIdx.x;
+  const int t = tid % tpr, r = tid / tpr;
+  const int c0 = blockIdx.y * cw + t * V;
+  const bool cok = (c0 < C) && (r < rpi);
+  float s[V], q[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) { s[i] = 0.f; q[i] = 0.f; }
+  const long rbeg = (long)blockIdx.x * slab_rows;
+  long rend = rbeg + slab_rows;
+  if (rend > rows) rend = rows;
+  if (cok) {
+    for (long row = rbeg + r; row < rend; row += rpi) {
+      float v[V];
+      load_vec<T, V>(x + row * C + c0, v);
+#pragma unroll
+      for (int i = 0; i < V; ++i) { s[i] += v[i]; q[i] += v[i] * v[i]; }
+    }
+  }
+  block_row_reduce<V>(s, q, lds, t, r, tpr, rpi);
+  if (r == 0 && c0 < C) {
+    float* ps = psum + (long)blockIdx.x * C + c0;
+    float* pq = psq + (long)blockIdx.x * C + c0;
+#pragma unroll
+    for (int i = 0; i < V; ++i) { ps[i] = s[i]; pq[i] = q[i]; }
+  }
+}
+
+// One thread per channel; folds the slab partials in double precision.
+__global__ void bn_finalize_stats_k(const float* __restrict__ psum, const float* __restrict__ psq,
+                                    int nslab, int C, long rows, const float* __restrict__ gamma,
+                                    const float* __restrict__ beta, float decay, float eps,
+                                    float* __restrict__ run_mean, float* __restrict__ run_var,
+                                    float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                    float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int k = 0; k < nslab; ++k) {
+    s += (double)psum[(long)k * C + c];
+    q += (double)psq[(long)k * C + c];
+  }
+  const double n = (double)rows;
+  const double mean = s / n;
+  double var = q / n - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  save_mean[c] = (float)mean;
+  save_invstd[c] = invstd;
+  scale[c] = g * invstd;
+  shift[c] = b - (float)mean * g * invstd;
+  if (run_mean) {
+    const double unbiased = rows > 1 ? var * n / (n - 1.0) : var;
+    run_mean[c] = run_mean[c] * decay + (float)mean * (1.f - decay);
+    run_var[c] = run_var[c] * decay + (float)unbiased * (1.f - decay);
+  }
+}
+
+__global__ void bn_infer_coefs_k(int C, const float* __restrict__ gamma,
+                                 const float* __restrict__ beta, const float* __restrict__ rm,
+                                 const float* __restrict__ rv, float eps, float* __restrict__ scale,
+                                 float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  const float sc = g * rsqrtf(rv[c] + eps);
+  scale[c] = sc;
+  shift[c] = b - rm[c] * sc;
+}
+
+template <typename T, int V, bool RES, bool RELU>
+__global__ void __launch_bounds__(256)
+bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y, long nvec, int C,
+           const float* __restrict__ scale, const float* __restrict__ shift) {
+  // nvec < 2^31 is checked on the host: 32-bit index math avoids 64-bit division.
+  const unsigned cv = (unsigned)(C / V);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)nvec;
+       i += gridDim.x * blockDim.x) {
+    const long e = (long)i * V;
+    const int c = (int)(i % cv) * V;
+    float v[V];
+    load_vec<T, V>(x + e, v);
+    float rr[V];
+    if (RES) load_vec<T, V>(res + e, rr);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      float o = v[k] * scale[c + k] + shift[c + k];
+      if (RES) o += rr[k];
+      if (RELU) o = fmaxf(o, 0.f);
+      v[k] = o;
+    }
+    store_vec<T, V>(y + e, v);
+  }
+}
+
+// ---------------------------------------------------------------- backward
+template <typename T, int V, bool MASK>
+__global__ void __launch_bounds__(BN_THREADS)
+bn_partial_grad_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __restrict__ x,
+                  const float* __restrict__ mean, long rows, int C, int cw, int tpr, int rpi,
+                  long slab_rows, float* __restrict__ pdy, float* __restrict__ pdyx) {
+  extern __shared__ float lds[];
+  const int tid = threadIdx.x;
+  const int t = tid % tpr, r = tid / tpr;
+  const int c0 = blockIdx.y * cw + t * V;
+  const bool cok = (c0 < C) && (r < rpi);
+  float s[V], q[V], m[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) { s[i] = 0.f; q[i] = 0.f; m[i] = cok ? mean[c0 + i] : 0.f; }
+  const long rbeg = (long)blockIdx.x * slab_rows;
+  long rend = rbeg + slab_rows;
+  if (rend > rows) rend = rows;
+  if (cok) {
+    for (long row = rbeg + r; row < rend; row += rpi) {
+      const long off = row * C + c0;
+      float g[V], xv[V];
+      load_vec<T, V>(dy + off, g);
+      load_vec<T, V>(x + off, xv);
+      if (MASK) {
+        float yv[V];
+        load_vec<T, V>(y + off, yv);
+#pragma unroll
+        for (int i = 0; i < V; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < V; ++i) { s[i] += g[i]; q[i] += g[i] * (xv[i] - m[i]); }
+    }
+  }
+  block_row_reduce<V>(s, q, lds, t, r, tpr, rpi);
+  if (r == 0 && c0 < C) {
+    float* ps = pdy + (long)blockIdx.x * C + c0;
+    float* pq = pdyx + (long)blockIdx.x * C + c0;
+#pragma unroll
+    for (int i = 0; i < V; ++i) { ps[i] = s[i]; pq[i] = q[i]; }
+  }
+}
+
+// dgamma = invstd * sum(dy'(x-mean)); dbeta = sum(dy').
+// dx = dy'*A + x*B + Cc  with A = g*invstd, B = -A*invstd^2*S2/n,
+// Cc = -A*S1/n - mean*B.
+__global__ void bn_finalize_grad_k(const float* __restrict__ pdy, const float* __restrict__ pdyx,
+                                   int nslab, int C, long rows, const float* __restrict__ gamma,
+                                   const float* __restrict__ mean, const float* __restrict__ invstd,
+                                   float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                   float* __restrict__ coefA, float* __restrict__ coefB,
+                                   float* __restrict__ coefC, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int k = 0; k < nslab; ++k) {
+    s1 += (double)pdy[(long)k * C + c];
+    s2 += (double)pdyx[(long)k * C + c];
+  }
+  const float is = invstd[c];
+  const float g = gamma ? gamma[c] : 1.f;
+  if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)(s2 * is);
+  if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)s1;
+  const double n = (double)rows;
+  const double A = (double)g * is;
+  const double B = -A * (double)is * (double)is * s2 / n;
+  coefA[c] = (float)A;
+  coefB[c] = (float)B;
+  coefC[c] = (float)(-A * s1 / n - (double)mean[c] * B);
+}
+
+template <typename T, int V, bool MASK, bool DRES>
+__global__ void __launch_bounds__(256)
+bn_bwd_apply_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __restrict__ x,
+               T* __restrict__ dx, T* __restrict__ dres, long nvec, int C,
+               const float* __restrict__ A, const float* __restrict__ B,
+               const float* __restrict__ Cc) {
+  // nvec < 2^31 is checked on the host: 32-bit index math avoids 64-bit division.
+  const unsigned cv = (unsigned)(C / V);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)nvec;
+       i += gridDim.x * blockDim.x) {
+    const long e = (long)i * V;
+    const int c = (int)(i % cv) * V;
+    float g[V], xv[V];
+    load_vec<T, V>(dy + e, g);
+    load_vec<T, V>(x + e, xv);
+    if (MASK) {
+      float yv[V];
+      load_vec<T, V>(y + e, yv);
+#pragma unroll
+      for (int k = 0; k < V; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+    }
+    if (DRES) store_vec<T, V>(dres + e, g);
+    float o[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) o[k] = g[k] * A[c + k] + xv[k] * B[c + k] + Cc[c + k];
+    store_vec<T, V>(dx + e, o);
+  }
+}
+
+static int stream_grid(long nvec) {
+  long b = (nvec + 255) / 256;
+  if (b > 256L * 16) b = 256L * 16;  // grid-stride beyond 16 blocks per CU
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+static long choose_slabs(long rows, int rpi, int nchunk) {
+  // Aim for ~2048 blocks in total and >= 8 row-iterations per thread.
+  long target = 2048 / nchunk;
+  if (target < 1) target = 1;
+  long max_by_work = rows / ((long)rpi * 8);
+  if (max_by_work < 1) max_by_work = 1;
+  long s = target < max_by_work ? target : max_by_work;
+  if (s > 4096) s = 4096;
+  return s;
+}
+
+template <typename T, int V, bool M, bool R>
+static void launch_bwd_apply(int gb, hipStream_t stream, const void* dy, const void* y,
+                             const void* x, void* dx, void* dres, long nvec, int C,
+                             const float* A, const float* B, const float* Cc) {
+  hipLaunchKernelGGL((bn_bwd_apply_k<T, V, M, R>), dim3(gb), dim3(256), 0, stream, (const T*)dy,
+                     (const T*)y, (const T*)x, (T*)dx, (T*)dres, nvec, C, A, B, Cc);
+}
+
+}  // namespace kfb
+
+using namespace kfb;
+
+// Number of slab partial rows the caller must allocate (per output array).
+KFB_API int kfb_bn_num_slabs(long rows, int C) {
+  const int V = vec_width(C);
+  int n = 0;
+  KFB_DISPATCH_VEC(V, VV, { Geo g = make_geo<VV>(C); n = (int)choose_slabs(rows, g.rpi, g.nchunk); });
+  return n;
+}
+
+// Forward, training mode. psum/psq: [nslab, C] fp32 scratch.
+KFB_API hipError_t kfb_bn_fwd_train(int dtype, const void* x, const void* res, void* y, long rows,
+                                    int C, const float* gamma, const float* beta, float decay,
+                                    float eps, float* run_mean, float* run_var, float* save_mean,
+                                    float* save_invstd, float* scale, float* shift, float* psum,
+                                    float* psq, int nslab, int relu, hipStream_t stream) {
+  const int V = vec_width(C);
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    KFB_DISPATCH_VEC(V, VV, {
+      Geo g = make_geo<VV>(C);
+      const long slab_rows = (rows + nslab - 1) / nslab;
+      dim3 grid(nslab, g.nchunk);
+      const size_t lds = 2 * (size_t)g.rpi * g.tpr * VV * sizeof(float);
+      hipLaunchKernelGGL((bn_partial_stats_k<T, VV>), grid, dim3(BN_THREADS), lds, stream,
+                         (const T*)x, rows, C, g.cw, g.tpr, g.rpi, slab_rows, psum, psq);
+      hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 256)), dim3(256), 0, stream, psum,
+                         psq, nslab, C, rows, gamma, beta, decay, eps, run_mean, run_var,
+                         save_mean, save_invstd, scale, shift);
+      const long nvec = rows * C / VV;
+      const int gb = stream_grid(nvec);
+      if (res) {
+        if (relu)
+          hipLaunchKernelGGL((bn_apply_k<T, VV, true, true>), dim3(gb), dim3(256), 0, stream,
+                             (const T*)x, (const T*)res, (T*)y, nvec, C, scale, shift);
+        else
+          hipLaunchKernelGGL((bn_apply_k<T, VV, true, false>), dim3(gb), dim3(256), 0, stream,
+                             (const T*)x, (const T*)res, (T*)y, nvec, C, scale, shift);
+      } else {
+        if (relu)
+          hipLaunchKernelGGL((bn_apply_k<T, VV, false, true>), dim3(gb), dim3(256), 0, stream,
+                             (const T*)x, (const T*)nullptr, (T*)y, nvec, C, scale, shift);
+        else
+          hipLaunchKernelGGL((bn_apply_k<T, VV, false, false>), dim3(gb), dim3(256), 0, stream,
+                             (const T*)x, (const T*)nullptr, (T*)y, nvec, C, scale, shift);
+      }
+    });
+  });
+  return hipGetLastError();
+}
+
+// Forward, inference mode (moving statistics).
+KFB_API hipError_t kfb_bn_fwd_infer(int dtype, const void* x, const void* res, void* y, long rows,
+                                    int C, const float* gamma, const float* beta,
+                                    const float* run_mean, const float* run_var, float eps,
+                                    float* scale, float* shift, int relu, hipStream_t stream) {
+  const int V = vec_width(C);
+  hipLaunchKernelGGL(bn_infer_coefs_k, dim3(ceil_div(C, 256)), dim3(256), 0, stream, C, gamma,
+                     beta, run_mean, run_var, eps, scale, shift);
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    KFB_DISPATCH_VEC(V, VV, {
+      const long nvec = rows * C / VV;
+      const int gb = stream_grid(nvec);
+      if (res) {
+        if (relu)
+          hipLaunchKernelGGL((bn_apply_k<T, VV, true, true>), dim3(gb), dim3(256), 0, stream,
+                             (const T*)x, (const T*)res, (T*)y, nvec, C, scale, shift);
+        else
+          hipLaunchKernelGGL((bn_apply_k<T, VV, true, false>), dim3(gb), dim3(256), 0, stream,
+                             (const T*)x, (const T*)res, (T*)y, nvec, C, scale, shift);
+      } else {
+        if (relu)
+          hipLaunchKernelGGL((bn_apply_k<T, VV, false, true>), dim3(gb), dim3(256), 0, stream,
+                             (const T*)x, (const T*)nullptr, (T*)y, nvec, C, scale, shift);
+        else
+          hipLaunchKernelGGL((bn_apply_k<T, VV, false, false>), dim3(gb), dim3(256), 0, stream,
+                             (const T*)x, (const T*)nullptr, (T*)y, nvec, C, scale, shift);
+      }
+    });
+  });
+  return hipGetLastError();
+}
+
+// Backward. y (forward output) supplies the ReLU mask when relu != 0.
+// dres (may be null) receives the gradient of the residual input.
+// dgamma/dbeta are written (accumulate=0) or added to (accumulate=1).
+KFB_API hipError_t kfb_bn_bwd(int dtype, const void* dy, const void* y, const void* x, void* dx,
+                              void* dres, long rows, int C, const float* gamma,
+                              const float* save_mean, const float* save_invstd, float* dgamma,
+                              float* dbeta, float* pdy, float* pdyx, int nslab, float* coefA,
+                              float* coefB, float* coefC, int relu, int accumulate,
+                              hipStream_t stream) {
+  const int V = vec_width(C);
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    KFB_DISPATCH_VEC(V, VV, {
+      Geo g = make_geo<VV>(C);
+      const long slab_rows = (rows + nslab - 1) / nslab;
+      dim3 grid(nslab, g.nchunk);
+      const size_t lds = 2 * (size_t)g.rpi * g.tpr * VV * sizeof(float);
+      if (relu)
+        hipLaunchKernelGGL((bn_partial_grad_k<T, VV, true>), grid, dim3(BN_THREADS), lds, stream,
+                           (const T*)dy, (const T*)y, (const T*)x, save_mean, rows, C, g.cw,
+                           g.tpr, g.rpi, slab_rows, pdy, pdyx);
+      else
+        hipLaunchKernelGGL((bn_partial_grad_k<T, VV, false>), grid, dim3(BN_THREADS), lds,
+                           stream, (const T*)dy, (const T*)y, (const T*)x, save_mean, rows, C,
+                           g.cw, g.tpr, g.rpi, slab_rows, pdy, pdyx);
+      hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 256)), dim3(256), 0, stream, pdy,
+                         pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta,
+                         coefA, coefB, coefC, accumulate);
+      const long nvec = rows * C / VV;
+      const int gb = stream_grid(nvec);
+      if (relu) {
+        if (dres) launch_bwd_apply<T, VV, true, true>(gb, stream, dy, y, x, dx, dres, nvec, C, coefA, coefB, coefC);
+        else launch_bwd_apply<T, VV, true, false>(gb, stream, dy, y, x, dx, dres, nvec, C, coefA, coefB, coefC);
+      } else {
+        if (dres) launch_bwd_apply<T, VV, false, true>(gb, stream, dy, y, x, dx, dres, nvec, C, coefA, coefB, coefC);
+        else launch_bwd_apply<T, VV, false, false>(gb, stream, dy, y, x, dx, dres, nvec, C, coefA, coefB, coefC);
+      }
+    });
+  });
+  return hipGetLastError();
+}

@@ -1,0 +1,271 @@
+// Elementwise / small-reduction kernels for the non-BN layers.
+//
+//   bias_act_fwd     y = act(x + b)            conv/affine bias + relu
+//                                               (tcb/convnet_builder.py:188-213, 311-345)
+//   act_bwd_bias     dx = dy * relu'(y); db += colsum(dx)
+//   dropout fwd/bwd  counter-based hash RNG: the mask is recomputed from
+//                    (seed, index) in the backward, nothing is stored
+//                    (tcb/convnet_builder.py:396-406)
+//   synthetic_fill   truncated normal(127, 60) images + uniform labels, made on
+//                    device (tcb/models/model.py:220-237)
+//   add              y = a + b (+relu)
+#include "common.h"
+
+namespace kfb {
+
+__device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
+  // lowbias32 (Wellons) - good avalanche, 6 ops.
+  x ^= x >> 16; x *= 0x7feb352dU;
+  x ^= x >> 15; x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ float u01(uint32_t seed, uint64_t i, uint32_t stream) {
+  uint32_t h = hash_u32((uint32_t)i ^ hash_u32(seed + 0x9e3779b9U * stream) ^
+                        hash_u32((uint32_t)(i >> 32) + 0x85ebca6bU));
+  return ((h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+template <typename T, int V, bool RELU>
+__global__ void __launch_bounds__(256)
+bias_act_k(const T* __restrict__ x, const float* __restrict__ b, T* __restrict__ y, long nvec,
+           int C) {
+  const unsigned cv = (unsigned)(C / V);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)nvec;
+       i += gridDim.x * blockDim.x) {
+    const long e = (long)i * V;
+    const int c = (int)(i % cv) * V;
+    float v[V];
+    load_vec<T, V>(x + e, v);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      float o = v[k] + (b ? b[c + k] : 0.f);
+      v[k] = RELU ? fmaxf(o, 0.f) : o;
+    }
+    store_vec<T, V>(y + e, v);
+  }
+}
+
+// dx = dy * (y > 0) [if RELU]; partial column sums of dx into pbias[blockIdx.x][C].
+// Grid: (nslab, nchunk) with a window of 256*V/... like the BN partial kernels:
+// each block owns cw channels and a slab of rows.
+template <typename T, int V, bool RELU>
+__global__ void __launch_bounds__(256)
+act_bwd_bias_k(const T* __restrict__ dy, const T* __restrict__ y, T* __restrict__ dx, long rows,
+               int C, int cw, int tpr, int rpi, long slab_rows, float* __restrict__ pbias) {
+  extern __shared__ float lds[];
+  const int tid = threadIdx.x;
+  const int t = tid % tpr, r = tid / tpr;
+  const int c0 = blockIdx.y * cw + t * V;
+  const bool cok = (c0 < C) && (r < rpi);
+  float s[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) s[k] = 0.f;
+  const long rbeg = (long)blockIdx.x * slab_rows;
+  long rend = rbeg + slab_rows;
+  if (rend > rows) rend = rows;
+  if (cok) {
+    for (long row = rbeg + r; row < rend; row += rpi) {
+      const long off = row * C + c0;
+      float g[V];
+      load_vec<T, V>(dy + off, g);
+      if (RELU) {
+        float yv[V];
+        load_vec<T, V>(y + off, yv);
+#pragma unroll
+        for (int k = 0; k < V; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+        if (dx) store_vec<T, V>(dx + off, g);
+      }
+#pragma unroll
+      for (int k = 0; k < V; ++k) s[k] += g[k];
+    }
+  }
+  if (pbias) {
+    if (r < rpi) {
+#pragma unroll
+      for (int k = 0; k < V; ++k) lds[(r * tpr + t) * V + k] = s[k];
+    }
+    __syncthreads();
+    if (r == 0 && c0 < C) {
+      for (int rr = 1; rr < rpi; ++rr)
+#pragma unroll
+        for (int k = 0; k < V; ++k) s[k] += lds[(rr * tpr + t) * V + k];
+#pragma unroll
+      for (int k = 0; k < V; ++k) pbias[(long)blockIdx.x * C + c0 + k] = s[k];
+    }
+  }
+}
+
+__global__ void colsum_finalize_k(const float* __restrict__ p, int nslab, int C,
+                                  float* __restrict__ out, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int k = 0; k < nslab; ++k) s += (double)p[(long)k * C + c];
+  out[c] = (accumulate ? out[c] : 0.f) + (float)s;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+dropout_k(const T* __restrict__ x, T* __restrict__ y, long n, float keep, uint32_t seed) {
+  const float inv = 1.f / keep;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    const float u = u01(seed, (uint64_t)i, 7u);
+    y[i] = from_f32<T>(u < keep ? to_f32(x[i]) * inv : 0.f);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+synthetic_images_k(T* __restrict__ x, long n, float mean, float std, uint32_t seed) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    // Truncated normal (|z| <= 2) by rejection over a few Box-Muller draws.
+    float z = 0.f;
+    for (uint32_t k = 0; k < 8; ++k) {
+      const float u1 = u01(seed, (uint64_t)i, 2 * k + 1), u2 = u01(seed, (uint64_t)i, 2 * k + 2);
+      z = sqrtf(-2.f * __logf(u1)) * __cosf(6.28318530718f * u2);
+      if (fabsf(z) <= 2.f) break;
+      z = 0.f;
+    }
+    x[i] = from_f32<T>(mean + std * z);
+  }
+}
+
+__global__ void __launch_bounds__(256)
+synthetic_labels_k(int* __restrict__ y, long n, int maxval, uint32_t seed) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    int v = (int)(u01(seed, (uint64_t)i, 99u) * (float)maxval);
+    y[i] = v >= maxval ? maxval - 1 : v;
+  }
+}
+
+template <typename T, int V, bool RELU>
+__global__ void __launch_bounds__(256)
+add_k(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ y, long nvec) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
+       i += (long)gridDim.x * blockDim.x) {
+    float va[V], vb[V];
+    load_vec<T, V>(a + i * V, va);
+    load_vec<T, V>(b + i * V, vb);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float o = va[k] + vb[k];
+      va[k] = RELU ? fmaxf(o, 0.f) : o;
+    }
+    store_vec<T, V>(y + i * V, va);
+  }
+}
+
+static int egrid(long n) {
+  long b = (n + 255) / 256;
+  if (b > 256L * 16) b = 256L * 16;
+  return (int)(b < 1 ? 1 : b);
+}
+
+}  // namespace kfb
+
+using namespace kfb;
+
+KFB_API hipError_t kfb_bias_act(int dtype, const void* x, const float* b, void* y, long rows, int C,
+                                int relu, hipStream_t stream) {
+  const int V = vec_width(C);
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    KFB_DISPATCH_VEC(V, VV, {
+      const long nvec = rows * C / VV;
+      if (relu)
+        hipLaunchKernelGGL((bias_act_k<T, VV, true>), dim3(egrid(nvec)), dim3(256), 0, stream,
+                           (const T*)x, b, (T*)y, nvec, C);
+      else
+        hipLaunchKernelGGL((bias_act_k<T, VV, false>), dim3(egrid(nvec)), dim3(256), 0, stream,
+                           (const T*)x, b, (T*)y, nvec, C);
+    });
+  });
+  return hipGetLastError();
+}
+
+KFB_API int kfb_colsum_num_slabs(long rows, int C) {
+  const int V = vec_width(C);
+  const int cw = C < 256 * V ? C : 256 * V;
+  const int tpr = cw / V, rpi = 256 / tpr;
+  const int nchunk = ceil_div(C, cw);
+  long target = 1024 / nchunk;
+  if (target < 1) target = 1;
+  long by_work = rows / ((long)rpi * 8);
+  if (by_work < 1) by_work = 1;
+  long s = target < by_work ? target : by_work;
+  return (int)(s > 4096 ? 4096 : s);
+}
+
+// relu-backward (if relu) and bias-gradient column sums in one pass.
+// dx may alias dy. db (may be null) is written or accumulated.
+KFB_API hipError_t kfb_act_bwd_bias(int dtype, const void* dy, const void* y, void* dx, long rows,
+                                    int C, int relu, float* pbias, int nslab, float* db,
+                                    int accumulate, hipStream_t stream) {
+  const int V = vec_width(C);
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    KFB_DISPATCH_VEC(V, VV, {
+      const int cw = C < 256 * VV ? C : 256 * VV;
+      const int tpr = cw / VV, rpi = 256 / tpr;
+      const int nchunk = ceil_div(C, cw);
+      const long slab_rows = (rows + nslab - 1) / nslab;
+      const size_t lds = (size_t)rpi * tpr * VV * sizeof(float);
+      dim3 grid(nslab, nchunk);
+      float* pb = db ? pbias : nullptr;
+      if (relu)
+        hipLaunchKernelGGL((act_bwd_bias_k<T, VV, true>), grid, dim3(256), lds, stream,
+                           (const T*)dy, (const T*)y, (T*)dx, rows, C, cw, tpr, rpi, slab_rows, pb);
+      else
+        hipLaunchKernelGGL((act_bwd_bias_k<T, VV, false>), grid, dim3(256), lds, stream,
+                           (const T*)dy, (const T*)y, (T*)dx, rows, C, cw, tpr, rpi, slab_rows, pb);
+      if (db)
+        hipLaunchKernelGGL(colsum_finalize_k, dim3(ceil_div(C, 256)), dim3(256), 0, stream,
+                           pbias, nslab, C, db, accumulate);
+    });
+  });
+  return hipGetLastError();
+}
+
+KFB_API hipError_t kfb_dropout(int dtype, const void* x, void* y, long n, float keep, uint32_t seed,
+                               hipStream_t stream) {
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((dropout_k<T>), dim3(egrid(n)), dim3(256), 0, stream, (const T*)x, (T*)y, n,
+                       keep, seed);
+  });
+  return hipGetLastError();
+}
+
+KFB_API hipError_t kfb_synthetic_images(int dtype, void* x, long n, float mean, float std,
+                                        uint32_t seed, hipStream_t stream) {
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((synthetic_images_k<T>), dim3(egrid(n)), dim3(256), 0, stream, (T*)x, n,
+                       mean, std, seed);
+  });
+  return hipGetLastError();
+}
+
+KFB_API hipError_t kfb_synthetic_labels(int* y, long n, int maxval, uint32_t seed,
+                                        hipStream_t stream) {
+  hipLaunchKernelGGL(synthetic_labels_k, dim3(egrid(n)), dim3(256), 0, stream, y, n, maxval, seed);
+  return hipGetLastError();
+}
+
+KFB_API hipError_t kfb_add(int dtype, const void* a, const void* b, void* y, long n, int relu,
+                           hipStream_t stream) {
+  const int V = (n % 8 == 0) ? 8 : (n % 4 == 0) ? 4 : (n % 2 == 0) ? 2 : 1;
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    KFB_DISPATCH_VEC(V, VV, {
+      const long nvec = n / VV;
+      if (relu)
+        hipLaunchKernelGGL((add_k<T, VV, true>), dim3(egrid(nvec)), dim3(256), 0, stream,
+                           (const T*)a, (const T*)b, (T*)y, nvec);
+      else
+        hipLaunchKernelGGL((add_k<T, VV, false>), dim3(egrid(nvec)), dim3(256), 0, stream,
+                           (const T*)a, (const T*)b, (T*)y, nvec);
+    });
+  });
+  return hipGetLastError();
+}

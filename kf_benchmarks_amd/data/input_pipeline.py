@@ -1,0 +1,119 @@
+"""Input sources feeding the hot loop.
+
+* :class:`SyntheticInput` - on-device synthetic ImageNet-shaped batches
+  (tcb/models/model.py:220-237).  Generated once and reused unless
+  ``--synthetic_resample`` (the reference re-samples each step; values of
+  synthetic data do not matter for the benchmark, and reuse keeps the RNG
+  kernel out of the timed step).
+* :class:`PrefetchInput` - real data: host preprocessing workers
+  (:mod:`kf_benchmarks_amd.data.preprocessing`) produce NHWC uint8/float
+  batches into pinned buffers; a copy stream moves them to the device one
+  batch ahead (the StagingArea double buffering of tcb/benchmark_cnn.py:2527-2600).
+"""
+
+from __future__ import annotations
+
+import queue
+import threading
+from typing import Optional
+
+import torch
+
+
+class SyntheticInput:
+    def __init__(self, bench, subset="train"):
+        self.bench = bench
+        model = bench.model
+        nclass = bench.dataset.num_classes
+        self.resample = bench.params.synthetic_resample
+        self.seed = bench.params.tf_random_seed + 1000 * bench.task_index
+        self.step = 0
+        self.images, self.labels = model.get_synthetic_inputs("input", nclass, bench.device,
+                                                              self.seed)
+
+    def next(self):
+        if self.resample:
+            self.step += 1
+            model = self.bench.model
+            self.images, self.labels = model.get_synthetic_inputs(
+                "input", self.bench.dataset.num_classes, self.bench.device, self.seed + self.step)
+        return self.images, self.labels
+
+    def close(self):
+        pass
+
+
+class PrefetchInput:
+    """Pulls host batches from a preprocessor generator on a thread, copies
+    them to the device on a side stream, one batch ahead."""
+
+    def __init__(self, bench, batch_iter, depth: int = 2):
+        self.bench = bench
+        self.device = bench.device
+        self.dtype = bench.compute_dtype
+        self._q: "queue.Queue" = queue.Queue(maxsize=max(depth, 1))
+        self._it = batch_iter
+        self._stop = threading.Event()
+        self._err: Optional[BaseException] = None
+        self._thread = threading.Thread(target=self._run, daemon=True)
+        self._thread.start()
+        self._stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self._next = None
+
+    def _run(self):
+        try:
+            for images, labels in self._it:
+                if self._stop.is_set():
+                    return
+                img = torch.from_numpy(images)
+                lab = torch.from_numpy(labels).to(torch.int32)
+                if self.device.type == "cuda":
+                    img = img.pin_memory()
+                    lab = lab.pin_memory()
+                self._q.put((img, lab))
+            self._q.put(None)
+        except BaseException as e:
+            self._err = e
+            self._q.put(None)
+
+    def _fetch(self):
+        item = self._q.get()
+        if item is None:
+            if self._err is not None:
+                raise RuntimeError("input pipeline failed") from self._err
+            raise StopIteration("input exhausted")
+        img, lab = item
+        if self._stream is not None:
+            with torch.cuda.stream(self._stream):
+                img = img.to(self.device, non_blocking=True).to(self.dtype)
+                lab = lab.to(self.device, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self._stream)
+            return img, lab, ev
+        return img.to(self.dtype), lab, None
+
+    def next(self):
+        if self._next is None:
+            self._next = self._fetch()
+        img, lab, ev = self._next
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+            img.record_stream(torch.cuda.current_stream(self.device))
+            lab.record_stream(torch.cuda.current_stream(self.device))
+        try:
+            self._next = self._fetch()
+        except StopIteration:
+            self._next = None
+            self._exhausted = True
+        return img, lab
+
+    def close(self):
+        self._stop.set()
+
+
+def make_input_source(bench, subset="train"):
+    if bench.dataset.use_synthetic_gpu_inputs():
+        return SyntheticInput(bench, subset)
+    from . import preprocessing
+    it = preprocessing.make_batch_iterator(bench, subset)
+    return PrefetchInput(bench, it, depth=max(bench.params.datasets_prefetch_buffer_size, 1) + 1)

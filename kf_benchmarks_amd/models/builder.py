@@ -1,0 +1,259 @@
+"""ConvNetBuilder: the layer DSL the model zoo is written in.
+
+Same vocabulary and naming as tcb/convnet_builder.py:29-469 (conv with
+SAME/VALID/SAME_RESNET, mpool, apool, reshape, affine, inception_module,
+spatial_mean, dropout, batch_norm, lrn, aux head), but eager: each call runs
+the op immediately on NHWC tensors through :mod:`kf_benchmarks_amd.ops`.
+
+Variables live in a :class:`Network` and are looked up by scope name, which
+plays the role of TF's variable scopes with reuse: the first (materializing)
+forward creates a layer, every later forward finds it under the same name.
+Two additions over the reference DSL, both pure fusions with identical
+semantics: ``conv(..., residual=t)`` computes relu(bn(conv(x)) + t) in the BN
+epilogue (the ResNet block tail), and ``add(a, b, relu)``.
+"""
+
+from __future__ import annotations
+
+import collections
+import contextlib
+import math
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..ops import nn as F
+from .layers import AffineLayer, BatchNormLayer, ConvLayer
+
+
+class ConvNetBuilder:
+    def __init__(self, net, input_op, input_nchan, phase_train, dtype):
+        self.net = net
+        self.top_layer = input_op
+        self.top_size = input_nchan
+        self.phase_train = phase_train
+        self.dtype = dtype
+        self.counts = collections.defaultdict(int)
+        self.use_batch_norm = False
+        self.batch_norm_config = {}
+        self.aux_top_layer = None
+        self.aux_top_size = 0
+        self._scopes = []
+        self.meta = input_op.device.type == "meta"
+        self.impl = net.kernel_impl
+
+    # ---------------------------------------------------------------- scopes
+    @contextlib.contextmanager
+    def scope(self, name):
+        self._scopes.append(name)
+        try:
+            yield
+        finally:
+            self._scopes.pop()
+
+    def _scoped(self, name):
+        return "/".join(self._scopes + [name])
+
+    def _p(self, t):
+        if t is None or not self.meta:
+            return t
+        return t.detach().to("meta")
+
+    def _layer(self, scope, factory):
+        return self.net.get_or_create(scope, factory)
+
+    @contextlib.contextmanager
+    def switch_to_aux_top_layer(self):
+        if self.aux_top_layer is None:
+            raise RuntimeError("Empty auxiliary top layer in the network.")
+        saved = (self.top_layer, self.top_size)
+        self.top_layer, self.top_size = self.aux_top_layer, self.aux_top_size
+        try:
+            yield
+        finally:
+            self.aux_top_layer, self.aux_top_size = self.top_layer, self.top_size
+            self.top_layer, self.top_size = saved
+
+    # ------------------------------------------------------------------ conv
+    def conv(self, num_out_channels, k_height, k_width, d_height=1, d_width=1, mode="SAME",
+             input_layer=None, num_channels_in=None, use_batch_norm=None, stddev=None,
+             activation="relu", bias=0.0, kernel_initializer=None, residual=None):
+        x = self.top_layer if input_layer is None else input_layer
+        cin = self.top_size if num_channels_in is None else num_channels_in
+        name = "conv%d" % self.counts["conv"]
+        self.counts["conv"] += 1
+        if use_batch_norm is None:
+            use_batch_norm = self.use_batch_norm
+        scope = self._scoped(name)
+        use_bias = (not use_batch_norm) and bias is not None
+        layer = self._layer(scope, lambda: ConvLayer(
+            scope, cin, num_out_channels, k_height, k_width, use_bias, bias or 0.0, stddev,
+            self.net.init_gen, self.net.param_device))
+        _, H, W, _ = x.shape
+        pads = F.resolve_pads(mode, H, W, k_height, k_width, d_height, d_width)
+        w = self._p(layer.weight)
+        y = F.conv2d(x, w, None if self.meta else layer.weight_lp, (d_height, d_width), pads,
+                     self.impl)
+        relu = activation == "relu"
+        if use_batch_norm:
+            with self.scope(name):
+                self.top_layer, self.top_size = y, num_out_channels
+                y = self.batch_norm(relu=relu, residual=residual, **self.batch_norm_config)
+            if activation not in ("relu", None, "linear"):
+                y = F.activation(y, activation)
+        else:
+            y = F.bias_act(y, self._p(layer.bias), relu)
+            if residual is not None:
+                y = F.add(y, residual)
+            if activation not in ("relu", None, "linear"):
+                y = F.activation(y, activation)
+        self.top_layer, self.top_size = y, num_out_channels
+        return y
+
+    # --------------------------------------------------------------- pooling
+    def _pool(self, pool_name, k_height, k_width, d_height, d_width, mode, input_layer,
+              num_channels_in):
+        if input_layer is None:
+            input_layer = self.top_layer
+        else:
+            self.top_size = num_channels_in
+        self.counts[pool_name] += 1
+        fn = F.max_pool if pool_name == "mpool" else F.avg_pool
+        y = fn(input_layer, k_height, k_width, d_height, d_width, mode)
+        self.top_layer = y
+        return y
+
+    def mpool(self, k_height, k_width, d_height=2, d_width=2, mode="VALID", input_layer=None,
+              num_channels_in=None):
+        return self._pool("mpool", k_height, k_width, d_height, d_width, mode, input_layer,
+                          num_channels_in)
+
+    def apool(self, k_height, k_width, d_height=2, d_width=2, mode="VALID", input_layer=None,
+              num_channels_in=None):
+        return self._pool("apool", k_height, k_width, d_height, d_width, mode, input_layer,
+                          num_channels_in)
+
+    # ----------------------------------------------------------------- shape
+    def reshape(self, shape, input_layer=None):
+        x = self.top_layer if input_layer is None else input_layer
+        self.top_layer = x.reshape(shape)
+        self.top_size = shape[-1]
+        return self.top_layer
+
+    def flatten(self):
+        """Flatten NHWC to [N, H*W*C] (the reference reshapes NCHW tensors;
+        element order therefore differs but the layer is equivalent)."""
+        x = self.top_layer
+        n = x.shape[0]
+        size = int(np.prod(x.shape[1:]))
+        self.top_layer = x.reshape(n, size)
+        self.top_size = size
+        return self.top_layer
+
+    # ---------------------------------------------------------------- affine
+    def affine(self, num_out_channels, input_layer=None, num_channels_in=None, bias=0.0,
+               stddev=None, activation="relu"):
+        x = self.top_layer if input_layer is None else input_layer
+        cin = self.top_size if num_channels_in is None else num_channels_in
+        name = "affine%d" % self.counts["affine"]
+        self.counts["affine"] += 1
+        scope = self._scoped(name)
+        init_factor = 2.0 if activation == "relu" else 1.0
+        std = stddev or math.sqrt(init_factor / cin)
+        layer = self._layer(scope, lambda: AffineLayer(
+            scope, cin, num_out_channels, bias, std, self.net.init_gen, self.net.param_device))
+        y = F.linear(x, self._p(layer.weights), self._p(layer.biases),
+                     None if self.meta else layer.weights_lp, relu=activation == "relu")
+        if activation not in ("relu", None, "linear"):
+            raise KeyError("Invalid activation type '%s'" % activation)
+        self.top_layer, self.top_size = y, num_out_channels
+        return y
+
+    # ------------------------------------------------------------- inception
+    def inception_module(self, name, cols, input_layer=None, in_size=None):
+        x = self.top_layer if input_layer is None else input_layer
+        cin = self.top_size if in_size is None else in_size
+        name = name + str(self.counts[name])
+        self.counts[name] += 1
+        with self.scope(name):
+            col_layers, col_sizes = [], []
+            for c, col in enumerate(cols):
+                col_layers.append([])
+                col_sizes.append([])
+                for li, layer in enumerate(col):
+                    ltype, args = layer[0], layer[1:]
+                    kwargs = {"input_layer": x, "num_channels_in": cin} if li == 0 else {}
+                    if ltype == "conv":
+                        self.conv(*args, **kwargs)
+                    elif ltype == "mpool":
+                        self.mpool(*args, **kwargs)
+                    elif ltype == "apool":
+                        self.apool(*args, **kwargs)
+                    elif ltype == "share":
+                        self.top_layer = col_layers[c - 1][li]
+                        self.top_size = col_sizes[c - 1][li]
+                    else:
+                        raise KeyError("Invalid layer type for inception module: '%s'" % ltype)
+                    col_layers[c].append(self.top_layer)
+                    col_sizes[c].append(self.top_size)
+            self.top_layer = F.concat_channels([l[-1] for l in col_layers])
+            self.top_size = sum(s[-1] for s in col_sizes)
+        return self.top_layer
+
+    # ----------------------------------------------------------------- misc
+    def spatial_mean(self, keep_dims=False):
+        self.counts["spatial_mean"] += 1
+        self.top_layer = F.spatial_mean(self.top_layer, keep_dims)
+        return self.top_layer
+
+    def dropout(self, keep_prob=0.5, input_layer=None):
+        x = self.top_layer if input_layer is None else input_layer
+        if input_layer is not None:
+            self.top_size = None
+        self.counts["dropout"] += 1
+        seed = self.net.next_dropout_seed()
+        self.top_layer = F.dropout(x, keep_prob, self.phase_train and not self.meta, seed)
+        return self.top_layer
+
+    def batch_norm(self, input_layer=None, decay=0.999, scale=False, epsilon=0.001, relu=False,
+                   residual=None):
+        x = self.top_layer if input_layer is None else input_layer
+        name = "batchnorm%d" % self.counts["batchnorm"]
+        self.counts["batchnorm"] += 1
+        scope = self._scoped(name)
+        C = x.shape[-1]
+        layer = self._layer(scope, lambda: BatchNormLayer(scope, C, scale, decay, epsilon,
+                                                          self.net.param_device))
+        training = self.phase_train and not self.meta
+        if self.meta:
+            y = F.batch_norm(x, self._p(layer.gamma), self._p(layer.beta),
+                             self._p(layer.moving_mean), self._p(layer.moving_variance),
+                             layer.decay, layer.eps, False, relu, residual)
+        else:
+            y = F.batch_norm(x, layer.gamma, layer.beta, layer.moving_mean,
+                             layer.moving_variance, layer.decay, layer.eps, training, relu,
+                             residual)
+        self.top_layer, self.top_size = y, C
+        return y
+
+    def relu(self, x=None):
+        x = self.top_layer if x is None else x
+        self.top_layer = F.relu(x)
+        return self.top_layer
+
+    def add(self, a, b, relu=False):
+        y = F.add(a, b, relu)
+        self.top_layer = y
+        return y
+
+    def concat(self, xs):
+        self.top_layer = F.concat_channels(xs)
+        self.top_size = self.top_layer.shape[-1]
+        return self.top_layer
+
+    def lrn(self, depth_radius, bias, alpha, beta):
+        self.counts["lrn"] += 1
+        self.top_layer = F.lrn(self.top_layer, depth_radius, bias, alpha, beta)
+        return self.top_layer

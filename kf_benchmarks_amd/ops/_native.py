@@ -1,0 +1,142 @@
+"""ctypes binding of ``_lib/libkfb_hip.so`` (our gfx950 kernels).
+
+Every op in :mod:`kf_benchmarks_amd.ops` that runs on a GPU tensor goes
+through this module.  If the library is missing or fails to load while a GPU
+is in use we raise immediately: there is deliberately no silent PyTorch
+fallback on the GPU path (the CPU path exists only for the ``--device=cpu``
+plumbing config and for numerics references in tests).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+from .. import build as _build
+
+_LIB = None
+_LOCK = threading.Lock()
+
+F32, BF16, F16 = 0, 1, 2
+_DT = {torch.float32: F32, torch.bfloat16: BF16, torch.float16: F16}
+
+c_void_p, c_int, c_long, c_float, c_uint32 = (ctypes.c_void_p, ctypes.c_int, ctypes.c_long,
+                                               ctypes.c_float, ctypes.c_uint32)
+P = c_void_p
+I = c_int
+L = c_long
+F = c_float
+
+# name -> argtypes (restype is int = hipError_t unless listed in _RESTYPES)
+_SIGS = {
+    "kfb_bn_num_slabs": [L, I],
+    "kfb_bn_fwd_train": [I, P, P, P, L, I, P, P, F, F, P, P, P, P, P, P, P, P, I, I, P],
+    "kfb_bn_fwd_infer": [I, P, P, P, L, I, P, P, P, P, F, P, P, I, P],
+    "kfb_bn_bwd": [I, P, P, P, P, P, L, I, P, P, P, P, P, P, P, I, P, P, P, I, I, P],
+    "kfb_opt_step": [I, P, P, P, P, P, I, P, L, F, F, F, F, F, F, F, F, F, I, P],
+    "kfb_nonfinite": [P, L, P, P],
+    "kfb_half_sumsq": [P, L, P, P],
+    "kfb_cast_f32": [P, P, I, L, P],
+    "kfb_xent_fwd": [I, P, P, L, I, P, P, P],
+    "kfb_xent_bwd": [I, P, P, P, P, F, L, I, P, P],
+    "kfb_in_top_k": [I, P, P, L, I, P, P, P],
+    "kfb_maxpool_fwd": [I, P, P, P] + [I] * 12 + [P],
+    "kfb_maxpool_bwd": [I, P, P, P] + [I] * 12 + [P],
+    "kfb_avgpool_fwd": [I, P, P] + [I] * 12 + [P],
+    "kfb_avgpool_bwd": [I, P, P] + [I] * 12 + [P],
+    "kfb_gap_fwd": [I, P, P, I, I, I, P],
+    "kfb_gap_bwd": [I, P, P, I, I, I, P],
+    "kfb_bias_act": [I, P, P, P, L, I, I, P],
+    "kfb_colsum_num_slabs": [L, I],
+    "kfb_act_bwd_bias": [I, P, P, P, L, I, I, P, I, P, I, P],
+    "kfb_dropout": [I, P, P, L, F, c_uint32, P],
+    "kfb_synthetic_images": [I, P, L, F, F, c_uint32, P],
+    "kfb_synthetic_labels": [P, L, I, c_uint32, P],
+    "kfb_add": [I, P, P, P, L, I, P],
+}
+_RESTYPES = {"kfb_bn_num_slabs": c_int, "kfb_colsum_num_slabs": c_int}
+# Optional symbols (added by later kernel files); bound if present.
+_OPTIONAL = {}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib_path() -> str:
+    return _build.HIP_LIB
+
+
+def available() -> bool:
+    return os.path.exists(lib_path())
+
+
+def load():
+    """Loads (building first if the .so is absent) and binds the library."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        path = lib_path()
+        if not os.path.exists(path):
+            if os.environ.get("KFB_NO_AUTOBUILD"):
+                raise NativeError("native kernel library missing: %s (run "
+                                  "`python -m kf_benchmarks_amd.build`)" % path)
+            _build.build_all()
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        for name, args in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPES.get(name, c_int)
+        for name, (args, res) in _OPTIONAL.items():
+            if hasattr(lib, name):
+                fn = getattr(lib, name)
+                fn.argtypes = args
+                fn.restype = res
+        _LIB = lib
+        return lib
+
+
+def register_optional(name, argtypes, restype=c_int):
+    _OPTIONAL[name] = (argtypes, restype)
+    if _LIB is not None and hasattr(_LIB, name):
+        fn = getattr(_LIB, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+
+
+def call(name, *args):
+    """Calls a kernel entry point and raises on a non-zero hipError_t."""
+    fn = getattr(load(), name)
+    err = fn(*args)
+    if err != 0:
+        raise NativeError("%s failed with hipError %d" % (name, err))
+    return err
+
+
+def query(name, *args):
+    return getattr(load(), name)(*args)
+
+
+def dt(t: torch.Tensor) -> int:
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise NativeError("unsupported dtype %s for native kernels" % t.dtype)
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def loaded_path():
+    return lib_path() if _LIB is not None else None

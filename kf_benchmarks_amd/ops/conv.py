@@ -1,0 +1,69 @@
+"""NHWC 2-D convolution: forward, data-gradient and weight-gradient.
+
+Weights are stored [Cout, KH, KW, Cin] so that, in the implicit-GEMM view
+(M = N*OH*OW rows, N = Cout columns, K = KH*KW*Cin), both MFMA operands are
+K-contiguous: an activation row of K is a run of Cin channels per tap, a
+weight column of K is contiguous.
+
+Implementations:
+  * ``hip``   - our gfx950 implicit-GEMM kernels (csrc/conv*.hip) when the
+                shape is supported by them;
+  * ``torch`` - PyTorch/MIOpen on channels-last views (A/B reference only);
+  * CPU       - PyTorch reference (plumbing config and test oracle).
+"""
+
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import _native as N
+
+Pads = Tuple[int, int, int, int]
+
+
+def out_hw(H, W, kh, kw, stride, pads):
+    sh, sw = stride
+    pt, pb, pl, pr = pads
+    return (H + pt + pb - kh) // sh + 1, (W + pl + pr - kw) // sw + 1
+
+
+def _torch_conv(x, w, stride, pads):
+    """Reference conv through PyTorch on NCHW views (any device)."""
+    pt, pb, pl, pr = pads
+    xc = x.permute(0, 3, 1, 2)
+    wc = w.permute(0, 3, 1, 2)
+    if pt == pb and pl == pr:
+        y = F.conv2d(xc, wc, stride=stride, padding=(pt, pl))
+    else:
+        y = F.conv2d(F.pad(xc, (pl, pr, pt, pb)), wc, stride=stride)
+    return y.permute(0, 2, 3, 1)
+
+
+def conv2d_reference(x, w, stride, pads):
+    """fp32 reference result (used by tests)."""
+    return _torch_conv(x.float(), w.float(), stride, pads).contiguous()
+
+
+def _hip_supported(x, w, stride, pads) -> bool:
+    try:
+        from . import conv_hip
+    except ImportError:
+        return False
+    return conv_hip.supported(x, w, stride, pads)
+
+
+def conv2d(x, w, w_lp, stride, pads, impl="hip"):
+    if not x.is_cuda:
+        y = _torch_conv(x.float(), w, stride, pads)
+        return y.to(x.dtype).contiguous()
+    if impl == "hip" and _hip_supported(x, w, stride, pads):
+        from . import conv_hip
+        return conv_hip.conv2d(x, w, w_lp, stride, pads)
+    # torch/MIOpen path on channels-last views; autograd routes the weight
+    # gradient through the cast back to the fp32 master.
+    wl = w.to(x.dtype)
+    y = _torch_conv(x, wl, stride, pads)
+    return y.contiguous()

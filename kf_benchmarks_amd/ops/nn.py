@@ -1,0 +1,514 @@
+"""Layer ops on NHWC activations, as autograd Functions.
+
+GPU tensors run our gfx950 kernels (``_native``); CPU tensors run stock
+PyTorch ops.  The CPU path is the ``--device=cpu`` plumbing config of the
+reference (BASELINE config #1) and the fp32 numerics reference the GPU tests
+compare against; it is never a fallback for a GPU tensor.
+
+Layouts:
+  activations  [N, H, W, C] contiguous (NHWC), dtype = compute dtype
+  conv weight  [Cout, KH, KW, Cin] fp32 master (+ optional low-precision copy)
+  affine       [Cin, Cout] fp32 master (TF layout, tcb/convnet_builder.py:331-336)
+  BN params    fp32 [C]
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import _native as N
+from . import conv as _conv
+
+Pads = Tuple[int, int, int, int]  # top, bottom, left, right
+
+
+def _on_gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# ----------------------------------------------------------------- padding math
+def same_pads(in_size: int, k: int, s: int) -> Tuple[int, int]:
+    """TF 'SAME' padding (begin, end) for one spatial dim."""
+    out = (in_size + s - 1) // s
+    total = max((out - 1) * s + k - in_size, 0)
+    return total // 2, total - total // 2
+
+
+def conv_out_size(in_size: int, k: int, s: int, pb: int, pe: int) -> int:
+    return (in_size + pb + pe - k) // s + 1
+
+
+def resolve_pads(mode: str, H: int, W: int, kh: int, kw: int, sh: int, sw: int) -> Pads:
+    """Padding for 'SAME', 'VALID' and 'SAME_RESNET' (explicit symmetric-ish
+    pad then VALID when strided, tcb/convnet_builder.py:159-183)."""
+    if mode == "VALID":
+        return (0, 0, 0, 0)
+    if mode == "SAME" or (mode == "SAME_RESNET" and sh == 1 and sw == 1):
+        pt, pb = same_pads(H, kh, sh)
+        pl, pr = same_pads(W, kw, sw)
+        return (pt, pb, pl, pr)
+    if mode == "SAME_RESNET":
+        pt = (kh - 1) // 2
+        pl = (kw - 1) // 2
+        return (pt, kh - 1 - pt, pl, kw - 1 - pl)
+    raise ValueError("unknown padding mode %r" % mode)
+
+
+# ------------------------------------------------------------------------ conv
+def conv2d(x, w, w_lp, stride: Tuple[int, int], pads: Pads, impl: str = "hip"):
+    """NHWC convolution, no bias.  ``w_lp`` is the compute-dtype copy of the
+    fp32 master ``w`` (None -> cast on the fly)."""
+    return _conv.conv2d(x, w, w_lp, stride, pads, impl)
+
+
+# ------------------------------------------------------------------ batch norm
+def _bn_cpu(x, gamma, beta, residual, rm, rv, decay, eps, relu, training):
+    xc = x.permute(0, 3, 1, 2)
+    g = gamma if gamma is not None else torch.ones_like(beta)
+    y = F.batch_norm(xc.float(), rm, rv, g, beta, training=training, momentum=1.0 - decay,
+                     eps=eps)
+    y = y.permute(0, 2, 3, 1)
+    if residual is not None:
+        y = y + residual.float()
+    if relu:
+        y = torch.relu(y)
+    return y.to(x.dtype).contiguous()
+
+
+class _BatchNormTrain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, residual, rm, rv, decay, eps, relu):
+        x = x.contiguous()
+        C = x.shape[-1]
+        rows = x.numel() // C
+        dev = x.device
+        nslab = N.query("kfb_bn_num_slabs", rows, C)
+        ws = torch.empty((2 * nslab * C + 4 * C,), dtype=torch.float32, device=dev)
+        psum, psq = ws[:nslab * C], ws[nslab * C:2 * nslab * C]
+        stats = torch.empty((2, C), dtype=torch.float32, device=dev)  # mean, invstd
+        coef = ws[2 * nslab * C:2 * nslab * C + 2 * C]
+        y = torch.empty_like(x)
+        res = residual.contiguous() if residual is not None else None
+        N.call("kfb_bn_fwd_train", N.dt(x), x.data_ptr(), N.ptr(res), y.data_ptr(), rows, C,
+               N.ptr(gamma), N.ptr(beta), float(decay), float(eps), N.ptr(rm), N.ptr(rv),
+               stats[0].data_ptr(), stats[1].data_ptr(), coef[:C].data_ptr(),
+               coef[C:].data_ptr(), psum.data_ptr(), psq.data_ptr(), nslab, int(relu),
+               N.stream(dev))
+        ctx.save_for_backward(x, y if relu else None, gamma, stats)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        ctx.has_gamma = gamma is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, gamma, stats = ctx.saved_tensors
+        dy = dy.contiguous()
+        C = x.shape[-1]
+        rows = x.numel() // C
+        dev = x.device
+        nslab = N.query("kfb_bn_num_slabs", rows, C)
+        ws = torch.empty((2 * nslab * C + 3 * C,), dtype=torch.float32, device=dev)
+        pdy, pdyx = ws[:nslab * C], ws[nslab * C:2 * nslab * C]
+        coef = ws[2 * nslab * C:]
+        dparams = torch.empty((2, C), dtype=torch.float32, device=dev)
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if ctx.has_res else None
+        N.call("kfb_bn_bwd", N.dt(x), dy.data_ptr(), N.ptr(y), x.data_ptr(), dx.data_ptr(),
+               N.ptr(dres), rows, C, N.ptr(gamma), stats[0].data_ptr(), stats[1].data_ptr(),
+               dparams[0].data_ptr(), dparams[1].data_ptr(), pdy.data_ptr(), pdyx.data_ptr(),
+               nslab, coef[:C].data_ptr(), coef[C:2 * C].data_ptr(), coef[2 * C:].data_ptr(),
+               int(ctx.relu), 0, N.stream(dev))
+        dgamma = dparams[0] if ctx.has_gamma else None
+        return dx, dgamma, dparams[1], dres, None, None, None, None, None
+
+
+def batch_norm(x, gamma: Optional[torch.Tensor], beta: torch.Tensor,
+               running_mean: torch.Tensor, running_var: torch.Tensor, decay: float, eps: float,
+               training: bool, relu: bool = False, residual: Optional[torch.Tensor] = None):
+    """y = relu?(bn(x) + residual?).  ``gamma=None`` means scale=False
+    (constant 1, tcb/convnet_builder.py:437-438 default)."""
+    if not _on_gpu(x):
+        return _bn_cpu(x, gamma, beta, residual, running_mean, running_var, decay, eps, relu,
+                       training)
+    if training:
+        return _BatchNormTrain.apply(x, gamma, beta, residual, running_mean, running_var,
+                                     decay, eps, relu)
+    return _bn_infer_gpu(x, gamma, beta, residual, running_mean, running_var, eps, relu)
+
+
+def _bn_infer_gpu(x, gamma, beta, residual, rm, rv, eps, relu):
+    x = x.contiguous()
+    C = x.shape[-1]
+    rows = x.numel() // C
+    coef = torch.empty((2, C), dtype=torch.float32, device=x.device)
+    y = torch.empty_like(x)
+    res = residual.contiguous() if residual is not None else None
+    N.call("kfb_bn_fwd_infer", N.dt(x), x.data_ptr(), N.ptr(res), y.data_ptr(), rows, C,
+           N.ptr(gamma), N.ptr(beta), rm.data_ptr(), rv.data_ptr(), float(eps),
+           coef[0].data_ptr(), coef[1].data_ptr(), int(relu), N.stream(x.device))
+    return y
+
+
+# -------------------------------------------------------------- bias + relu
+class _BiasAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, b, relu):
+        x = x.contiguous()
+        C = x.shape[-1]
+        rows = x.numel() // C
+        y = torch.empty_like(x)
+        N.call("kfb_bias_act", N.dt(x), x.data_ptr(), N.ptr(b), y.data_ptr(), rows, C, int(relu),
+               N.stream(x.device))
+        ctx.save_for_backward(y if relu else None)
+        ctx.relu, ctx.has_b, ctx.C = relu, b is not None, C
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        C = ctx.C
+        rows = dy.numel() // C
+        dx = torch.empty_like(dy) if ctx.relu else dy
+        db = None
+        pb = None
+        nslab = 1
+        if ctx.has_b:
+            nslab = N.query("kfb_colsum_num_slabs", rows, C)
+            pb = torch.empty((nslab * C,), dtype=torch.float32, device=dy.device)
+            db = torch.empty((C,), dtype=torch.float32, device=dy.device)
+        if ctx.relu or ctx.has_b:
+            N.call("kfb_act_bwd_bias", N.dt(dy), dy.data_ptr(), N.ptr(y), dx.data_ptr(), rows, C,
+                   int(ctx.relu), N.ptr(pb), nslab, N.ptr(db), 0, N.stream(dy.device))
+        return dx, db, None
+
+
+def bias_act(x, b: Optional[torch.Tensor], relu: bool):
+    if b is None and not relu:
+        return x
+    if not _on_gpu(x):
+        y = x.float() + b if b is not None else x.float()
+        if relu:
+            y = torch.relu(y)
+        return y.to(x.dtype)
+    return _BiasAct.apply(x, b, relu)
+
+
+def relu(x):
+    return bias_act(x, None, True)
+
+
+def activation(x, kind: Optional[str]):
+    if kind in (None, "linear"):
+        return x
+    if kind == "relu":
+        return relu(x)
+    if kind == "tanh":
+        return torch.tanh(x)
+    raise KeyError("Invalid activation type '%s'" % kind)
+
+
+class _Add(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b, relu):
+        a, b = a.contiguous(), b.contiguous()
+        y = torch.empty_like(a)
+        N.call("kfb_add", N.dt(a), a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(),
+               int(relu), N.stream(a.device))
+        ctx.save_for_backward(y if relu else None)
+        ctx.relu = relu
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        if ctx.relu:
+            dy = dy.contiguous()
+            C = dy.shape[-1]
+            dx = torch.empty_like(dy)
+            N.call("kfb_act_bwd_bias", N.dt(dy), dy.data_ptr(), y.data_ptr(), dx.data_ptr(),
+                   dy.numel() // C, C, 1, None, 1, None, 0, N.stream(dy.device))
+            return dx, dx, None
+        return dy, dy, None
+
+
+def add(a, b, relu: bool = False):
+    if not _on_gpu(a):
+        y = a + b
+        return torch.relu(y) if relu else y
+    return _Add.apply(a, b, relu)
+
+
+# --------------------------------------------------------------------- pooling
+def pool_geometry(x_shape, kh, kw, sh, sw, mode):
+    n, H, W, C = x_shape
+    pt, pb, pl, pr = resolve_pads(mode, H, W, kh, kw, sh, sw)
+    OH = conv_out_size(H, kh, sh, pt, pb)
+    OW = conv_out_size(W, kw, sw, pl, pr)
+    return (pt, pb, pl, pr), OH, OW
+
+
+def _pool_cpu(x, kh, kw, sh, sw, pads, kind):
+    pt, pb, pl, pr = pads
+    xc = x.permute(0, 3, 1, 2).float()
+    if kind == "max":
+        xp = F.pad(xc, (pl, pr, pt, pb), value=-math.inf)
+        y = F.max_pool2d(xp, (kh, kw), (sh, sw))
+    else:
+        xp = F.pad(xc, (pl, pr, pt, pb))
+        ones = F.pad(torch.ones_like(xc[:1, :1]), (pl, pr, pt, pb))
+        s = F.avg_pool2d(xp, (kh, kw), (sh, sw)) * (kh * kw)
+        cnt = F.avg_pool2d(ones, (kh, kw), (sh, sw)) * (kh * kw)
+        y = s / cnt
+    return y.permute(0, 2, 3, 1).to(x.dtype).contiguous()
+
+
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, kh, kw, sh, sw, pads, OH, OW):
+        x = x.contiguous()
+        n, H, W, C = x.shape
+        y = torch.empty((n, OH, OW, C), dtype=x.dtype, device=x.device)
+        idx = torch.empty((n, OH, OW, C), dtype=torch.uint8, device=x.device)
+        geo = (n, H, W, C, OH, OW, kh, kw, sh, sw, pads[0], pads[2])
+        N.call("kfb_maxpool_fwd", N.dt(x), x.data_ptr(), y.data_ptr(), idx.data_ptr(), *geo,
+               N.stream(x.device))
+        ctx.save_for_backward(idx)
+        ctx.geo = geo
+        ctx.dtype = x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        n, H, W, C = ctx.geo[:4]
+        dx = torch.empty((n, H, W, C), dtype=dy.dtype, device=dy.device)
+        N.call("kfb_maxpool_bwd", N.dt(dy), dy.data_ptr(), idx.data_ptr(), dx.data_ptr(),
+               *ctx.geo, N.stream(dy.device))
+        return dx, None, None, None, None, None, None, None
+
+
+class _AvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, kh, kw, sh, sw, pads, OH, OW):
+        x = x.contiguous()
+        n, H, W, C = x.shape
+        y = torch.empty((n, OH, OW, C), dtype=x.dtype, device=x.device)
+        geo = (n, H, W, C, OH, OW, kh, kw, sh, sw, pads[0], pads[2])
+        N.call("kfb_avgpool_fwd", N.dt(x), x.data_ptr(), y.data_ptr(), *geo, N.stream(x.device))
+        ctx.geo = geo
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        n, H, W, C = ctx.geo[:4]
+        dx = torch.empty((n, H, W, C), dtype=dy.dtype, device=dy.device)
+        N.call("kfb_avgpool_bwd", N.dt(dy), dy.data_ptr(), dx.data_ptr(), *ctx.geo,
+               N.stream(dy.device))
+        return dx, None, None, None, None, None, None, None
+
+
+def max_pool(x, kh, kw, sh, sw, mode="VALID"):
+    pads, OH, OW = pool_geometry(x.shape, kh, kw, sh, sw, mode)
+    if not _on_gpu(x):
+        return _pool_cpu(x, kh, kw, sh, sw, pads, "max")
+    return _MaxPool.apply(x, kh, kw, sh, sw, pads, OH, OW)
+
+
+def avg_pool(x, kh, kw, sh, sw, mode="VALID"):
+    pads, OH, OW = pool_geometry(x.shape, kh, kw, sh, sw, mode)
+    if not _on_gpu(x):
+        return _pool_cpu(x, kh, kw, sh, sw, pads, "avg")
+    if kh == 1 and kw == 1 and pads == (0, 0, 0, 0):
+        # 1x1 average pool == strided subsample (ResNet v1 shortcut).
+        return x[:, ::sh, ::sw, :].contiguous()
+    return _AvgPool.apply(x, kh, kw, sh, sw, pads, OH, OW)
+
+
+class _GlobalAvg(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        n, H, W, C = x.shape
+        y = torch.empty((n, C), dtype=x.dtype, device=x.device)
+        N.call("kfb_gap_fwd", N.dt(x), x.data_ptr(), y.data_ptr(), n, H * W, C,
+               N.stream(x.device))
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        n, H, W, C = ctx.shape
+        dx = torch.empty(ctx.shape, dtype=dy.dtype, device=dy.device)
+        N.call("kfb_gap_bwd", N.dt(dy), dy.data_ptr(), dx.data_ptr(), n, H * W, C,
+               N.stream(dy.device))
+        return dx
+
+
+def spatial_mean(x, keep_dims=False):
+    if not _on_gpu(x):
+        y = x.float().mean(dim=(1, 2), keepdim=keep_dims).to(x.dtype)
+        return y
+    y = _GlobalAvg.apply(x)
+    return y.view(y.shape[0], 1, 1, y.shape[1]) if keep_dims else y
+
+
+# ---------------------------------------------------------------------- affine
+class _Linear(torch.autograd.Function):
+    """y = x @ W + b with W the fp32 master [Cin, Cout] and W_lp its compute
+    copy.  Plain GEMMs: these go to the vendor BLAS (hipBLASLt)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, w_lp):
+        wl = w_lp if w_lp is not None else w.to(x.dtype)
+        y = torch.mm(x, wl)
+        ctx.save_for_backward(x, wl)
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wl = ctx.saved_tensors
+        dx = torch.mm(dy, wl.t())
+        dw = torch.mm(x.t(), dy).float()
+        db = dy.float().sum(0) if ctx.has_b else None
+        return dx, dw, db, None
+
+
+def linear(x, w, b, w_lp=None, relu=False):
+    if not _on_gpu(x):
+        y = x.float() @ w
+        if b is not None:
+            y = y + b
+        if relu:
+            y = torch.relu(y)
+        return y.to(x.dtype)
+    y = _Linear.apply(x, w, None, w_lp)
+    return bias_act(y, b, relu)
+
+
+# --------------------------------------------------------------------- dropout
+class _Dropout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, keep, seed):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        N.call("kfb_dropout", N.dt(x), x.data_ptr(), y.data_ptr(), x.numel(), float(keep),
+               int(seed) & 0xFFFFFFFF, N.stream(x.device))
+        ctx.keep, ctx.seed = keep, seed
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        N.call("kfb_dropout", N.dt(dy), dy.data_ptr(), dx.data_ptr(), dy.numel(),
+               float(ctx.keep), int(ctx.seed) & 0xFFFFFFFF, N.stream(dy.device))
+        return dx, None, None
+
+
+def dropout(x, keep_prob: float, training: bool, seed: int):
+    if not training or keep_prob >= 1.0:
+        return x
+    if not _on_gpu(x):
+        return F.dropout(x, p=1.0 - keep_prob, training=True)
+    return _Dropout.apply(x, keep_prob, seed)
+
+
+# ------------------------------------------------------------------------- LRN
+def lrn(x, depth_radius, bias, alpha, beta):
+    """tf.nn.lrn over the channel dim of NHWC x (sum over 2r+1 channels)."""
+    xf = x.float()
+    sq = (xf * xf).permute(0, 3, 1, 2).unsqueeze(1)  # N,1,C,H,W
+    k = 2 * depth_radius + 1
+    s = F.avg_pool3d(F.pad(sq, (0, 0, 0, 0, depth_radius, depth_radius)), (k, 1, 1),
+                     stride=1) * k
+    s = s.squeeze(1).permute(0, 2, 3, 1)
+    return (xf / (bias + alpha * s).pow(beta)).to(x.dtype)
+
+
+# ------------------------------------------------------------------------ loss
+class _SoftmaxXent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels):
+        logits = logits.contiguous()
+        labels = labels.to(torch.int32).contiguous()
+        n, k = logits.shape
+        loss = torch.empty((n,), dtype=torch.float32, device=logits.device)
+        lse = torch.empty((n,), dtype=torch.float32, device=logits.device)
+        N.call("kfb_xent_fwd", N.dt(logits), logits.data_ptr(), labels.data_ptr(), n, k,
+               loss.data_ptr(), lse.data_ptr(), N.stream(logits.device))
+        ctx.save_for_backward(logits, labels, lse)
+        return loss.mean()
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, labels, lse = ctx.saved_tensors
+        n, k = logits.shape
+        g = g.float().reshape(1).contiguous()
+        dl = torch.empty_like(logits)
+        N.call("kfb_xent_bwd", N.dt(logits), logits.data_ptr(), labels.data_ptr(),
+               lse.data_ptr(), g.data_ptr(), 1.0 / n, n, k, dl.data_ptr(),
+               N.stream(logits.device))
+        return dl, None
+
+
+def softmax_cross_entropy(logits, labels):
+    """Mean sparse softmax cross-entropy (fp32 result)."""
+    if not _on_gpu(logits):
+        return F.cross_entropy(logits.float(), labels.long())
+    return _SoftmaxXent.apply(logits, labels)
+
+
+def in_top_k(logits, labels):
+    """(#top-1 correct, #top-5 correct) as fp32 device scalars."""
+    if not _on_gpu(logits):
+        lf = logits.float()
+        t = lf.gather(1, labels.long().view(-1, 1))
+        cnt = (lf > t).sum(1)
+        fin = torch.isfinite(t.view(-1))
+        return ((cnt < 1) & fin).float().sum(), ((cnt < 5) & fin).float().sum()
+    logits = logits.contiguous()
+    labels = labels.to(torch.int32).contiguous()
+    n, k = logits.shape
+    out = torch.empty((2, n), dtype=torch.float32, device=logits.device)
+    N.call("kfb_in_top_k", N.dt(logits), logits.data_ptr(), labels.data_ptr(), n, k,
+           out[0].data_ptr(), out[1].data_ptr(), N.stream(logits.device))
+    s = out.sum(1)
+    return s[0], s[1]
+
+
+# ------------------------------------------------------------------- synthetic
+def synthetic_images(shape, dtype, device, seed: int, mean=127.0, std=60.0):
+    if torch.device(device).type != "cuda":
+        g = torch.Generator().manual_seed(seed)
+        x = torch.randn(shape, generator=g).clamp_(-2, 2) * std + mean
+        return x.to(dtype)
+    x = torch.empty(shape, dtype=dtype, device=device)
+    N.call("kfb_synthetic_images", N.dt(x), x.data_ptr(), x.numel(), float(mean), float(std),
+           seed & 0xFFFFFFFF, N.stream(x.device))
+    return x
+
+
+def synthetic_labels(n, nclass, device, seed: int):
+    # Reference: uniform in [0, nclass-1) (tcb/models/model.py:232-236).
+    maxval = max(nclass - 1, 1)
+    if torch.device(device).type != "cuda":
+        g = torch.Generator().manual_seed(seed + 1)
+        return torch.randint(0, maxval, (n,), generator=g, dtype=torch.int32)
+    y = torch.empty((n,), dtype=torch.int32, device=device)
+    N.call("kfb_synthetic_labels", y.data_ptr(), n, maxval, (seed + 1) & 0xFFFFFFFF,
+           N.stream(device))
+    return y
+
+
+def concat_channels(xs: Sequence[torch.Tensor]):
+    return torch.cat(list(xs), dim=-1)

@@ -1,0 +1,194 @@
+"""Gradient-aggregation strategies (--variable_update / --kungfu_option).
+
+The reference implements each mode as a TF VariableMgr (tcb/variable_mgr.py)
+that places variables and rewires the gradient graph.  On MI355X every mode
+runs as one process per GPU over RCCL, and what distinguishes the modes is
+only *what is reduced, how it is scaled, and when*:
+
+=========================  =============================================  ====================
+mode                       reference semantics                            here
+=========================  =============================================  ====================
+parameter_server           grads averaged over towers, applied on PS      all-reduce SUM of per
+                           vars by each worker (W updates / step)         worker mean grads
+distributed_replicated     same aggregation via PS shadow vars            as parameter_server
+replicated                 towers' grads SUMMED (LR /num_gpus in model)   all-reduce SUM
+collective_all_reduce      CollectiveReduce SUM over all devices          all-reduce SUM
+distributed_all_reduce     all-reduce SUM over workers x towers           all-reduce SUM
+horovod                    hvd.allreduce(average=False)                   all-reduce SUM
+independent                no communication                               none
+kungfu sync_sgd            SynchronousSGDOptimizer: sum / cluster size    all-reduce, x 1/W
+kungfu async_sgd           PairAveragingOptimizer                         P2P model store
+kungfu sma                 SynchronousAveragingOptimizer                  all-reduce of weights
+kungfu ada_sgd             (not wired in the reference)                   SMA -> S-SGD switch
+=========================  =============================================  ====================
+
+The 1/W of S-SGD, the loss-scale unscale and the weight decay are folded
+into the fused optimizer launch (grad_scale), so the all-reduce itself is a
+plain SUM on contiguous gradient buckets overlapped with backward.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import comm
+from .bucket import BucketReducer
+
+
+class Strategy:
+    name = "none"
+    reduces_gradients = False
+    each_tower_has_variables = True
+
+    def __init__(self, params, world: comm.World, flat, bucket_mb=64.0, wire_dtype=None,
+                 overlap=True):
+        self.params = params
+        self.world = world
+        self.flat = flat
+        self.reducer: Optional[BucketReducer] = None
+        if self.reduces_gradients and world.size > 1:
+            self.reducer = BucketReducer(flat, bucket_mb, wire_dtype, overlap=overlap)
+
+    @property
+    def grad_scale(self) -> float:
+        return 1.0
+
+    def broadcast_initial_model(self, slots=()):
+        """Rank-0 broadcast of every variable (+ optimizer slots, BN stats):
+        what horovod.broadcast_global_variables(0) / kungfu broadcast do at
+        init (tcb/benchmark_cnn.py:2094-2100)."""
+        if self.world.size <= 1:
+            return
+        comm.broadcast(self.flat.flat, 0)
+        for t in slots:
+            comm.broadcast(t, 0)
+        for layer in self.flat.net.ordered_layers():
+            for b in layer.buffers(recurse=False):
+                comm.broadcast(b, 0)
+        self.flat.refresh_lp()
+
+    def before_backward(self, step: int):
+        if self.reducer is not None:
+            self.reducer.begin()
+
+    def after_backward(self, step: int):
+        if self.reducer is not None:
+            self.reducer.finish()
+
+    def before_update(self, step: int):
+        pass
+
+    def after_update(self, step: int):
+        pass
+
+    def describe(self) -> str:
+        return self.name
+
+
+class IndependentStrategy(Strategy):
+    name = "independent"
+
+
+class SumAllReduceStrategy(Strategy):
+    """parameter_server / replicated / distributed_* / collective / horovod."""
+    reduces_gradients = True
+
+    def __init__(self, name, *a, **kw):
+        self.name = name
+        super().__init__(*a, **kw)
+
+
+class KungFuSyncSGD(Strategy):
+    """SynchronousSGDOptimizer: all-reduce(sum) every gradient, divide by the
+    cluster size, then apply the wrapped optimizer."""
+    name = "kungfu/sync_sgd"
+    reduces_gradients = True
+
+    @property
+    def grad_scale(self):
+        return 1.0 / self.world.size
+
+
+class KungFuSMA(Strategy):
+    """SynchronousAveragingOptimizer: every step all-reduce-average the model,
+    move the local model toward it (w <- w - alpha (w - avg)), then apply the
+    local gradient."""
+    name = "kungfu/sma"
+
+    def __init__(self, *a, alpha=0.1, **kw):
+        super().__init__(*a, **kw)
+        self.alpha = float(alpha)
+        self._avg = None
+
+    def before_update(self, step):
+        if self.world.size <= 1:
+            return
+        w = self.flat.flat
+        if self._avg is None:
+            self._avg = torch.empty_like(w)
+        self._avg.copy_(w)
+        comm.all_reduce(self._avg)
+        # w <- (1-alpha) w + alpha * avg
+        w.mul_(1.0 - self.alpha).add_(self._avg, alpha=self.alpha / self.world.size)
+
+
+class KungFuAdaSGD(Strategy):
+    """Adaptive variant (not wired in the reference, tcb/benchmark_cnn.py:1202-1204):
+    SMA for the first ``switch_step`` steps, synchronous SGD afterwards."""
+    name = "kungfu/ada_sgd"
+    reduces_gradients = True
+
+    def __init__(self, *a, alpha=0.1, switch_step=100, **kw):
+        super().__init__(*a, **kw)
+        self.sma = KungFuSMA(*a, alpha=alpha, **{k: v for k, v in kw.items()})
+        self.switch_step = int(switch_step)
+        self._step = 0
+
+    @property
+    def grad_scale(self):
+        return 1.0 / self.world.size if self._step >= self.switch_step else 1.0
+
+    def before_backward(self, step):
+        self._step = step
+        if step >= self.switch_step:
+            super().before_backward(step)
+
+    def after_backward(self, step):
+        if step >= self.switch_step:
+            super().after_backward(step)
+
+    def before_update(self, step):
+        if step < self.switch_step:
+            self.sma.before_update(step)
+
+
+def make_strategy(params, world, flat):
+    vu = params.variable_update
+    wire = {"auto": None, "fp32": None, "bf16": torch.bfloat16,
+            "fp16": torch.float16}[params.gradient_wire_dtype]
+    if params.gradient_wire_dtype == "auto" and params.compact_gradient_transfer \
+            and params.gradient_repacking:
+        wire = torch.float16
+    kw = dict(bucket_mb=params.bucket_size_mb, wire_dtype=wire,
+              overlap=params.overlap_gradient_allreduce)
+    if vu == "independent":
+        return IndependentStrategy(params, world, flat, **kw)
+    if vu == "kungfu":
+        opt = params.kungfu_option
+        if opt == "sync_sgd":
+            return KungFuSyncSGD(params, world, flat, **kw)
+        if opt == "sma":
+            return KungFuSMA(params, world, flat, alpha=params.kungfu_sma_alpha, **kw)
+        if opt == "ada_sgd":
+            return KungFuAdaSGD(params, world, flat, alpha=params.kungfu_sma_alpha,
+                                switch_step=params.kungfu_ada_switch_step, **kw)
+        if opt == "async_sgd":
+            from .kungfu import PairAveraging
+            return PairAveraging(params, world, flat, **kw)
+        raise ValueError('KungFu distributed option "%s" was not recognized' % opt)
+    if vu in ("parameter_server", "replicated", "distributed_replicated", "collective_all_reduce",
+              "distributed_all_reduce", "horovod"):
+        return SumAllReduceStrategy(vu, params, world, flat, **kw)
+    raise ValueError("Invalid variable_update in local mode: %s" % vu)

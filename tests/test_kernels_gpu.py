@@ -1,0 +1,187 @@
+"""Numerics of the gfx950 kernels against plain PyTorch fp32 references.
+
+Every test runs the op on cuda:0 through libkfb_hip.so and the same op on
+CPU in fp32 (stock PyTorch), for forward and backward.
+"""
+
+import pytest
+import torch
+
+from kf_benchmarks_amd.ops import nn as F
+
+pytestmark = pytest.mark.gpu
+
+DT = [torch.float32, torch.bfloat16]
+
+
+def tol(dt):
+    return dict(rtol=2e-2, atol=2e-2) if dt == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
+
+
+def _pair(x, dev, dt):
+    a = x.clone().to(dev, dt).requires_grad_(True)
+    b = x.clone().float().requires_grad_(True)
+    return a, b
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("shape", [(4, 7, 7, 64), (2, 5, 6, 24), (3, 4, 4, 2048), (2, 3, 3, 20)])
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
+def test_batch_norm_train(cuda, dt, shape, relu, res):
+    torch.manual_seed(0)
+    C = shape[-1]
+    x = torch.randn(shape) * 2 + 0.5
+    r = torch.randn(shape)
+    g0 = torch.rand(C) + 0.5
+    b0 = torch.randn(C)
+    xa, xb = _pair(x, cuda, dt)
+    ra, rb = (_pair(r, cuda, dt) if res else (None, None))
+    ga, gb = g0.clone().to(cuda).requires_grad_(True), g0.clone().requires_grad_(True)
+    ba, bb = b0.clone().to(cuda).requires_grad_(True), b0.clone().requires_grad_(True)
+    rma, rva = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    rmb, rvb = torch.zeros(C), torch.ones(C)
+    ya = F.batch_norm(xa, ga, ba, rma, rva, 0.9, 1e-5, True, relu, ra)
+    yb = F.batch_norm(xb, gb, bb, rmb, rvb, 0.9, 1e-5, True, relu, rb)
+    torch.testing.assert_close(ya.float().cpu(), yb, **tol(dt))
+    torch.testing.assert_close(rma.cpu(), rmb, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(rva.cpu(), rvb, rtol=1e-3, atol=1e-3)
+    dy = torch.randn(shape)
+    ya.backward(dy.to(cuda, dt))
+    yb.backward(dy)
+    t = tol(dt)
+    torch.testing.assert_close(xa.grad.float().cpu(), xb.grad, rtol=t["rtol"] * 3, atol=t["atol"] * 3)
+    torch.testing.assert_close(ga.grad.cpu(), gb.grad, rtol=5e-2 if dt != torch.float32 else 1e-3,
+                               atol=0.5 if dt != torch.float32 else 1e-3)
+    torch.testing.assert_close(ba.grad.cpu(), bb.grad, rtol=5e-2 if dt != torch.float32 else 1e-3,
+                               atol=0.5 if dt != torch.float32 else 1e-3)
+    if res:
+        torch.testing.assert_close(ra.grad.float().cpu(), rb.grad, **tol(dt))
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_batch_norm_infer(cuda, dt):
+    C = 32
+    x = torch.randn(2, 5, 5, C)
+    g, b, rm, rv = torch.rand(C) + 0.5, torch.randn(C), torch.randn(C), torch.rand(C) + 0.5
+    ya = F.batch_norm(x.to(cuda, dt), g.to(cuda), b.to(cuda), rm.to(cuda), rv.to(cuda), 0.9,
+                      1e-3, False, True)
+    yb = F.batch_norm(x, g, b, rm.clone(), rv.clone(), 0.9, 1e-3, False, True)
+    torch.testing.assert_close(ya.float().cpu(), yb, **tol(dt))
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("kind,k,s,mode,hw", [("max", 3, 2, "SAME", 16), ("max", 2, 2, "VALID", 8),
+                                              ("avg", 3, 1, "SAME", 9), ("avg", 3, 2, "VALID", 9),
+                                              ("max", 3, 2, "VALID", 13)])
+def test_pool(cuda, dt, kind, k, s, mode, hw):
+    torch.manual_seed(1)
+    x = torch.randn(2, hw, hw, 16)
+    xa, xb = _pair(x, cuda, dt)
+    fn = F.max_pool if kind == "max" else F.avg_pool
+    ya, yb = fn(xa, k, k, s, s, mode), fn(xb, k, k, s, s, mode)
+    torch.testing.assert_close(ya.float().cpu(), yb, **tol(dt))
+    dy = torch.randn(yb.shape)
+    ya.backward(dy.to(cuda, dt))
+    yb.backward(dy)
+    torch.testing.assert_close(xa.grad.float().cpu(), xb.grad, **tol(dt))
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_spatial_mean(cuda, dt):
+    x = torch.randn(3, 7, 7, 256)
+    xa, xb = _pair(x, cuda, dt)
+    ya, yb = F.spatial_mean(xa), F.spatial_mean(xb)
+    torch.testing.assert_close(ya.float().cpu(), yb, **tol(dt))
+    dy = torch.randn(yb.shape)
+    ya.backward(dy.to(cuda, dt))
+    yb.backward(dy)
+    torch.testing.assert_close(xa.grad.float().cpu(), xb.grad, **tol(dt))
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_softmax_xent_and_topk(cuda, dt):
+    torch.manual_seed(2)
+    logits = torch.randn(16, 1001) * 3
+    labels = torch.randint(0, 1000, (16,), dtype=torch.int32)
+    la, lb = _pair(logits, cuda, dt)
+    a = F.softmax_cross_entropy(la, labels.to(cuda))
+    b = F.softmax_cross_entropy(lb, labels)
+    torch.testing.assert_close(a.cpu(), b, rtol=1e-2 if dt != torch.float32 else 1e-5, atol=1e-2)
+    (a * 2).backward()
+    (b * 2).backward()
+    torch.testing.assert_close(la.grad.float().cpu(), lb.grad, rtol=2e-2, atol=1e-3)
+    t1a, t5a = F.in_top_k(la.detach().float(), labels.to(cuda))
+    t1b, t5b = F.in_top_k(lb.detach(), labels)
+    assert float(t1a) == float(t1b) and float(t5a) == float(t5b)
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("relu", [False, True])
+def test_bias_act(cuda, dt, relu):
+    x = torch.randn(4, 6, 6, 40)
+    bias = torch.randn(40)
+    xa, xb = _pair(x, cuda, dt)
+    ba, bb = bias.clone().to(cuda).requires_grad_(True), bias.clone().requires_grad_(True)
+    ya, yb = F.bias_act(xa, ba, relu), F.bias_act(xb, bb, relu)
+    torch.testing.assert_close(ya.float().cpu(), yb, **tol(dt))
+    dy = torch.randn(yb.shape)
+    ya.backward(dy.to(cuda, dt))
+    yb.backward(dy)
+    torch.testing.assert_close(xa.grad.float().cpu(), xb.grad, **tol(dt))
+    torch.testing.assert_close(ba.grad.cpu(), bb.grad, rtol=2e-2, atol=0.2 if dt != torch.float32 else 1e-3)
+
+
+@pytest.mark.parametrize("relu", [False, True])
+def test_add(cuda, relu):
+    a, b = torch.randn(3, 4, 4, 8), torch.randn(3, 4, 4, 8)
+    aa, ab = _pair(a, cuda, torch.float32)
+    ba, bb = _pair(b, cuda, torch.float32)
+    ya, yb = F.add(aa, ba, relu), F.add(ab, bb, relu)
+    torch.testing.assert_close(ya.cpu(), yb)
+    dy = torch.randn(yb.shape)
+    ya.backward(dy.to(cuda))
+    yb.backward(dy)
+    torch.testing.assert_close(aa.grad.cpu(), ab.grad)
+    torch.testing.assert_close(ba.grad.cpu(), bb.grad)
+
+
+def test_dropout_statistics(cuda):
+    x = torch.ones(1 << 20, device=cuda)
+    y = F.dropout(x, 0.5, True, seed=123)
+    keep = (y > 0).float().mean().item()
+    assert abs(keep - 0.5) < 0.01
+    assert torch.allclose(y[y > 0], torch.full_like(y[y > 0], 2.0))
+    x.requires_grad_(True)
+    y = F.dropout(x, 0.5, True, seed=123)
+    y.sum().backward()
+    assert torch.equal((x.grad > 0), (y.detach() > 0))
+
+
+def test_synthetic_inputs(cuda):
+    img = F.synthetic_images((8, 32, 32, 3), torch.float32, cuda, 7)
+    assert abs(img.mean().item() - 127) < 3
+    assert img.min().item() >= 127 - 120 - 1e-3 and img.max().item() <= 127 + 120 + 1e-3
+    lab = F.synthetic_labels(4096, 1001, cuda, 7)
+    assert lab.min().item() >= 0 and lab.max().item() < 1000
+
+
+@pytest.mark.parametrize("kind", ["sgd", "momentum", "rmsprop", "adam"])
+def test_fused_optimizer(cuda, kind):
+    from kf_benchmarks_amd import optim
+    from kf_benchmarks_amd.models.model import Network
+    from kf_benchmarks_amd.models.resnet_model import create_resnet20_cifar_model
+
+    res = {}
+    for dev in ("cpu", cuda):
+        model = create_resnet20_cifar_model(None)
+        net = Network(model, 11, dev, torch.float32, seed=5)
+        flat = optim.FlatParams(net, torch.bfloat16)
+        opt = optim.FusedOptimizer(flat, kind)
+        g = torch.Generator().manual_seed(3)
+        for i in range(3):
+            flat.grad.copy_(torch.randn(flat.numel, generator=g).to(flat.grad.device))
+            opt.step(0.01, grad_scale=0.5, weight_decay=1e-3, clip=1.5)
+        res[str(dev)] = (flat.flat.cpu().clone(), flat.lp.float().cpu().clone())
+    a, b = res["cpu"], res[str(cuda)]
+    torch.testing.assert_close(b[0], a[0], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(b[1], a[1], rtol=1e-2, atol=1e-2)
