@@ -16,7 +16,7 @@
 
 namespace kfb {
 
-constexpr int BN_THREADS = 256;
+constexpr int BN_THREADS = 512;
 
 struct Geo {
   int cw;    // channels per block window
@@ -35,7 +35,8 @@ static Geo make_geo(int C) {
   return g;
 }
 
-// Sum of per-lane vectors over the rpi row-lanes of the block, via LDS.
+// Sum of per-lane vectors over the rpi row-lanes of the block: LDS tree
+// reduction (row-lane 0 ends with the block totals).
 template <int V>
 __device__ __forceinline__ void block_row_reduce(float (&a)[V], float (&b)[V], float* lds, int t,
                                                  int r, int tpr, int rpi) {
@@ -49,13 +50,31 @@ __device__ __forceinline__ void block_row_reduce(float (&a)[V], float (&b)[V], f
     }
   }
   __syncthreads();
-  if (r == 0) {
-    for (int rr = 1; rr < rpi; ++rr) {
+  int p2 = 1;
+  while (p2 * 2 <= rpi) p2 *= 2;
+  if (r < rpi - p2) {  // fold the non-power-of-two tail
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      lds[(r * tpr + t) * V + i] += lds[((r + p2) * tpr + t) * V + i];
+      lds[stride + (r * tpr + t) * V + i] += lds[stride + ((r + p2) * tpr + t) * V + i];
+    }
+  }
+  __syncthreads();
+  for (int h = p2 / 2; h > 0; h /= 2) {
+    if (r < h) {
 #pragma unroll
       for (int i = 0; i < V; ++i) {
-        a[i] += lds[(rr * tpr + t) * V + i];
-        b[i] += lds[stride + (rr * tpr + t) * V + i];
+        lds[(r * tpr + t) * V + i] += lds[((r + h) * tpr + t) * V + i];
+        lds[stride + (r * tpr + t) * V + i] += lds[stride + ((r + h) * tpr + t) * V + i];
       }
+    }
+    __syncthreads();
+  }
+  if (r == 0) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      a[i] = lds[t * V + i];
+      b[i] = lds[stride + t * V + i];
     }
   }
 }
@@ -93,20 +112,47 @@ bn_partial_stats_k(const T* __restrict__ x, long rows, int C, int cw, int tpr, i
   }
 }
 
-// One thread per channel; folds the slab partials in double precision.
-__global__ void bn_finalize_stats_k(const float* __restrict__ psum, const float* __restrict__ psq,
-                                    int nslab, int C, long rows, const float* __restrict__ gamma,
-                                    const float* __restrict__ beta, float decay, float eps,
-                                    float* __restrict__ run_mean, float* __restrict__ run_var,
-                                    float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                                    float* __restrict__ scale, float* __restrict__ shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int k = 0; k < nslab; ++k) {
-    s += (double)psum[(long)k * C + c];
-    q += (double)psq[(long)k * C + c];
+// Slab partials -> per-channel totals.  Block = 64 channels x 4 slab lanes,
+// each lane sums every 4th slab with 4 independent accumulators (the slab
+// loop is latency-bound otherwise), lanes combine through LDS.
+__device__ __forceinline__ void fold_slabs(const float* __restrict__ pa,
+                                           const float* __restrict__ pb, int nslab, int C,
+                                           int c, double& sa, double& sb) {
+  __shared__ double red[2][4][64];
+  const int lane = threadIdx.y, cx = threadIdx.x;
+  float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    int k = lane;
+    for (; k + 12 < nslab; k += 16) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] += pa[(long)(k + 4 * u) * C + c];
+        b[u] += pb[(long)(k + 4 * u) * C + c];
+      }
+    }
+    for (; k < nslab; k += 4) {
+      a[0] += pa[(long)k * C + c];
+      b[0] += pb[(long)k * C + c];
+    }
   }
+  red[0][lane][cx] = (double)a[0] + a[1] + a[2] + a[3];
+  red[1][lane][cx] = (double)b[0] + b[1] + b[2] + b[3];
+  __syncthreads();
+  sa = red[0][0][cx] + red[0][1][cx] + red[0][2][cx] + red[0][3][cx];
+  sb = red[1][0][cx] + red[1][1][cx] + red[1][2][cx] + red[1][3][cx];
+}
+
+__global__ void __launch_bounds__(256)
+bn_finalize_stats_k(const float* __restrict__ psum, const float* __restrict__ psq,
+                    int nslab, int C, long rows, const float* __restrict__ gamma,
+                    const float* __restrict__ beta, float decay, float eps,
+                    float* __restrict__ run_mean, float* __restrict__ run_var,
+                    float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                    float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  double s, q;
+  fold_slabs(psum, psq, nslab, C, c, s, q);
+  if (threadIdx.y != 0 || c >= C) return;
   const double n = (double)rows;
   const double mean = s / n;
   double var = q / n - mean * mean;
@@ -208,19 +254,17 @@ bn_partial_grad_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __
 // dgamma = invstd * sum(dy'(x-mean)); dbeta = sum(dy').
 // dx = dy'*A + x*B + Cc  with A = g*invstd, B = -A*invstd^2*S2/n,
 // Cc = -A*S1/n - mean*B.
-__global__ void bn_finalize_grad_k(const float* __restrict__ pdy, const float* __restrict__ pdyx,
-                                   int nslab, int C, long rows, const float* __restrict__ gamma,
-                                   const float* __restrict__ mean, const float* __restrict__ invstd,
-                                   float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                   float* __restrict__ coefA, float* __restrict__ coefB,
-                                   float* __restrict__ coefC, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int k = 0; k < nslab; ++k) {
-    s1 += (double)pdy[(long)k * C + c];
-    s2 += (double)pdyx[(long)k * C + c];
-  }
+__global__ void __launch_bounds__(256)
+bn_finalize_grad_k(const float* __restrict__ pdy, const float* __restrict__ pdyx,
+                   int nslab, int C, long rows, const float* __restrict__ gamma,
+                   const float* __restrict__ mean, const float* __restrict__ invstd,
+                   float* __restrict__ dgamma, float* __restrict__ dbeta,
+                   float* __restrict__ coefA, float* __restrict__ coefB,
+                   float* __restrict__ coefC, int accumulate) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  double s1, s2;
+  fold_slabs(pdy, pdyx, nslab, C, c, s1, s2);
+  if (threadIdx.y != 0 || c >= C) return;
   const float is = invstd[c];
   const float g = gamma ? gamma[c] : 1.f;
   if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)(s2 * is);
@@ -270,13 +314,14 @@ static int stream_grid(long nvec) {
 }
 
 static long choose_slabs(long rows, int rpi, int nchunk) {
-  // Aim for ~2048 blocks in total and >= 8 row-iterations per thread.
-  long target = 2048 / nchunk;
+  // ~2 blocks of 512 threads per CU in total, at most 256 slabs (so the
+  // finalize pass stays short) and >= 8 row-iterations per thread.
+  long target = 512 / nchunk;
   if (target < 1) target = 1;
   long max_by_work = rows / ((long)rpi * 8);
   if (max_by_work < 1) max_by_work = 1;
   long s = target < max_by_work ? target : max_by_work;
-  if (s > 4096) s = 4096;
+  if (s > 256) s = 256;
   return s;
 }
 
@@ -315,7 +360,7 @@ KFB_API hipError_t kfb_bn_fwd_train(int dtype, const void* x, const void* res, v
       const size_t lds = 2 * (size_t)g.rpi * g.tpr * VV * sizeof(float);
       hipLaunchKernelGGL((bn_partial_stats_k<T, VV>), grid, dim3(BN_THREADS), lds, stream,
                          (const T*)x, rows, C, g.cw, g.tpr, g.rpi, slab_rows, psum, psq);
-      hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 256)), dim3(256), 0, stream, psum,
+      hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, 4), 0, stream, psum,
                          psq, nslab, C, rows, gamma, beta, decay, eps, run_mean, run_var,
                          save_mean, save_invstd, scale, shift);
       const long nvec = rows * C / VV;
@@ -396,7 +441,7 @@ KFB_API hipError_t kfb_bn_bwd(int dtype, const void* dy, const void* y, const vo
         hipLaunchKernelGGL((bn_partial_grad_k<T, VV, false>), grid, dim3(BN_THREADS), lds,
                            stream, (const T*)dy, (const T*)y, (const T*)x, save_mean, rows, C,
                            g.cw, g.tpr, g.rpi, slab_rows, pdy, pdyx);
-      hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 256)), dim3(256), 0, stream, pdy,
+      hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, 4), 0, stream, pdy,
                          pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta,
                          coefA, coefB, coefC, accumulate);
       const long nvec = rows * C / VV;

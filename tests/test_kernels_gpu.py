@@ -19,8 +19,9 @@ def tol(dt):
 
 
 def _pair(x, dev, dt):
+    # the fp32 reference sees the same (rounded) input values as the kernel
     a = x.clone().to(dev, dt).requires_grad_(True)
-    b = x.clone().float().requires_grad_(True)
+    b = x.clone().to(dt).float().requires_grad_(True)
     return a, b
 
 
