@@ -1,0 +1,432 @@
+// Implicit-GEMM NHWC convolution on gfx950 MFMA (bf16/fp16 in, fp32 acc).
+//
+// Replaces cuDNN conv fwd / bwd-data / bwd-filter (tf.nn.conv2d and its
+// autodiff in tcb/convnet_builder.py:107-213).
+//
+//   fwd   : y[m][n]  = sum_k  X(m,k) * Wt[n][k]      m=(img,oh,ow) n=cout k=(kh,kw,cin)
+//   dgrad : dx[m][n] = sum_k dY'(m,k) * Wd[n][k]     m=(img,h,w)   n=cin  k=(kh,kw,cout)
+//           ("transposed" gather: dY row (h+pt-kh)/s when divisible), or a
+//           plain 1x1 GEMM scattered into every s-th output pixel for
+//           strided 1x1 convs (ResNet v1 projection shortcuts).
+//   wgrad : dW[n][k] = sum_m  dY[m][n] * X(m,k)      reduction over m = N*OH*OW,
+//           split over workgroups, fp32 atomic accumulation.
+//
+// Tiling (igemm_k): 256 threads = 4 waves in a 2x2 grid; a workgroup computes
+// BN(out-channel) x BM(pixel) with v_mfma_f32_16x16x32_bf16, the weight tile
+// as the A operand and the pixel tile as the B operand, so each lane's four
+// accumulator registers are four consecutive output channels of one pixel
+// (one 8-byte store per lane-row).  K advances 64 per step through a
+// double-buffered LDS image with 128-byte rows whose 16-byte chunks are
+// XOR-swizzled by (row>>1)&7: the ds_read_b128 fragment reads of every
+// 16-lane group then hit 16 distinct bank slots (conflict-free).  The global
+// loads of step k+1 are issued before the MFMAs of step k.  Workgroup ids
+// are remapped so each XCD works on a contiguous run of tiles (L2 reuse of
+// the pixel rows across the output-channel tiles).
+//
+// wgrad_k reads both operands transposed (reduction index m is the row of
+// both LDS images) with ds_read_b64_tr_b16; its images use 256-byte rows
+// with 32-byte units XOR-swizzled so the 8 rows a 32-lane half reads land in
+// 8 distinct 32-byte bank windows.
+#include "common.h"
+
+namespace kfb {
+
+typedef __attribute__((ext_vector_type(8))) short v8s;
+typedef __attribute__((ext_vector_type(4))) float v4f;
+typedef __attribute__((ext_vector_type(4))) short v4s;
+
+template <typename T> struct Mfma;
+template <> struct Mfma<bf16> {
+  static __device__ __forceinline__ v4f run(v8s a, v8s b, v4f c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Mfma<f16> {
+  static __device__ __forceinline__ v4f run(v8s a, v8s b, v4f c) {
+    typedef __attribute__((ext_vector_type(8))) _Float16 v8h;
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(v8h, a),
+                                                  __builtin_bit_cast(v8h, b), c, 0, 0, 0);
+  }
+};
+
+struct IgArgs {
+  const void* x;  // gathered operand (NHWC [N,H,W,C])
+  const void* w;  // [Ncol][Ktot]
+  void* y;        // output rows
+  int N, H, W, C;
+  int OH, OW;     // GEMM row space (M = N*OH*OW)
+  int KH, KW, sh, sw, pt, pl;
+  int Ncol, Ktot, M;
+  int YH, YW, ys, ldy;  // row m=(img,oh,ow) -> ((img*YH + oh*ys)*YW + ow*ys)*ldy
+};
+
+constexpr int IG_BK = 64;
+
+__device__ __forceinline__ int swz_off(int row, int chunk) {
+  // element offset of 16-byte chunk `chunk` (0..7) of 128-byte row `row`
+  return row * IG_BK + ((chunk ^ ((row >> 1) & 7)) << 3);
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <typename T, int BM, int BN, bool TRANS>
+__global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
+  constexpr int XC = BM / 32;  // 16-byte X chunks per thread per K step
+  constexpr int WC = BN / 32;  // 16-byte W chunks per thread per K step
+  constexpr int TM = BM / 32;  // 16-wide pixel subtiles per wave
+  constexpr int TN = BN / 32;  // 16-wide channel subtiles per wave
+  __shared__ __attribute__((aligned(16))) T smem[2 * (BM + BN) * IG_BK];
+
+  const T* __restrict__ x = (const T*)a.x;
+  const T* __restrict__ w = (const T*)a.w;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int mtiles = (a.M + BM - 1) / BM, ntiles = (a.Ncol + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int m0 = (bid / ntiles) * BM, n0 = (bid % ntiles) * BN;
+  const int kc = tid & 7;  // this thread's 16-byte chunk within a 64-wide K step
+  const int OHW = a.OH * a.OW;
+
+  // Per-thread pixel rows of the X tile.
+  int xbase[XC], xh[XC], xw[XC];
+  bool xok[XC];
+#pragma unroll
+  for (int i = 0; i < XC; ++i) {
+    const int m = m0 + (tid >> 3) + i * 32;
+    xok[i] = m < a.M;
+    const int mm = xok[i] ? m : 0;
+    const int img = mm / OHW, rem = mm - img * OHW;
+    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+    xbase[i] = img * a.H * a.W * a.C;
+    if (TRANS) { xh[i] = oh + a.pt; xw[i] = ow + a.pl; }
+    else { xh[i] = oh * a.sh - a.pt; xw[i] = ow * a.sw - a.pl; }
+  }
+  const T* wrow[WC];
+  bool wok[WC];
+#pragma unroll
+  for (int i = 0; i < WC; ++i) {
+    const int n = n0 + (tid >> 3) + i * 32;
+    wok[i] = n < a.Ncol;
+    wrow[i] = w + (long)(wok[i] ? n : 0) * a.Ktot;
+  }
+
+  uint4 xr[XC], wr[WC];
+  auto load = [&](int kt) {
+    const int k = kt * IG_BK + kc * 8;
+    const bool kok = k < a.Ktot;
+    const int tap = k / a.C, cc = k - tap * a.C;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+#pragma unroll
+    for (int i = 0; i < XC; ++i) {
+      bool ok = kok && xok[i];
+      int hi, wi;
+      if (TRANS) {
+        const int hh = xh[i] - kh, ww = xw[i] - kw;
+        ok = ok && hh >= 0 && ww >= 0;
+        hi = hh / a.sh; wi = ww / a.sw;
+        ok = ok && hi * a.sh == hh && wi * a.sw == ww && hi < a.H && wi < a.W;
+      } else {
+        hi = xh[i] + kh; wi = xw[i] + kw;
+        ok = ok && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+      }
+      xr[i] = ok ? *(const uint4*)(x + xbase[i] + (hi * a.W + wi) * a.C + cc)
+                 : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+      wr[i] = (kok && wok[i]) ? *(const uint4*)(wrow[i] + k) : make_uint4(0, 0, 0, 0);
+  };
+  auto store = [&](int buf) {
+    T* xs = smem + buf * (BM + BN) * IG_BK;
+    T* ws = xs + BM * IG_BK;
+#pragma unroll
+    for (int i = 0; i < XC; ++i) *(uint4*)(xs + swz_off((tid >> 3) + i * 32, kc)) = xr[i];
+#pragma unroll
+    for (int i = 0; i < WC; ++i) *(uint4*)(ws + swz_off((tid >> 3) + i * 32, kc)) = wr[i];
+  };
+
+  v4f acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int wn = wid >> 1, wm = wid & 1;
+  const int nk = (a.Ktot + IG_BK - 1) / IG_BK;
+  load(0);
+  store(0);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) load(kt + 1);
+    const T* xs = smem + cur * (BM + BN) * IG_BK;
+    const T* ws = xs + BM * IG_BK;
+#pragma unroll
+    for (int ks = 0; ks < IG_BK / 32; ++ks) {
+      const int chunk = ks * 4 + (lane >> 4);
+      v8s af[TN], bfr[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+        af[i] = *(const v8s*)(ws + swz_off(wn * (BN / 2) + i * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+        bfr[j] = *(const v8s*)(xs + swz_off(wm * (BM / 2) + j * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = Mfma<T>::run(af[i], bfr[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) store(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // Epilogue: lane holds channels n..n+3 of pixel m for each (i, j) subtile.
+  T* __restrict__ y = (T*)a.y;
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    const int m = m0 + wm * (BM / 2) + j * 16 + (lane & 15);
+    if (m >= a.M) continue;
+    long rowoff;
+    if (a.ys == 1 && a.YH == a.OH && a.YW == a.OW) {
+      rowoff = (long)m * a.ldy;
+    } else {
+      const int img = m / OHW, rem = m - img * OHW;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      rowoff = ((long)(img * a.YH + oh * a.ys) * a.YW + ow * a.ys) * a.ldy;
+    }
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int n = n0 + wn * (BN / 2) + i * 16 + (lane >> 4) * 4;
+      if (n >= a.Ncol) continue;
+      Vec<T, 4> o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o.v[r] = (T)acc[i][j][r];
+      *reinterpret_cast<Vec<T, 4>*>(y + rowoff + n) = o;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ wgrad
+struct WgArgs {
+  const void* dy;  // [M][Ncol]  (NHWC output gradient, Ncol = Cout)
+  const void* x;   // NHWC input [N,H,W,C]
+  float* dw;       // [Ncol][Ktot] fp32, accumulated atomically
+  int N, H, W, C;
+  int OH, OW;
+  int KH, KW, sh, sw, pt, pl;
+  int Ncol, Ktot, M;
+  int mper;        // rows of m per split
+};
+
+constexpr int WG_BK = 32;  // reduction rows per step
+
+// 256-byte rows (128 elements); 32-byte unit u (0..7) of row r stored at
+// u ^ f(r), f(r) = (r & 3) | ((r >> 3) & 1) << 2.
+__device__ __forceinline__ int tr_off(int row, int col) {
+  const int f = (row & 3) | (((row >> 3) & 1) << 2);
+  const int u = col >> 4;
+  return row * 128 + (((u ^ f) << 4) | (col & 15));
+}
+
+template <typename T>
+__device__ __forceinline__ v4s ds_read_tr(const T* p) {
+  typedef __attribute__((address_space(3))) v4s lds_v4s;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p));
+}
+
+template <typename T, int BMC, int BNK>
+__global__ void __launch_bounds__(256, 2) wgrad_k(WgArgs a) {
+  // BMC = output-channel tile (rows of dW), BNK = k tile (cols of dW); both 128 or 64.
+  constexpr int TN = BMC / 32, TM = BNK / 32;
+  constexpr int DC = WG_BK * BMC / 8 / 256;  // dy chunks per thread
+  constexpr int XC = WG_BK * BNK / 8 / 256;  // x chunks per thread
+  __shared__ __attribute__((aligned(16))) T smem[2 * WG_BK * 256];  // [buf][dy 32x128 | x 32x128]
+
+  const T* __restrict__ dy = (const T*)a.dy;
+  const T* __restrict__ x = (const T*)a.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ctiles = (a.Ncol + BMC - 1) / BMC, ktiles = (a.Ktot + BNK - 1) / BNK;
+  const int tiles = ctiles * ktiles;
+  const int split = blockIdx.x / tiles;
+  const int tile = blockIdx.x - split * tiles;
+  const int c0 = (tile / ktiles) * BMC, k0 = (tile % ktiles) * BNK;
+  const int mbeg = split * a.mper;
+  const int mend = min(a.M, mbeg + a.mper);
+  const int OHW = a.OH * a.OW;
+
+  // Loader geometry: dy rows are m (WG_BK per step), BMC/8 chunks per row.
+  constexpr int DCPR = BMC / 8, XCPR = BNK / 8;
+  int dcol[DC], drow[DC];
+#pragma unroll
+  for (int i = 0; i < DC; ++i) {
+    const int c = tid + i * 256;
+    drow[i] = c / DCPR;
+    dcol[i] = (c % DCPR) * 8;
+  }
+  // x chunks: fixed k per thread (col), row = m
+  int xcol[XC], xrow[XC], xtap_h[XC], xtap_w[XC], xcc[XC];
+  bool xkok[XC];
+#pragma unroll
+  for (int i = 0; i < XC; ++i) {
+    const int c = tid + i * 256;
+    xrow[i] = c / XCPR;
+    xcol[i] = (c % XCPR) * 8;
+    const int k = k0 + xcol[i];
+    xkok[i] = k < a.Ktot;
+    const int tap = k / a.C;
+    xcc[i] = k - tap * a.C;
+    xtap_h[i] = tap / a.KW;
+    xtap_w[i] = tap - xtap_h[i] * a.KW;
+  }
+  uint4 dr[DC], xr[XC];
+  auto load = [&](int mstep) {
+#pragma unroll
+    for (int i = 0; i < DC; ++i) {
+      const int m = mstep + drow[i];
+      const int col = c0 + dcol[i];
+      dr[i] = (m < mend && col < a.Ncol) ? *(const uint4*)(dy + (long)m * a.Ncol + col)
+                                         : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < XC; ++i) {
+      const int m = mstep + xrow[i];
+      bool ok = xkok[i] && m < mend;
+      const int mm = ok ? m : 0;
+      const int img = mm / OHW, rem = mm - img * OHW;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      const int hi = oh * a.sh - a.pt + xtap_h[i], wi = ow * a.sw - a.pl + xtap_w[i];
+      ok = ok && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+      xr[i] = ok ? *(const uint4*)(x + ((long)(img * a.H + hi) * a.W + wi) * a.C + xcc[i])
+                 : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store = [&](int buf) {
+    T* ds = smem + buf * WG_BK * 256;
+    T* xs = ds + WG_BK * 128;
+#pragma unroll
+    for (int i = 0; i < DC; ++i) *(uint4*)(ds + tr_off(drow[i], dcol[i])) = dr[i];
+#pragma unroll
+    for (int i = 0; i < XC; ++i) *(uint4*)(xs + tr_off(xrow[i], xcol[i])) = xr[i];
+  };
+
+  v4f acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int wn = wid >> 1, wm = wid & 1;
+  // Transposed-read addressing: group g = lane>>4 needs rows 8g..8g+7
+  // (two reads of 4 rows); lane 4q+p of the group addresses row q, cols 4p..4p+3.
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int nsteps = (mend - mbeg + WG_BK - 1) / WG_BK;
+  if (nsteps > 0) {
+    load(mbeg);
+    store(0);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int s = 0; s < nsteps; ++s) {
+    if (s + 1 < nsteps) load(mbeg + (s + 1) * WG_BK);
+    const T* ds = smem + cur * WG_BK * 256;
+    const T* xs = ds + WG_BK * 128;
+    v8s af[TN], bfr[TM];
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int col = wn * (BMC / 2) + i * 16 + 4 * p;
+      v4s lo = ds_read_tr<T>(ds + tr_off(8 * g + q, col));
+      v4s hi = ds_read_tr<T>(ds + tr_off(8 * g + 4 + q, col));
+      af[i] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int col = wm * (BNK / 2) + j * 16 + 4 * p;
+      v4s lo = ds_read_tr<T>(xs + tr_off(8 * g + q, col));
+      v4s hi = ds_read_tr<T>(xs + tr_off(8 * g + 4 + q, col));
+      bfr[j] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) acc[i][j] = Mfma<T>::run(af[i], bfr[j], acc[i][j]);
+    if (s + 1 < nsteps) store(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // acc[i][j]: rows (dW output channel) c0 + wn*BMC/2 + i*16 + (lane>>4)*4 + r,
+  // col (k) k0 + wm*BNK/2 + j*16 + (lane&15).
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int k = k0 + wm * (BNK / 2) + j * 16 + (lane & 15);
+      if (k >= a.Ktot) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = c0 + wn * (BMC / 2) + i * 16 + (lane >> 4) * 4 + r;
+        if (c < a.Ncol) atomicAdd(a.dw + (long)c * a.Ktot + k, acc[i][j][r]);
+      }
+    }
+}
+
+template <typename T, int BM, int BN>
+static void launch_ig(const IgArgs& a, bool trans, hipStream_t s) {
+  const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
+  if (trans)
+    hipLaunchKernelGGL((igemm_k<T, BM, BN, true>), dim3(nwg), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((igemm_k<T, BM, BN, false>), dim3(nwg), dim3(256), 0, s, a);
+}
+
+}  // namespace kfb
+
+using namespace kfb;
+
+// Forward conv or dgrad (trans=1) or scattered 1x1 GEMM (ys>1).
+// Requirements: C % 8 == 0, Ncol % 4 == 0, 16-byte aligned pointers.
+KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void* y, int N, int H,
+                                  int W, int C, int OH, int OW, int KH, int KW, int sh, int sw,
+                                  int pt, int pl, int Ncol, int YH, int YW, int ys, int ldy,
+                                  int trans, hipStream_t stream) {
+  if (C % 8 || Ncol % 4) return hipErrorInvalidValue;
+  IgArgs a{x, w, y, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
+           N * OH * OW, YH, YW, ys, ldy};
+  const bool t = trans != 0;
+  if (dtype == BF16) {
+    if (Ncol <= 64) launch_ig<bf16, 128, 64>(a, t, stream);
+    else launch_ig<bf16, 128, 128>(a, t, stream);
+  } else if (dtype == F16) {
+    if (Ncol <= 64) launch_ig<f16, 128, 64>(a, t, stream);
+    else launch_ig<f16, 128, 128>(a, t, stream);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// Weight gradient: dw [Ncol][KH*KW*C] fp32 must be zeroed by the caller.
+KFB_API hipError_t kfb_conv_wgrad(int dtype, const void* dy, const void* x, float* dw, int N,
+                                  int H, int W, int C, int OH, int OW, int KH, int KW, int sh,
+                                  int sw, int pt, int pl, int Ncol, int target_blocks,
+                                  hipStream_t stream) {
+  if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
+  WgArgs a{dy, x, dw, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
+           N * OH * OW, 0};
+  const int tiles = ((Ncol + 127) / 128) * ((a.Ktot + 127) / 128);
+  int split = target_blocks > 0 ? target_blocks / tiles : 1024 / tiles;
+  const int max_split = (a.M + WG_BK * 8 - 1) / (WG_BK * 8);  // >= 8 steps per block
+  if (split > max_split) split = max_split;
+  if (split < 1) split = 1;
+  a.mper = ((a.M + split - 1) / split + WG_BK - 1) / WG_BK * WG_BK;
+  split = (a.M + a.mper - 1) / a.mper;
+  if (dtype == BF16)
+    hipLaunchKernelGGL((wgrad_k<bf16, 128, 128>), dim3(tiles * split), dim3(256), 0, stream, a);
+  else if (dtype == F16)
+    hipLaunchKernelGGL((wgrad_k<f16, 128, 128>), dim3(tiles * split), dim3(256), 0, stream, a);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
