@@ -30,7 +30,13 @@ step smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
   step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
 fi
+if [ "${CONV_BENCH:-0}" = "1" ]; then
+  step conv_bench 600 python scripts/bench_conv.py --json "$OUT/conv_bench.json"
+fi
 step bench 900 python bench.py --verbose "$@"
+if [ -n "${BENCH_B:-}" ]; then
+  step bench_b 900 python bench.py --verbose $BENCH_B
+fi
 if [ "${SKIP_PROF:-0}" != "1" ]; then
   cd /tmp && export TMPDIR=/tmp
   step rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
