@@ -184,28 +184,42 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
   }
 
   // Epilogue: lane holds channels n..n+3 of pixel m for each (i, j) subtile.
+  // Stage the BM x BN tile through LDS (rows = pixels, 16-byte chunks
+  // XOR-swizzled by row) so every global store is a full 16-byte lane write
+  // and each pixel row goes out as one contiguous BN*2-byte run.
   T* __restrict__ y = (T*)a.y;
+  T* cs = smem;  // reuse the operand buffers (the final __syncthreads above retired them)
+  constexpr int CPR = BN / 8;  // 16-byte chunks per staged row
 #pragma unroll
   for (int j = 0; j < TM; ++j) {
-    const int m = m0 + wm * (BM / 2) + j * 16 + (lane & 15);
-    if (m >= a.M) continue;
+    const int ml = wm * (BM / 2) + j * 16 + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int nl = wn * (BN / 2) + i * 16 + (lane >> 4) * 4;
+      Vec<T, 4> o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o.v[r] = (T)acc[i][j][r];
+      const int chunk = (nl >> 3) ^ (ml & (CPR - 1));
+      *reinterpret_cast<Vec<T, 4>*>(cs + ml * BN + chunk * 8 + (nl & 7)) = o;
+    }
+  }
+  __syncthreads();
+  const bool dense = (a.ys == 1 && a.YH == a.OH && a.YW == a.OW);
+#pragma unroll
+  for (int pass = 0; pass < BM * CPR / 256; ++pass) {
+    const int t = tid + pass * 256;
+    const int ml = t / CPR, ch = t % CPR;
+    const int m = m0 + ml, n = n0 + ch * 8;
+    if (m >= a.M || n >= a.Ncol) continue;
     long rowoff;
-    if (a.ys == 1 && a.YH == a.OH && a.YW == a.OW) {
+    if (dense) {
       rowoff = (long)m * a.ldy;
     } else {
       const int img = m / OHW, rem = m - img * OHW;
       const int oh = rem / a.OW, ow = rem - oh * a.OW;
       rowoff = ((long)(img * a.YH + oh * a.ys) * a.YW + ow * a.ys) * a.ldy;
     }
-#pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      const int n = n0 + wn * (BN / 2) + i * 16 + (lane >> 4) * 4;
-      if (n >= a.Ncol) continue;
-      Vec<T, 4> o;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o.v[r] = (T)acc[i][j][r];
-      *reinterpret_cast<Vec<T, 4>*>(y + rowoff + n) = o;
-    }
+    *(uint4*)(y + rowoff + n) = *(const uint4*)(cs + ml * BN + ((ch ^ (ml & (CPR - 1))) * 8));
   }
 }
 
@@ -391,7 +405,7 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
                                   int W, int C, int OH, int OW, int KH, int KW, int sh, int sw,
                                   int pt, int pl, int Ncol, int YH, int YW, int ys, int ldy,
                                   int trans, hipStream_t stream) {
-  if (C % 8 || Ncol % 4) return hipErrorInvalidValue;
+  if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
   IgArgs a{x, w, y, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
            N * OH * OW, YH, YW, ys, ldy};
   const bool t = trans != 0;
@@ -415,18 +429,26 @@ KFB_API hipError_t kfb_conv_wgrad(int dtype, const void* dy, const void* x, floa
   if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
   WgArgs a{dy, x, dw, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
            N * OH * OW, 0};
-  const int tiles = ((Ncol + 127) / 128) * ((a.Ktot + 127) / 128);
+  const int bmc = Ncol <= 64 ? 64 : 128;
+  const int tiles = ((Ncol + bmc - 1) / bmc) * ((a.Ktot + 127) / 128);
   int split = target_blocks > 0 ? target_blocks / tiles : 1024 / tiles;
   const int max_split = (a.M + WG_BK * 8 - 1) / (WG_BK * 8);  // >= 8 steps per block
   if (split > max_split) split = max_split;
   if (split < 1) split = 1;
   a.mper = ((a.M + split - 1) / split + WG_BK - 1) / WG_BK * WG_BK;
   split = (a.M + a.mper - 1) / a.mper;
-  if (dtype == BF16)
-    hipLaunchKernelGGL((wgrad_k<bf16, 128, 128>), dim3(tiles * split), dim3(256), 0, stream, a);
-  else if (dtype == F16)
-    hipLaunchKernelGGL((wgrad_k<f16, 128, 128>), dim3(tiles * split), dim3(256), 0, stream, a);
-  else
+  if (dtype == BF16) {
+    if (bmc == 64)
+      hipLaunchKernelGGL((wgrad_k<bf16, 64, 128>), dim3(tiles * split), dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL((wgrad_k<bf16, 128, 128>), dim3(tiles * split), dim3(256), 0, stream, a);
+  } else if (dtype == F16) {
+    if (bmc == 64)
+      hipLaunchKernelGGL((wgrad_k<f16, 64, 128>), dim3(tiles * split), dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL((wgrad_k<f16, 128, 128>), dim3(tiles * split), dim3(256), 0, stream, a);
+  } else {
     return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }

@@ -70,6 +70,15 @@ def conv_dgrad(dy, wl, x_shape, stride, pads):
             return None
         _igemm(dy, wt, dx, n, OH, OW, cout, OH, OW, 1, 1, 1, 1, 0, 0, C, H, W, ys, C, False)
         return dx
+    if sh == 1 and sw == 1 and KH - 1 - pt >= 0 and KH - 1 - pb >= 0 \
+            and KW - 1 - pl >= 0 and KW - 1 - pr >= 0:
+        # stride-1 transposed conv == forward conv of dY with the spatially
+        # flipped, channel-transposed kernel and complementary padding.
+        wf = wl.flip(1, 2).permute(3, 1, 2, 0).contiguous()  # [Cin][KH][KW][Cout]
+        dx = torch.empty((n, H, W, C), dtype=dy.dtype, device=dy.device)
+        _igemm(dy, wf, dx, n, OH, OW, cout, H, W, KH, KW, 1, 1, KH - 1 - pt, KW - 1 - pl, C,
+               H, W, 1, C, False)
+        return dx
     wd = wl.permute(3, 1, 2, 0).contiguous()  # [Cin][KH][KW][Cout]
     dx = torch.empty((n, H, W, C), dtype=dy.dtype, device=dy.device)
     _igemm(dy, wd, dx, n, OH, OW, cout, H, W, KH, KW, sh, sw, pt, pl, C, H, W, 1, C, True)
