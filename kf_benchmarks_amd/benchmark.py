@@ -471,6 +471,11 @@ class BenchmarkCNN:
             eval_hook = EvalDuringTraining(self)
         from .utils.tracing import StepTracer
         tracer = StepTracer(self)
+        self.summary_writer = None
+        if (p.summary_verbosity > 0 and p.save_summaries_steps > 0 and p.train_dir
+                and self.world.is_chief):
+            from .utils.summary import SummaryWriter
+            self.summary_writer = SummaryWriter(p.train_dir)
         timer = _EventTimer(self.device)
         step_train_times: List[float] = []
         forward_only = p.forward_only
@@ -492,7 +497,7 @@ class BenchmarkCNN:
             if local_step == 0:
                 log_fn("Done warm up")
                 if not header_printed:
-                    header = "Step\tImg/sec\t" + p.loss_type_to_report.replace("_", " ")
+                    header = "Step\tImg/sec\t" + p.loss_type_to_report.replace("/", " ")
                     if p.print_training_accuracy:
                         header += "\ttop_1_accuracy\ttop_5_accuracy"
                     log_fn(header)
@@ -511,11 +516,17 @@ class BenchmarkCNN:
                 self.forward_only_step()
                 loss, acc = None, None
             else:
-                loss, acc = self.train_step(need_loss=display or local_step >= total_steps - 1,
+                want_sum = (p.summary_verbosity > 0 and p.save_summaries_steps > 0 and
+                            (local_step + 1) % p.save_summaries_steps == 0)
+                loss, acc = self.train_step(need_loss=display or want_sum or
+                                            local_step >= total_steps - 1,
                                             need_accuracy=display and p.print_training_accuracy)
             tracer.end(local_step)
             if local_step >= 0:
                 timer.mark()
+            if (self.summary_writer is not None and local_step >= 0
+                    and (local_step + 1) % p.save_summaries_steps == 0 and loss is not None):
+                self._write_summaries(loss)
             if display:
                 step_train_times.extend(timer.collect())
                 if step_train_times:
@@ -562,6 +573,29 @@ class BenchmarkCNN:
         if p.print_json_result and self.world.is_chief:
             print(json.dumps(stats))
         return stats
+
+    def _write_summaries(self, loss):
+        """Scalars (verbosity>=1), log|grad| histogram (>=2), per-variable and
+        per-gradient histograms (>=3), as tcb/benchmark_cnn.py:2811-2846."""
+        p = self.params
+        step = self.global_step
+        scalars = {"learning_rate": self.learning_rate(step - 1),
+                   p.loss_type_to_report: float(loss)}
+        if self.loss_scale is not None:
+            scalars["loss_scale"] = float(self.loss_scale)
+        if self.loss_scale_normal_steps:
+            scalars["loss_scale_normal_steps"] = float(self.loss_scale_normal_steps)
+        self.summary_writer.add_scalars(scalars, step)
+        if p.summary_verbosity >= 2:
+            g = self.flat.grad.detach().abs()
+            g = g[g != 0].float().log().cpu().numpy()
+            self.summary_writer.add_histograms({"log_gradients": g}, step)
+        if p.summary_verbosity >= 3:
+            hists = {}
+            for name, param, off, n in self.flat.segments():
+                hists[name + "/gradients"] = self.flat.grad[off:off + n].detach().cpu().numpy()
+                hists[name] = param.detach().cpu().numpy()
+            self.summary_writer.add_histograms(hists, step)
 
     def _log_step(self, local_step, step_train_times, lossval, acc):
         p = self.params

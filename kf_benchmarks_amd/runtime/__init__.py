@@ -1,0 +1,233 @@
+"""ctypes binding of the native host runtime ``_lib/libkfb_rt.so``
+(csrc/runtime/kfb_runtime.cpp): CRC32C, TFRecord reader/writer,
+tf.train.Example decoding and the LevelDB-format table used by TF V2
+checkpoint indexes."""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+import threading
+from typing import Dict, Iterator, List, Tuple
+
+from .. import build as _build
+
+_LIB = None
+_LOCK = threading.Lock()
+
+c_char_p_p = ctypes.POINTER(ctypes.c_char_p)
+
+
+def _load():
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        if not os.path.exists(_build.RT_LIB):
+            _build.build_rt()
+        lib = ctypes.CDLL(_build.RT_LIB)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        sz = ctypes.c_size_t
+        lib.kfbrt_crc32c.argtypes = [ctypes.c_char_p, sz]
+        lib.kfbrt_crc32c.restype = ctypes.c_uint32
+        lib.kfbrt_crc32c_extend.argtypes = [ctypes.c_uint32, ctypes.c_char_p, sz]
+        lib.kfbrt_crc32c_extend.restype = ctypes.c_uint32
+        lib.kfbrt_masked_crc32c.argtypes = [ctypes.c_char_p, sz]
+        lib.kfbrt_masked_crc32c.restype = ctypes.c_uint32
+        lib.kfbrt_record_reader_open.argtypes = [ctypes.c_char_p, ctypes.c_int]
+        lib.kfbrt_record_reader_open.restype = ctypes.c_void_p
+        lib.kfbrt_record_reader_next.argtypes = [ctypes.c_void_p, ctypes.POINTER(u8p)]
+        lib.kfbrt_record_reader_next.restype = ctypes.c_long
+        lib.kfbrt_record_reader_close.argtypes = [ctypes.c_void_p]
+        lib.kfbrt_record_writer_open.argtypes = [ctypes.c_char_p]
+        lib.kfbrt_record_writer_open.restype = ctypes.c_void_p
+        lib.kfbrt_record_writer_write.argtypes = [ctypes.c_void_p, ctypes.c_char_p, sz]
+        lib.kfbrt_record_writer_write.restype = ctypes.c_int
+        lib.kfbrt_record_writer_close.argtypes = [ctypes.c_void_p]
+        lib.kfbrt_table_write.argtypes = [ctypes.c_char_p, ctypes.c_int, c_char_p_p,
+                                          ctypes.POINTER(sz), c_char_p_p, ctypes.POINTER(sz)]
+        lib.kfbrt_table_write.restype = ctypes.c_int
+        lib.kfbrt_table_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
+        lib.kfbrt_table_read.restype = ctypes.c_void_p
+        lib.kfbrt_table_size.argtypes = [ctypes.c_void_p]
+        lib.kfbrt_table_size.restype = ctypes.c_int
+        cpp = ctypes.POINTER(ctypes.c_void_p)
+        lib.kfbrt_table_entry.argtypes = [ctypes.c_void_p, ctypes.c_int, cpp, ctypes.POINTER(sz),
+                                          cpp, ctypes.POINTER(sz)]
+        lib.kfbrt_table_free.argtypes = [ctypes.c_void_p]
+        lib.kfbrt_parse_example.argtypes = [ctypes.c_char_p, sz, ctypes.c_void_p, sz]
+        lib.kfbrt_parse_example.restype = ctypes.c_long
+        _LIB = lib
+        return lib
+
+
+def crc32c(data: bytes, crc: int = 0) -> int:
+    lib = _load()
+    if crc:
+        return lib.kfbrt_crc32c_extend(crc, data, len(data))
+    return lib.kfbrt_crc32c(data, len(data))
+
+
+def masked_crc32c(data: bytes) -> int:
+    return _load().kfbrt_masked_crc32c(data, len(data))
+
+
+def mask(crc: int) -> int:
+    return (((crc >> 15) | (crc << 17)) + 0xA282EAD8) & 0xFFFFFFFF
+
+
+# ------------------------------------------------------------------ TFRecord
+class TFRecordCorrupt(IOError):
+    pass
+
+
+def tf_record_iterator(path: str, verify: bool = True) -> Iterator[bytes]:
+    lib = _load()
+    h = lib.kfbrt_record_reader_open(path.encode(), int(verify))
+    if not h:
+        raise IOError("cannot open %s" % path)
+    try:
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        while True:
+            n = lib.kfbrt_record_reader_next(h, ctypes.byref(out))
+            if n == -1:
+                return
+            if n < 0:
+                raise TFRecordCorrupt("corrupt record in %s" % path)
+            yield ctypes.string_at(out, n)
+    finally:
+        lib.kfbrt_record_reader_close(h)
+
+
+class TFRecordWriter:
+    def __init__(self, path: str):
+        self._lib = _load()
+        self._h = self._lib.kfbrt_record_writer_open(path.encode())
+        if not self._h:
+            raise IOError("cannot open %s for writing" % path)
+
+    def write(self, record: bytes):
+        if self._lib.kfbrt_record_writer_write(self._h, record, len(record)) != 0:
+            raise IOError("write failed")
+
+    def close(self):
+        if self._h:
+            self._lib.kfbrt_record_writer_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+# ------------------------------------------------------------- tf.Example
+def parse_example(record: bytes) -> Dict[str, list]:
+    """{feature key: list of bytes | float | int}."""
+    lib = _load()
+    cap = max(4 * len(record) + 256, 4096)
+    while True:
+        buf = ctypes.create_string_buffer(cap)
+        n = lib.kfbrt_parse_example(record, len(record), buf, cap)
+        if n == -2:
+            cap *= 4
+            continue
+        if n < 0:
+            raise ValueError("malformed tf.Example")
+        break
+    raw = buf.raw[:n]
+    out: Dict[str, list] = {}
+    i = 0
+    while i < n:
+        (klen,) = struct.unpack_from("<I", raw, i)
+        i += 4
+        key = raw[i:i + klen].decode()
+        i += klen
+        kind = raw[i]
+        (count,) = struct.unpack_from("<I", raw, i + 1)
+        i += 5
+        vals: list = []
+        if kind == 1:
+            for _ in range(count):
+                (bl,) = struct.unpack_from("<I", raw, i)
+                i += 4
+                vals.append(raw[i:i + bl])
+                i += bl
+        elif kind == 2:
+            vals = list(struct.unpack_from("<%df" % count, raw, i))
+            i += 4 * count
+        elif kind == 3:
+            vals = list(struct.unpack_from("<%dq" % count, raw, i))
+            i += 8 * count
+        out[key] = vals
+    return out
+
+
+# --- minimal protobuf encoding used by the writers (tf.Example for test data)
+def _varint(v: int) -> bytes:
+    out = bytearray()
+    v &= (1 << 64) - 1
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def _ld(field: int, payload: bytes) -> bytes:
+    return _varint((field << 3) | 2) + _varint(len(payload)) + payload
+
+
+def make_example(features: Dict[str, list]) -> bytes:
+    """Encode a tf.train.Example from {key: [bytes...] | [float...] | [int...]}."""
+    entries = b""
+    for key in sorted(features):
+        vals = features[key]
+        if vals and isinstance(vals[0], (bytes, bytearray)):
+            lst = b"".join(_ld(1, bytes(v)) for v in vals)
+            feat = _ld(1, lst)
+        elif vals and isinstance(vals[0], float):
+            lst = _ld(1, struct.pack("<%df" % len(vals), *vals))
+            feat = _ld(2, lst)
+        else:
+            lst = _ld(1, b"".join(_varint(int(v)) for v in vals))
+            feat = _ld(3, lst)
+        entries += _ld(1, _ld(1, key.encode()) + _ld(2, feat))
+    return _ld(1, entries)
+
+
+# -------------------------------------------------------------------- tables
+def table_write(path: str, items: List[Tuple[bytes, bytes]]):
+    lib = _load()
+    items = sorted(items)
+    n = len(items)
+    keys = (ctypes.c_char_p * n)(*[k for k, _ in items])
+    klens = (ctypes.c_size_t * n)(*[len(k) for k, _ in items])
+    vals = (ctypes.c_char_p * n)(*[v for _, v in items])
+    vlens = (ctypes.c_size_t * n)(*[len(v) for _, v in items])
+    rc = lib.kfbrt_table_write(path.encode(), n, keys, klens, vals, vlens)
+    if rc != 0:
+        raise IOError("table write failed (%d): %s" % (rc, path))
+
+
+def table_read(path: str) -> List[Tuple[bytes, bytes]]:
+    lib = _load()
+    err = ctypes.c_int(0)
+    h = lib.kfbrt_table_read(path.encode(), ctypes.byref(err))
+    if not h:
+        raise IOError("table read failed (%d): %s" % (err.value, path))
+    try:
+        out = []
+        kp, vp = ctypes.c_void_p(), ctypes.c_void_p()
+        kl, vl = ctypes.c_size_t(), ctypes.c_size_t()
+        for i in range(lib.kfbrt_table_size(h)):
+            lib.kfbrt_table_entry(h, i, ctypes.byref(kp), ctypes.byref(kl), ctypes.byref(vp),
+                                  ctypes.byref(vl))
+            out.append((ctypes.string_at(kp, kl.value), ctypes.string_at(vp, vl.value)))
+        return out
+    finally:
+        lib.kfbrt_table_free(h)
