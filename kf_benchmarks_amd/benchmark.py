@@ -363,6 +363,11 @@ class BenchmarkCNN:
         from .data.input_pipeline import make_input_source
         return make_input_source(self, subset="validation" if self._doing_eval else "train")
 
+    def set_fake_data(self, images, labels):
+        """Feed these NHWC numpy images/labels instead of synthetic or real
+        data (tests; role of TestImagePreprocessor.set_fake_data)."""
+        self.fake_data = (images, labels)
+
     # ------------------------------------------------------------------ step
     def l2_loss_value(self):
         """sum(w^2)/2 over trainable variables (device scalar)."""
@@ -399,6 +404,9 @@ class BenchmarkCNN:
         self.strategy.before_backward(step)
         loss, acc = self.forward_backward(images, labels, need_accuracy)
         self.strategy.after_backward(step)
+        if need_loss and p.loss_type_to_report == "total_loss" and p.weight_decay:
+            # the reported total loss uses the weights of this step's forward
+            loss = loss + len(self.devices) * p.weight_decay * self.l2_loss_value()
         grad_scale = self.strategy.grad_scale
         if self.loss_scale:
             grad_scale /= self.loss_scale
@@ -412,8 +420,6 @@ class BenchmarkCNN:
                                 weight_decay=wd, clip=p.gradient_clip)
             self.strategy.after_update(step)
         self.global_step += 1
-        if need_loss and p.loss_type_to_report == "total_loss" and p.weight_decay:
-            loss = loss + len(self.devices) * p.weight_decay * self.l2_loss_value()
         return loss, acc
 
     def _auto_loss_scale_check(self) -> bool:
@@ -559,6 +565,7 @@ class BenchmarkCNN:
         if p.train_dir and self.world.is_chief and not forward_only:
             self.saver.save(p.train_dir, self.global_step)
         tracer.finish()
+        self.strategy.close()
         if p.variable_update == "kungfu" or p.sync_on_finish:
             self.world.barrier(self.device if self.device_type == "cuda" else None)
         if last_loss is None and loss is not None:

@@ -43,6 +43,36 @@ class SyntheticInput:
         pass
 
 
+class FakeDataInput:
+    """Cycles through a user-provided numpy batch set (tests; the
+    TestImagePreprocessor.set_fake_data of tcb/preprocessing.py:896-974).
+    Images are normalized like real data (x / 127.5 - 1); each worker starts
+    at shift_ratio = rank / num_workers of the data, as in the reference."""
+
+    def __init__(self, bench, images, labels):
+        import numpy as np
+        from .. import cnn_util
+        self.bench = bench
+        bs = bench.batch_size
+        shift = bench.task_index / float(max(bench.num_workers, 1))
+        imgs = cnn_util.roll_numpy_batches(np.asarray(images, dtype=np.float32), bs, shift)
+        labs = cnn_util.roll_numpy_batches(np.asarray(labels), bs, shift)
+        self.images = torch.from_numpy(imgs / 127.5 - 1.0).to(bench.device, bench.compute_dtype)
+        self.labels = torch.from_numpy(labs.astype("int32")).to(bench.device)
+        self.n = imgs.shape[0] // bs
+        self.i = 0
+
+    def next(self):
+        bs = self.bench.batch_size
+        k = self.i % self.n
+        self.i += 1
+        return (self.images[k * bs:(k + 1) * bs].contiguous(),
+                self.labels[k * bs:(k + 1) * bs].contiguous())
+
+    def close(self):
+        pass
+
+
 class PrefetchInput:
     """Pulls host batches from a preprocessor generator on a thread, copies
     them to the device on a side stream, one batch ahead."""
@@ -112,6 +142,9 @@ class PrefetchInput:
 
 
 def make_input_source(bench, subset="train"):
+    fake = getattr(bench, "fake_data", None)
+    if fake is not None:
+        return FakeDataInput(bench, *fake)
     if bench.dataset.use_synthetic_gpu_inputs():
         return SyntheticInput(bench, subset)
     from . import preprocessing

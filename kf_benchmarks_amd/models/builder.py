@@ -90,7 +90,7 @@ class ConvNetBuilder:
         use_bias = (not use_batch_norm) and bias is not None
         layer = self._layer(scope, lambda: ConvLayer(
             scope, cin, num_out_channels, k_height, k_width, use_bias, bias or 0.0, stddev,
-            self.net.init_gen, self.net.param_device))
+            self.net.init_gen, self.net.param_device, kernel_initializer))
         _, H, W, _ = x.shape
         pads = F.resolve_pads(mode, H, W, k_height, k_width, d_height, d_width)
         w = self._p(layer.weight)

@@ -52,12 +52,18 @@ class ConvLayer(Layer):
     """Weight stored [Cout, KH, KW, Cin] (kernel layout); TF layout is
     [KH, KW, Cin, Cout] and is produced on checkpoint export."""
 
-    def __init__(self, scope, cin, cout, kh, kw, use_bias, bias_init, stddev, gen, device):
+    def __init__(self, scope, cin, cout, kh, kw, use_bias, bias_init, stddev, gen, device,
+                 kernel_initializer=None):
         super().__init__()
         self.tf_scope = scope
         self.cin, self.cout, self.kh, self.kw = cin, cout, kh, kw
         w = torch.empty((cout, kh, kw, cin), dtype=torch.float32)
-        if stddev is not None:
+        if kernel_initializer is not None:
+            if callable(kernel_initializer):
+                kernel_initializer(w)
+            else:
+                w.fill_(float(kernel_initializer))
+        elif stddev is not None:
             truncated_normal_(w, stddev, gen)
         else:  # tf.layers default kernel initializer
             glorot_uniform_(w, cin * kh * kw, cout * kh * kw, gen)

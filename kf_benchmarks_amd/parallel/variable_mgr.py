@@ -86,6 +86,9 @@ class Strategy:
     def describe(self) -> str:
         return self.name
 
+    def close(self):
+        pass
+
 
 class IndependentStrategy(Strategy):
     name = "independent"

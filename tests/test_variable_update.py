@@ -1,0 +1,118 @@
+"""Analytic-oracle tests of every --variable_update mode (the role of
+tcb/benchmark_cnn_test.py:1236-1365 VariableUpdateTest and
+tcb/benchmark_cnn_distributed_test.py DistributedVariableUpdateTest).
+
+Single-process runs check the update rule; 2-rank gloo runs (one OS process
+per rank, rendezvous on 127.0.0.1) check the cross-worker aggregation."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import kfb_test_util as tu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("vu", ["parameter_server", "replicated", "independent", "horovod",
+                                "collective_all_reduce", "distributed_replicated",
+                                "distributed_all_reduce", "kungfu"])
+def test_single_worker_updates(vu):
+    params = tu.get_var_update_params(variable_update=vu)
+    losses, _ = tu.run_test_model(params)
+    expected = tu.manually_compute_losses(tu.get_fake_var_update_inputs(), 1, params, "sum")[0]
+    np.testing.assert_allclose(losses, expected, rtol=1e-5, atol=0)
+
+
+@pytest.mark.parametrize("opt", ["sgd", "momentum"])
+@pytest.mark.parametrize("loss_type", ["base_loss", "total_loss"])
+def test_optimizer_and_loss_type(opt, loss_type):
+    params = tu.get_var_update_params(optimizer=opt, loss_type_to_report=loss_type,
+                                      num_batches=6)
+    losses, _ = tu.run_test_model(params)
+    expected = tu.manually_compute_losses(tu.get_fake_var_update_inputs(), 1, params, "sum")[0]
+    np.testing.assert_allclose(losses, expected, rtol=1e-5, atol=0)
+
+
+def test_print_training_accuracy_columns():
+    params = tu.get_var_update_params(print_training_accuracy=True)
+    _, logs = tu.run_test_model(params)
+    outs = tu.get_training_outputs_from_logs(logs, True)
+    assert len(outs) == params.num_batches
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def run_workers(nworkers, flag_kwargs, tmp_path, timeout=240):
+    """Launch nworkers processes of tests/dist_worker.py; returns per-rank losses."""
+    port = _free_port()
+    procs = []
+    for r in range(nworkers):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(nworkers), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1",
+                   PYTHONPATH=ROOT + os.pathsep + os.path.join(ROOT, "tests"))
+        out = tmp_path / ("rank%d.json" % r)
+        cmd = [sys.executable, os.path.join(ROOT, "tests", "dist_worker.py"), str(out),
+               json.dumps(flag_kwargs)]
+        procs.append((subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE,
+                                       stderr=subprocess.STDOUT, text=True), out))
+    results = []
+    for p, out in procs:
+        try:
+            log, _ = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q, _ in procs:
+                q.kill()
+            raise
+        assert p.returncode == 0, log
+        with open(out) as f:
+            results.append(json.load(f))
+    return results
+
+
+@pytest.mark.parametrize("vu,kopt,agg", [("parameter_server", None, "sum"),
+                                         ("replicated", None, "sum"),
+                                         ("horovod", None, "sum"),
+                                         ("independent", None, "none"),
+                                         ("kungfu", "sync_sgd", "mean")])
+def test_two_workers(vu, kopt, agg, tmp_path):
+    kw = dict(variable_update=vu, num_batches=4)
+    if kopt:
+        kw["kungfu_option"] = kopt
+    res = run_workers(2, kw, tmp_path)
+    params = tu.get_var_update_params(**kw)
+    expected = tu.manually_compute_losses(tu.get_fake_var_update_inputs(), 2, params, agg)
+    for r in range(2):
+        np.testing.assert_allclose(res[r]["losses"], expected[r], rtol=1e-5, atol=0)
+
+
+def test_two_workers_sma_keeps_models_close(tmp_path):
+    """kungfu sma: models are pulled toward the average every step, so the two
+    workers' variables end closer than with independent training."""
+    sma = run_workers(2, dict(variable_update="kungfu", kungfu_option="sma", num_batches=6,
+                              kungfu_sma_alpha=0.5), tmp_path)
+    ind = run_workers(2, dict(variable_update="independent", num_batches=6), tmp_path)
+    d_sma = np.abs(np.array(sma[0]["vars"]) - np.array(sma[1]["vars"])).sum()
+    d_ind = np.abs(np.array(ind[0]["vars"]) - np.array(ind[1]["vars"])).sum()
+    assert d_sma < d_ind
+
+
+def test_two_workers_async_pair_averaging(tmp_path):
+    """kungfu async_sgd (PairAveraging): every worker trains and publishes;
+    models stay finite and the run completes without a global barrier per step."""
+    res = run_workers(2, dict(variable_update="kungfu", kungfu_option="async_sgd",
+                              num_batches=6), tmp_path)
+    for r in res:
+        assert len(r["losses"]) == 6
+        assert all(np.isfinite(r["losses"]))
