@@ -566,6 +566,8 @@ class BenchmarkCNN:
             self.saver.save(p.train_dir, self.global_step)
         tracer.finish()
         self.strategy.close()
+        if self.summary_writer is not None:
+            self.summary_writer.close()
         if p.variable_update == "kungfu" or p.sync_on_finish:
             self.world.barrier(self.device if self.device_type == "cuda" else None)
         if last_loss is None and loss is not None:

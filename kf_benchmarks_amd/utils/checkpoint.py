@@ -138,7 +138,9 @@ def _to_numpy(t) -> Tuple[np.ndarray, int]:
             return a, _DT_BF16
         a = t.cpu().contiguous().numpy()
     else:
-        a = np.ascontiguousarray(t)
+        a = np.asarray(t)
+        if not a.flags["C_CONTIGUOUS"]:
+            a = a.copy(order="C")  # (np.ascontiguousarray would turn scalars 1-d)
     return a, _DT[a.dtype]
 
 
@@ -185,7 +187,7 @@ def read_bundle(prefix: str, verify: bool = True) -> Dict[str, np.ndarray]:
             a = torch.frombuffer(bytearray(raw), dtype=torch.bfloat16).float().numpy()
         else:
             a = np.frombuffer(raw, dtype=_NP[dtype]).copy()
-        out[key.decode()] = a.reshape(shape)
+        out[key.decode()] = a.reshape(tuple(shape))
     return out
 
 
