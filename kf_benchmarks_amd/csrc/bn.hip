@@ -350,7 +350,8 @@ KFB_API hipError_t kfb_bn_fwd_train(int dtype, const void* x, const void* res, v
                                     int C, const float* gamma, const float* beta, float decay,
                                     float eps, float* run_mean, float* run_var, float* save_mean,
                                     float* save_invstd, float* scale, float* shift, float* psum,
-                                    float* psq, int nslab, int relu, hipStream_t stream) {
+                                    float* psq, int nslab, int relu, int have_partials,
+                                    hipStream_t stream) {
   const int V = vec_width(C);
   KFB_DISPATCH_DTYPE(dtype, T, {
     KFB_DISPATCH_VEC(V, VV, {
@@ -358,8 +359,9 @@ KFB_API hipError_t kfb_bn_fwd_train(int dtype, const void* x, const void* res, v
       const long slab_rows = (rows + nslab - 1) / nslab;
       dim3 grid(nslab, g.nchunk);
       const size_t lds = 2 * (size_t)g.rpi * g.tpr * VV * sizeof(float);
-      hipLaunchKernelGGL((bn_partial_stats_k<T, VV>), grid, dim3(BN_THREADS), lds, stream,
-                         (const T*)x, rows, C, g.cw, g.tpr, g.rpi, slab_rows, psum, psq);
+      if (!have_partials)  // else the producing conv's epilogue already summed y, y^2
+        hipLaunchKernelGGL((bn_partial_stats_k<T, VV>), grid, dim3(BN_THREADS), lds, stream,
+                           (const T*)x, rows, C, g.cw, g.tpr, g.rpi, slab_rows, psum, psq);
       hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, 4), 0, stream, psum,
                          psq, nslab, C, rows, gamma, beta, decay, eps, run_mean, run_var,
                          save_mean, save_invstd, scale, shift);
@@ -425,15 +427,19 @@ KFB_API hipError_t kfb_bn_bwd(int dtype, const void* dy, const void* y, const vo
                               const float* save_mean, const float* save_invstd, float* dgamma,
                               float* dbeta, float* pdy, float* pdyx, int nslab, float* coefA,
                               float* coefB, float* coefC, int relu, int accumulate,
-                              hipStream_t stream) {
+                              int have_partials, hipStream_t stream) {
   const int V = vec_width(C);
+  // have_partials: dy arrives already ReLU-masked and its partial sums were
+  // produced by the consuming conv's dgrad epilogue.
+  if (have_partials) relu = 0;
   KFB_DISPATCH_DTYPE(dtype, T, {
     KFB_DISPATCH_VEC(V, VV, {
       Geo g = make_geo<VV>(C);
       const long slab_rows = (rows + nslab - 1) / nslab;
       dim3 grid(nslab, g.nchunk);
       const size_t lds = 2 * (size_t)g.rpi * g.tpr * VV * sizeof(float);
-      if (relu)
+      if (have_partials) {
+      } else if (relu)
         hipLaunchKernelGGL((bn_partial_grad_k<T, VV, true>), grid, dim3(BN_THREADS), lds, stream,
                            (const T*)dy, (const T*)y, (const T*)x, save_mean, rows, C, g.cw,
                            g.tpr, g.rpi, slab_rows, pdy, pdyx);

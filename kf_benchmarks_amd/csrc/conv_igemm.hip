@@ -58,9 +58,22 @@ struct IgArgs {
   int KH, KW, sh, sw, pt, pl;
   int Ncol, Ktot, M;
   int YH, YW, ys, ldy;  // row m=(img,oh,ow) -> ((img*YH + oh*ys)*YW + ow*ys)*ldy
+  // Fused epilogue (optional):
+  //   stats != null, mask == null : BN forward statistics of the output,
+  //       stats[slot][0][n] += sum y, stats[slot][1][n] += sum y^2
+  //   stats != null, xbn != null  : BN backward partials of the *producer* BN
+  //       of this conv's input: y' = y * (mask > 0) (mask may be null = no
+  //       ReLU), stats[slot][0][n] += sum y', stats[slot][1][n] += sum y'(xbn - mean)
+  //   layout [2][IG_SPREAD][Ncol]; slot = workgroup % IG_SPREAD (spreads the
+  //   atomics over 32 copies; the BN finalize folds the 32 slots).
+  float* stats;
+  const void* mask;
+  const void* xbn;
+  const float* mean;
 };
 
 constexpr int IG_BK = 64;
+constexpr int IG_SPREAD = 32;
 
 __device__ __forceinline__ int swz_off(int row, int chunk) {
   // element offset of 16-byte chunk `chunk` (0..7) of 128-byte row `row`
@@ -205,6 +218,9 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
   }
   __syncthreads();
   const bool dense = (a.ys == 1 && a.YH == a.OH && a.YW == a.OW);
+  float s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
 #pragma unroll
   for (int pass = 0; pass < BM * CPR / 256; ++pass) {
     const int t = tid + pass * 256;
@@ -219,7 +235,64 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
       const int oh = rem / a.OW, ow = rem - oh * a.OW;
       rowoff = ((long)(img * a.YH + oh * a.ys) * a.YW + ow * a.ys) * a.ldy;
     }
-    *(uint4*)(y + rowoff + n) = *(const uint4*)(cs + ml * BN + ((ch ^ (ml & (CPR - 1))) * 8));
+    const uint4 raw = *(const uint4*)(cs + ml * BN + ((ch ^ (ml & (CPR - 1))) * 8));
+    if (!a.stats) {
+      *(uint4*)(y + rowoff + n) = raw;
+      continue;
+    }
+    float v[8];
+    {
+      Vec<T, 8> tv = __builtin_bit_cast(Vec<T, 8>, raw);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = (float)tv.v[k];
+    }
+    if (a.xbn) {
+      if (a.mask) {
+        float mk[8];
+        load_vec<T, 8>((const T*)a.mask + rowoff + n, mk);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = mk[k] > 0.f ? v[k] : 0.f;
+      }
+      float xb[8];
+      load_vec<T, 8>((const T*)a.xbn + rowoff + n, xb);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s1[k] += v[k];
+        s2[k] += v[k] * (xb[k] - a.mean[n + k]);
+      }
+      store_vec<T, 8>(y + rowoff + n, v);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s1[k] += v[k];
+        s2[k] += v[k] * v[k];
+      }
+      *(uint4*)(y + rowoff + n) = raw;
+    }
+  }
+  if (a.stats) {
+    // Fold the per-thread sums of threads sharing a chunk column, then one
+    // atomic add per channel per workgroup into a spread slot.
+    __syncthreads();
+    float* red = (float*)smem;  // [256/CPR][CPR][16]
+    const int ch = tid % CPR, rg = tid / CPR;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[(rg * CPR + ch) * 16 + k] = s1[k];
+      red[(rg * CPR + ch) * 16 + 8 + k] = s2[k];
+    }
+    __syncthreads();
+    constexpr int RG = 256 / CPR;
+    if (tid < CPR * 16) {
+      const int c = tid / 16, k = tid % 16;
+      float acc2 = 0.f;
+      for (int r = 0; r < RG; ++r) acc2 += red[(r * CPR + c) * 16 + k];
+      const int n = n0 + c * 8 + (k & 7);
+      if (n < a.Ncol) {
+        float* dst = a.stats + ((long)(k >> 3) * IG_SPREAD + blockIdx.x % IG_SPREAD) * a.Ncol + n;
+        atomicAdd(dst, acc2);
+      }
+    }
   }
 }
 
@@ -404,10 +477,11 @@ using namespace kfb;
 KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void* y, int N, int H,
                                   int W, int C, int OH, int OW, int KH, int KW, int sh, int sw,
                                   int pt, int pl, int Ncol, int YH, int YW, int ys, int ldy,
-                                  int trans, hipStream_t stream) {
+                                  int trans, float* stats, const void* mask, const void* xbn,
+                                  const float* mean, hipStream_t stream) {
   if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
   IgArgs a{x, w, y, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
-           N * OH * OW, YH, YW, ys, ldy};
+           N * OH * OW, YH, YW, ys, ldy, stats, mask, xbn, mean};
   const bool t = trans != 0;
   if (dtype == BF16) {
     if (Ncol <= 64) launch_ig<bf16, 128, 64>(a, t, stream);
@@ -420,6 +494,8 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
   }
   return hipGetLastError();
 }
+
+KFB_API int kfb_conv_stats_spread() { return IG_SPREAD; }
 
 // Weight gradient: dw [Ncol][KH*KW*C] fp32 must be zeroed by the caller.
 KFB_API hipError_t kfb_conv_wgrad(int dtype, const void* dy, const void* x, float* dw, int N,

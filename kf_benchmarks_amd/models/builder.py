@@ -24,6 +24,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..ops import conv as conv_ops
 from ..ops import nn as F
 from .layers import AffineLayer, BatchNormLayer, ConvLayer
 
@@ -64,6 +65,17 @@ class ConvNetBuilder:
     def _layer(self, scope, factory):
         return self.net.get_or_create(scope, factory)
 
+    @staticmethod
+    def _use(t, conv=False):
+        """Count a consumer of a BN output (see ops.nn.BNLink): the conv
+        dgrad/BN-backward fusion needs the BN output to feed exactly one conv."""
+        link = getattr(t, "_kfb_bn_link", None) if t is not None else None
+        if link is not None:
+            if conv:
+                link.uses += 1
+            else:
+                link.other = True
+
     @contextlib.contextmanager
     def switch_to_aux_top_layer(self):
         if self.aux_top_layer is None:
@@ -91,16 +103,24 @@ class ConvNetBuilder:
         layer = self._layer(scope, lambda: ConvLayer(
             scope, cin, num_out_channels, k_height, k_width, use_bias, bias or 0.0, stddev,
             self.net.init_gen, self.net.param_device, kernel_initializer))
+        self._use(x, conv=True)
+        self._use(residual)
         _, H, W, _ = x.shape
         pads = F.resolve_pads(mode, H, W, k_height, k_width, d_height, d_width)
         w = self._p(layer.weight)
+        stats = None
+        if use_batch_norm and self.phase_train and not self.meta and \
+                conv_ops.fills_bn_stats(x, num_out_channels, self.impl):
+            from ..ops import conv_hip
+            stats = conv_hip.stats_buffer(num_out_channels, x.device)
         y = F.conv2d(x, w, None if self.meta else layer.weight_lp, (d_height, d_width), pads,
-                     self.impl)
+                     self.impl, stats)
         relu = activation == "relu"
         if use_batch_norm:
             with self.scope(name):
                 self.top_layer, self.top_size = y, num_out_channels
-                y = self.batch_norm(relu=relu, residual=residual, **self.batch_norm_config)
+                y = self._batch_norm(y, relu=relu, residual=residual, stats=stats,
+                                     **self.batch_norm_config)
             if activation not in ("relu", None, "linear"):
                 y = F.activation(y, activation)
         else:
@@ -119,6 +139,7 @@ class ConvNetBuilder:
             input_layer = self.top_layer
         else:
             self.top_size = num_channels_in
+        self._use(input_layer)
         self.counts[pool_name] += 1
         fn = F.max_pool if pool_name == "mpool" else F.avg_pool
         y = fn(input_layer, k_height, k_width, d_height, d_width, mode)
@@ -138,6 +159,7 @@ class ConvNetBuilder:
     # ----------------------------------------------------------------- shape
     def reshape(self, shape, input_layer=None):
         x = self.top_layer if input_layer is None else input_layer
+        self._use(x)
         self.top_layer = x.reshape(shape)
         self.top_size = shape[-1]
         return self.top_layer
@@ -146,6 +168,7 @@ class ConvNetBuilder:
         """Flatten NHWC to [N, H*W*C] (the reference reshapes NCHW tensors;
         element order therefore differs but the layer is equivalent)."""
         x = self.top_layer
+        self._use(x)
         n = x.shape[0]
         size = int(np.prod(x.shape[1:]))
         self.top_layer = x.reshape(n, size)
@@ -156,6 +179,7 @@ class ConvNetBuilder:
     def affine(self, num_out_channels, input_layer=None, num_channels_in=None, bias=0.0,
                stddev=None, activation="relu"):
         x = self.top_layer if input_layer is None else input_layer
+        self._use(x)
         cin = self.top_size if num_channels_in is None else num_channels_in
         name = "affine%d" % self.counts["affine"]
         self.counts["affine"] += 1
@@ -198,18 +222,22 @@ class ConvNetBuilder:
                         raise KeyError("Invalid layer type for inception module: '%s'" % ltype)
                     col_layers[c].append(self.top_layer)
                     col_sizes[c].append(self.top_size)
+            for l in col_layers:
+                self._use(l[-1])
             self.top_layer = F.concat_channels([l[-1] for l in col_layers])
             self.top_size = sum(s[-1] for s in col_sizes)
         return self.top_layer
 
     # ----------------------------------------------------------------- misc
     def spatial_mean(self, keep_dims=False):
+        self._use(self.top_layer)
         self.counts["spatial_mean"] += 1
         self.top_layer = F.spatial_mean(self.top_layer, keep_dims)
         return self.top_layer
 
     def dropout(self, keep_prob=0.5, input_layer=None):
         x = self.top_layer if input_layer is None else input_layer
+        self._use(x)
         if input_layer is not None:
             self.top_size = None
         self.counts["dropout"] += 1
@@ -220,6 +248,13 @@ class ConvNetBuilder:
     def batch_norm(self, input_layer=None, decay=0.999, scale=False, epsilon=0.001, relu=False,
                    residual=None):
         x = self.top_layer if input_layer is None else input_layer
+        return self._batch_norm(x, decay=decay, scale=scale, epsilon=epsilon, relu=relu,
+                                residual=residual)
+
+    def _batch_norm(self, x, decay=0.999, scale=False, epsilon=0.001, relu=False,
+                    residual=None, stats=None):
+        self._use(x)
+        self._use(residual)
         name = "batchnorm%d" % self.counts["batchnorm"]
         self.counts["batchnorm"] += 1
         scope = self._scoped(name)
@@ -234,26 +269,32 @@ class ConvNetBuilder:
         else:
             y = F.batch_norm(x, layer.gamma, layer.beta, layer.moving_mean,
                              layer.moving_variance, layer.decay, layer.eps, training, relu,
-                             residual)
+                             residual, stats=stats if training else None)
         self.top_layer, self.top_size = y, C
         return y
 
     def relu(self, x=None):
         x = self.top_layer if x is None else x
+        self._use(x)
         self.top_layer = F.relu(x)
         return self.top_layer
 
     def add(self, a, b, relu=False):
+        self._use(a)
+        self._use(b)
         y = F.add(a, b, relu)
         self.top_layer = y
         return y
 
     def concat(self, xs):
+        for t in xs:
+            self._use(t)
         self.top_layer = F.concat_channels(xs)
         self.top_size = self.top_layer.shape[-1]
         return self.top_layer
 
     def lrn(self, depth_radius, bias, alpha, beta):
+        self._use(self.top_layer)
         self.counts["lrn"] += 1
         self.top_layer = F.lrn(self.top_layer, depth_radius, bias, alpha, beta)
         return self.top_layer

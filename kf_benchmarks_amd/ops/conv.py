@@ -55,13 +55,22 @@ def _hip_supported(x, w, stride, pads) -> bool:
     return conv_hip.supported(x, w, stride, pads)
 
 
-def conv2d(x, w, w_lp, stride, pads, impl="hip"):
+def fills_bn_stats(x, cout, impl="hip") -> bool:
+    """True when conv2d(..., stats=buf) fills ``buf`` with the BN partial sums
+    of its output (HIP implicit-GEMM path)."""
+    return (x.is_cuda and impl == "hip" and x.dtype in (torch.bfloat16, torch.float16)
+            and cout % 8 == 0)
+
+
+def conv2d(x, w, w_lp, stride, pads, impl="hip", stats=None):
+    """Returns y, or (y, stats_filled) when a stats buffer was requested and
+    the HIP kernel filled it (the caller passes it on to the BN)."""
     if not x.is_cuda:
         y = _torch_conv(x.float(), w, stride, pads)
         return y.to(x.dtype).contiguous()
     if impl == "hip" and _hip_supported(x, w, stride, pads):
         from . import conv_hip
-        return conv_hip.conv2d(x, w, w_lp, stride, pads)
+        return conv_hip.conv2d(x, w, w_lp, stride, pads, stats)
     # torch/MIOpen path on channels-last views; autograd routes the weight
     # gradient through the cast back to the fp32 master.
     wl = w.to(x.dtype)

@@ -18,8 +18,9 @@ import torch
 
 from . import _native as N
 
-_SIG = [N.I, N.P, N.P, N.P] + [N.I] * 17 + [N.I, N.P]
+_SIG = [N.I, N.P, N.P, N.P] + [N.I] * 17 + [N.I, N.P, N.P, N.P, N.P, N.P]
 N.register_optional("kfb_conv_igemm", _SIG)
+N.register_optional("kfb_conv_stats_spread", [], N.c_int)
 N.register_optional("kfb_conv_wgrad", [N.I, N.P, N.P, N.P] + [N.I] * 12 + [N.I, N.I, N.P])
 
 _WGRAD_TARGET_BLOCKS = 1024
@@ -33,14 +34,24 @@ def _pad8(n):
     return (n + 7) // 8 * 8
 
 
+STATS_SPREAD = 32  # must match IG_SPREAD in csrc/conv_igemm.hip
+
+
+def stats_buffer(channels, device):
+    """Zeroed [2][STATS_SPREAD][C] fp32 buffer for fused BN partial sums."""
+    return torch.zeros((2 * STATS_SPREAD * channels,), dtype=torch.float32, device=device)
+
+
 def _igemm(x, wmat, y, N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy,
-           trans):
+           trans, stats=None, mask=None, xbn=None, mean=None):
     N.call("kfb_conv_igemm", N.dt(x), x.data_ptr(), wmat.data_ptr(), y.data_ptr(), N_, H, W, C,
-           OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy, int(trans), N.stream(x.device))
+           OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy, int(trans), N.ptr(stats),
+           N.ptr(mask), N.ptr(xbn), N.ptr(mean), N.stream(x.device))
 
 
-def conv_fwd(x, wl, stride, pads):
-    """x [N,H,W,C] (C%8==0), wl [Cout,KH,KW,C] compute dtype -> y [N,OH,OW,Cout]."""
+def conv_fwd(x, wl, stride, pads, stats=None):
+    """x [N,H,W,C] (C%8==0), wl [Cout,KH,KW,C] compute dtype -> y [N,OH,OW,Cout].
+    ``stats``: optional zeroed stats_buffer(Cout) receiving sum(y), sum(y^2)."""
     n, H, W, C = x.shape
     cout, KH, KW, _ = wl.shape
     sh, sw = stride
@@ -48,12 +59,16 @@ def conv_fwd(x, wl, stride, pads):
     OH = (H + pt + pb - KH) // sh + 1
     OW = (W + pl + pr - KW) // sw + 1
     y = torch.empty((n, OH, OW, cout), dtype=x.dtype, device=x.device)
-    _igemm(x, wl, y, n, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, cout, OH, OW, 1, cout, False)
+    _igemm(x, wl, y, n, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, cout, OH, OW, 1, cout, False,
+           stats)
     return y
 
 
-def conv_dgrad(dy, wl, x_shape, stride, pads):
+def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None):
+    """``fuse`` = (stats, mask, xbn, mean): also apply the producer BN's ReLU
+    mask to dX and accumulate its backward partial sums (see BNLink)."""
     n, H, W, C = x_shape
+    fz = fuse if fuse is not None else (None, None, None, None)
     cout, KH, KW, _ = wl.shape
     _, OH, OW, _ = dy.shape
     sh, sw = stride
@@ -68,7 +83,7 @@ def conv_dgrad(dy, wl, x_shape, stride, pads):
         ys = sh if sh == sw else None
         if ys is None:
             return None
-        _igemm(dy, wt, dx, n, OH, OW, cout, OH, OW, 1, 1, 1, 1, 0, 0, C, H, W, ys, C, False)
+        _igemm(dy, wt, dx, n, OH, OW, cout, OH, OW, 1, 1, 1, 1, 0, 0, C, H, W, ys, C, False, *fz)
         return dx
     if sh == 1 and sw == 1 and KH - 1 - pt >= 0 and KH - 1 - pb >= 0 \
             and KW - 1 - pl >= 0 and KW - 1 - pr >= 0:
@@ -77,21 +92,24 @@ def conv_dgrad(dy, wl, x_shape, stride, pads):
         wf = wl.flip(1, 2).permute(3, 1, 2, 0).contiguous()  # [Cin][KH][KW][Cout]
         dx = torch.empty((n, H, W, C), dtype=dy.dtype, device=dy.device)
         _igemm(dy, wf, dx, n, OH, OW, cout, H, W, KH, KW, 1, 1, KH - 1 - pt, KW - 1 - pl, C,
-               H, W, 1, C, False)
+               H, W, 1, C, False, *fz)
         return dx
     wd = wl.permute(3, 1, 2, 0).contiguous()  # [Cin][KH][KW][Cout]
     dx = torch.empty((n, H, W, C), dtype=dy.dtype, device=dy.device)
-    _igemm(dy, wd, dx, n, OH, OW, cout, H, W, KH, KW, sh, sw, pt, pl, C, H, W, 1, C, True)
+    _igemm(dy, wd, dx, n, OH, OW, cout, H, W, KH, KW, sh, sw, pt, pl, C, H, W, 1, C, True, *fz)
     return dx
 
 
-def conv_wgrad(dy, x, w_shape, stride, pads):
+def conv_wgrad(dy, x, w_shape, stride, pads, out=None):
+    """Accumulates dW into ``out`` (fp32 [Cout,KH,KW,C], e.g. the parameter's
+    view of the zeroed flat gradient buffer) or into a fresh zeroed tensor."""
     cout, KH, KW, C = w_shape
     n, H, W, _ = x.shape
     _, OH, OW, _ = dy.shape
     sh, sw = stride
     pt, pb, pl, pr = pads
-    dw = torch.zeros((cout, KH, KW, C), dtype=torch.float32, device=x.device)
+    dw = out if out is not None else torch.zeros((cout, KH, KW, C), dtype=torch.float32,
+                                                 device=x.device)
     N.call("kfb_conv_wgrad", N.dt(x), dy.data_ptr(), x.data_ptr(), dw.data_ptr(), n, H, W, C, OH,
            OW, KH, KW, sh, sw, pt, pl, cout, _WGRAD_TARGET_BLOCKS, N.stream(x.device))
     return dw
@@ -99,7 +117,7 @@ def conv_wgrad(dy, x, w_shape, stride, pads):
 
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, wl, stride, pads):
+    def forward(ctx, x, w, wl, stride, pads, stats):
         x = x.contiguous()
         if wl is None or wl.dtype != x.dtype:
             wl = w.detach().to(x.dtype)
@@ -112,13 +130,16 @@ class _Conv2d(torch.autograd.Function):
             wp = torch.nn.functional.pad(wp, (0, cin_p - cin))
         if cout_p != cout:
             wp = torch.nn.functional.pad(wp, (0, 0, 0, 0, 0, 0, 0, cout_p - cout))
+            stats = None
         wp = wp.contiguous()
-        y = conv_fwd(xp, wp, stride, pads)
+        y = conv_fwd(xp, wp, stride, pads, stats)
         if cout_p != cout:
             y = y[..., :cout].contiguous()
         ctx.save_for_backward(xp, wp)
         ctx.meta = (stride, pads, cin, cout, x.shape)
         ctx.x_needs_grad = ctx.needs_input_grad[0]
+        ctx.w = w
+        ctx.link = getattr(x, "_kfb_bn_link", None) if cin_p == cin else None
         return y
 
     @staticmethod
@@ -131,18 +152,33 @@ class _Conv2d(torch.autograd.Function):
             dy = torch.nn.functional.pad(dy, (0, cout_p - cout))
         dx = None
         if ctx.x_needs_grad:
-            dx = conv_dgrad(dy, wp, xp.shape, stride, pads)
+            link = ctx.link
+            fuse = None
+            if link is not None and link.fusable:
+                parts = stats_buffer(cin, dy.device)
+                fuse = (parts, xp if link.relu else None, link.x_bn, link.mean)
+            dx = conv_dgrad(dy, wp, xp.shape, stride, pads, fuse)
             if dx is None:
                 raise NotImplementedError("anisotropic strided 1x1 dgrad")
+            if fuse is not None:
+                link.partials = fuse[0]
             if dx.shape[-1] != cin:
                 dx = dx[..., :cin].contiguous()
         dw = None
         if ctx.needs_input_grad[1]:
-            dw = conv_wgrad(dy, xp, wp.shape, stride, pads)
-            if dw.shape[0] != cout or dw.shape[-1] != cin:
+            w = ctx.w
+            sink = getattr(w, "_kfb_grad_sink", None)
+            direct = sink is not None and cout_p == cout and wp.shape[-1] == cin
+            dw = conv_wgrad(dy, xp, wp.shape, stride, pads, out=sink if direct else None)
+            if direct:
+                cb = getattr(w, "_kfb_ready_cb", None)
+                if cb is not None:
+                    cb(w)
+                dw = None
+            elif dw.shape[0] != cout or dw.shape[-1] != cin:
                 dw = dw[:cout, :, :, :cin].contiguous()
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
-def conv2d(x, w, wl, stride, pads):
-    return _Conv2d.apply(x, w, wl, tuple(stride), tuple(pads))
+def conv2d(x, w, wl, stride, pads, stats=None):
+    return _Conv2d.apply(x, w, wl, tuple(stride), tuple(pads), stats)

@@ -59,10 +59,12 @@ def resolve_pads(mode: str, H: int, W: int, kh: int, kw: int, sh: int, sw: int) 
 
 
 # ------------------------------------------------------------------------ conv
-def conv2d(x, w, w_lp, stride: Tuple[int, int], pads: Pads, impl: str = "hip"):
+def conv2d(x, w, w_lp, stride: Tuple[int, int], pads: Pads, impl: str = "hip",
+           stats: Optional[torch.Tensor] = None):
     """NHWC convolution, no bias.  ``w_lp`` is the compute-dtype copy of the
-    fp32 master ``w`` (None -> cast on the fly)."""
-    return _conv.conv2d(x, w, w_lp, stride, pads, impl)
+    fp32 master ``w`` (None -> cast on the fly).  ``stats`` (GPU): zeroed
+    [2*32*Cout] fp32 buffer that receives the BN statistics of the output."""
+    return _conv.conv2d(x, w, w_lp, stride, pads, impl, stats)
 
 
 # ------------------------------------------------------------------ batch norm
@@ -79,65 +81,127 @@ def _bn_cpu(x, gamma, beta, residual, rm, rv, decay, eps, relu, training):
     return y.to(x.dtype).contiguous()
 
 
+class BNLink:
+    """Ties a training-mode BN to the single conv that consumes its output so
+    the conv's dgrad epilogue can apply the BN's ReLU mask and produce the BN
+    backward partial sums (csrc/conv_igemm.hip fused epilogue).  ``uses`` /
+    ``other`` are counted by the ConvNetBuilder; fusion happens only when the
+    BN output feeds exactly one conv and nothing else."""
+
+    __slots__ = ("x_bn", "mean", "relu", "uses", "other", "partials")
+
+    def __init__(self, x_bn, mean, relu):
+        self.x_bn, self.mean, self.relu = x_bn, mean, relu
+        self.uses, self.other, self.partials = 0, False, None
+
+    @property
+    def fusable(self):
+        return self.uses == 1 and not self.other
+
+
+def _grad_sink(p):
+    """The flat-buffer gradient view of a FlatParams-managed parameter (the
+    kernels accumulate straight into it), or None."""
+    return getattr(p, "_kfb_grad_sink", None) if p is not None else None
+
+
+def _grad_ready(p):
+    cb = getattr(p, "_kfb_ready_cb", None)
+    if cb is not None:
+        cb(p)
+
+
 class _BatchNormTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, residual, rm, rv, decay, eps, relu):
+    def forward(ctx, x, gamma, beta, residual, rm, rv, decay, eps, relu, stats):
         x = x.contiguous()
         C = x.shape[-1]
         rows = x.numel() // C
         dev = x.device
-        nslab = N.query("kfb_bn_num_slabs", rows, C)
-        ws = torch.empty((2 * nslab * C + 4 * C,), dtype=torch.float32, device=dev)
-        psum, psq = ws[:nslab * C], ws[nslab * C:2 * nslab * C]
-        stats = torch.empty((2, C), dtype=torch.float32, device=dev)  # mean, invstd
-        coef = ws[2 * nslab * C:2 * nslab * C + 2 * C]
+        if stats is not None:  # partial sums from the producing conv's epilogue
+            nslab = stats.numel() // (2 * C)
+            psum, psq = stats[:nslab * C], stats[nslab * C:]
+            ws = torch.empty((4 * C,), dtype=torch.float32, device=dev)
+            coef = ws[:2 * C]
+        else:
+            nslab = N.query("kfb_bn_num_slabs", rows, C)
+            ws = torch.empty((2 * nslab * C + 4 * C,), dtype=torch.float32, device=dev)
+            psum, psq = ws[:nslab * C], ws[nslab * C:2 * nslab * C]
+            coef = ws[2 * nslab * C:2 * nslab * C + 2 * C]
+        st = torch.empty((2, C), dtype=torch.float32, device=dev)  # mean, invstd
         y = torch.empty_like(x)
         res = residual.contiguous() if residual is not None else None
         N.call("kfb_bn_fwd_train", N.dt(x), x.data_ptr(), N.ptr(res), y.data_ptr(), rows, C,
                N.ptr(gamma), N.ptr(beta), float(decay), float(eps), N.ptr(rm), N.ptr(rv),
-               stats[0].data_ptr(), stats[1].data_ptr(), coef[:C].data_ptr(),
+               st[0].data_ptr(), st[1].data_ptr(), coef[:C].data_ptr(),
                coef[C:].data_ptr(), psum.data_ptr(), psq.data_ptr(), nslab, int(relu),
-               N.stream(dev))
-        ctx.save_for_backward(x, y if relu else None, gamma, stats)
+               int(stats is not None), N.stream(dev))
+        ctx.save_for_backward(x, y if relu else None, gamma, st)
         ctx.relu = relu
         ctx.has_res = residual is not None
-        ctx.has_gamma = gamma is not None
+        ctx.gamma, ctx.beta = gamma, beta
+        link = None
+        if residual is None:
+            link = BNLink(x, st[0], relu)
+            y._kfb_bn_link = link
+        ctx.link = link
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, gamma, stats = ctx.saved_tensors
+        x, y, gamma, st = ctx.saved_tensors
         dy = dy.contiguous()
         C = x.shape[-1]
         rows = x.numel() // C
         dev = x.device
-        nslab = N.query("kfb_bn_num_slabs", rows, C)
-        ws = torch.empty((2 * nslab * C + 3 * C,), dtype=torch.float32, device=dev)
-        pdy, pdyx = ws[:nslab * C], ws[nslab * C:2 * nslab * C]
-        coef = ws[2 * nslab * C:]
-        dparams = torch.empty((2, C), dtype=torch.float32, device=dev)
+        link = ctx.link
+        pre = link is not None and link.partials is not None
+        if pre:
+            parts = link.partials
+            nslab = parts.numel() // (2 * C)
+            pdy, pdyx = parts[:nslab * C], parts[nslab * C:]
+            coef = torch.empty((3 * C,), dtype=torch.float32, device=dev)
+            link.partials = None
+        else:
+            nslab = N.query("kfb_bn_num_slabs", rows, C)
+            ws = torch.empty((2 * nslab * C + 3 * C,), dtype=torch.float32, device=dev)
+            pdy, pdyx = ws[:nslab * C], ws[nslab * C:2 * nslab * C]
+            coef = ws[2 * nslab * C:]
+        gsink, bsink = _grad_sink(ctx.gamma), _grad_sink(ctx.beta)
+        direct = bsink is not None and (ctx.gamma is None or gsink is not None)
+        if direct:
+            dgp, dbp = N.ptr(gsink), bsink.data_ptr()
+        else:
+            dparams = torch.empty((2, C), dtype=torch.float32, device=dev)
+            dgp, dbp = dparams[0].data_ptr(), dparams[1].data_ptr()
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if ctx.has_res else None
         N.call("kfb_bn_bwd", N.dt(x), dy.data_ptr(), N.ptr(y), x.data_ptr(), dx.data_ptr(),
-               N.ptr(dres), rows, C, N.ptr(gamma), stats[0].data_ptr(), stats[1].data_ptr(),
-               dparams[0].data_ptr(), dparams[1].data_ptr(), pdy.data_ptr(), pdyx.data_ptr(),
+               N.ptr(dres), rows, C, N.ptr(gamma), st[0].data_ptr(), st[1].data_ptr(),
+               dgp, dbp, pdy.data_ptr(), pdyx.data_ptr(),
                nslab, coef[:C].data_ptr(), coef[C:2 * C].data_ptr(), coef[2 * C:].data_ptr(),
-               int(ctx.relu), 0, N.stream(dev))
-        dgamma = dparams[0] if ctx.has_gamma else None
-        return dx, dgamma, dparams[1], dres, None, None, None, None, None
+               int(ctx.relu), int(direct), int(pre), N.stream(dev))
+        if direct:
+            _grad_ready(ctx.gamma)
+            _grad_ready(ctx.beta)
+            return dx, None, None, dres, None, None, None, None, None, None
+        dgamma = dparams[0] if ctx.gamma is not None else None
+        return dx, dgamma, dparams[1], dres, None, None, None, None, None, None
 
 
 def batch_norm(x, gamma: Optional[torch.Tensor], beta: torch.Tensor,
                running_mean: torch.Tensor, running_var: torch.Tensor, decay: float, eps: float,
-               training: bool, relu: bool = False, residual: Optional[torch.Tensor] = None):
+               training: bool, relu: bool = False, residual: Optional[torch.Tensor] = None,
+               stats: Optional[torch.Tensor] = None):
     """y = relu?(bn(x) + residual?).  ``gamma=None`` means scale=False
-    (constant 1, tcb/convnet_builder.py:437-438 default)."""
+    (constant 1, tcb/convnet_builder.py:437-438 default).  ``stats``: the
+    [2][32][C] partial sums the producing conv kernel already accumulated."""
     if not _on_gpu(x):
         return _bn_cpu(x, gamma, beta, residual, running_mean, running_var, decay, eps, relu,
                        training)
     if training:
         return _BatchNormTrain.apply(x, gamma, beta, residual, running_mean, running_var,
-                                     decay, eps, relu)
+                                     decay, eps, relu, stats)
     return _bn_infer_gpu(x, gamma, beta, residual, running_mean, running_var, eps, relu)
 
 

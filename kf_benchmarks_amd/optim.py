@@ -48,6 +48,9 @@ class FlatParams:
             self.flat[o:o + n].copy_(p.detach().reshape(-1))
             p.data = self.flat[o:o + n].view(p.shape)
             p.grad = self.grad[o:o + n].view(p.shape)
+            # GPU kernels (conv wgrad, BN dgamma/dbeta) accumulate straight into
+            # this view and skip autograd's AccumulateGrad (see ops/conv_hip.py).
+            p._kfb_grad_sink = p.grad
         self.lp_dtype = lp_dtype if lp_dtype not in (None, torch.float32) else None
         self.lp = None
         if self.lp_dtype is not None:

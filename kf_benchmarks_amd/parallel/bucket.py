@@ -64,6 +64,8 @@ class BucketReducer:
         if overlap:
             for _, p, _, _ in segs:
                 self._handles.append(p.register_post_accumulate_grad_hook(self._hook))
+                # kernels that write the flat gradient directly notify through this
+                p._kfb_ready_cb = self._hook
 
     @property
     def num_buckets(self):
@@ -120,3 +122,6 @@ class BucketReducer:
         for h in self._handles:
             h.remove()
         self._handles = []
+        for _, p, _, _ in self.flat.segments():
+            if getattr(p, "_kfb_ready_cb", None) == self._hook:
+                p._kfb_ready_cb = None
