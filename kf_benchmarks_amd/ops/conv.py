@@ -14,6 +14,7 @@ Implementations:
 
 from __future__ import annotations
 
+import os
 from typing import Tuple
 
 import torch
@@ -55,11 +56,14 @@ def _hip_supported(x, w, stride, pads) -> bool:
     return conv_hip.supported(x, w, stride, pads)
 
 
+FUSE_BN = os.environ.get("KFB_DISABLE_FUSION", "0") != "1"
+
+
 def fills_bn_stats(x, cout, impl="hip") -> bool:
     """True when conv2d(..., stats=buf) fills ``buf`` with the BN partial sums
     of its output (HIP implicit-GEMM path)."""
-    return (x.is_cuda and impl == "hip" and x.dtype in (torch.bfloat16, torch.float16)
-            and cout % 8 == 0)
+    return (FUSE_BN and x.is_cuda and impl == "hip"
+            and x.dtype in (torch.bfloat16, torch.float16) and cout % 8 == 0)
 
 
 def conv2d(x, w, w_lp, stride, pads, impl="hip", stats=None):

@@ -30,6 +30,11 @@ def supported(x, w, stride, pads) -> bool:
     return x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.dim() == 4
 
 
+def _fuse_enabled():
+    from .conv import FUSE_BN
+    return FUSE_BN
+
+
 def _pad8(n):
     return (n + 7) // 8 * 8
 
@@ -154,7 +159,7 @@ class _Conv2d(torch.autograd.Function):
         if ctx.x_needs_grad:
             link = ctx.link
             fuse = None
-            if link is not None and link.fusable:
+            if link is not None and link.fusable and _fuse_enabled():
                 parts = stats_buffer(cin, dy.device)
                 fuse = (parts, xp if link.relu else None, link.x_bn, link.mean)
             dx = conv_dgrad(dy, wp, xp.shape, stride, pads, fuse)
@@ -168,7 +173,8 @@ class _Conv2d(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             w = ctx.w
             sink = getattr(w, "_kfb_grad_sink", None)
-            direct = sink is not None and cout_p == cout and wp.shape[-1] == cin
+            direct = (sink is not None and cout_p == cout and wp.shape[-1] == cin
+                      and _fuse_enabled())
             dw = conv_wgrad(dy, xp, wp.shape, stride, pads, out=sink if direct else None)
             if direct:
                 cb = getattr(w, "_kfb_ready_cb", None)

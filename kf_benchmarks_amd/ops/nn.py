@@ -168,7 +168,8 @@ class _BatchNormTrain(torch.autograd.Function):
             pdy, pdyx = ws[:nslab * C], ws[nslab * C:2 * nslab * C]
             coef = ws[2 * nslab * C:]
         gsink, bsink = _grad_sink(ctx.gamma), _grad_sink(ctx.beta)
-        direct = bsink is not None and (ctx.gamma is None or gsink is not None)
+        direct = bsink is not None and (ctx.gamma is None or gsink is not None) and \
+            _conv.FUSE_BN
         if direct:
             dgp, dbp = N.ptr(gsink), bsink.data_ptr()
         else:
