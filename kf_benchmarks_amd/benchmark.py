@@ -351,6 +351,10 @@ class BenchmarkCNN:
                            kernel_impl=p.kernel_impl, seed=seed)
         lp = self.compute_dtype if self.compute_dtype != torch.float32 else None
         self.flat = optim.FlatParams(self.net, lp)
+        if self.device_type == "cuda" and lp is not None and p.kernel_impl == "hip":
+            from .ops.conv_hip import DgradWeights
+            dgw = DgradWeights(self.net, self.flat)
+            self.flat.add_update_hook(dgw.run)
         self.optimizer = optim.FusedOptimizer(
             self.flat, p.optimizer, momentum=p.momentum, rmsprop_decay=p.rmsprop_decay,
             rmsprop_momentum=p.rmsprop_momentum, rmsprop_epsilon=p.rmsprop_epsilon,

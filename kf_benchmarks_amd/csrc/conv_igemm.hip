@@ -70,6 +70,10 @@ struct IgArgs {
   const void* mask;
   const void* xbn;
   const float* mean;
+  // addend != null: y = conv(...) + addend (same layout as y) before the
+  // mask / statistics - the gradient other consumers of the conv input
+  // already produced (residual / second-branch accumulation).
+  const void* addend;
 };
 
 constexpr int IG_BK = 64;
@@ -236,7 +240,7 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
       rowoff = ((long)(img * a.YH + oh * a.ys) * a.YW + ow * a.ys) * a.ldy;
     }
     const uint4 raw = *(const uint4*)(cs + ml * BN + ((ch ^ (ml & (CPR - 1))) * 8));
-    if (!a.stats) {
+    if (!a.stats && !a.addend) {
       *(uint4*)(y + rowoff + n) = raw;
       continue;
     }
@@ -245,6 +249,16 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
       Vec<T, 8> tv = __builtin_bit_cast(Vec<T, 8>, raw);
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = (float)tv.v[k];
+    }
+    if (a.addend) {
+      float ad[8];
+      load_vec<T, 8>((const T*)a.addend + rowoff + n, ad);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += ad[k];
+      if (!a.stats) {
+        store_vec<T, 8>(y + rowoff + n, v);
+        continue;
+      }
     }
     if (a.xbn) {
       if (a.mask) {
@@ -267,7 +281,8 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
         s1[k] += v[k];
         s2[k] += v[k] * v[k];
       }
-      *(uint4*)(y + rowoff + n) = raw;
+      if (a.addend) store_vec<T, 8>(y + rowoff + n, v);
+      else *(uint4*)(y + rowoff + n) = raw;
     }
   }
   if (a.stats) {
@@ -478,10 +493,10 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
                                   int W, int C, int OH, int OW, int KH, int KW, int sh, int sw,
                                   int pt, int pl, int Ncol, int YH, int YW, int ys, int ldy,
                                   int trans, float* stats, const void* mask, const void* xbn,
-                                  const float* mean, hipStream_t stream) {
+                                  const float* mean, const void* addend, hipStream_t stream) {
   if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
   IgArgs a{x, w, y, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
-           N * OH * OW, YH, YW, ys, ldy, stats, mask, xbn, mean};
+           N * OH * OW, YH, YW, ys, ldy, stats, mask, xbn, mean, addend};
   const bool t = trans != 0;
   if (dtype == BF16) {
     if (Ncol <= 64) launch_ig<bf16, 128, 64>(a, t, stream);

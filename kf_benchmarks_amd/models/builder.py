@@ -66,13 +66,15 @@ class ConvNetBuilder:
         return self.net.get_or_create(scope, factory)
 
     @staticmethod
-    def _use(t, conv=False):
-        """Count a consumer of a BN output (see ops.nn.BNLink): the conv
-        dgrad/BN-backward fusion needs the BN output to feed exactly one conv."""
+    def _use(t, conv=False, resid=False):
+        """Count a consumer of a BN output (see ops.nn.BNLink): the fused BN
+        backward needs every consumer to be a conv or a residual-adding BN."""
         link = getattr(t, "_kfb_bn_link", None) if t is not None else None
         if link is not None:
             if conv:
-                link.uses += 1
+                link.convs += 1
+            elif resid:
+                link.resid += 1
             else:
                 link.other = True
 
@@ -103,8 +105,9 @@ class ConvNetBuilder:
         layer = self._layer(scope, lambda: ConvLayer(
             scope, cin, num_out_channels, k_height, k_width, use_bias, bias or 0.0, stddev,
             self.net.init_gen, self.net.param_device, kernel_initializer))
-        self._use(x, conv=True)
-        self._use(residual)
+        self._use(x, conv=conv_ops.runs_hip_kernel(x, self.impl))
+        if residual is not None and not use_batch_norm:
+            self._use(residual)
         _, H, W, _ = x.shape
         pads = F.resolve_pads(mode, H, W, k_height, k_width, d_height, d_width)
         w = self._p(layer.weight)
@@ -113,8 +116,9 @@ class ConvNetBuilder:
                 conv_ops.fills_bn_stats(x, num_out_channels, self.impl):
             from ..ops import conv_hip
             stats = conv_hip.stats_buffer(num_out_channels, x.device)
+        layer.stride = (d_height, d_width)
         y = F.conv2d(x, w, None if self.meta else layer.weight_lp, (d_height, d_width), pads,
-                     self.impl, stats)
+                     self.impl, stats, None if self.meta else layer.weight_t)
         relu = activation == "relu"
         if use_batch_norm:
             with self.scope(name):
@@ -254,7 +258,7 @@ class ConvNetBuilder:
     def _batch_norm(self, x, decay=0.999, scale=False, epsilon=0.001, relu=False,
                     residual=None, stats=None):
         self._use(x)
-        self._use(residual)
+        self._use(residual, resid=True)
         name = "batchnorm%d" % self.counts["batchnorm"]
         self.counts["batchnorm"] += 1
         scope = self._scoped(name)

@@ -72,6 +72,8 @@ class ConvLayer(Layer):
         if use_bias:
             self.bias = nn.Parameter(torch.full((cout,), float(bias_init), device=device))
         self.weight_lp: Optional[torch.Tensor] = None
+        self.weight_t: Optional[torch.Tensor] = None  # dgrad layout (ops.conv_hip.DgradWeights)
+        self.stride = None
 
     def tf_variables(self):
         out = {"conv2d/kernel": self.weight.detach().permute(1, 2, 3, 0)}

@@ -66,15 +66,21 @@ def fills_bn_stats(x, cout, impl="hip") -> bool:
             and x.dtype in (torch.bfloat16, torch.float16) and cout % 8 == 0)
 
 
-def conv2d(x, w, w_lp, stride, pads, impl="hip", stats=None):
-    """Returns y, or (y, stats_filled) when a stats buffer was requested and
-    the HIP kernel filled it (the caller passes it on to the BN)."""
+def runs_hip_kernel(x, impl="hip") -> bool:
+    """True when conv2d on ``x`` goes through the HIP autograd Function (which
+    takes part in the BN-link gradient protocol of ops.nn.BNLink)."""
+    return x.is_cuda and impl == "hip" and x.dtype in (torch.bfloat16, torch.float16)
+
+
+def conv2d(x, w, w_lp, stride, pads, impl="hip", stats=None, w_t=None):
+    """NHWC conv.  ``stats``: see fills_bn_stats.  ``w_t``: optional
+    dgrad-ready weight copy (ops.conv_hip.DgradWeights)."""
     if not x.is_cuda:
         y = _torch_conv(x.float(), w, stride, pads)
         return y.to(x.dtype).contiguous()
     if impl == "hip" and _hip_supported(x, w, stride, pads):
         from . import conv_hip
-        return conv_hip.conv2d(x, w, w_lp, stride, pads, stats)
+        return conv_hip.conv2d(x, w, w_lp, stride, pads, stats, w_t)
     # torch/MIOpen path on channels-last views; autograd routes the weight
     # gradient through the cast back to the fp32 master.
     wl = w.to(x.dtype)

@@ -18,7 +18,7 @@ import torch
 
 from . import _native as N
 
-_SIG = [N.I, N.P, N.P, N.P] + [N.I] * 17 + [N.I, N.P, N.P, N.P, N.P, N.P]
+_SIG = [N.I, N.P, N.P, N.P] + [N.I] * 17 + [N.I, N.P, N.P, N.P, N.P, N.P, N.P]
 N.register_optional("kfb_conv_igemm", _SIG)
 N.register_optional("kfb_conv_stats_spread", [], N.c_int)
 N.register_optional("kfb_conv_wgrad", [N.I, N.P, N.P, N.P] + [N.I] * 12 + [N.I, N.I, N.P])
@@ -48,10 +48,10 @@ def stats_buffer(channels, device):
 
 
 def _igemm(x, wmat, y, N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy,
-           trans, stats=None, mask=None, xbn=None, mean=None):
+           trans, stats=None, mask=None, xbn=None, mean=None, addend=None):
     N.call("kfb_conv_igemm", N.dt(x), x.data_ptr(), wmat.data_ptr(), y.data_ptr(), N_, H, W, C,
            OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy, int(trans), N.ptr(stats),
-           N.ptr(mask), N.ptr(xbn), N.ptr(mean), N.stream(x.device))
+           N.ptr(mask), N.ptr(xbn), N.ptr(mean), N.ptr(addend), N.stream(x.device))
 
 
 def conv_fwd(x, wl, stride, pads, stats=None):
@@ -69,19 +69,31 @@ def conv_fwd(x, wl, stride, pads, stats=None):
     return y
 
 
-def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None):
+def is_scatter_dgrad(w_shape, stride, pads):
+    cout, KH, KW, _ = w_shape
+    return KH == 1 and KW == 1 and pads[0] == 0 and pads[2] == 0 and stride != (1, 1)
+
+
+def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None, addend=None, wt=None):
     """``fuse`` = (stats, mask, xbn, mean): also apply the producer BN's ReLU
-    mask to dX and accumulate its backward partial sums (see BNLink)."""
+    mask to dX and accumulate its backward partial sums (see BNLink).
+    ``addend``: gradient already produced by other consumers, added to dX
+    (not combined with ``fuse`` on the strided-1x1 scatter path)."""
     n, H, W, C = x_shape
-    fz = fuse if fuse is not None else (None, None, None, None)
+    fz = tuple(fuse if fuse is not None else (None, None, None, None)) + (addend,)
     cout, KH, KW, _ = wl.shape
     _, OH, OW, _ = dy.shape
     sh, sw = stride
     pt, pb, pl, pr = pads
     if KH == 1 and KW == 1 and pt == 0 and pl == 0:
-        wt = wl.reshape(cout, C).t().contiguous()  # [Cin][Cout]
+        wt = wl.reshape(cout, C).t().contiguous() if wt is None else wt  # [Cin][Cout]
         if sh == 1 and sw == 1 and OH == H and OW == W:
             dx = torch.empty((n, H, W, C), dtype=dy.dtype, device=dy.device)
+        elif addend is not None:
+            # unsampled pixels keep the addend; sampled ones accumulate in place
+            assert fuse is None
+            dx = addend.clone()
+            fz = (None, None, None, None, dx)
         else:
             dx = torch.zeros((n, H, W, C), dtype=dy.dtype, device=dy.device)
         # GEMM over dY pixels (1x1, stride 1 in dY space), scattered by ys.
@@ -94,12 +106,12 @@ def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None):
             and KW - 1 - pl >= 0 and KW - 1 - pr >= 0:
         # stride-1 transposed conv == forward conv of dY with the spatially
         # flipped, channel-transposed kernel and complementary padding.
-        wf = wl.flip(1, 2).permute(3, 1, 2, 0).contiguous()  # [Cin][KH][KW][Cout]
+        wf = wl.flip(1, 2).permute(3, 1, 2, 0).contiguous() if wt is None else wt
         dx = torch.empty((n, H, W, C), dtype=dy.dtype, device=dy.device)
         _igemm(dy, wf, dx, n, OH, OW, cout, H, W, KH, KW, 1, 1, KH - 1 - pt, KW - 1 - pl, C,
                H, W, 1, C, False, *fz)
         return dx
-    wd = wl.permute(3, 1, 2, 0).contiguous()  # [Cin][KH][KW][Cout]
+    wd = wl.permute(3, 1, 2, 0).contiguous() if wt is None else wt  # [Cin][KH][KW][Cout]
     dx = torch.empty((n, H, W, C), dtype=dy.dtype, device=dy.device)
     _igemm(dy, wd, dx, n, OH, OW, cout, H, W, KH, KW, sh, sw, pt, pl, C, H, W, 1, C, True, *fz)
     return dx
@@ -122,7 +134,7 @@ def conv_wgrad(dy, x, w_shape, stride, pads, out=None):
 
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, wl, stride, pads, stats):
+    def forward(ctx, x, w, wl, stride, pads, stats, wt):
         x = x.contiguous()
         if wl is None or wl.dtype != x.dtype:
             wl = w.detach().to(x.dtype)
@@ -144,7 +156,8 @@ class _Conv2d(torch.autograd.Function):
         ctx.meta = (stride, pads, cin, cout, x.shape)
         ctx.x_needs_grad = ctx.needs_input_grad[0]
         ctx.w = w
-        ctx.link = getattr(x, "_kfb_bn_link", None) if cin_p == cin else None
+        ctx.wt = wt if (cin_p == cin and cout_p == cout) else None
+        ctx.link = getattr(x, "_kfb_bn_link", None)
         return y
 
     @staticmethod
@@ -158,17 +171,30 @@ class _Conv2d(torch.autograd.Function):
         dx = None
         if ctx.x_needs_grad:
             link = ctx.link
-            fuse = None
-            if link is not None and link.fusable and _fuse_enabled():
-                parts = stats_buffer(cin, dy.device)
-                fuse = (parts, xp if link.relu else None, link.x_bn, link.mean)
-            dx = conv_dgrad(dy, wp, xp.shape, stride, pads, fuse)
-            if dx is None:
-                raise NotImplementedError("anisotropic strided 1x1 dgrad")
-            if fuse is not None:
-                link.partials = fuse[0]
-            if dx.shape[-1] != cin:
-                dx = dx[..., :cin].contiguous()
+            padded = wp.shape[-1] != cin
+            if link is not None and link.fusable:
+                if link.arrive():
+                    pend = link.pending
+                    link.pending = None
+                    if padded:
+                        dx = conv_dgrad(dy, wp, xp.shape, stride, pads)[..., :cin]
+                        dx = (dx + pend if pend is not None else dx).contiguous()
+                    else:
+                        fuse = None
+                        if not (pend is not None and is_scatter_dgrad(wp.shape, stride, pads)):
+                            parts = stats_buffer(cin, dy.device)
+                            fuse = (parts, xp if link.relu else None, link.x_bn, link.mean)
+                        dx = conv_dgrad(dy, wp, xp.shape, stride, pads, fuse, addend=pend,
+                                        wt=ctx.wt)
+                        if fuse is not None:
+                            link.partials = fuse[0]
+                else:
+                    g = conv_dgrad(dy, wp, xp.shape, stride, pads, wt=ctx.wt)
+                    link.deposit(g[..., :cin].contiguous() if padded else g)
+            else:
+                dx = conv_dgrad(dy, wp, xp.shape, stride, pads, wt=ctx.wt)
+                if dx is not None and padded:
+                    dx = dx[..., :cin].contiguous()
         dw = None
         if ctx.needs_input_grad[1]:
             w = ctx.w
@@ -183,8 +209,68 @@ class _Conv2d(torch.autograd.Function):
                 dw = None
             elif dw.shape[0] != cout or dw.shape[-1] != cin:
                 dw = dw[:cout, :, :, :cin].contiguous()
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
-def conv2d(x, w, wl, stride, pads, stats=None):
-    return _Conv2d.apply(x, w, wl, tuple(stride), tuple(pads), stats)
+def conv2d(x, w, wl, stride, pads, stats=None, wt=None):
+    return _Conv2d.apply(x, w, wl, tuple(stride), tuple(pads), stats, wt)
+
+
+N.register_optional("kfb_wtrans_item_bytes", [], N.c_int)
+N.register_optional("kfb_weight_transforms", [N.I, N.P, N.P, N.P, N.I, N.P])
+
+_ITEM = None
+
+
+def _item_dtype():
+    import numpy as np
+    return np.dtype([("src", "<i8"), ("dst", "<i8"), ("cout", "<i4"), ("cin", "<i4"),
+                     ("kh", "<i4"), ("kw", "<i4"), ("a", "<i4"), ("b", "<i4"),
+                     ("flip", "<i4"), ("co0", "<i4"), ("ci0", "<i4"), ("pad", "<i4")])
+
+
+class DgradWeights:
+    """Keeps a dgrad-ready copy ([Cin][KH][KW][Cout], flipped for stride-1
+    kernels) of every conv weight, refreshed by ONE batched launch
+    (csrc/wtrans.hip) after each optimizer update instead of per-conv
+    permute/flip copies in backward."""
+
+    def __init__(self, net, flat):
+        import numpy as np
+        self.flat = flat
+        lp = flat.lp
+        base = lp.data_ptr()
+        esz = lp.element_size()
+        items, total, views = [], 0, []
+        for layer in net.ordered_layers():
+            wl = getattr(layer, "weight_lp", None)
+            stride = getattr(layer, "stride", None)
+            if wl is None or stride is None:
+                continue
+            cout, kh, kw, cin = wl.shape
+            if cin % 8 or cout % 8:
+                continue
+            flip = int(tuple(stride) == (1, 1) and (kh, kw) != (1, 1))
+            src = (wl.data_ptr() - base) // esz
+            dst = total
+            total += (wl.numel() + 63) // 64 * 64
+            views.append((layer, dst, (cin, kh, kw, cout)))
+            for a in range(kh):
+                for b in range(kw):
+                    for co0 in range(0, cout, 64):
+                        for ci0 in range(0, cin, 64):
+                            items.append((src, dst, cout, cin, kh, kw, a, b, flip, co0, ci0, 0))
+        self.n = len(items)
+        self.buf = torch.empty((max(total, 1),), dtype=lp.dtype, device=lp.device)
+        for layer, off, shape in views:
+            layer.weight_t = self.buf[off:off + int(np.prod(shape))].view(shape)
+        arr = np.array(items, dtype=_item_dtype())
+        assert arr.dtype.itemsize == N.query("kfb_wtrans_item_bytes")
+        self.items = torch.from_numpy(arr.view(np.uint8).copy()).to(lp.device)
+        self.run()
+
+    def run(self):
+        if self.n:
+            lp = self.flat.lp
+            N.call("kfb_weight_transforms", N.dt(lp), lp.data_ptr(), self.buf.data_ptr(),
+                   self.items.data_ptr(), self.n, N.stream(lp.device))

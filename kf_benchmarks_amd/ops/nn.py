@@ -60,11 +60,11 @@ def resolve_pads(mode: str, H: int, W: int, kh: int, kw: int, sh: int, sw: int) 
 
 # ------------------------------------------------------------------------ conv
 def conv2d(x, w, w_lp, stride: Tuple[int, int], pads: Pads, impl: str = "hip",
-           stats: Optional[torch.Tensor] = None):
+           stats: Optional[torch.Tensor] = None, w_t: Optional[torch.Tensor] = None):
     """NHWC convolution, no bias.  ``w_lp`` is the compute-dtype copy of the
     fp32 master ``w`` (None -> cast on the fly).  ``stats`` (GPU): zeroed
     [2*32*Cout] fp32 buffer that receives the BN statistics of the output."""
-    return _conv.conv2d(x, w, w_lp, stride, pads, impl, stats)
+    return _conv.conv2d(x, w, w_lp, stride, pads, impl, stats, w_t)
 
 
 # ------------------------------------------------------------------ batch norm
@@ -82,21 +82,44 @@ def _bn_cpu(x, gamma, beta, residual, rm, rv, decay, eps, relu, training):
 
 
 class BNLink:
-    """Ties a training-mode BN to the single conv that consumes its output so
-    the conv's dgrad epilogue can apply the BN's ReLU mask and produce the BN
-    backward partial sums (csrc/conv_igemm.hip fused epilogue).  ``uses`` /
-    ``other`` are counted by the ConvNetBuilder; fusion happens only when the
-    BN output feeds exactly one conv and nothing else."""
+    """Ties a training-mode BN's output y to its consumers so their backward
+    kernels can finish the BN's backward work in their epilogues
+    (csrc/conv_igemm.hip):
 
-    __slots__ = ("x_bn", "mean", "relu", "uses", "other", "partials")
+    * every consumer is a conv (input) or a BN that adds y as its residual;
+      the ConvNetBuilder counts them (``convs``, ``resid``) and marks any other
+      use (``other``), which disables the fusion;
+    * in backward, all but the last contributor *deposit* their gradient of y
+      here (``pending``) and return None to autograd; the last one, if it is a
+      conv, adds ``pending`` in its dgrad epilogue, applies y's ReLU mask and
+      accumulates the BN backward partial sums (``partials``), so the BN
+      backward is only finalize + apply.  A residual-BN last contributor
+      returns the summed gradient instead (unfused path).
+    """
+
+    __slots__ = ("x_bn", "mean", "relu", "convs", "resid", "other", "partials", "pending",
+                 "arrived")
 
     def __init__(self, x_bn, mean, relu):
         self.x_bn, self.mean, self.relu = x_bn, mean, relu
-        self.uses, self.other, self.partials = 0, False, None
+        self.convs, self.resid, self.other = 0, 0, False
+        self.partials, self.pending, self.arrived = None, None, 0
 
     @property
     def fusable(self):
-        return self.uses == 1 and not self.other
+        return not self.other and self.convs >= 1 and _conv.FUSE_BN
+
+    @property
+    def total(self):
+        return self.convs + self.resid
+
+    def arrive(self) -> bool:
+        """Registers one gradient contribution; True if it is the last."""
+        self.arrived += 1
+        return self.arrived >= self.total
+
+    def deposit(self, g):
+        self.pending = g if self.pending is None else self.pending + g
 
 
 def _grad_sink(p):
@@ -140,11 +163,10 @@ class _BatchNormTrain(torch.autograd.Function):
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.gamma, ctx.beta = gamma, beta
-        link = None
-        if residual is None:
-            link = BNLink(x, st[0], relu)
-            y._kfb_bn_link = link
+        link = BNLink(x, st[0], relu)
+        y._kfb_bn_link = link
         ctx.link = link
+        ctx.res_link = getattr(residual, "_kfb_bn_link", None) if residual is not None else None
         return y
 
     @staticmethod
@@ -176,12 +198,26 @@ class _BatchNormTrain(torch.autograd.Function):
             dparams = torch.empty((2, C), dtype=torch.float32, device=dev)
             dgp, dbp = dparams[0].data_ptr(), dparams[1].data_ptr()
         dx = torch.empty_like(x)
-        dres = torch.empty_like(x) if ctx.has_res else None
+        rl = ctx.res_link
+        res_fused = ctx.has_res and rl is not None and rl.fusable
+        # the residual's gradient is dy' (masked dy): with a pre-masked dy it
+        # is dy itself, no kernel write needed
+        dres = torch.empty_like(x) if ctx.has_res and not (pre and res_fused) else None
         N.call("kfb_bn_bwd", N.dt(x), dy.data_ptr(), N.ptr(y), x.data_ptr(), dx.data_ptr(),
                N.ptr(dres), rows, C, N.ptr(gamma), st[0].data_ptr(), st[1].data_ptr(),
                dgp, dbp, pdy.data_ptr(), pdyx.data_ptr(),
                nslab, coef[:C].data_ptr(), coef[C:2 * C].data_ptr(), coef[2 * C:].data_ptr(),
                int(ctx.relu), int(direct), int(pre), N.stream(dev))
+        if ctx.has_res and dres is None:
+            dres = dy
+        if res_fused:
+            if rl.arrive():
+                if rl.pending is not None:
+                    dres = dres + rl.pending
+                    rl.pending = None
+            else:
+                rl.deposit(dres)
+                dres = None
         if direct:
             _grad_ready(ctx.gamma)
             _grad_ready(ctx.beta)

@@ -71,6 +71,16 @@ class FlatParams:
         checkpoint restore or a model broadcast)."""
         if self.lp is not None:
             self.lp.copy_(self.flat)
+        self.after_update()
+
+    def add_update_hook(self, fn):
+        """fn() runs after every write of the weights (optimizer step, restore)."""
+        self._hooks = getattr(self, "_hooks", [])
+        self._hooks.append(fn)
+
+    def after_update(self):
+        for fn in getattr(self, "_hooks", []):
+            fn()
 
     def zero_grad(self):
         self.grad.zero_()
@@ -133,8 +143,10 @@ class FusedOptimizer:
                    N.dt(f.lp) if f.lp is not None else 0, None, f.numel, float(lr),
                    float(grad_scale), float(weight_decay), clipv, float(mom), float(b1),
                    float(b2), float(eps), float(lr_t), int(self.nesterov), N.stream(f.device))
+            f.after_update()
             return
         self._step_torch(g, lr, grad_scale, weight_decay, clipv, mom, b1, b2, eps, lr_t)
+        f.after_update()
 
     @torch.no_grad()
     def _step_torch(self, g, lr, grad_scale, wd, clip, mom, b1, b2, eps, lr_t):

@@ -48,3 +48,29 @@ def test_conv_fwd_bwd(cuda, shape, dt):
     torch.testing.assert_close(xa.grad.float().cpu(), xb.grad, rtol=3e-2, atol=3e-2 * scale * 4)
     gw = wb.grad
     torch.testing.assert_close(wa.grad.cpu(), gw, rtol=3e-2, atol=2e-2 * gw.abs().max().item())
+
+
+def test_dgrad_weight_relayout_matches(cuda):
+    from kf_benchmarks_amd import datasets, optim, params as P
+    from kf_benchmarks_amd.models import model_config
+    from kf_benchmarks_amd.models.model import Network
+    from kf_benchmarks_amd.ops.conv_hip import DgradWeights
+    d = datasets.create_dataset(None, "imagenet")
+    for name in ("resnet50", "inception3"):
+        m = model_config.get_model_config(name, d, P.make_params(model=name))
+        net = Network(m, 1001, cuda, torch.bfloat16, seed=1)
+        flat = optim.FlatParams(net, torch.bfloat16)
+        DgradWeights(net, flat)
+        n = 0
+        for layer in net.ordered_layers():
+            wt = getattr(layer, "weight_t", None)
+            if wt is None:
+                continue
+            wl = layer.weight_lp
+            if tuple(layer.stride) == (1, 1) and wl.shape[1:3] != (1, 1):
+                ref = wl.flip(1, 2).permute(3, 1, 2, 0)
+            else:
+                ref = wl.permute(3, 1, 2, 0)
+            assert torch.equal(wt, ref.contiguous()), layer.tf_scope
+            n += 1
+        assert n > 10
