@@ -225,64 +225,85 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
   float s1[8], s2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
+  const bool fused = a.stats || a.addend;
+  constexpr int NPASS = BM * CPR / 256;
+  constexpr int PB = NPASS >= 2 ? 2 : 1;  // passes whose global loads are issued together
 #pragma unroll
-  for (int pass = 0; pass < BM * CPR / 256; ++pass) {
-    const int t = tid + pass * 256;
-    const int ml = t / CPR, ch = t % CPR;
-    const int m = m0 + ml, n = n0 + ch * 8;
-    if (m >= a.M || n >= a.Ncol) continue;
-    long rowoff;
-    if (dense) {
-      rowoff = (long)m * a.ldy;
-    } else {
-      const int img = m / OHW, rem = m - img * OHW;
-      const int oh = rem / a.OW, ow = rem - oh * a.OW;
-      rowoff = ((long)(img * a.YH + oh * a.ys) * a.YW + ow * a.ys) * a.ldy;
+  for (int p0 = 0; p0 < NPASS; p0 += PB) {
+    uint4 raw[PB], ad[PB], mk[PB], xb[PB];
+    long off[PB];
+    bool ok[PB];
+    int nq[PB];
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+      const int t = tid + (p0 + q) * 256;
+      const int ml = t / CPR, ch = t % CPR;
+      const int m = m0 + ml, n = n0 + ch * 8;
+      nq[q] = n;
+      ok[q] = m < a.M && n < a.Ncol;
+      long rowoff = 0;
+      if (ok[q]) {
+        if (dense) {
+          rowoff = (long)m * a.ldy;
+        } else {
+          const int img = m / OHW, rem = m - img * OHW;
+          const int oh = rem / a.OW, ow = rem - oh * a.OW;
+          rowoff = ((long)(img * a.YH + oh * a.ys) * a.YW + ow * a.ys) * a.ldy;
+        }
+      }
+      off[q] = rowoff + n;
+      raw[q] = *(const uint4*)(cs + ml * BN + ((ch ^ (ml & (CPR - 1))) * 8));
     }
-    const uint4 raw = *(const uint4*)(cs + ml * BN + ((ch ^ (ml & (CPR - 1))) * 8));
-    if (!a.stats && !a.addend) {
-      *(uint4*)(y + rowoff + n) = raw;
+    if (!fused) {
+#pragma unroll
+      for (int q = 0; q < PB; ++q)
+        if (ok[q]) *(uint4*)(y + off[q]) = raw[q];
       continue;
     }
-    float v[8];
-    {
-      Vec<T, 8> tv = __builtin_bit_cast(Vec<T, 8>, raw);
+    // issue every extra operand load of the batch before the first use
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+      ad[q] = (ok[q] && a.addend) ? *(const uint4*)((const T*)a.addend + off[q]) : make_uint4(0, 0, 0, 0);
+      mk[q] = (ok[q] && a.xbn && a.mask) ? *(const uint4*)((const T*)a.mask + off[q]) : make_uint4(0, 0, 0, 0);
+      xb[q] = (ok[q] && a.xbn) ? *(const uint4*)((const T*)a.xbn + off[q]) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+      if (!ok[q]) continue;
+      const int n = nq[q];
+      float v[8];
+      Vec<T, 8> tv = __builtin_bit_cast(Vec<T, 8>, raw[q]);
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = (float)tv.v[k];
-    }
-    if (a.addend) {
-      float ad[8];
-      load_vec<T, 8>((const T*)a.addend + rowoff + n, ad);
+      if (a.addend) {
+        Vec<T, 8> av = __builtin_bit_cast(Vec<T, 8>, ad[q]);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] += ad[k];
-      if (!a.stats) {
-        store_vec<T, 8>(y + rowoff + n, v);
-        continue;
+        for (int k = 0; k < 8; ++k) v[k] += (float)av.v[k];
       }
-    }
-    if (a.xbn) {
-      if (a.mask) {
-        float mk[8];
-        load_vec<T, 8>((const T*)a.mask + rowoff + n, mk);
+      if (a.xbn) {
+        if (a.mask) {
+          Vec<T, 8> mv = __builtin_bit_cast(Vec<T, 8>, mk[q]);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = mk[k] > 0.f ? v[k] : 0.f;
-      }
-      float xb[8];
-      load_vec<T, 8>((const T*)a.xbn + rowoff + n, xb);
+          for (int k = 0; k < 8; ++k) v[k] = (float)mv.v[k] > 0.f ? v[k] : 0.f;
+        }
+        Vec<T, 8> xv = __builtin_bit_cast(Vec<T, 8>, xb[q]);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        s1[k] += v[k];
-        s2[k] += v[k] * (xb[k] - a.mean[n + k]);
-      }
-      store_vec<T, 8>(y + rowoff + n, v);
-    } else {
+        for (int k = 0; k < 8; ++k) {
+          s1[k] += v[k];
+          s2[k] += v[k] * ((float)xv.v[k] - a.mean[n + k]);
+        }
+        store_vec<T, 8>(y + off[q], v);
+      } else if (a.stats) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        s1[k] += v[k];
-        s2[k] += v[k] * v[k];
+        for (int k = 0; k < 8; ++k) {
+          s1[k] += v[k];
+          s2[k] += v[k] * v[k];
+        }
+        if (a.addend) store_vec<T, 8>(y + off[q], v);
+        else *(uint4*)(y + off[q]) = raw[q];
+      } else {
+        store_vec<T, 8>(y + off[q], v);
       }
-      if (a.addend) store_vec<T, 8>(y + rowoff + n, v);
-      else *(uint4*)(y + rowoff + n) = raw;
     }
   }
   if (a.stats) {

@@ -220,6 +220,9 @@ class Network(nn.Module):
     # ------------------------------------------------------------- forward
     def forward(self, images, phase_train=True):
         model = self.model
+        if phase_train and images.is_cuda:
+            from ..ops.conv_hip import STATS_ARENA
+            STATS_ARENA.reset(images.device)
         cnn = ConvNetBuilder(self, images, model.depth, phase_train, self.compute_dtype)
         model.add_inference(cnn)
         if model.skip_final_affine_layer():

@@ -42,9 +42,47 @@ def _pad8(n):
 STATS_SPREAD = 32  # must match IG_SPREAD in csrc/conv_igemm.hip
 
 
+class _StatsArena:
+    """Per-step pool of zeroed fp32 partial-sum buffers: one memset per
+    training step instead of one per BN (reset by Network.forward)."""
+
+    def __init__(self):
+        self.buf = {}
+        self.off = {}
+        self.need = {}
+
+    def reset(self, device):
+        key = str(device)
+        need = self.need.get(key, 0)
+        buf = self.buf.get(key)
+        if buf is None or buf.numel() < need:
+            self.buf[key] = buf = torch.zeros((max(need, 1 << 16),), dtype=torch.float32,
+                                              device=device)
+        else:
+            buf.zero_()
+        self.off[key] = 0
+
+    def take(self, n, device):
+        key = str(device)
+        buf = self.buf.get(key)
+        off = self.off.get(key, 0)
+        n = (n + 63) // 64 * 64
+        if buf is None or off + n > buf.numel():
+            # grow next step; this step falls back to a fresh zeroed buffer
+            self.need[key] = max(self.need.get(key, 0), off + n) * 2
+            self.off[key] = off + n
+            return torch.zeros((n,), dtype=torch.float32, device=device)
+        self.off[key] = off + n
+        self.need[key] = max(self.need.get(key, 0), off + n)
+        return buf[off:off + n]
+
+
+STATS_ARENA = _StatsArena()
+
+
 def stats_buffer(channels, device):
     """Zeroed [2][STATS_SPREAD][C] fp32 buffer for fused BN partial sums."""
-    return torch.zeros((2 * STATS_SPREAD * channels,), dtype=torch.float32, device=device)
+    return STATS_ARENA.take(2 * STATS_SPREAD * channels, device)[:2 * STATS_SPREAD * channels]
 
 
 def _igemm(x, wmat, y, N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy,
