@@ -14,6 +14,8 @@ Channel counts that are not multiples of 8 (the RGB stem, DenseNet growth
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _native as N
@@ -51,29 +53,32 @@ class _StatsArena:
         self.off = {}
         self.need = {}
 
+    enabled = os.environ.get("KFB_STATS_ARENA", "1") != "0"
+
     def reset(self, device):
-        key = str(device)
+        key = str(torch.device(device))
+        # high-water mark of the previous step (+25% headroom)
         need = self.need.get(key, 0)
+        need = (need + need // 4 + 4095) // 4096 * 4096
         buf = self.buf.get(key)
         if buf is None or buf.numel() < need:
             self.buf[key] = buf = torch.zeros((max(need, 1 << 16),), dtype=torch.float32,
                                               device=device)
         else:
-            buf.zero_()
+            # only the part handed out last step can be dirty
+            buf[:min(self.off.get(key, buf.numel()), buf.numel())].zero_()
         self.off[key] = 0
 
     def take(self, n, device):
-        key = str(device)
-        buf = self.buf.get(key)
-        off = self.off.get(key, 0)
+        key = str(torch.device(device))
         n = (n + 63) // 64 * 64
-        if buf is None or off + n > buf.numel():
-            # grow next step; this step falls back to a fresh zeroed buffer
-            self.need[key] = max(self.need.get(key, 0), off + n) * 2
-            self.off[key] = off + n
-            return torch.zeros((n,), dtype=torch.float32, device=device)
+        buf = self.buf.get(key) if self.enabled else None
+        off = self.off.get(key, 0)
         self.off[key] = off + n
         self.need[key] = max(self.need.get(key, 0), off + n)
+        if buf is None or off + n > buf.numel():
+            # grows at the next reset; this step falls back to a fresh buffer
+            return torch.zeros((n,), dtype=torch.float32, device=device)
         return buf[off:off + n]
 
 

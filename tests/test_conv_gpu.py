@@ -74,3 +74,70 @@ def test_dgrad_weight_relayout_matches(cuda):
             assert torch.equal(wt, ref.contiguous()), layer.tf_scope
             n += 1
         assert n > 10
+
+
+FUSED_SHAPES = [
+    (2, 14, 14, 64, 256, 1, 1, 1, "SAME"),
+    (2, 7, 7, 128, 128, 3, 3, 1, "SAME_RESNET"),     # M=98 < one tile
+    (3, 9, 9, 64, 96, 3, 3, 2, "SAME_RESNET"),       # transposed gather
+    (4, 2, 2, 512, 2048, 1, 1, 1, "SAME"),           # M=16
+    (2, 13, 13, 64, 128, 1, 1, 2, "SAME"),           # scatter (addend only)
+]
+
+
+@pytest.mark.parametrize("shape", FUSED_SHAPES, ids=[str(s) for s in FUSED_SHAPES])
+@pytest.mark.parametrize("with_addend", [False, True])
+def test_dgrad_fused_epilogue(cuda, shape, with_addend):
+    """dgrad epilogue: dX = (conv^T(dY) + addend) * [x > 0] and the producer
+    BN's backward partials sum(dX), sum(dX * (x_bn - mean)) per channel."""
+    from kf_benchmarks_amd.ops import conv_hip
+    n, H, W, cin, cout, kh, kw, s, mode = shape
+    scatter = kh == 1 and s > 1
+    if scatter and not with_addend:
+        pytest.skip("scatter path fuses only the addend")
+    g = torch.Generator().manual_seed(1)
+    dt = torch.bfloat16
+    x = torch.randn(n, H, W, cin, generator=g).to(dt)
+    w = (torch.randn(cout, kh, kw, cin, generator=g) / (kh * kw * cin) ** 0.5).to(dt)
+    pads = F.resolve_pads(mode, H, W, kh, kw, s, s)
+    yb = conv_ops.conv2d_reference(x.float(), w.float(), (s, s), pads)
+    dy = torch.randn(yb.shape, generator=g).to(dt)
+    xb = torch.randn(n, H, W, cin, generator=g).to(dt)
+    mean = torch.randn(cin, generator=g)
+    add = torch.randn(n, H, W, cin, generator=g).to(dt) if with_addend else None
+    xr = x.float().requires_grad_(True)
+    conv_ops.conv2d_reference(xr, w.float(), (s, s), pads).backward(dy.float())
+    ref = xr.grad + (add.float() if add is not None else 0)
+    parts = None
+    fuse = None
+    if not scatter:
+        ref = ref * (x.float() > 0)
+        parts = conv_hip.stats_buffer(cin, cuda).zero_()
+        fuse = (parts, x.to(cuda), xb.to(cuda), mean.to(cuda))
+    dx = conv_hip.conv_dgrad(dy.to(cuda), w.to(cuda), x.shape, (s, s), pads, fuse,
+                             addend=add.to(cuda) if add is not None else None)
+    torch.testing.assert_close(dx.float().cpu(), ref, rtol=3e-2, atol=3e-2)
+    if parts is not None:
+        p = parts.view(2, conv_hip.STATS_SPREAD, cin).sum(1).cpu()
+        r = dx.float().cpu()
+        s1 = r.sum((0, 1, 2))
+        s2 = (r * (xb.float() - mean)).sum((0, 1, 2))
+        tol = 4e-3 * (r.abs() * (1 + (xb.float() - mean).abs())).sum((0, 1, 2)).max().item()
+        torch.testing.assert_close(p[0], s1, rtol=1e-2, atol=tol)
+        torch.testing.assert_close(p[1], s2, rtol=1e-2, atol=tol)
+
+
+@pytest.mark.parametrize("shape", FUSED_SHAPES[:4], ids=[str(s) for s in FUSED_SHAPES[:4]])
+def test_fwd_stats_epilogue(cuda, shape):
+    from kf_benchmarks_amd.ops import conv_hip
+    n, H, W, cin, cout, kh, kw, s, mode = shape
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(n, H, W, cin, generator=g).to(torch.bfloat16)
+    w = (torch.randn(cout, kh, kw, cin, generator=g) / (kh * kw * cin) ** 0.5).to(torch.bfloat16)
+    pads = F.resolve_pads(mode, H, W, kh, kw, s, s)
+    st = conv_hip.stats_buffer(cout, cuda).zero_()
+    y = conv_hip.conv_fwd(x.to(cuda), w.to(cuda), (s, s), pads, st).float().cpu()
+    p = st.view(2, conv_hip.STATS_SPREAD, cout).sum(1).cpu()
+    tol = 4e-3 * (y.abs() + y * y).sum((0, 1, 2)).max().item()
+    torch.testing.assert_close(p[0], y.sum((0, 1, 2)), rtol=1e-2, atol=tol)
+    torch.testing.assert_close(p[1], (y * y).sum((0, 1, 2)), rtol=1e-2, atol=tol)
