@@ -17,6 +17,7 @@ import queue
 import threading
 from typing import Optional
 
+import numpy as np
 import torch
 
 
@@ -92,19 +93,28 @@ class PrefetchInput:
 
     def _run(self):
         try:
-            for images, labels in self._it:
+            for batch in self._it:
                 if self._stop.is_set():
                     return
-                img = torch.from_numpy(images)
-                lab = torch.from_numpy(labels).to(torch.int32)
+                ts = [torch.from_numpy(np.ascontiguousarray(x)) for x in batch]
                 if self.device.type == "cuda":
-                    img = img.pin_memory()
-                    lab = lab.pin_memory()
-                self._q.put((img, lab))
+                    ts = [t.pin_memory() for t in ts]
+                self._q.put(ts)
             self._q.put(None)
         except BaseException as e:
             self._err = e
             self._q.put(None)
+
+    def _to_device(self, ts):
+        img = ts[0].to(self.device, non_blocking=True)
+        if img.dtype == torch.uint8:
+            # raw pixels: normalize on the device (x / 127.5 - 1)
+            img = img.to(torch.float32).mul_(1.0 / 127.5).sub_(1.0)
+        out = [img.to(self.dtype)]
+        for t in ts[1:]:
+            t = t.to(self.device, non_blocking=True)
+            out.append(t.to(torch.int32) if t.dtype == torch.int64 else t)
+        return out
 
     def _fetch(self):
         item = self._q.get()
@@ -112,30 +122,29 @@ class PrefetchInput:
             if self._err is not None:
                 raise RuntimeError("input pipeline failed") from self._err
             raise StopIteration("input exhausted")
-        img, lab = item
         if self._stream is not None:
             with torch.cuda.stream(self._stream):
-                img = img.to(self.device, non_blocking=True).to(self.dtype)
-                lab = lab.to(self.device, non_blocking=True)
+                out = self._to_device(item)
                 ev = torch.cuda.Event()
                 ev.record(self._stream)
-            return img, lab, ev
-        return img.to(self.dtype), lab, None
+            return out, ev
+        return self._to_device(item), None
 
     def next(self):
         if self._next is None:
             self._next = self._fetch()
-        img, lab, ev = self._next
+        out, ev = self._next
         if ev is not None:
-            torch.cuda.current_stream(self.device).wait_event(ev)
-            img.record_stream(torch.cuda.current_stream(self.device))
-            lab.record_stream(torch.cuda.current_stream(self.device))
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_event(ev)
+            for t in out:
+                t.record_stream(cur)
         try:
             self._next = self._fetch()
         except StopIteration:
             self._next = None
             self._exhausted = True
-        return img, lab
+        return tuple(out)
 
     def close(self):
         self._stop.set()

@@ -200,6 +200,116 @@ def make_example(features: Dict[str, list]) -> bytes:
     return _ld(1, entries)
 
 
+def _feature_bytes(vals) -> bytes:
+    if vals and isinstance(vals[0], (bytes, bytearray)):
+        return _ld(1, b"".join(_ld(1, bytes(v)) for v in vals))
+    if vals and isinstance(vals[0], float):
+        return _ld(2, _ld(1, struct.pack("<%df" % len(vals), *vals)))
+    return _ld(3, _ld(1, b"".join(_varint(int(v)) for v in vals)))
+
+
+def _features_bytes(features: Dict[str, list]) -> bytes:
+    return b"".join(_ld(1, _ld(1, k.encode()) + _ld(2, _feature_bytes(features[k])))
+                    for k in sorted(features))
+
+
+def make_sequence_example(context: Dict[str, list], feature_lists: Dict[str, list]) -> bytes:
+    """Encode a tf.train.SequenceExample: ``feature_lists`` maps a key to a
+    list of per-step value lists."""
+    fl = b"".join(_ld(1, _ld(1, k.encode()) +
+                      _ld(2, b"".join(_ld(1, _feature_bytes(step)) for step in feature_lists[k])))
+                  for k in sorted(feature_lists))
+    return _ld(1, _features_bytes(context)) + _ld(2, fl)
+
+
+# --- protobuf wire decoding (SequenceExample; tf.Example goes through C++)
+def _read_varint(b: bytes, i: int):
+    shift = v = 0
+    while True:
+        c = b[i]
+        i += 1
+        v |= (c & 0x7F) << shift
+        if c < 0x80:
+            return v, i
+        shift += 7
+
+
+def _fields(b: bytes):
+    """Yields (field number, wire type, value) of one message."""
+    i, n = 0, len(b)
+    while i < n:
+        key, i = _read_varint(b, i)
+        f, wt = key >> 3, key & 7
+        if wt == 0:
+            v, i = _read_varint(b, i)
+        elif wt == 2:
+            ln, i = _read_varint(b, i)
+            v = b[i:i + ln]
+            i += ln
+        elif wt == 5:
+            v = b[i:i + 4]
+            i += 4
+        elif wt == 1:
+            v = b[i:i + 8]
+            i += 8
+        else:
+            raise ValueError("unsupported protobuf wire type %d" % wt)
+        yield f, wt, v
+
+
+def _decode_feature(b: bytes) -> list:
+    for f, wt, v in _fields(b):
+        if f == 1:
+            return [bytes(x) for ff, _, x in _fields(v) if ff == 1]
+        if f == 2:
+            out = []
+            for ff, w2, x in _fields(v):
+                if w2 == 2:
+                    out.extend(struct.unpack("<%df" % (len(x) // 4), x))
+                elif w2 == 5:
+                    out.append(struct.unpack("<f", x)[0])
+            return out
+        if f == 3:
+            out = []
+            for ff, w2, x in _fields(v):
+                if w2 == 2:
+                    j = 0
+                    while j < len(x):
+                        val, j = _read_varint(x, j)
+                        out.append(val - (1 << 64) if val >= 1 << 63 else val)
+                else:
+                    out.append(x - (1 << 64) if x >= 1 << 63 else x)
+            return out
+    return []
+
+
+def _decode_map(b: bytes, value_fn) -> Dict[str, object]:
+    out = {}
+    for f, _, entry in _fields(b):
+        if f != 1:
+            continue
+        key, val = "", b""
+        for ef, _, ev in _fields(entry):
+            if ef == 1:
+                key = bytes(ev).decode()
+            elif ef == 2:
+                val = ev
+        out[key] = value_fn(val)
+    return out
+
+
+def parse_sequence_example(record: bytes):
+    """-> (context {key: values}, feature_lists {key: [values per step]})."""
+    ctx, lists = {}, {}
+    for f, _, v in _fields(record):
+        if f == 1:
+            ctx = _decode_map(v, _decode_feature)
+        elif f == 2:
+            lists = _decode_map(v, lambda fl: [_decode_feature(x) for ff, _, x in _fields(fl)
+                                               if ff == 1])
+    return ctx, lists
+
+
 # -------------------------------------------------------------------- tables
 def table_write(path: str, items: List[Tuple[bytes, bytes]]):
     lib = _load()
