@@ -104,13 +104,29 @@ def build_rt(force=False):
     return RT_LIB
 
 
+RUN_BIN = os.path.join(LIBDIR, "kfb-run")
+
+
+def build_launcher(force=False):
+    """``kfb-run``: the multi-process launcher (csrc/launcher/kfb_run.cpp)."""
+    src = os.path.join(CSRC, "launcher", "kfb_run.cpp")
+    if not os.path.exists(src):
+        return None
+    os.makedirs(LIBDIR, exist_ok=True)
+    if force or not os.path.exists(RUN_BIN) or os.path.getmtime(RUN_BIN) < os.path.getmtime(src):
+        tmp = RUN_BIN + ".tmp"
+        _run([CXX, "-O2", "-std=c++17", "-Wall", "-o", tmp, src])
+        os.replace(tmp, RUN_BIN)
+    return RUN_BIN
+
+
 def build_all(force=False, jobs=None, verbose=False):
     if shutil.which(HIPCC) is None and not os.path.exists(HIPCC):
         raise RuntimeError("hipcc not found at %s" % HIPCC)
     libs = [build_hip(force=force, jobs=jobs, verbose=verbose)]
-    rt = build_rt(force=force)
-    if rt:
-        libs.append(rt)
+    for extra in (build_rt(force=force), build_launcher(force=force)):
+        if extra:
+            libs.append(extra)
     return libs
 
 

@@ -1,0 +1,58 @@
+"""kfb-run (the kungfu-run equivalent): env, prefixed output, per-peer logs,
+fail-fast, and a 2-peer gloo training run through it."""
+
+import os
+import subprocess
+import sys
+
+import pytest
+
+from kf_benchmarks_amd.parallel import launcher
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env():
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    return env
+
+
+def test_env_prefix_and_logs(tmp_path):
+    code = ("import os,sys; print('rank', os.environ['RANK'], os.environ['WORLD_SIZE'], "
+            "os.environ['LOCAL_RANK'], os.environ['MASTER_ADDR'], os.environ['KUNGFU_SELF_SPEC']);"
+            "print('warn', file=sys.stderr)")
+    r = launcher.run(3, [sys.executable, "-c", code], logdir=str(tmp_path), capture=True,
+                     port_range="23000-23100", env=_env())
+    assert r.returncode == 0, r.stderr
+    for k in range(3):
+        port = 23000 + k
+        assert "127.0.0.1.%d" % port in r.stdout
+        with open(tmp_path / ("127.0.0.1.%d.stdout.log" % port)) as f:
+            line = f.read().split()
+        assert line[:6] == ["rank", str(k), "3", str(k), "127.0.0.1", "127.0.0.1:%d" % port]
+        with open(tmp_path / ("127.0.0.1.%d.stderr.log" % port)) as f:
+            assert f.read().strip() == "warn"
+    assert "all 3/3 local peers finished" in r.stdout
+
+
+def test_fail_fast(tmp_path):
+    code = ("import os,sys,time; r=int(os.environ['RANK']); "
+            "time.sleep(0.2 if r == 1 else 60); sys.exit(3 if r == 1 else 0)")
+    r = launcher.run(3, [sys.executable, "-c", code], logdir=str(tmp_path), capture=True,
+                     port_range="23100-23200", env=_env(), timeout=120)
+    assert r.returncode == 1
+    assert "exited with error: exit status 3" in r.stderr
+    assert "tasks failed" in r.stderr
+
+
+def test_two_peer_kungfu_training(tmp_path):
+    cmd = [sys.executable, os.path.join(ROOT, "tf_cnn_benchmarks.py"), "--device=cpu",
+           "--data_format=NHWC", "--model=trivial", "--batch_size=4", "--num_batches=3",
+           "--num_warmup_batches=1", "--variable_update=kungfu", "--kungfu_option=sync_sgd"]
+    r = launcher.run(2, cmd, logdir=str(tmp_path), quiet=True, capture=True,
+                     port_range="23200-23300", env=_env(), timeout=300)
+    assert r.returncode == 0, r.stderr
+    for port in (23200, 23201):
+        with open(tmp_path / ("127.0.0.1.%d.stdout.log" % port)) as f:
+            assert "total images/sec" in f.read()
