@@ -236,24 +236,45 @@ class BenchmarkCNN:
             self.gpu_indices = list(range(self.num_gpus))
         if params.batch_size > 0:
             self.model.set_batch_size(params.batch_size)
-        self.batch_size = self.model.get_batch_size() * self.num_gpus
+        per_device_batch = self.model.get_batch_size()
+        self.batch_size = per_device_batch * self.num_gpus
         self.batch_group_size = params.batch_group_size
         self.enable_auto_loss_scale = params.use_fp16 and params.fp16_enable_auto_loss_scale
         self.mode = get_mode_from_params(params)
         self.job_name = params.job_name
 
-        # ---- world & devices (one process per GPU; in-process towers are
-        # created by parallel.towers when --num_gpus > 1).
+        # ---- world & devices: one process per GPU.  --num_gpus=N in one
+        # command is run as N "tower" processes (cli.py relaunches through
+        # kfb-run with KFB_TOWER_GROUP=1): each tower is a rank, but the job
+        # reports as ONE worker with an N-device global batch, as the
+        # reference's in-process towers do (tcb/benchmark_cnn.py:1355-1357).
         self.device_type = "cuda" if params.device.lower() == "gpu" else "cpu"
         if self.device_type == "cuda" and not torch.cuda.is_available():
             raise RuntimeError("--device=gpu but no GPU is visible; use --device=cpu "
                                "--data_format=NHWC for the plumbing config")
-        self.world = comm.init_world(self.device_type)
-        self.num_workers = self.world.size
+        self.world = comm.init_world(self.device_type, params.all_reduce_spec)
+        self.tower_mode = (os.environ.get("KFB_TOWER_GROUP") == "1" and self.num_gpus > 1
+                           and self.world.size == self.num_gpus)
         self.task_index = self.world.rank
+        self.num_replicas = self.world.size  # data shards / gradient contributors
+        if self.tower_mode:
+            self.num_workers = 1
+            self.local_batch_size = per_device_batch
+        else:
+            self.num_workers = self.world.size
+            self.local_batch_size = self.batch_size
+            if self.num_gpus > 1:
+                # no launcher: the towers' batches run as one batch on one
+                # device (tower-mean gradient; see Strategy.tower_factor)
+                self.model.set_batch_size(self.batch_size)
         if self.device_type == "cuda":
             local = self.world.local_rank if self.world.size > 1 else 0
-            dev_index = self.gpu_indices[0] + local if self.num_gpus == 1 else self.gpu_indices[0]
+            if self.num_gpus == 1:
+                dev_index = self.gpu_indices[0] + local
+            elif self.tower_mode:
+                dev_index = self.gpu_indices[local % len(self.gpu_indices)]
+            else:
+                dev_index = self.gpu_indices[0]
             dev_index = dev_index % max(torch.cuda.device_count(), 1)
             torch.cuda.set_device(dev_index)
             self.device = torch.device("cuda", dev_index)
@@ -359,7 +380,7 @@ class BenchmarkCNN:
             self.flat, p.optimizer, momentum=p.momentum, rmsprop_decay=p.rmsprop_decay,
             rmsprop_momentum=p.rmsprop_momentum, rmsprop_epsilon=p.rmsprop_epsilon,
             adam_beta1=p.adam_beta1, adam_beta2=p.adam_beta2, adam_epsilon=p.adam_epsilon)
-        self.strategy = make_strategy(p, self.world, self.flat)
+        self.strategy = make_strategy(p, self.world, self.flat, self.tower_mode, self.num_gpus)
         self.input = self._make_input()
         self._built = True
 
@@ -411,6 +432,11 @@ class BenchmarkCNN:
         if need_loss and p.loss_type_to_report == "total_loss" and p.weight_decay:
             # the reported total loss uses the weights of this step's forward
             loss = loss + len(self.devices) * p.weight_decay * self.l2_loss_value()
+        if need_loss and self.tower_mode:
+            # the reported loss of one worker is the mean over its towers
+            lt = loss.detach().reshape(1).float().clone()
+            comm.all_reduce(lt)
+            loss = lt[0] / self.num_gpus
         grad_scale = self.strategy.grad_scale
         if self.loss_scale:
             grad_scale /= self.loss_scale
@@ -419,12 +445,27 @@ class BenchmarkCNN:
             skip = self._auto_loss_scale_check()
         if not skip:
             self.strategy.before_update(step)
-            wd = (p.weight_decay or 0.0) * len(self.devices)
+            wd = (p.weight_decay or 0.0) * self._l2_multiplier()
+            if self.strategy.update_is_empty:
+                wd = 0.0
             self.optimizer.step(self.learning_rate(step), grad_scale=grad_scale,
                                 weight_decay=wd, clip=p.gradient_clip)
             self.strategy.after_update(step)
         self.global_step += 1
         return loss, acc
+
+    def _l2_multiplier(self) -> float:
+        """Copies of wd * w in the applied gradient.  The reference adds the
+        L2 loss (x num_devices) on the last tower only and aggregates tower /
+        worker gradients before applying (tcb/benchmark_cnn.py:3070-3099); the
+        fused optimizer adds wd * w after grad_scale, so the multiplier is
+        grad_scale x (L2 copies summed by the aggregation)."""
+        s = self.strategy.grad_scale
+        if self.tower_mode:
+            return s * self.num_gpus
+        if self.num_gpus > 1:
+            return s
+        return s * (self.world.size if self.strategy.reduces_gradients else 1)
 
     def _auto_loss_scale_check(self) -> bool:
         """Dynamic loss scaling (tcb/variable_mgr_util.py:51-139): halve the

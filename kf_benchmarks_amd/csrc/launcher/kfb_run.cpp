@@ -15,7 +15,11 @@
 // "exit on error: <k> tasks failed".
 //
 // usage: kfb-run -np N [-port-range 10000-11000] [-logdir DIR] [-q]
-//                [-timeout SECONDS] [-H 127.0.0.1:N] [-master-port P] prog args...
+//                [-timeout SECONDS] [-H 127.0.0.1:N] [-master-port P] [-chief-only]
+//                prog args...
+// -chief-only echoes rank 0's output unprefixed and keeps the other ranks'
+// output in their log files only (used when one --num_gpus=N command is run
+// as N tower processes, so the console looks like a single-process run).
 
 #include <fcntl.h>
 #include <poll.h>
@@ -89,11 +93,20 @@ bool port_free(int port) {
   return ok;
 }
 
+bool g_chief_only = false;  // -chief-only: echo rank 0 verbatim, others to logs only
+
 void emit(Peer& p, Stream& s, const std::string& line, bool quiet, int color) {
   if (s.log) {
     fwrite(line.data(), 1, line.size(), s.log);
     fputc('\n', s.log);
     fflush(s.log);
+  }
+  if (g_chief_only) {
+    if (p.rank != 0) return;
+    FILE* o = s.is_err ? stderr : stdout;
+    fprintf(o, "%s\n", line.c_str());
+    fflush(o);
+    return;
   }
   if (quiet) return;
   FILE* o = s.is_err ? stderr : stdout;
@@ -162,6 +175,8 @@ int main(int argc, char** argv) {
       logdir = need("-logdir");
     } else if (a == "-q") {
       quiet = true;
+    } else if (a == "-chief-only") {
+      g_chief_only = true;
     } else if (a == "-timeout") {
       timeout = atof(need("-timeout"));
     } else if (a == "-grace") {
@@ -219,7 +234,7 @@ int main(int argc, char** argv) {
   for (int r = 0; r < np; ++r)
     peers_spec += (r ? "," : "") + std::string("127.0.0.1:") + std::to_string(ports[r]);
 
-  if (!quiet) {
+  if (!quiet && !g_chief_only) {
     fprintf(stdout, "[I] will parallel run %d instances of %s with [", np, cmd[0]);
     for (size_t k = 1; cmd[k]; ++k) fprintf(stdout, "%s\"%s\"", k > 1 ? " " : "", cmd[k]);
     fprintf(stdout, "]\n");
@@ -355,9 +370,11 @@ int main(int argc, char** argv) {
     if (p.out.log) fclose(p.out.log);
     if (p.err.log) fclose(p.err.log);
   }
-  fprintf(stdout, "[I] all %d/%d local peers finished, took %.3fs\n", finished, np,
-          now_s() - t0);
-  fflush(stdout);
+  if (!g_chief_only) {
+    fprintf(stdout, "[I] all %d/%d local peers finished, took %.3fs\n", finished, np,
+            now_s() - t0);
+    fflush(stdout);
+  }
   if (failed) {
     fprintf(stderr, "exit on error: %d tasks failed\n", failed);
     return 1;

@@ -54,8 +54,8 @@ class FakeDataInput:
         import numpy as np
         from .. import cnn_util
         self.bench = bench
-        bs = bench.batch_size
-        shift = bench.task_index / float(max(bench.num_workers, 1))
+        bs = bench.local_batch_size
+        shift = bench.task_index / float(max(bench.num_replicas, 1))
         imgs = cnn_util.roll_numpy_batches(np.asarray(images, dtype=np.float32), bs, shift)
         labs = cnn_util.roll_numpy_batches(np.asarray(labels), bs, shift)
         self.images = torch.from_numpy(imgs / 127.5 - 1.0).to(bench.device, bench.compute_dtype)
@@ -64,7 +64,7 @@ class FakeDataInput:
         self.i = 0
 
     def next(self):
-        bs = self.bench.batch_size
+        bs = self.bench.local_batch_size
         k = self.i % self.n
         self.i += 1
         return (self.images[k * bs:(k + 1) * bs].contiguous(),

@@ -662,10 +662,11 @@ def get_preprocessor(bench, subset):
     cls = dataset.get_input_preprocessor(params.input_preprocessor or "default")
     train = subset == "train"
     shapes = bench.model.get_input_shapes(subset)
-    shift = bench.task_index / float(max(bench.num_workers, 1))
+    shift = bench.task_index / float(max(bench.num_replicas, 1))
+    bs = bench.local_batch_size
     if cls is LibrispeechPreprocessor:
-        return cls(bench.batch_size, shapes, 1, np.float32, train)
-    return cls(bench.batch_size, shapes, 1, np.float32, train, params.distortions,
+        return cls(bs, shapes, 1, np.float32, train)
+    return cls(bs, shapes, 1, np.float32, train, params.distortions,
                params.resize_method, shift_ratio=shift,
                summary_verbosity=params.summary_verbosity,
                distort_color_in_yiq=params.distort_color_in_yiq,
@@ -674,5 +675,5 @@ def get_preprocessor(bench, subset):
 
 def make_batch_iterator(bench, subset="train"):
     pre = get_preprocessor(bench, subset)
-    shift = bench.task_index / float(max(bench.num_workers, 1))
+    shift = bench.task_index / float(max(bench.num_replicas, 1))
     return pre.minibatch(bench.dataset, subset, bench.params, shift_ratio=shift)

@@ -17,6 +17,8 @@ from . import cnn_util
 from .constants import BenchmarkMode
 from .utils import checkpoint as ckpt_lib
 
+from .parallel import comm  # noqa: E402
+
 log_fn = cnn_util.log_fn
 
 
@@ -35,8 +37,15 @@ def eval_once(bench, input_source, num_batches, global_step, summary_writer=None
         with torch.no_grad():
             res = bench.net(images, phase_train=False)
             acc = bench.model.accuracy_function((images, labels), res.logits)
-        results = {"top_1_accuracy": float(acc["top_1_accuracy"]) / batch,
-                   "top_5_accuracy": float(acc["top_5_accuracy"]) / batch,
+            counts = torch.stack([torch.as_tensor(acc["top_1_accuracy"], dtype=torch.float32),
+                                  torch.as_tensor(acc["top_5_accuracy"], dtype=torch.float32)])
+            if getattr(bench, "tower_mode", False):
+                # towers of one worker: the accuracy is over the global batch
+                counts = counts.to(bench.device)
+                comm.all_reduce(counts)
+            counts = counts.cpu()
+        results = {"top_1_accuracy": float(counts[0]) / batch,
+                   "top_5_accuracy": float(counts[1]) / batch,
                    "global_step": global_step}
         results = bench.model.postprocess(results)
         top1 += results["top_1_accuracy"]

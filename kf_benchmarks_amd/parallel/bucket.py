@@ -17,6 +17,14 @@ each MI355X; per-message latency is ~10-30 us, so buckets of tens of MB keep
 the links busy while leaving enough buckets (ResNet-50: 102 MB fp32 -> 4 at
 25 MB) to overlap with backward.  ``--gradient_wire_dtype=bf16|fp16`` halves
 the bytes on the wire (the reference's --compact_gradient_transfer).
+
+``num_buckets`` (``--gradient_repacking=k``) splits the flat gradient into k
+equal buckets instead of size-capped ones; ``shards`` (``alg#shards`` in
+``--all_reduce_spec``) issues each bucket as that many concurrent
+collectives; ``relaxed`` (``--variable_consistency=relaxed``) defers the
+gradients by one step: step t's reduction runs while step t+1 computes, and
+step t applies step t-1's result (zeros at the first step), as the
+StagingArea deferral of tcb/batch_allreduce.py:353-389.
 """
 
 from __future__ import annotations
@@ -30,12 +38,24 @@ from . import comm
 
 class BucketReducer:
     def __init__(self, flat, bucket_mb: float = 25.0, wire_dtype: Optional[torch.dtype] = None,
-                 overlap: bool = True, op: str = "sum", group=None):
+                 overlap: bool = True, op: str = "sum", group=None, num_buckets: int = 0,
+                 relaxed: bool = False, shards: int = 1):
         self.flat = flat
         self.wire_dtype = wire_dtype if wire_dtype not in (None, torch.float32) else None
         self.op = op
         self.group = group
-        limit = max(int(bucket_mb * (1 << 20) / 4), 1)
+        self.shards = max(int(shards), 1)
+        self.relaxed = bool(relaxed)
+        self._stash = None
+        self._stash_works = None
+        self._relaxed_step = 0
+        self.deferred_empty = False
+        if relaxed:
+            overlap = False
+        if num_buckets and num_buckets > 0:
+            limit = max((flat.numel + num_buckets - 1) // num_buckets, 1)
+        else:
+            limit = max(int(bucket_mb * (1 << 20) / 4), 1)
         self.buckets: List[List[int]] = []  # [start, end) in elements
         self.param_bucket = {}
         segs = flat.segments()
@@ -92,23 +112,55 @@ class BucketReducer:
                 self._launch(self._next)
                 self._next += 1
 
-    def _launch(self, b):
+    def _launch(self, b, src=None):
         s, e = self.buckets[b]
-        view = self.flat.grad[s:e]
+        view = (self.flat.grad if src is None else src)[s:e]
         buf = view.to(self.wire_dtype) if self.wire_dtype is not None else view
-        work = comm.all_reduce(buf, op=self.op, async_op=True)
-        self._works.append((work, buf, view))
+        pieces = torch.tensor_split(buf, self.shards) if self.shards > 1 else (buf,)
+        for piece in pieces:
+            work = comm.all_reduce(piece, op=self.op, async_op=True)
+            self._works.append((work, None, None))
+        self._works[-1] = (self._works[-1][0], buf, view)
+
+    def _finish_relaxed(self):
+        """Apply last step's reduced gradients; start reducing this step's."""
+        g = self.flat.grad
+        if self._stash is None:
+            self._stash = [torch.empty_like(g), torch.empty_like(g)]
+        cur = self._stash[self._relaxed_step % 2]
+        cur.copy_(g)
+        prev_works = self._stash_works
+        self._works = []
+        for b in range(len(self.buckets)):
+            self._launch(b, src=cur)
+        self._stash_works = self._works
+        self._works = []
+        self.deferred_empty = prev_works is None
+        if prev_works is None:
+            g.zero_()  # first step: nothing reduced yet
+        else:
+            for work, buf, view in prev_works:
+                if work is not None:
+                    work.wait()
+                if buf is not None and buf is not view:
+                    view.copy_(buf)
+            g.copy_(self._stash[(self._relaxed_step - 1) % 2])
+        self._relaxed_step += 1
+        self._active = False
 
     def finish(self):
         """Launch whatever did not fire (unused params, overlap off) and make
         the current stream wait for every bucket."""
+        if self.relaxed:
+            self._finish_relaxed()
+            return
         while self._next < len(self.buckets):
             self._launch(self._next)
             self._next += 1
         for work, buf, view in self._works:
             if work is not None:
                 work.wait()
-            if buf is not view:
+            if buf is not None and buf is not view:
                 view.copy_(buf)
         self._works = []
         self._active = False

@@ -60,8 +60,11 @@ def env_world_size() -> int:
     return int(os.environ.get("WORLD_SIZE", "1"))
 
 
-def init_world(device_type: str = "cuda", timeout_s: int = 1800) -> World:
-    """Initializes the default process group once (idempotent)."""
+def init_world(device_type: str = "cuda", all_reduce_spec: Optional[str] = None,
+               timeout_s: int = 1800) -> World:
+    """Initializes the default process group once (idempotent).
+    ``all_reduce_spec`` picks RCCL's algorithm / channel count before the
+    communicator exists (parallel/allreduce.py:rccl_env_for_spec)."""
     global _WORLD
     if _WORLD is not None:
         return _WORLD
@@ -72,6 +75,10 @@ def init_world(device_type: str = "cuda", timeout_s: int = 1800) -> World:
         _WORLD = World(0, 1, local_rank, None)
         return _WORLD
     backend = "nccl" if device_type == "cuda" else "gloo"
+    if backend == "nccl" and all_reduce_spec:
+        from .allreduce import rccl_env_for_spec
+        for k, v in rccl_env_for_spec(all_reduce_spec).items():
+            os.environ.setdefault(k, v)
     here = False
     if not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

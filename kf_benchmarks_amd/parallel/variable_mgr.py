@@ -43,17 +43,20 @@ class Strategy:
     each_tower_has_variables = True
 
     def __init__(self, params, world: comm.World, flat, bucket_mb=64.0, wire_dtype=None,
-                 overlap=True):
+                 overlap=True, tower_scale=1.0, num_buckets=0, relaxed=False, shards=1):
         self.params = params
         self.world = world
         self.flat = flat
+        self.tower_scale = float(tower_scale)
         self.reducer: Optional[BucketReducer] = None
         if self.reduces_gradients and world.size > 1:
-            self.reducer = BucketReducer(flat, bucket_mb, wire_dtype, overlap=overlap)
+            self.reducer = BucketReducer(flat, bucket_mb, wire_dtype, overlap=overlap,
+                                         num_buckets=num_buckets, relaxed=relaxed,
+                                         shards=shards)
 
     @property
     def grad_scale(self) -> float:
-        return 1.0
+        return self.tower_scale
 
     def broadcast_initial_model(self, slots=()):
         """Rank-0 broadcast of every variable (+ optimizer slots, BN stats):
@@ -83,6 +86,12 @@ class Strategy:
     def after_update(self, step: int):
         pass
 
+    @property
+    def update_is_empty(self) -> bool:
+        """True when the gradient to apply is the all-zero first step of
+        --variable_consistency=relaxed (no weight decay either)."""
+        return self.reducer is not None and self.reducer.deferred_empty
+
     def describe(self) -> str:
         return self.name
 
@@ -111,7 +120,7 @@ class KungFuSyncSGD(Strategy):
 
     @property
     def grad_scale(self):
-        return 1.0 / self.world.size
+        return self.tower_scale / self.world.size
 
 
 class KungFuSMA(Strategy):
@@ -167,15 +176,36 @@ class KungFuAdaSGD(Strategy):
             self.sma.before_update(step)
 
 
-def make_strategy(params, world, flat):
+MEAN_OVER_TOWERS = ("parameter_server", "distributed_replicated")
+
+
+def make_strategy(params, world, flat, tower_mode=False, num_gpus=1):
+    """``tower_mode``: the ranks are the towers of ONE worker (--num_gpus=N
+    relaunched as N processes).  The reference averages tower gradients in
+    parameter_server mode and sums them in the replicated/all-reduce modes;
+    with a SUM all-reduce that is a 1/N scale for the former.  Without a
+    launcher the N towers run as one big batch (already a tower mean), so
+    the sum modes scale by N instead."""
     vu = params.variable_update
     wire = {"auto": None, "fp32": None, "bf16": torch.bfloat16,
             "fp16": torch.float16}[params.gradient_wire_dtype]
     if params.gradient_wire_dtype == "auto" and params.compact_gradient_transfer \
             and params.gradient_repacking:
         wire = torch.float16
+    if tower_mode:
+        tower_scale = 1.0 / num_gpus if vu in MEAN_OVER_TOWERS else 1.0
+    elif num_gpus > 1:
+        tower_scale = 1.0 if vu in MEAN_OVER_TOWERS else float(num_gpus)
+    else:
+        tower_scale = 1.0
+    shards = 1
+    if params.all_reduce_spec:
+        from .allreduce import parse_all_reduce_spec
+        shards = max(s.shards for s in parse_all_reduce_spec(params.all_reduce_spec))
     kw = dict(bucket_mb=params.bucket_size_mb, wire_dtype=wire,
-              overlap=params.overlap_gradient_allreduce)
+              overlap=params.overlap_gradient_allreduce, tower_scale=tower_scale,
+              num_buckets=params.gradient_repacking,
+              relaxed=params.variable_consistency == "relaxed", shards=shards)
     if vu == "independent":
         return IndependentStrategy(params, world, flat, **kw)
     if vu == "kungfu":

@@ -67,7 +67,7 @@ D.DEFINE_integer("per_gpu_thread_count", 0, "Threads per GPU (TF knob; ignored).
 D.DEFINE_boolean("hierarchical_copy", False,
                  "Two-level reduce for --variable_update=replicated.")
 D.DEFINE_enum("network_topology", NetworkTopology.DGX1,
-              (NetworkTopology.DGX1, NetworkTopology.GCP_V100),
+              (NetworkTopology.DGX1, NetworkTopology.GCP_V100, NetworkTopology.XGMI_MESH),
               "Topology used by --hierarchical_copy.")
 D.DEFINE_integer("gradient_repacking", 0,
                  "Concat all grads and re-split into this many packs before all-reduce.",

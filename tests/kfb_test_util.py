@@ -157,7 +157,11 @@ def manually_compute_losses(inputs, num_workers, params, aggregation):
             losses[w].append(base if params.loss_type_to_report == "base_loss" else total)
             grads.append((m * b, m * a))  # data gradient; wd added at update
         if aggregation == "sum":
-            agg = [(sum(g[0] for g in grads), sum(g[1] for g in grads))] * num_workers
+            # every worker's gradient carries its own wd * w term (the
+            # reference oracle applies each worker's total-loss gradient,
+            # tcb/test_util.py:365-443); replicas are identical in sum modes
+            agg = [(sum(g[0] for g in grads) + (num_workers - 1) * wd * A[0],
+                    sum(g[1] for g in grads) + (num_workers - 1) * wd * B[0])] * num_workers
         elif aggregation == "mean":
             agg = [(sum(g[0] for g in grads) / num_workers,
                     sum(g[1] for g in grads) / num_workers)] * num_workers

@@ -56,3 +56,22 @@ def test_two_peer_kungfu_training(tmp_path):
     for port in (23200, 23201):
         with open(tmp_path / ("127.0.0.1.%d.stdout.log" % port)) as f:
             assert "total images/sec" in f.read()
+
+
+def test_num_gpus_runs_as_tower_processes(tmp_path):
+    """One --num_gpus=2 command -> 2 tower ranks; the console shows one
+    worker's output (tower 0) with the 2-device global batch."""
+    code = ("import sys; from kf_benchmarks_amd import cli, params as P, flags;"
+            "argv=sys.argv[1:]; p=P.make_params(**flags.parse_flags(argv));"
+            "sys.exit(cli._launch_towers(p, argv))")
+    args = ["--device=cpu", "--data_format=NHWC", "--model=trivial", "--batch_size=4",
+            "--num_batches=3", "--num_warmup_batches=1", "--num_gpus=2",
+            "--variable_update=replicated"]
+    env = _env()
+    env["KFB_TOWER_LOGDIR"] = str(tmp_path)
+    r = subprocess.run([sys.executable, "-c", code] + args, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.count("total images/sec") == 1
+    assert "8 global" in r.stdout and "[127.0.0.1" not in r.stdout
+    assert len(list(tmp_path.glob("127.0.0.1.*.stdout.log"))) == 2

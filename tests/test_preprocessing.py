@@ -111,7 +111,7 @@ def test_generated_fixture_and_batches(tmp_path):
     b.model = model_config.get_model_config("trivial", b.dataset, b.params)
     b.batch_size = 8
     b.model.set_batch_size(8)
-    b.task_index, b.num_workers = 0, 1
+    b.task_index, b.num_workers, b.num_replicas, b.local_batch_size = 0, 1, 1, 8
     it = pre.make_batch_iterator(b, "train")
     imgs, labels = next(it)
     assert imgs.shape == (8, 227, 227, 3) and imgs.dtype == np.uint8

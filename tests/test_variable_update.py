@@ -54,14 +54,15 @@ def _free_port():
     return port
 
 
-def run_workers(nworkers, flag_kwargs, tmp_path, timeout=240):
+def run_workers(nworkers, flag_kwargs, tmp_path, timeout=240, extra_env=None):
     """Launch nworkers processes of tests/dist_worker.py; returns per-rank losses."""
     port = _free_port()
     procs = []
     for r in range(nworkers):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(nworkers), LOCAL_RANK=str(r),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1",
-                   PYTHONPATH=ROOT + os.pathsep + os.path.join(ROOT, "tests"))
+                   PYTHONPATH=ROOT + os.pathsep + os.path.join(ROOT, "tests"),
+                   **(extra_env or {}))
         out = tmp_path / ("rank%d.json" % r)
         cmd = [sys.executable, os.path.join(ROOT, "tests", "dist_worker.py"), str(out),
                json.dumps(flag_kwargs)]
@@ -116,3 +117,84 @@ def test_two_workers_async_pair_averaging(tmp_path):
     for r in res:
         assert len(r["losses"]) == 6
         assert all(np.isfinite(r["losses"]))
+
+
+def _tower_oracle(inputs, ntowers, params, mean):
+    """One worker with ``ntowers`` towers (tower t reads the data rolled by
+    t/ntowers): tower gradients averaged (parameter_server) or summed
+    (replicated), L2 counted once per tower sum as the reference's
+    last-tower x num_devices term; reported loss = mean tower loss."""
+    bs = params.batch_size
+    x = inputs.astype(np.float64) / 127.5 - 1.0
+    nb = x.shape[0] // bs
+    from kf_benchmarks_amd import cnn_util
+    data = [cnn_util.roll_numpy_batches(x, bs, t / float(ntowers)).reshape(nb, bs)
+            for t in range(ntowers)]
+    a, b = tu.TestCNNModel.VAR_A_INITIAL_VALUE, tu.TestCNNModel.VAR_B_INITIAL_VALUE
+    wd, lr = params.weight_decay, params.init_learning_rate
+    losses = []
+    for step in range(params.num_batches):
+        ms = [data[t][step % nb].mean() for t in range(ntowers)]
+        losses.append(float(np.mean([m * a * b for m in ms])))
+        ga = sum(m * b for m in ms)
+        gb = sum(m * a for m in ms)
+        if mean:
+            ga, gb = ga / ntowers + wd * a, gb / ntowers + wd * b
+        else:
+            ga, gb = ga + ntowers * wd * a, gb + ntowers * wd * b
+        a, b = a - lr * ga, b - lr * gb
+    return losses
+
+
+@pytest.mark.parametrize("vu,mean", [("parameter_server", True), ("replicated", False)])
+def test_two_towers_one_worker(vu, mean, tmp_path):
+    """--num_gpus=2 in one command runs as 2 tower processes (KFB_TOWER_GROUP)
+    reporting as one worker."""
+    kw = dict(variable_update=vu, num_batches=4, num_gpus=2, loss_type_to_report="base_loss")
+    res = run_workers(2, kw, tmp_path, extra_env={"KFB_TOWER_GROUP": "1"})
+    params = tu.get_var_update_params(**kw)
+    expected = _tower_oracle(tu.get_fake_var_update_inputs(), 2, params, mean)
+    np.testing.assert_allclose(res[0]["losses"], expected, rtol=1e-5, atol=0)
+
+
+@pytest.mark.parametrize("extra", [dict(gradient_repacking=3, compact_gradient_transfer=False),
+                                   dict(gradient_repacking=3),  # fp16 on the wire
+                                   dict(all_reduce_spec="xring#2"), dict(bucket_size_mb=1e-6)])
+def test_two_workers_bucket_options_match_sum(extra, tmp_path):
+    """Repacking into k buckets, sharded collectives and one-tensor buckets
+    reduce exactly like the default plan."""
+    kw = dict(variable_update="replicated", num_batches=4, **extra)
+    res = run_workers(2, kw, tmp_path)
+    params = tu.get_var_update_params(**kw)
+    expected = tu.manually_compute_losses(tu.get_fake_var_update_inputs(), 2, params, "sum")
+    compact = params.gradient_repacking and params.compact_gradient_transfer
+    for r in range(2):
+        np.testing.assert_allclose(res[r]["losses"], expected[r], rtol=1e-3 if compact else 1e-5,
+                                   atol=0)
+
+
+def test_two_workers_relaxed_consistency(tmp_path):
+    """--variable_consistency=relaxed applies the previous step's reduced
+    gradients (nothing at the first step)."""
+    kw = dict(variable_update="replicated", num_batches=5, variable_consistency="relaxed",
+              loss_type_to_report="base_loss")
+    res = run_workers(2, kw, tmp_path)
+    params = tu.get_var_update_params(**kw)
+    from kf_benchmarks_amd import cnn_util
+    x = tu.get_fake_var_update_inputs().astype(np.float64) / 127.5 - 1.0
+    bs = params.batch_size
+    data = [cnn_util.roll_numpy_batches(x, bs, w / 2.0).reshape(-1, bs) for w in range(2)]
+    a, b = tu.TestCNNModel.VAR_A_INITIAL_VALUE, tu.TestCNNModel.VAR_B_INITIAL_VALUE
+    wd, lr = params.weight_decay, params.init_learning_rate
+    prev = None
+    exp = [[], []]
+    for step in range(params.num_batches):
+        ms = [data[w][step % data[w].shape[0]].mean() for w in range(2)]
+        for w in range(2):
+            exp[w].append(ms[w] * a * b)
+        cur = (sum(m * b for m in ms), sum(m * a for m in ms))
+        if prev is not None:
+            a, b = a - lr * (prev[0] + 2 * wd * a), b - lr * (prev[1] + 2 * wd * b)
+        prev = cur
+    for r in range(2):
+        np.testing.assert_allclose(res[r]["losses"], exp[r], rtol=1e-5, atol=0)
