@@ -252,6 +252,30 @@ class BenchmarkCNN:
         if self.device_type == "cuda" and not torch.cuda.is_available():
             raise RuntimeError("--device=gpu but no GPU is visible; use --device=cpu "
                                "--data_format=NHWC for the plumbing config")
+        self.cluster_manager = None
+        if params.job_name:
+            from .platforms import util as platforms_util
+            self.cluster_manager = platforms_util.get_cluster_manager(params)
+            if params.job_name in ("ps", "controller"):
+                # stateless roles: no world, no device (see join_server)
+                self.world = comm.World()
+                self.num_workers = self.cluster_manager.num_workers()
+                self.num_replicas, self.task_index = self.num_workers, params.task_index
+                self.tower_mode = False
+                self.local_batch_size = self.batch_size
+                self.device = torch.device("cpu")
+                self.devices = ["/job:%s/task:%d/cpu:0" % (params.job_name, params.task_index)]
+                self.num_batches, self.num_epochs = get_num_batches_and_epochs(
+                    params, self.batch_size * self.num_workers,
+                    self.dataset.num_examples_per_epoch("train"))
+                self.compute_dtype = self.model.data_type
+                self.ignored_flags = []
+                self._built = False
+                self.global_step = 0
+                self.loss_scale = None
+                self.benchmark_logger = None
+                return
+            self.cluster_manager.setup_worker_env()
         self.world = comm.init_world(self.device_type, params.all_reduce_spec)
         self.tower_mode = (os.environ.get("KFB_TOWER_GROUP") == "1" and self.num_gpus > 1
                            and self.world.size == self.num_gpus)
@@ -497,6 +521,11 @@ class BenchmarkCNN:
 
     # ------------------------------------------------------------------- run
     def run(self):
+        if self.params.job_name in ("ps", "controller"):
+            log_fn("Running %s %d: waiting for the workers to finish"
+                   % (self.params.job_name, self.params.task_index))
+            self.cluster_manager.join_server()
+            return {}
         if self._doing_eval:
             from .eval import run_eval
             return run_eval(self)
@@ -611,6 +640,10 @@ class BenchmarkCNN:
             self.saver.save(p.train_dir, self.global_step)
         tracer.finish()
         self.strategy.close()
+        if self.cluster_manager is not None:
+            self.world.barrier(self.device if self.device_type == "cuda" else None)
+            if self.world.is_chief:
+                self.cluster_manager.mark_done()
         if self.summary_writer is not None:
             self.summary_writer.close()
         if p.variable_update == "kungfu" or p.sync_on_finish:

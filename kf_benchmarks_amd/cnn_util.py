@@ -118,23 +118,87 @@ class ImageProducer:
 
 
 class BaseClusterManager:
-    """Cluster description for the distributed modes.  On this stack the
-    'cluster' is the torch.distributed world; ps/worker host lists are
-    accepted for CLI compatibility and only their counts are used."""
+    """Cluster description from --ps_hosts / --worker_hosts
+    (tcb/cnn_util.py:201-230)."""
 
     def __init__(self, params):
         self._ps = [h for h in (params.ps_hosts or "").split(",") if h]
         self._workers = [h for h in (params.worker_hosts or "").split(",") if h]
+        self._cluster_spec = {"worker": list(self._workers)}
+        if self._ps:
+            self._cluster_spec["ps"] = list(self._ps)
 
     def get_target(self):
         return ""
 
+    def get_cluster_spec(self):
+        return self._cluster_spec
+
     def join_server(self):
-        raise RuntimeError("parameter-server processes are not used on this stack: every "
-                           "rank is a worker (run with --job_name=worker or no job_name)")
+        raise NotImplementedError("join must be implemented by subclass")
 
     def num_workers(self):
         return max(len(self._workers), 1)
 
     def num_ps(self):
         return len(self._ps)
+
+
+DONE_KEY = "kfb/job_done"
+
+
+class TorchClusterManager(BaseClusterManager):
+    """The reference's gRPC cluster (tcb/cnn_util.py:232-251) mapped onto a
+    torch.distributed world: each ``--job_name=worker --task_index=i`` task
+    is rank i of ``len(worker_hosts)``; the first worker's host:port is the
+    rendezvous (TCPStore) address.  Variables are replicated on every GPU,
+    so ``ps`` and ``controller`` tasks hold no state: ``join_server`` blocks
+    until worker 0 marks the job done in the store, so launch scripts that
+    start ps tasks keep working."""
+
+    def __init__(self, params, config_proto=None):
+        super().__init__(params)
+        del config_proto
+        self.params = params
+        if not self._workers:
+            raise ValueError("--worker_hosts must be set with --job_name")
+        host, port = self._workers[0].rsplit(":", 1)
+        self.master_addr = "127.0.0.1" if host in ("localhost", "") else host
+        self.master_port = int(port)
+
+    def setup_worker_env(self):
+        """Exports RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* for this task."""
+        import os
+        p = self.params
+        if p.job_name != "worker":
+            return
+        me = self._workers[p.task_index].rsplit(":", 1)[0]
+        local = sum(1 for h in self._workers[:p.task_index] if h.rsplit(":", 1)[0] == me)
+        os.environ.setdefault("RANK", str(p.task_index))
+        os.environ.setdefault("WORLD_SIZE", str(len(self._workers)))
+        os.environ.setdefault("LOCAL_RANK", str(local))
+        os.environ.setdefault("MASTER_ADDR", self.master_addr)
+        os.environ.setdefault("MASTER_PORT", str(self.master_port))
+
+    def join_server(self, timeout_s: float = 7 * 24 * 3600):
+        import datetime
+        from torch.distributed import TCPStore
+        store = TCPStore(self.master_addr, self.master_port, is_master=False,
+                         timeout=datetime.timedelta(seconds=timeout_s))
+        try:
+            store.wait([DONE_KEY])
+        except RuntimeError:
+            pass  # worker 0 closed the store: the job is over
+
+    @staticmethod
+    def mark_done():
+        """Called by worker 0 at the end of the run."""
+        import torch.distributed as dist
+        if dist.is_initialized():
+            try:
+                dist.distributed_c10d._get_default_store().set(DONE_KEY, "1")
+            except Exception:  # pragma: no cover - store already gone
+                pass
+
+
+GrpcClusterManager = TorchClusterManager

@@ -75,3 +75,60 @@ def test_num_gpus_runs_as_tower_processes(tmp_path):
     assert r.stdout.count("total images/sec") == 1
     assert "8 global" in r.stdout and "[127.0.0.1" not in r.stdout
     assert len(list(tmp_path.glob("127.0.0.1.*.stdout.log"))) == 2
+
+
+def test_all_reduce_benchmark_two_ranks(tmp_path):
+    """tcb/all_reduce_benchmark_test.py: the last log line is
+    'Average time per step: <float>' (here per rank, via kfb-run)."""
+    import re
+    cmd = [sys.executable, "-m", "kf_benchmarks_amd.all_reduce_benchmark", "--device=cpu",
+           "--data_format=NHWC", "--model=lenet", "--variable_update=replicated",
+           "--num_batches=3", "--num_warmup_batches=1", "--iters_per_step=2",
+           "--gradient_repacking=2", "--compact_gradient_transfer=false"]
+    r = launcher.run(2, cmd, logdir=str(tmp_path), quiet=True, capture=True,
+                     port_range="23300-23400", env=_env(), timeout=300)
+    assert r.returncode == 0, r.stderr
+    for port in (23300, 23301):
+        with open(tmp_path / ("127.0.0.1.%d.stdout.log" % port)) as f:
+            lines = [ln for ln in f.read().splitlines() if ln.strip()]
+        avg = [ln for ln in lines if ln.startswith("Average time per step")]
+        assert avg and re.match(r"^Average time per step: [0-9.e-]+$", avg[-1])
+
+
+def test_ps_worker_cluster_flags(tmp_path):
+    """--job_name/--task_index/--worker_hosts/--ps_hosts (the reference's
+    gRPC cluster) as a torch.distributed world; the ps task waits for the
+    workers and exits cleanly."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    common = ["--device=cpu", "--data_format=NHWC", "--model=trivial", "--batch_size=4",
+              "--num_batches=3", "--num_warmup_batches=1", "--variable_update=parameter_server",
+              "--worker_hosts=127.0.0.1:%d,127.0.0.1:%d" % (port, port + 1),
+              "--ps_hosts=127.0.0.1:%d" % (port + 2)]
+    env = _env()
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    script = os.path.join(ROOT, "tf_cnn_benchmarks.py")
+    procs = [subprocess.Popen([sys.executable, script, "--job_name=ps", "--task_index=0"] + common,
+                              env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                              text=True)]
+    for t in range(2):
+        procs.append(subprocess.Popen([sys.executable, script, "--job_name=worker",
+                                       "--task_index=%d" % t] + common, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      text=True))
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=240)
+            outs.append(out)
+            assert p.returncode == 0, out
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert "total images/sec" in outs[1] and "total images/sec" in outs[2]
+    assert "Running ps 0" in outs[0]
