@@ -27,7 +27,7 @@ import torch
 
 from . import benchmark, flags, optim, params as params_lib
 from .cnn_util import log_fn
-from .models.model import Network
+from .models.model import make_network
 from .parallel.bucket import BucketReducer
 from .parallel.variable_mgr import make_strategy
 
@@ -43,7 +43,7 @@ def run_benchmark(bench, num_iters: int):
                          "the all-reduce benchmark")
     if p.variable_consistency == "relaxed":
         raise ValueError("--variable_consistency=relaxed is not supported")
-    net = Network(bench.model, bench.dataset.num_classes, bench.device, bench.compute_dtype,
+    net = make_network(bench.model, bench.dataset.num_classes, bench.device, bench.compute_dtype,
                   kernel_impl=p.kernel_impl, seed=p.tf_random_seed)
     flat = optim.FlatParams(net, None)
     strategy = make_strategy(p, bench.world, flat, bench.tower_mode, bench.num_gpus)

@@ -29,7 +29,7 @@ import torch
 from . import cnn_util, datasets, flags, optim, params as params_lib
 from .constants import BenchmarkMode
 from .models import model_config
-from .models.model import Network
+from .models.model import make_network
 from .ops import _native
 from .parallel import comm
 from .parallel.variable_mgr import make_strategy
@@ -392,7 +392,7 @@ class BenchmarkCNN:
         torch.manual_seed(seed + self.task_index)
         np.random.seed(4321 + self.task_index)
         nclass = self.dataset.num_classes
-        self.net = Network(self.model, nclass, self.device, self.compute_dtype,
+        self.net = make_network(self.model, nclass, self.device, self.compute_dtype,
                            kernel_impl=p.kernel_impl, seed=seed)
         lp = self.compute_dtype if self.compute_dtype != torch.float32 else None
         self.flat = optim.FlatParams(self.net, lp)
@@ -434,24 +434,25 @@ class BenchmarkCNN:
         return optim.get_learning_rate(self.params, step, ex, self.model,
                                        self.batch_size * self.num_workers)
 
-    def forward_backward(self, images, labels, need_accuracy=False):
-        res = self.net(images, phase_train=True)
-        loss = self.model.loss_function((images, labels), res)
+    def forward_backward(self, inputs, need_accuracy=False):
+        res = self.net.forward_inputs(inputs, phase_train=True)
+        loss = self.model.loss_function(inputs, res)
         scaled = loss * self.loss_scale if self.loss_scale else loss
         scaled.backward()
         acc = None
         if need_accuracy:
-            acc = self.model.accuracy_function((images, labels), res.logits.detach())
+            acc = self.model.accuracy_function(inputs, res.logits.detach())
         return loss.detach(), acc
 
     def train_step(self, need_loss=False, need_accuracy=False):
         """One full training step; returns (loss_tensor, accuracy_dict)."""
         p = self.params
-        images, labels = self.input.next()
+        inputs = tuple(self.input.next())
+        self.net.global_step = self.global_step  # NASNet drop-path schedule
         self.flat.zero_grad()
         step = self.global_step
         self.strategy.before_backward(step)
-        loss, acc = self.forward_backward(images, labels, need_accuracy)
+        loss, acc = self.forward_backward(inputs, need_accuracy)
         self.strategy.after_backward(step)
         if need_loss and p.loss_type_to_report == "total_loss" and p.weight_decay:
             # the reported total loss uses the weights of this step's forward
@@ -514,9 +515,9 @@ class BenchmarkCNN:
         return False
 
     def forward_only_step(self):
-        images, labels = self.input.next()
+        inputs = tuple(self.input.next())
         with torch.no_grad():
-            res = self.net(images, phase_train=False)
+            res = self.net.forward_inputs(inputs, phase_train=False)
         return res
 
     # ------------------------------------------------------------------- run

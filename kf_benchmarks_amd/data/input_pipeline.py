@@ -29,16 +29,16 @@ class SyntheticInput:
         self.resample = bench.params.synthetic_resample
         self.seed = bench.params.tf_random_seed + 1000 * bench.task_index
         self.step = 0
-        self.images, self.labels = model.get_synthetic_inputs("input", nclass, bench.device,
-                                                              self.seed)
+        self.inputs = tuple(model.get_synthetic_inputs("input", nclass, bench.device,
+                                                       self.seed))
 
     def next(self):
         if self.resample:
             self.step += 1
             model = self.bench.model
-            self.images, self.labels = model.get_synthetic_inputs(
-                "input", self.bench.dataset.num_classes, self.bench.device, self.seed + self.step)
-        return self.images, self.labels
+            self.inputs = tuple(model.get_synthetic_inputs(
+                "input", self.bench.dataset.num_classes, self.bench.device, self.seed + self.step))
+        return self.inputs
 
     def close(self):
         pass

@@ -33,10 +33,10 @@ def eval_once(bench, input_source, num_batches, global_step, summary_writer=None
     batch = bench.batch_size
     loop_start = start = time.time()
     for step in range(num_batches):
-        images, labels = input_source.next()
+        inputs = tuple(input_source.next())
         with torch.no_grad():
-            res = bench.net(images, phase_train=False)
-            acc = bench.model.accuracy_function((images, labels), res.logits)
+            res = bench.net.forward_inputs(inputs, phase_train=False)
+            acc = bench.model.accuracy_function(inputs, res.logits)
             counts = torch.stack([torch.as_tensor(acc["top_1_accuracy"], dtype=torch.float32),
                                   torch.as_tensor(acc["top_5_accuracy"], dtype=torch.float32)])
             if getattr(bench, "tower_mode", False):

@@ -26,7 +26,7 @@ import torch
 from .. import ops
 from ..ops import conv as conv_ops
 from ..ops import nn as F
-from .layers import AffineLayer, BatchNormLayer, ConvLayer
+from .layers import AffineLayer, BatchNormLayer, ConvLayer, DepthwiseConvLayer
 
 
 class ConvNetBuilder:
@@ -135,6 +135,50 @@ class ConvNetBuilder:
                 y = F.activation(y, activation)
         self.top_layer, self.top_size = y, num_out_channels
         return y
+
+    def depthwise_conv(self, k_height, k_width, d_height=1, d_width=1, mode="SAME",
+                       input_layer=None, use_batch_norm=None, stddev=None, activation="relu",
+                       name=None):
+        """Depthwise conv (channel multiplier 1) + optional BN + activation
+        (slim.separable_conv2d with num_outputs=None)."""
+        from ..ops import depthwise as dw_ops
+        x = self.top_layer if input_layer is None else input_layer
+        C = x.shape[-1]
+        name = name or "depthwise%d" % self.counts["depthwise"]
+        self.counts["depthwise"] += 1
+        if use_batch_norm is None:
+            use_batch_norm = self.use_batch_norm
+        scope = self._scoped(name)
+        layer = self._layer(scope, lambda: DepthwiseConvLayer(
+            scope, C, k_height, k_width, stddev, self.net.init_gen, self.net.param_device))
+        self._use(x)
+        _, H, W, _ = x.shape
+        pads = F.resolve_pads(mode, H, W, k_height, k_width, d_height, d_width)
+        y = dw_ops.depthwise_conv2d(x, self._p(layer.weight),
+                                    None if self.meta else layer.weight_lp,
+                                    (d_height, d_width), pads, self.impl)
+        if use_batch_norm:
+            with self.scope(name):
+                y = self._batch_norm(y, relu=activation == "relu", **self.batch_norm_config)
+            if activation not in ("relu", None, "linear"):
+                y = F.activation(y, activation)
+        elif activation not in (None, "linear"):
+            y = F.activation(y, activation)
+        self.top_layer, self.top_size = y, C
+        return y
+
+    def separable_conv(self, num_out_channels, k_height, k_width, d_height=1, d_width=1,
+                       mode="SAME", input_layer=None, use_batch_norm=None, stddev=None,
+                       activation="relu"):
+        """Depthwise k x k then pointwise 1x1 (slim.separable_conv2d)."""
+        x = self.top_layer if input_layer is None else input_layer
+        name = "separable%d" % self.counts["separable"]
+        self.counts["separable"] += 1
+        with self.scope(name):
+            self.depthwise_conv(k_height, k_width, d_height, d_width, mode, input_layer=x,
+                                use_batch_norm=False, stddev=stddev, activation=None)
+            return self.conv(num_out_channels, 1, 1, use_batch_norm=use_batch_norm,
+                             stddev=stddev, activation=activation)
 
     # --------------------------------------------------------------- pooling
     def _pool(self, pool_name, k_height, k_width, d_height, d_width, mode, input_layer,

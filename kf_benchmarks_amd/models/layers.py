@@ -92,6 +92,34 @@ class ConvLayer(Layer):
                 raise KeyError(name)
 
 
+class DepthwiseConvLayer(Layer):
+    """Depthwise filter [KH, KW, C] (channel multiplier 1); TF layout
+    [KH, KW, C, 1] (slim.separable_conv2d ``depthwise_weights``)."""
+
+    def __init__(self, scope, channels, kh, kw, stddev, gen, device):
+        super().__init__()
+        self.tf_scope = scope
+        self.cin = self.cout = channels
+        self.kh, self.kw = kh, kw
+        w = torch.empty((kh, kw, channels), dtype=torch.float32)
+        if stddev is not None:
+            truncated_normal_(w, stddev, gen)
+        else:  # xavier over the depthwise fan (slim's default initializer)
+            glorot_uniform_(w, kh * kw, kh * kw, gen)
+        self.weight = nn.Parameter(w.to(device))
+        self.weight_lp: Optional[torch.Tensor] = None
+
+    def tf_variables(self):
+        return {"depthwise_weights": self.weight.detach().unsqueeze(-1)}
+
+    def load_tf_variable(self, name, value):
+        if name != "depthwise_weights":
+            raise KeyError(name)
+        with torch.no_grad():
+            self.weight.copy_(torch.as_tensor(value, dtype=torch.float32).reshape(
+                self.weight.shape))
+
+
 class BatchNormLayer(Layer):
     def __init__(self, scope, channels, scale, decay, eps, device):
         super().__init__()

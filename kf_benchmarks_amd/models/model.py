@@ -22,7 +22,7 @@ from torch import nn
 
 from ..ops import nn as F
 from .builder import ConvNetBuilder
-from .layers import AffineLayer, BatchNormLayer, ConvLayer, Layer
+from .layers import AffineLayer, BatchNormLayer, ConvLayer, DepthwiseConvLayer, Layer
 
 BuildNetworkResult = collections.namedtuple("BuildNetworkResult", ["logits", "extra_info"])
 
@@ -218,6 +218,11 @@ class Network(nn.Module):
             self._building = False
 
     # ------------------------------------------------------------- forward
+    def forward_inputs(self, inputs, phase_train=True):
+        """Engine entry: ``inputs`` is the tuple the input source yields
+        (images, labels) for image models."""
+        return self.forward(inputs[0], phase_train=phase_train)
+
     def forward(self, images, phase_train=True):
         model = self.model
         if phase_train and images.is_cuda:
@@ -271,7 +276,83 @@ class Network(nn.Module):
         return sum(p.numel() for _, p in self.trainable_variables())
 
 
+class ModuleModel(Model):
+    """Base for models that are not ConvNetBuilder image CNNs (NCF,
+    DeepSpeech2, ...): the model supplies a torch module whose
+    ``forward(inputs, phase_train)`` returns a BuildNetworkResult, and its own
+    inputs, loss and accuracy (the reference's model.Model API,
+    tcb/models/model.py:31-160)."""
+
+    def make_module(self, nclass: int, device, dtype, gen: torch.Generator) -> nn.Module:
+        raise NotImplementedError
+
+    def accuracy_function(self, inputs, logits):
+        return {}
+
+
+class ModuleNetwork(nn.Module):
+    """Network-compatible wrapper (trainable_variables / ordered_layers /
+    tf_variables) around a ModuleModel's torch module."""
+
+    def __init__(self, model: ModuleModel, nclass: int, device, compute_dtype=None,
+                 kernel_impl: str = "hip", seed: int = 1234):
+        super().__init__()
+        self.model = model
+        self.nclass = nclass
+        self.param_device = torch.device(device)
+        self.compute_dtype = compute_dtype or model.data_type
+        self.kernel_impl = kernel_impl
+        self.init_gen = torch.Generator().manual_seed(seed)
+        self.body = model.make_module(nclass, self.param_device, self.compute_dtype,
+                                      self.init_gen)
+
+    def forward_inputs(self, inputs, phase_train=True):
+        return self.body(inputs, phase_train)
+
+    def forward(self, inputs, phase_train=True):
+        return self.body(inputs, phase_train)
+
+    def ordered_layers(self):
+        return [m for m in self.body.modules()
+                if any(True for _ in m.parameters(recurse=False))
+                or any(True for _ in m.buffers(recurse=False))]
+
+    def trainable_variables(self):
+        return [(n.replace(".", "/"), p) for n, p in self.body.named_parameters()
+                if p.requires_grad]
+
+    def tf_variables(self, prefix="v0/cg/"):
+        out = {prefix + n.replace(".", "/"): p.detach() for n, p in self.body.named_parameters()}
+        for n, b in self.body.named_buffers():
+            out[prefix + n.replace(".", "/")] = b
+        return out
+
+    def load_tf_variables(self, values, prefix="v0/cg/", strict=True):
+        loaded = 0
+        named = dict(self.body.named_parameters())
+        named.update(dict(self.body.named_buffers()))
+        for n, t in named.items():
+            full = prefix + n.replace(".", "/")
+            if full in values:
+                with torch.no_grad():
+                    t.copy_(torch.as_tensor(values[full], dtype=t.dtype).reshape(t.shape))
+                loaded += 1
+            elif strict:
+                raise KeyError("checkpoint is missing %s" % full)
+        return loaded
+
+    def num_params(self):
+        return sum(p.numel() for _, p in self.trainable_variables())
+
+
+def make_network(model, nclass, device, compute_dtype=None, kernel_impl="hip", seed=1234):
+    cls = ModuleNetwork if isinstance(model, ModuleModel) else Network
+    return cls(model, nclass, device, compute_dtype, kernel_impl=kernel_impl, seed=seed)
+
+
 def _tf_param_name(layer, attr):
+    if isinstance(layer, DepthwiseConvLayer):
+        return "depthwise_weights"
     if isinstance(layer, ConvLayer):
         return {"weight": "conv2d/kernel", "bias": "biases"}[attr]
     if isinstance(layer, AffineLayer):

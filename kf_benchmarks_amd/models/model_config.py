@@ -39,6 +39,7 @@ _IMAGENET = {
     "mobilenet": _lazy("mobilenet_v2", "MobilenetModel"),
     "nasnet": _lazy("nasnet_model", "NasnetModel"),
     "nasnetlarge": _lazy("nasnet_model", "NasnetLargeModel"),
+    "ncf": _lazy("ncf_model", "NcfModel"),
 }
 for _d in (18, 34, 50, 101, 152, 200):
     _IMAGENET["official_resnet%d" % _d] = _lazy("official_resnet_model", "official_v1_%d" % _d)
@@ -65,7 +66,6 @@ _CIFAR = {
 
 _LIBRISPEECH = {"deepspeech2": _lazy("deepspeech", "DeepSpeech2Model")}
 _COCO = {"ssd300": _lazy("ssd_model", "SSD300Model")}
-_RECOMMENDATION = {"ncf": _lazy("ncf_model", "NcfModel")}
 
 
 def _get_model_map(dataset_name):

@@ -311,6 +311,8 @@ def activation(x, kind: Optional[str]):
         return relu(x)
     if kind == "tanh":
         return torch.tanh(x)
+    if kind == "relu6":
+        return torch.clamp(x, 0.0, 6.0)
     raise KeyError("Invalid activation type '%s'" % kind)
 
 

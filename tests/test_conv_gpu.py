@@ -141,3 +141,32 @@ def test_fwd_stats_epilogue(cuda, shape):
     tol = 4e-3 * (y.abs() + y * y).sum((0, 1, 2)).max().item()
     torch.testing.assert_close(p[0], y.sum((0, 1, 2)), rtol=1e-2, atol=tol)
     torch.testing.assert_close(p[1], (y * y).sum((0, 1, 2)), rtol=1e-2, atol=tol)
+
+
+DW_SHAPES = [(2, 14, 14, 32, 3, 1), (2, 15, 15, 24, 3, 2), (2, 9, 9, 16, 5, 1),
+             (1, 11, 11, 8, 7, 2), (2, 8, 8, 11, 3, 1)]
+
+
+@pytest.mark.parametrize("shape", DW_SHAPES, ids=[str(s) for s in DW_SHAPES])
+def test_depthwise_fwd_bwd(cuda, shape):
+    """csrc/depthwise.hip fwd / dgrad / wgrad vs the fp32 PyTorch grouped conv."""
+    from kf_benchmarks_amd.ops import depthwise as dw
+    n, H, W, C, k, s = shape
+    g = torch.Generator().manual_seed(4)
+    dt = torch.bfloat16
+    x = torch.randn(n, H, W, C, generator=g).to(dt).float()
+    w = (torch.randn(k, k, C, generator=g) / k).to(dt).float()
+    pads = F.resolve_pads("SAME", H, W, k, k, s, s)
+    xa = x.to(cuda, dt).requires_grad_(True)
+    wa = w.to(cuda).requires_grad_(True)
+    ya = dw.depthwise_conv2d(xa, wa, wa.detach().to(dt), (s, s), pads, "hip")
+    xb = x.clone().requires_grad_(True)
+    wb = w.clone().requires_grad_(True)
+    yb = dw.depthwise_reference(xb, wb, (s, s), pads)
+    torch.testing.assert_close(ya.float().cpu(), yb, rtol=2e-2, atol=2e-2)
+    dy = torch.randn(yb.shape, generator=g).to(dt).float()
+    ya.backward(dy.to(cuda, dt))
+    yb.backward(dy)
+    torch.testing.assert_close(xa.grad.float().cpu(), xb.grad, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(wa.grad.cpu(), wb.grad, rtol=3e-2,
+                               atol=2e-2 * wb.grad.abs().max().item())
