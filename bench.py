@@ -89,9 +89,11 @@ def main(argv=None):
     images = a.batch_size * n * a.steps
     value = images / elapsed
     if world.is_chief:
-        base = BASELINE_IMG_PER_SEC.get(n)
+        headline = a.model == "resnet50"
+        base = BASELINE_IMG_PER_SEC.get(n) if headline else None
         out = {
-            "metric": "images/sec (whole node) ResNet-50 synthetic at 1/2/4/8 MI355X",
+            "metric": ("images/sec (whole node) ResNet-50 synthetic at 1/2/4/8 MI355X"
+                       if headline else "images/sec (whole node) %s synthetic" % a.model),
             "value": round(value, 2),
             "unit": "images/sec",
             "n_gpus": n,
@@ -102,7 +104,8 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": round(value / base, 3) if base else None,
             "dtype": a.dtype,
-            "data": "synthetic (224x224x3 ImageNet-shaped images, random-init weights)",
+            "data": "synthetic (%dx%dx3 ImageNet-shaped images, random-init weights)"
+                    % (bench.model.image_size, bench.model.image_size),
             "config": {"model": a.model, "global_batch": a.batch_size * n, "seq_len": None,
                        "per_gpu_batch": a.batch_size, "parallelism": "dp%d" % n,
                        "variable_update": "kungfu/sync_sgd", "optimizer": a.optimizer,

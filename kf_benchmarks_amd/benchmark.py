@@ -405,6 +405,14 @@ class BenchmarkCNN:
             rmsprop_momentum=p.rmsprop_momentum, rmsprop_epsilon=p.rmsprop_epsilon,
             adam_beta1=p.adam_beta1, adam_beta2=p.adam_beta2, adam_epsilon=p.adam_epsilon)
         self.strategy = make_strategy(p, self.world, self.flat, self.tower_mode, self.num_gpus)
+        keep = [bool(self.model.l2_param_filter(n)) for n in self.flat.names]
+        self.l2_mask = None
+        if not all(keep):
+            mask = torch.zeros(self.flat.numel, dtype=torch.float32, device=self.device)
+            for k, (_, _, off, n) in zip(keep, self.flat.segments()):
+                if k:
+                    mask[off:off + n] = 1.0
+            self.l2_mask = mask
         self.input = self._make_input()
         self._built = True
 
@@ -419,8 +427,10 @@ class BenchmarkCNN:
 
     # ------------------------------------------------------------------ step
     def l2_loss_value(self):
-        """sum(w^2)/2 over trainable variables (device scalar)."""
+        """sum(w^2)/2 over the L2-regularized trainable variables (device scalar)."""
         w = self.flat.flat
+        if self.l2_mask is not None:
+            return 0.5 * (w * w * self.l2_mask).sum()
         if w.is_cuda:
             out = torch.zeros(1, dtype=torch.float32, device=w.device)
             _native.call("kfb_half_sumsq", w.data_ptr(), w.numel(), out.data_ptr(),
@@ -472,6 +482,12 @@ class BenchmarkCNN:
             self.strategy.before_update(step)
             wd = (p.weight_decay or 0.0) * self._l2_multiplier()
             if self.strategy.update_is_empty:
+                wd = 0.0
+            if wd and self.l2_mask is not None:
+                # model-specific L2 subset (custom_l2_loss, e.g. SSD without
+                # batch-norm variables): add wd * w on the masked elements
+                # before the gradient scale the optimizer applies
+                self.flat.grad.addcmul_(self.l2_mask, self.flat.flat, value=wd / grad_scale)
                 wd = 0.0
             self.optimizer.step(self.learning_rate(step), grad_scale=grad_scale,
                                 weight_decay=wd, clip=p.gradient_clip)

@@ -37,6 +37,13 @@ def eval_once(bench, input_source, num_batches, global_step, summary_writer=None
         with torch.no_grad():
             res = bench.net.forward_inputs(inputs, phase_train=False)
             acc = bench.model.accuracy_function(inputs, res.logits)
+            if "top_1_accuracy" not in acc:
+                # unreduced outputs (e.g. DeepSpeech2 probabilities): the model
+                # reduces them on the host (tcb/benchmark_cnn.py postprocess)
+                host = bench.model.postprocess(
+                    {k: v.detach().float().cpu().numpy() for k, v in acc.items()})
+                acc = {"top_1_accuracy": host["top_1_accuracy"] * batch,
+                       "top_5_accuracy": host["top_5_accuracy"] * batch}
             counts = torch.stack([torch.as_tensor(acc["top_1_accuracy"], dtype=torch.float32),
                                   torch.as_tensor(acc["top_5_accuracy"], dtype=torch.float32)])
             if getattr(bench, "tower_mode", False):
@@ -47,7 +54,6 @@ def eval_once(bench, input_source, num_batches, global_step, summary_writer=None
         results = {"top_1_accuracy": float(counts[0]) / batch,
                    "top_5_accuracy": float(counts[1]) / batch,
                    "global_step": global_step}
-        results = bench.model.postprocess(results)
         top1 += results["top_1_accuracy"]
         top5 += results["top_5_accuracy"]
         if (step + 1) % p.display_every == 0:

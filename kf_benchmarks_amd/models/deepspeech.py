@@ -1,0 +1,204 @@
+"""DeepSpeech2 (role of tcb/models/experimental/deepspeech.py).
+
+Spectrogram [B, 3494, 161, 1] -> two conv+ReLU6+BN layers (41x11/2x2 pad
+20x5, 21x11/2x1 pad 10x5, 32 filters) -> 5 bidirectional LSTM(800) layers
+with BN on the inputs of layers 2..5 -> BN -> dense(29) -> CTC loss (blank =
+class 28) over length-scaled inputs (tcb/models/experimental/
+deepspeech.py:121-389).  Batch 128, LR 0.0005.  The LSTMs run in fp32 on
+MIOpen's fused RNN kernels; the greedy decoder and CER/WER (edit distance
+implemented here, no nltk) report eval quality like the reference's
+postprocess.
+"""
+
+from __future__ import annotations
+
+import itertools
+from typing import List, Sequence
+
+import numpy as np
+import torch
+from torch import nn
+
+from .. import cnn_util
+from . import model as model_lib
+
+SPEECH_LABELS = " abcdefghijklmnopqrstuvwxyz'-"
+
+
+def edit_distance(a: Sequence, b: Sequence) -> int:
+    """Levenshtein distance."""
+    prev = list(range(len(b) + 1))
+    for i, ca in enumerate(a, 1):
+        cur = [i] + [0] * len(b)
+        for j, cb in enumerate(b, 1):
+            cur[j] = min(prev[j] + 1, cur[j - 1] + 1, prev[j - 1] + (ca != cb))
+        prev = cur
+    return prev[-1]
+
+
+class DeepSpeechDecoder:
+    """Greedy CTC decoder with CER / WER."""
+
+    def __init__(self, labels=SPEECH_LABELS, blank_index=28):
+        self.labels = labels
+        self.blank_index = blank_index
+        self.int_to_char = dict(enumerate(labels))
+
+    def convert_to_string(self, sequence):
+        return "".join(self.int_to_char[int(i)] for i in sequence)
+
+    def wer(self, decode, target):
+        words = set(decode.split() + target.split())
+        w2c = dict(zip(words, range(len(words))))
+        return edit_distance([w2c[w] for w in decode.split()], [w2c[w] for w in target.split()])
+
+    def cer(self, decode, target):
+        return edit_distance(decode, target)
+
+    def decode(self, char_indexes):
+        merged = [k for k, _ in itertools.groupby(char_indexes)]
+        return self.convert_to_string([k for k in merged if k != self.blank_index])
+
+    def decode_logits(self, logits):
+        return self.decode(list(np.argmax(logits, axis=1)))
+
+
+class _ConvBN(nn.Module):
+    def __init__(self, cin, cout, k, stride, pad, gen, device):
+        super().__init__()
+        self.pad = pad
+        self.stride = stride
+        fan_in, fan_out = cin * k[0] * k[1], cout * k[0] * k[1]
+        lim = (6.0 / (fan_in + fan_out)) ** 0.5
+        w = (torch.rand((cout, cin, k[0], k[1]), generator=gen) * 2 - 1) * lim
+        self.weight = nn.Parameter(w.to(device))
+        self.bn = nn.BatchNorm2d(cout, eps=1e-5, momentum=1 - 0.997, device=device)
+
+    def forward(self, x):  # x NCHW
+        y = torch.nn.functional.conv2d(x, self.weight.to(x.dtype), stride=self.stride,
+                                       padding=self.pad)
+        y = torch.clamp(y, 0.0, 6.0)  # relu6 before BN, as the reference
+        return self.bn(y.float()).to(x.dtype)
+
+
+class DeepSpeech2(nn.Module):
+    def __init__(self, nclass, num_rnn_layers, rnn_type, bidirectional, hidden, use_bias,
+                 feature_bins, gen, device):
+        super().__init__()
+        self.conv1 = _ConvBN(1, 32, (41, 11), (2, 2), (20, 5), gen, device)
+        self.conv2 = _ConvBN(32, 32, (21, 11), (2, 1), (10, 5), gen, device)
+        f = (feature_bins + 10 - 11) // 2 + 1
+        f = (f + 10 - 11) // 1 + 1
+        rnn_cls = {"lstm": nn.LSTM, "gru": nn.GRU, "rnn": nn.RNN}[rnn_type]
+        dirs = 2 if bidirectional else 1
+        self.rnns = nn.ModuleList()
+        self.bns = nn.ModuleList()
+        din = f * 32
+        for i in range(num_rnn_layers):
+            self.bns.append(nn.BatchNorm1d(din, eps=1e-5, momentum=1 - 0.997, device=device)
+                            if i > 0 else nn.Identity())
+            self.rnns.append(rnn_cls(din, hidden, batch_first=True, bidirectional=bidirectional,
+                                     device=device))
+            din = hidden * dirs
+        self.final_bn = nn.BatchNorm1d(din, eps=1e-5, momentum=1 - 0.997, device=device)
+        self.fc = nn.Linear(din, nclass, bias=use_bias, device=device)
+
+    @staticmethod
+    def _bn_seq(bn, x):
+        if isinstance(bn, nn.Identity):
+            return x
+        B, T, C = x.shape
+        return bn(x.reshape(B * T, C)).reshape(B, T, C)
+
+    def forward(self, inputs, phase_train=True):
+        self.train(phase_train)
+        x = inputs[0]  # [B, T, F, 1] (NHWC)
+        x = x.permute(0, 3, 1, 2)  # NCHW [B, 1, T, F]
+        x = self.conv2(self.conv1(x))
+        B, C, T, F = x.shape
+        x = x.permute(0, 2, 3, 1).reshape(B, T, F * C).float()
+        for bn, rnn in zip(self.bns, self.rnns):
+            x = self._bn_seq(bn, x)
+            x, _ = rnn(x)
+        x = self._bn_seq(self.final_bn, x)
+        logits = self.fc(x)
+        return model_lib.BuildNetworkResult(logits=logits, extra_info=None)
+
+
+class DeepSpeech2Model(model_lib.ModuleModel):
+    SUPPORTED_RNNS = ("lstm", "rnn", "gru")
+    BATCH_NORM_EPSILON = 1e-5
+    BATCH_NORM_DECAY = 0.997
+    CONV_FILTERS = 32
+
+    def __init__(self, num_rnn_layers=5, rnn_type="lstm", is_bidirectional=True,
+                 rnn_hidden_size=800, use_bias=True, params=None):
+        super().__init__("deepspeech2", batch_size=128, learning_rate=0.0005,
+                         fp16_loss_scale=128, params=params)
+        if rnn_type not in self.SUPPORTED_RNNS:
+            raise ValueError("rnn_type must be one of %s" % (self.SUPPORTED_RNNS,))
+        self.num_rnn_layers = num_rnn_layers
+        self.rnn_type = rnn_type
+        self.is_bidirectional = is_bidirectional
+        self.rnn_hidden_size = rnn_hidden_size
+        self.use_bias = use_bias
+        self.num_feature_bins = 161
+        self.max_time_steps = 3494
+        self.max_label_length = 576
+
+    def make_module(self, nclass, device, dtype, gen):
+        return DeepSpeech2(nclass, self.num_rnn_layers, self.rnn_type, self.is_bidirectional,
+                           self.rnn_hidden_size, self.use_bias, self.num_feature_bins, gen,
+                           device)
+
+    def get_input_data_types(self, subset):
+        del subset
+        return [self.data_type, torch.int32, torch.int32, torch.int32]
+
+    def get_input_shapes(self, subset):
+        del subset
+        return [[self.batch_size, self.max_time_steps, self.num_feature_bins, 1],
+                [self.batch_size, self.max_label_length], [self.batch_size, 1],
+                [self.batch_size, 1]]
+
+    def get_synthetic_inputs(self, input_name, nclass, device="cpu", seed=0):
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        shapes = self.get_input_shapes("train")
+        feats = torch.rand(shapes[0], generator=g).to(device, self.data_type)
+        labels = torch.randint(0, 28, shapes[1], generator=g, dtype=torch.int32).to(device)
+        ilen = torch.full(shapes[2], self.max_time_steps, dtype=torch.int32, device=device)
+        llen = torch.full(shapes[3], self.max_label_length, dtype=torch.int32, device=device)
+        return feats, labels, ilen, llen
+
+    def loss_function(self, inputs, build_network_result):
+        logits = build_network_result.logits.float()  # [B, T', nclass]
+        T = logits.shape[1]
+        ctc_len = (inputs[2].reshape(-1).long() * T) // self.max_time_steps
+        log_probs = torch.log_softmax(logits, dim=-1).transpose(0, 1)  # [T', B, C]
+        blank = logits.shape[-1] - 1
+        labels = inputs[1].long()
+        llen = inputs[3].reshape(-1).long()
+        losses = torch.nn.functional.ctc_loss(log_probs, labels, ctc_len, llen, blank=blank,
+                                              reduction="none", zero_infinity=True)
+        return losses.mean()
+
+    def accuracy_function(self, inputs, logits):
+        return {"probs": torch.softmax(logits.float(), dim=-1), "labels": inputs[1]}
+
+    def postprocess(self, results):
+        probs = np.asarray(results["probs"])
+        targets = np.asarray(results["labels"])
+        dec = DeepSpeechDecoder()
+        total_wer = total_cer = 0.0
+        n = probs.shape[0]
+        for i in range(n):
+            pred = dec.decode_logits(probs[i])
+            exp = dec.decode(list(targets[i]))
+            total_cer += dec.cer(pred, exp) / float(max(len(exp), 1))
+            total_wer += dec.wer(pred, exp) / float(max(len(exp.split()), 1))
+        total_cer /= n
+        total_wer /= n
+        cnn_util.log_fn("total CER: {:f}; total WER: {:f}; total example: {:d}.".format(
+            total_cer, total_wer, n))
+        return {"top_1_accuracy": 1.0 - total_cer, "top_5_accuracy": 1.0 - total_wer,
+                "cer": total_cer, "wer": total_wer}

@@ -13,7 +13,7 @@ import importlib
 def _lazy(module, fn):
     def ctor(params):
         mod = importlib.import_module("kf_benchmarks_amd.models." + module)
-        return getattr(mod, fn)(params)
+        return getattr(mod, fn)(params=params)
     ctor.__name__ = fn
     return ctor
 
