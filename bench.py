@@ -39,6 +39,11 @@ def main(argv=None):
     ap.add_argument("--bucket_size_mb", type=float, default=64.0)
     ap.add_argument("--wire_dtype", default="fp32")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--variable_update", default="kungfu",
+                    help="kungfu (headline) | replicated | horovod | parameter_server | ...")
+    ap.add_argument("--kungfu_option", default="sync_sgd",
+                    help="sync_sgd (headline) | async_sgd (PairAveraging) | sma | ada_sgd")
+    ap.add_argument("--data_name", default=None, help="dataset (coco for ssd300, ...)")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
@@ -50,8 +55,9 @@ def main(argv=None):
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env != a.gpus:
         print("warning: --gpus=%d but WORLD_SIZE=%d" % (a.gpus, world_env), file=sys.stderr)
-    p = P.make_params(model=a.model, batch_size=a.batch_size, num_gpus=1,
-                      variable_update="kungfu", kungfu_option="sync_sgd",
+    data_name = a.data_name or {"ssd300": "coco", "deepspeech2": "librispeech"}.get(a.model)
+    p = P.make_params(model=a.model, batch_size=a.batch_size, num_gpus=1, data_name=data_name,
+                      variable_update=a.variable_update, kungfu_option=a.kungfu_option,
                       optimizer=a.optimizer, use_bf16=a.dtype == "bf16",
                       use_fp16=a.dtype == "fp16", data_format="NHWC",
                       kernel_impl=a.kernel_impl, bucket_size_mb=a.bucket_size_mb,
@@ -104,11 +110,16 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": round(value / base, 3) if base else None,
             "dtype": a.dtype,
-            "data": "synthetic (%dx%dx3 ImageNet-shaped images, random-init weights)"
-                    % (bench.model.image_size, bench.model.image_size),
+            "data": ("synthetic (%dx%dx3 ImageNet-shaped images, random-init weights)"
+                     % (bench.model.image_size, bench.model.image_size)
+                     if hasattr(bench.model, "image_size")
+                     else "synthetic inputs of the model's shape, random-init weights"),
             "config": {"model": a.model, "global_batch": a.batch_size * n, "seq_len": None,
                        "per_gpu_batch": a.batch_size, "parallelism": "dp%d" % n,
-                       "variable_update": "kungfu/sync_sgd", "optimizer": a.optimizer,
+                       "variable_update": (a.variable_update + "/" + a.kungfu_option
+                                           if a.variable_update == "kungfu"
+                                           else a.variable_update),
+                       "optimizer": a.optimizer,
                        "kernel_impl": a.kernel_impl, "loss_first": warm_loss,
                        "loss_last": final_loss},
         }
