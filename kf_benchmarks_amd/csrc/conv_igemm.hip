@@ -344,7 +344,7 @@ struct WgArgs {
   int mper;        // rows of m per split
 };
 
-constexpr int WG_BK = 32;  // reduction rows per step
+constexpr int WG_BK = 32;  // reduction rows per step (64 measured no faster)
 
 // 256-byte rows (128 elements); 32-byte unit u (0..7) of row r stored at
 // u ^ f(r), f(r) = (r & 3) | ((r >> 3) & 1) << 2.
@@ -456,25 +456,29 @@ __global__ void __launch_bounds__(256, 2) wgrad_k(WgArgs a) {
     if (s + 1 < nsteps) load(mbeg + (s + 1) * WG_BK);
     const T* ds = smem + cur * WG_BK * 256;
     const T* xs = ds + WG_BK * 128;
-    v8s af[TN], bfr[TM];
 #pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      const int col = wn * (BMC / 2) + i * 16 + 4 * p;
-      v4s lo = ds_read_tr<T>(ds + tr_off(8 * g + q, col));
-      v4s hi = ds_read_tr<T>(ds + tr_off(8 * g + 4 + q, col));
-      af[i] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    for (int kk = 0; kk < WG_BK / 32; ++kk) {
+      const int r0 = kk * 32 + 8 * g;
+      v8s af[TN], bfr[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int col = wn * (BMC / 2) + i * 16 + 4 * p;
+        v4s lo = ds_read_tr<T>(ds + tr_off(r0 + q, col));
+        v4s hi = ds_read_tr<T>(ds + tr_off(r0 + 4 + q, col));
+        af[i] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int col = wm * (BNK / 2) + j * 16 + 4 * p;
+        v4s lo = ds_read_tr<T>(xs + tr_off(r0 + q, col));
+        v4s hi = ds_read_tr<T>(xs + tr_off(r0 + 4 + q, col));
+        bfr[j] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = Mfma<T>::run(af[i], bfr[j], acc[i][j]);
     }
-#pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      const int col = wm * (BNK / 2) + j * 16 + 4 * p;
-      v4s lo = ds_read_tr<T>(xs + tr_off(8 * g + q, col));
-      v4s hi = ds_read_tr<T>(xs + tr_off(8 * g + 4 + q, col));
-      bfr[j] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    }
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int j = 0; j < TM; ++j) acc[i][j] = Mfma<T>::run(af[i], bfr[j], acc[i][j]);
     if (s + 1 < nsteps) store(cur ^ 1);
     __syncthreads();
     cur ^= 1;

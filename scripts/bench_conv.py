@@ -61,14 +61,19 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--hip_only", action="store_true", help="skip MIOpen (profiling runs)")
+    ap.add_argument("--shapes", default=None, help="comma list of RESNET50 indices")
     a = ap.parse_args()
+    only = {int(i) for i in a.shapes.split(",")} if a.shapes else None
     dev = torch.device("cuda", 0)
     dt = torch.bfloat16
     tot = {"hip": [0.0, 0.0, 0.0], "miopen": [0.0, 0.0, 0.0]}
     rows = []
     print("%-28s %8s | %9s %7s | %9s %7s | %9s %7s" % ("shape", "pass", "hip_us", "TF/s",
                                                         "miopen_us", "TF/s", "", ""))
-    for (H, cin, cout, k, s, cnt) in RESNET50:
+    for si, (H, cin, cout, k, s, cnt) in enumerate(RESNET50):
+        if only is not None and si not in only:
+            continue
         n = a.batch
         mode = "SAME_RESNET"
         pads = F.resolve_pads(mode, H, H, k, k, s, s)
@@ -104,7 +109,7 @@ def main():
             if pas == "dgrad" and cin == 3:
                 continue
             th = timeit(hip[pas], a.iters)
-            tm = timeit(mi[pas], a.iters)
+            tm = timeit(mi[pas], a.iters) if not a.hip_only else float("nan")
             tot["hip"][i] += th * cnt
             tot["miopen"][i] += tm * cnt
             name = "%dx%d %d->%d k%d s%d" % (H, H, cin, cout, k, s)
