@@ -29,6 +29,8 @@
 // 8 distinct 32-byte bank windows.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace kfb {
 
 typedef __attribute__((ext_vector_type(8))) short v8s;
@@ -74,6 +76,8 @@ struct IgArgs {
   // mask / statistics - the gradient other consumers of the conv input
   // already produced (residual / second-branch accumulation).
   const void* addend;
+  // FAST path only: byte sizes of x and w (buffer-descriptor range checks)
+  int xbytes, wbytes;
 };
 
 constexpr int IG_BK = 64;
@@ -89,7 +93,15 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-template <typename T, int BM, int BN, bool TRANS>
+typedef __attribute__((ext_vector_type(4))) unsigned int v4u;
+
+// FAST (forward / stride-1 gather, C % 64 == 0, operands < 2 GiB): every
+// 64-deep K step lies inside one filter tap, so the tap (kh, kw) and the
+// channel offset advance as wave-uniform scalars; each pixel row carries a
+// bitmask of its in-bounds taps, and operands are read with range-checked
+// buffer loads (an out-of-range offset returns zeros), so the loads need no
+// per-lane branches and no 64-bit address math.
+template <typename T, int BM, int BN, bool TRANS, bool FAST>
 __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
   constexpr int XC = BM / 32;  // 16-byte X chunks per thread per K step
   constexpr int WC = BN / 32;  // 16-byte W chunks per thread per K step
@@ -130,6 +142,50 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
   }
 
   uint4 xr[XC], wr[WC];
+  // ---- FAST-path state
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, a.wbytes, 0x00020000);
+  unsigned long long tapmask[XC];
+  int xoff[XC], woff[WC];
+  int s_cc = 0, s_kh = 0, s_kw = 0, s_tap = 0, s_tapi = 0, s_k = 0;
+  if constexpr (FAST) {
+#pragma unroll
+    for (int i = 0; i < XC; ++i) {
+      unsigned long long mk = 0;
+      for (int kh = 0; kh < a.KH; ++kh)
+        for (int kw = 0; kw < a.KW; ++kw) {
+          const bool in = (unsigned)(xh[i] + kh) < (unsigned)a.H &&
+                          (unsigned)(xw[i] + kw) < (unsigned)a.W;
+          mk |= (unsigned long long)(in && xok[i]) << (kh * a.KW + kw);
+        }
+      tapmask[i] = mk;
+      xoff[i] = xbase[i] + (xh[i] * a.W + xw[i]) * a.C + kc * 8;
+    }
+#pragma unroll
+    for (int i = 0; i < WC; ++i) woff[i] = (n0 + (tid >> 3) + i * 32) * a.Ktot + kc * 8;
+  }
+  auto load_fast = [&]() {
+#pragma unroll
+    for (int i = 0; i < XC; ++i) {
+      const bool ok = (tapmask[i] >> s_tapi) & 1ull;
+      const int off = ok ? (xoff[i] + s_tap + s_cc) * (int)sizeof(T) : -1;
+      xr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+      wr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           wrs, (woff[i] + s_k) * (int)sizeof(T), 0, 0));
+    s_k += IG_BK;
+    s_cc += IG_BK;
+    if (s_cc == a.C) {
+      s_cc = 0;
+      ++s_tapi;
+      if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
+      s_tap = (s_kh * a.W + s_kw) * a.C;
+    }
+  };
   auto load = [&](int kt) {
     const int k = kt * IG_BK + kc * 8;
     const bool kok = k < a.Ktot;
@@ -172,12 +228,14 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
 
   const int wn = wid >> 1, wm = wid & 1;
   const int nk = (a.Ktot + IG_BK - 1) / IG_BK;
-  load(0);
+  if constexpr (FAST) load_fast(); else load(0);
   store(0);
   __syncthreads();
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) load(kt + 1);
+    if (kt + 1 < nk) {
+      if constexpr (FAST) load_fast(); else load(kt + 1);
+    }
     const T* xs = smem + cur * (BM + BN) * IG_BK;
     const T* ws = xs + BM * IG_BK;
 #pragma unroll
@@ -499,13 +557,20 @@ __global__ void __launch_bounds__(256, 2) wgrad_k(WgArgs a) {
     }
 }
 
+static bool igemm_fast_disabled() {
+  static const bool off = getenv("KFB_IGEMM_NOFAST") != nullptr;  // A/B switch
+  return off;
+}
+
 template <typename T, int BM, int BN>
-static void launch_ig(const IgArgs& a, bool trans, hipStream_t s) {
+static void launch_ig(const IgArgs& a, bool trans, bool fast, hipStream_t s) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
   if (trans)
-    hipLaunchKernelGGL((igemm_k<T, BM, BN, true>), dim3(nwg), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((igemm_k<T, BM, BN, true, false>), dim3(nwg), dim3(256), 0, s, a);
+  else if (fast)
+    hipLaunchKernelGGL((igemm_k<T, BM, BN, false, true>), dim3(nwg), dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((igemm_k<T, BM, BN, false>), dim3(nwg), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((igemm_k<T, BM, BN, false, false>), dim3(nwg), dim3(256), 0, s, a);
 }
 
 }  // namespace kfb
@@ -520,15 +585,19 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
                                   int trans, float* stats, const void* mask, const void* xbn,
                                   const float* mean, const void* addend, hipStream_t stream) {
   if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
+  const long xbytes = (long)N * H * W * C * 2, wbytes = (long)Ncol * KH * KW * C * 2;
   IgArgs a{x, w, y, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
-           N * OH * OW, YH, YW, ys, ldy, stats, mask, xbn, mean, addend};
+           N * OH * OW, YH, YW, ys, ldy, stats, mask, xbn, mean, addend,
+           (int)(xbytes < (1L << 31) ? xbytes : 0), (int)(wbytes < (1L << 31) ? wbytes : 0)};
   const bool t = trans != 0;
+  const bool fast = !t && C % IG_BK == 0 && KH * KW <= 64 && xbytes < (1L << 31) &&
+                    wbytes < (1L << 31) && !igemm_fast_disabled();
   if (dtype == BF16) {
-    if (Ncol <= 64) launch_ig<bf16, 128, 64>(a, t, stream);
-    else launch_ig<bf16, 128, 128>(a, t, stream);
+    if (Ncol <= 64) launch_ig<bf16, 128, 64>(a, t, fast, stream);
+    else launch_ig<bf16, 128, 128>(a, t, fast, stream);
   } else if (dtype == F16) {
-    if (Ncol <= 64) launch_ig<f16, 128, 64>(a, t, stream);
-    else launch_ig<f16, 128, 128>(a, t, stream);
+    if (Ncol <= 64) launch_ig<f16, 128, 64>(a, t, fast, stream);
+    else launch_ig<f16, 128, 128>(a, t, fast, stream);
   } else {
     return hipErrorInvalidValue;
   }
