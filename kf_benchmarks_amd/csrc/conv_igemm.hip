@@ -400,6 +400,7 @@ struct WgArgs {
   int KH, KW, sh, sw, pt, pl;
   int Ncol, Ktot, M;
   int mper;        // rows of m per split
+  int dybytes, xbytes;  // GATHER / PLAIN loaders: operand byte sizes (< 2 GiB)
 };
 
 constexpr int WG_BK = 32;  // reduction rows per step (64 measured no faster)
@@ -418,7 +419,14 @@ __device__ __forceinline__ v4s ds_read_tr(const T* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p));
 }
 
-template <typename T, int BMC, int BNK>
+// Loader modes: WG_GENERIC re-derives (img, oh, ow) of every row each step;
+// WG_GATHER walks them incrementally (wave-uniform step of WG_BK rows) and
+// reads with range-checked buffer loads; WG_PLAIN (1x1, stride 1, no
+// padding) reads x rows as a plain [M][C] matrix.  GATHER/PLAIN need both
+// operands < 2 GiB.
+enum { WG_GENERIC = 0, WG_GATHER = 1, WG_PLAIN = 2 };
+
+template <typename T, int BMC, int BNK, int MODE>
 __global__ void __launch_bounds__(256, 2) wgrad_k(WgArgs a) {
   // BMC = output-channel tile (rows of dW), BNK = k tile (cols of dW); both 128 or 64.
   constexpr int TN = BMC / 32, TM = BNK / 32;
@@ -463,7 +471,66 @@ __global__ void __launch_bounds__(256, 2) wgrad_k(WgArgs a) {
     xtap_w[i] = tap - xtap_h[i] * a.KW;
   }
   uint4 dr[DC], xr[XC];
+  // ---- incremental (GATHER / PLAIN) loader state
+  const __amdgpu_buffer_rsrc_t drs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)dy, (short)0, a.dybytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, a.xbytes, 0x00020000);
+  int doff[DC], xo[XC], ximg[XC], xoh[XC], xow[XC], xh0[XC], xw0[XC];
+  bool dcok[DC];
+  int s_m = mbeg;  // first row of the next step to load
+  const int dq = WG_BK / a.OW, dr_ = WG_BK - dq * a.OW;
+  if constexpr (MODE != WG_GENERIC) {
+#pragma unroll
+    for (int i = 0; i < DC; ++i) {
+      dcok[i] = c0 + dcol[i] < a.Ncol;
+      doff[i] = (mbeg + drow[i]) * a.Ncol + c0 + dcol[i];
+    }
+#pragma unroll
+    for (int i = 0; i < XC; ++i) {
+      const int m = mbeg + xrow[i];
+      if constexpr (MODE == WG_PLAIN) {
+        xo[i] = m * a.C + xcc[i];
+      } else {
+        ximg[i] = m / OHW;
+        const int rem = m - ximg[i] * OHW;
+        xoh[i] = rem / a.OW;
+        xow[i] = rem - xoh[i] * a.OW;
+        xh0[i] = xtap_h[i] - a.pt;
+        xw0[i] = xtap_w[i] - a.pl;
+      }
+    }
+  }
+  auto load_inc = [&]() {
+#pragma unroll
+    for (int i = 0; i < DC; ++i) {
+      const bool ok = dcok[i] && s_m + drow[i] < mend;
+      dr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            drs, ok ? doff[i] * (int)sizeof(T) : -1, 0, 0));
+      doff[i] += WG_BK * a.Ncol;
+    }
+#pragma unroll
+    for (int i = 0; i < XC; ++i) {
+      const bool mok = xkok[i] && s_m + xrow[i] < mend;
+      int off;
+      if constexpr (MODE == WG_PLAIN) {
+        off = mok ? xo[i] * (int)sizeof(T) : -1;
+        xo[i] += WG_BK * a.C;
+      } else {
+        const int hi = xoh[i] * a.sh + xh0[i], wi = xow[i] * a.sw + xw0[i];
+        const bool ok = mok && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+        off = ok ? (((ximg[i] * a.H + hi) * a.W + wi) * a.C + xcc[i]) * (int)sizeof(T) : -1;
+        xow[i] += dr_;
+        xoh[i] += dq;
+        if (xow[i] >= a.OW) { xow[i] -= a.OW; ++xoh[i]; }
+        while (xoh[i] >= a.OH) { xoh[i] -= a.OH; ++ximg[i]; }
+      }
+      xr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+    }
+    s_m += WG_BK;
+  };
   auto load = [&](int mstep) {
+    if constexpr (MODE != WG_GENERIC) { load_inc(); return; }
 #pragma unroll
     for (int i = 0; i < DC; ++i) {
       const int m = mstep + drow[i];
@@ -573,6 +640,16 @@ static void launch_ig(const IgArgs& a, bool trans, bool fast, hipStream_t s) {
     hipLaunchKernelGGL((igemm_k<T, BM, BN, false, false>), dim3(nwg), dim3(256), 0, s, a);
 }
 
+template <typename T, int BMC>
+static void launch_wg(const WgArgs& a, int mode, dim3 grid, hipStream_t s) {
+  if (mode == WG_PLAIN)
+    hipLaunchKernelGGL((wgrad_k<T, BMC, 128, WG_PLAIN>), grid, dim3(256), 0, s, a);
+  else if (mode == WG_GATHER)
+    hipLaunchKernelGGL((wgrad_k<T, BMC, 128, WG_GATHER>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((wgrad_k<T, BMC, 128, WG_GENERIC>), grid, dim3(256), 0, s, a);
+}
+
 }  // namespace kfb
 
 using namespace kfb;
@@ -612,8 +689,10 @@ KFB_API hipError_t kfb_conv_wgrad(int dtype, const void* dy, const void* x, floa
                                   int sw, int pt, int pl, int Ncol, int target_blocks,
                                   hipStream_t stream) {
   if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
+  const long dybytes = (long)N * OH * OW * Ncol * 2, xbytes = (long)N * H * W * C * 2;
   WgArgs a{dy, x, dw, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
-           N * OH * OW, 0};
+           N * OH * OW, 0, (int)(dybytes < (1L << 31) ? dybytes : 0),
+           (int)(xbytes < (1L << 31) ? xbytes : 0)};
   const int bmc = Ncol <= 64 ? 64 : 128;
   const int tiles = ((Ncol + bmc - 1) / bmc) * ((a.Ktot + 127) / 128);
   int split = target_blocks > 0 ? target_blocks / tiles : 1024 / tiles;
@@ -622,16 +701,17 @@ KFB_API hipError_t kfb_conv_wgrad(int dtype, const void* dy, const void* x, floa
   if (split < 1) split = 1;
   a.mper = ((a.M + split - 1) / split + WG_BK - 1) / WG_BK * WG_BK;
   split = (a.M + a.mper - 1) / a.mper;
+  int mode = WG_GENERIC;
+  if (dybytes < (1L << 31) && xbytes < (1L << 31) && !igemm_fast_disabled())
+    mode = (KH == 1 && KW == 1 && sh == 1 && sw == 1 && pt == 0 && pl == 0 && OH == H && OW == W)
+               ? WG_PLAIN : WG_GATHER;
+  const dim3 grid(tiles * split);
   if (dtype == BF16) {
-    if (bmc == 64)
-      hipLaunchKernelGGL((wgrad_k<bf16, 64, 128>), dim3(tiles * split), dim3(256), 0, stream, a);
-    else
-      hipLaunchKernelGGL((wgrad_k<bf16, 128, 128>), dim3(tiles * split), dim3(256), 0, stream, a);
+    if (bmc == 64) launch_wg<bf16, 64>(a, mode, grid, stream);
+    else launch_wg<bf16, 128>(a, mode, grid, stream);
   } else if (dtype == F16) {
-    if (bmc == 64)
-      hipLaunchKernelGGL((wgrad_k<f16, 64, 128>), dim3(tiles * split), dim3(256), 0, stream, a);
-    else
-      hipLaunchKernelGGL((wgrad_k<f16, 128, 128>), dim3(tiles * split), dim3(256), 0, stream, a);
+    if (bmc == 64) launch_wg<f16, 64>(a, mode, grid, stream);
+    else launch_wg<f16, 128>(a, mode, grid, stream);
   } else {
     return hipErrorInvalidValue;
   }

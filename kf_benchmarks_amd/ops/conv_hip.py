@@ -25,7 +25,7 @@ N.register_optional("kfb_conv_igemm", _SIG)
 N.register_optional("kfb_conv_stats_spread", [], N.c_int)
 N.register_optional("kfb_conv_wgrad", [N.I, N.P, N.P, N.P] + [N.I] * 12 + [N.I, N.I, N.P])
 
-_WGRAD_TARGET_BLOCKS = 1024
+_WGRAD_TARGET_BLOCKS = int(os.environ.get("KFB_WGRAD_BLOCKS", "1024"))
 
 
 def supported(x, w, stride, pads) -> bool:

@@ -22,6 +22,8 @@ SHAPES = [
     (2, 11, 11, 64, 96, 3, 3, 2, "VALID"),
     (1, 7, 7, 512, 2048, 1, 1, 1, "SAME"),        # M < one tile
     (2, 8, 8, 20, 36, 3, 3, 1, "SAME"),           # Cin, Cout not multiples of 8
+    (9, 2, 2, 64, 64, 3, 3, 1, "SAME"),           # rows wrap several images per K step
+    (40, 1, 1, 256, 128, 1, 1, 1, "SAME"),        # 1x1 spatial (FC-like)
 ]
 
 
