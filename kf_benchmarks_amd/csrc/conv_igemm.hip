@@ -401,6 +401,10 @@ struct WgArgs {
   int Ncol, Ktot, M;
   int mper;        // rows of m per split
   int dybytes, xbytes;  // GATHER / PLAIN loaders: operand byte sizes (< 2 GiB)
+  // slab != null: each split stores its partial dW tile with plain stores to
+  // slab[split][Ncol][Ktot] (every element of every split is written) and
+  // wgrad_reduce_k folds the slabs into dw; else fp32 atomics into dw.
+  float* slab;
 };
 
 constexpr int WG_BK = 32;  // reduction rows per step (64 measured no faster)
@@ -610,6 +614,41 @@ __global__ void __launch_bounds__(256, 2) wgrad_k(WgArgs a) {
   }
   // acc[i][j]: rows (dW output channel) c0 + wn*BMC/2 + i*16 + (lane>>4)*4 + r,
   // col (k) k0 + wm*BNK/2 + j*16 + (lane&15).
+  if (a.slab) {
+    // Plain-store slab epilogue: stage half the tile (BMC/2 rows x BNK fp32)
+    // at a time through LDS so each lane stores 16 contiguous bytes of a row.
+    // Float atomics run at the memory side at ~1.3 TB/s (every lane-dword an
+    // uncached request); plain 16-byte stores stream at ~6 TB/s.
+    constexpr int HR = BMC / 2;              // rows per half (one wave row wn)
+    constexpr int LDR = BNK;  // ds_write_b32 rows 4 apart: 2-way, free per the LDS table
+    static_assert(HR * LDR * 4 <= (int)sizeof(smem), "slab staging exceeds LDS");
+    float* st = (float*)smem;
+    float* dst = a.slab + (long)split * a.Ncol * a.Ktot;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (wn == h) {
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              st[(i * 16 + (lane >> 4) * 4 + r) * LDR + wm * (BNK / 2) + j * 16 + (lane & 15)] =
+                  acc[i][j][r];
+      }
+      __syncthreads();
+      constexpr int CPR = BNK / 4;  // float4 chunks per row
+#pragma unroll
+      for (int t = tid; t < HR * CPR; t += 256) {
+        const int row = t / CPR, cc = (t % CPR) * 4;
+        const int c = c0 + h * HR + row, k = k0 + cc;
+        if (c < a.Ncol && k < a.Ktot)
+          *(float4*)(dst + (long)c * a.Ktot + k) = *(const float4*)(st + row * LDR + cc);
+      }
+      __syncthreads();
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < TN; ++i)
 #pragma unroll
@@ -622,6 +661,51 @@ __global__ void __launch_bounds__(256, 2) wgrad_k(WgArgs a) {
         if (c < a.Ncol) atomicAdd(a.dw + (long)c * a.Ktot + k, acc[i][j][r]);
       }
     }
+}
+
+// dw[i] += sum_s slab[s][i]   (n4 = elements / 4), one thread per float4.
+__global__ void __launch_bounds__(256) wgrad_reduce_k(const float4* __restrict__ slab,
+                                                      float4* __restrict__ dw, long n4,
+                                                      int nsplit) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 acc = dw[i];
+    int s = 0;
+    for (; s + 4 <= nsplit; s += 4) {  // four independent loads in flight
+      const float4 v0 = slab[(long)s * n4 + i], v1 = slab[(long)(s + 1) * n4 + i];
+      const float4 v2 = slab[(long)(s + 2) * n4 + i], v3 = slab[(long)(s + 3) * n4 + i];
+      acc.x += (v0.x + v1.x) + (v2.x + v3.x);
+      acc.y += (v0.y + v1.y) + (v2.y + v3.y);
+      acc.z += (v0.z + v1.z) + (v2.z + v3.z);
+      acc.w += (v0.w + v1.w) + (v2.w + v3.w);
+    }
+    for (; s < nsplit; ++s) {
+      const float4 v = slab[(long)s * n4 + i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    dw[i] = acc;
+  }
+}
+
+// Small dW with many splits: blockIdx.y sums a group of splits for one float
+// per thread and adds it atomically (lane-contiguous: one 256-byte run per
+// wave-instruction).
+__global__ void __launch_bounds__(256) wgrad_reduce_grouped_k(const float* __restrict__ slab,
+                                                              float* __restrict__ dw, long n,
+                                                              int nsplit) {
+  const long i = blockIdx.x * 256L + threadIdx.x;
+  if (i >= n) return;
+  const int s0 = (int)((long)nsplit * blockIdx.y / gridDim.y);
+  const int s1 = (int)((long)nsplit * (blockIdx.y + 1) / gridDim.y);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s = s0;
+  for (; s + 4 <= s1; s += 4) {
+    a0 += slab[(long)s * n + i];
+    a1 += slab[(long)(s + 1) * n + i];
+    a2 += slab[(long)(s + 2) * n + i];
+    a3 += slab[(long)(s + 3) * n + i];
+  }
+  for (; s < s1; ++s) a0 += slab[(long)s * n + i];
+  atomicAdd(dw + i, (a0 + a1) + (a2 + a3));
 }
 
 static bool igemm_fast_disabled() {
@@ -638,6 +722,20 @@ static void launch_ig(const IgArgs& a, bool trans, bool fast, hipStream_t s) {
     hipLaunchKernelGGL((igemm_k<T, BM, BN, false, true>), dim3(nwg), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL((igemm_k<T, BM, BN, false, false>), dim3(nwg), dim3(256), 0, s, a);
+}
+
+// Reduction split of a wgrad launch: ~target_blocks workgroups, >= 8 steps
+// per workgroup; returns the split count and the rows per split.
+static int wgrad_split(int M, int Ktot, int Ncol, int target_blocks, int* mper_out) {
+  const int bmc = Ncol <= 64 ? 64 : 128;
+  const int tiles = ((Ncol + bmc - 1) / bmc) * ((Ktot + 127) / 128);
+  int split = target_blocks > 0 ? target_blocks / tiles : 1024 / tiles;
+  const int max_split = (M + WG_BK * 8 - 1) / (WG_BK * 8);
+  if (split > max_split) split = max_split;
+  if (split < 1) split = 1;
+  const int mper = ((M + split - 1) / split + WG_BK - 1) / WG_BK * WG_BK;
+  if (mper_out) *mper_out = mper;
+  return (M + mper - 1) / mper;
 }
 
 template <typename T, int BMC>
@@ -683,24 +781,28 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
 
 KFB_API int kfb_conv_stats_spread() { return IG_SPREAD; }
 
+// Number of reduction splits kfb_conv_wgrad uses for this geometry (the
+// slab workspace needs splits * Ncol * KH*KW*C floats).
+KFB_API int kfb_conv_wgrad_splits(int N, int OH, int OW, int KH, int KW, int C, int Ncol,
+                                  int target_blocks) {
+  return wgrad_split(N * OH * OW, KH * KW * C, Ncol, target_blocks, nullptr);
+}
+
 // Weight gradient: dw [Ncol][KH*KW*C] fp32 must be zeroed by the caller.
 KFB_API hipError_t kfb_conv_wgrad(int dtype, const void* dy, const void* x, float* dw, int N,
                                   int H, int W, int C, int OH, int OW, int KH, int KW, int sh,
                                   int sw, int pt, int pl, int Ncol, int target_blocks,
-                                  hipStream_t stream) {
+                                  float* slab, long slab_elems, hipStream_t stream) {
   if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
   const long dybytes = (long)N * OH * OW * Ncol * 2, xbytes = (long)N * H * W * C * 2;
   WgArgs a{dy, x, dw, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
            N * OH * OW, 0, (int)(dybytes < (1L << 31) ? dybytes : 0),
-           (int)(xbytes < (1L << 31) ? xbytes : 0)};
+           (int)(xbytes < (1L << 31) ? xbytes : 0), nullptr};
   const int bmc = Ncol <= 64 ? 64 : 128;
   const int tiles = ((Ncol + bmc - 1) / bmc) * ((a.Ktot + 127) / 128);
-  int split = target_blocks > 0 ? target_blocks / tiles : 1024 / tiles;
-  const int max_split = (a.M + WG_BK * 8 - 1) / (WG_BK * 8);  // >= 8 steps per block
-  if (split > max_split) split = max_split;
-  if (split < 1) split = 1;
-  a.mper = ((a.M + split - 1) / split + WG_BK - 1) / WG_BK * WG_BK;
-  split = (a.M + a.mper - 1) / a.mper;
+  const int split = wgrad_split(a.M, a.Ktot, Ncol, target_blocks, &a.mper);
+  const long per_split = (long)Ncol * a.Ktot;
+  if (slab && split > 1 && (long)split * per_split <= slab_elems) a.slab = slab;
   int mode = WG_GENERIC;
   if (dybytes < (1L << 31) && xbytes < (1L << 31) && !igemm_fast_disabled())
     mode = (KH == 1 && KW == 1 && sh == 1 && sw == 1 && pt == 0 && pl == 0 && OH == H && OW == W)
@@ -714,6 +816,25 @@ KFB_API hipError_t kfb_conv_wgrad(int dtype, const void* dy, const void* x, floa
     else launch_wg<f16, 128>(a, mode, grid, stream);
   } else {
     return hipErrorInvalidValue;
+  }
+  if (a.slab) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const long n4 = per_split / 4;
+    if (n4 >= 65536) {
+      long blocks = (n4 + 255) / 256;
+      if (blocks > 4096) blocks = 4096;
+      hipLaunchKernelGGL(wgrad_reduce_k, dim3((unsigned)blocks), dim3(256), 0, stream,
+                         (const float4*)slab, (float4*)dw, n4, split);
+    } else {
+      // >= ~1024 workgroups, <= 16 splits per thread
+      const long blocks = (per_split + 255) / 256;
+      long groups = (1024 + blocks - 1) / blocks;
+      if (groups < (split + 15) / 16) groups = (split + 15) / 16;
+      if (groups > split) groups = split;
+      hipLaunchKernelGGL(wgrad_reduce_grouped_k, dim3((unsigned)blocks, (unsigned)groups),
+                         dim3(256), 0, stream, (const float*)slab, dw, per_split, split);
+    }
   }
   return hipGetLastError();
 }

@@ -23,9 +23,13 @@ from . import _native as N
 _SIG = [N.I, N.P, N.P, N.P] + [N.I] * 17 + [N.I, N.P, N.P, N.P, N.P, N.P, N.P]
 N.register_optional("kfb_conv_igemm", _SIG)
 N.register_optional("kfb_conv_stats_spread", [], N.c_int)
-N.register_optional("kfb_conv_wgrad", [N.I, N.P, N.P, N.P] + [N.I] * 12 + [N.I, N.I, N.P])
+N.register_optional("kfb_conv_wgrad", [N.I, N.P, N.P, N.P] + [N.I] * 12 + [N.I, N.I, N.P, N.L, N.P])
+N.register_optional("kfb_conv_wgrad_splits", [N.I] * 8, N.c_int)
 
-_WGRAD_TARGET_BLOCKS = int(os.environ.get("KFB_WGRAD_BLOCKS", "1024"))
+_WGRAD_TARGET_BLOCKS = int(os.environ.get("KFB_WGRAD_BLOCKS", "768"))
+# Split partial sums go to a plain-store fp32 slab + one reduce launch
+# (KFB_WGRAD_SLAB=0: fp32 atomics into dW, ~1.3 TB/s at the memory side).
+_WGRAD_SLAB = os.environ.get("KFB_WGRAD_SLAB", "1") != "0"
 
 
 def supported(x, w, stride, pads) -> bool:
@@ -160,6 +164,51 @@ def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None, addend=None, wt=None):
     return dx
 
 
+def _wgrad_launch(dy, x, dw, geo, target):
+    n, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, cout = geo
+    slab, slab_elems = None, 0
+    if _WGRAD_SLAB:
+        splits = N.load().kfb_conv_wgrad_splits(n, OH, OW, KH, KW, C, cout, target)
+        if splits > 1:
+            slab_elems = splits * cout * KH * KW * C
+            slab = torch.empty((slab_elems,), dtype=torch.float32, device=x.device)
+    N.call("kfb_conv_wgrad", N.dt(x), dy.data_ptr(), x.data_ptr(), dw.data_ptr(), n, H, W, C, OH,
+           OW, KH, KW, sh, sw, pt, pl, cout, target,
+           slab.data_ptr() if slab is not None else None, slab_elems, N.stream(x.device))
+
+
+# Launch-shape autotuning (the role cuDNN's algorithm autotune plays for the
+# reference, TF_CUDNN_USE_AUTOTUNE): the first wgrad of each geometry times
+# the candidate workgroup targets on the real operands and caches the best.
+# KFB_CONV_AUTOTUNE=0 pins _WGRAD_TARGET_BLOCKS.
+_AUTOTUNE = os.environ.get("KFB_CONV_AUTOTUNE", "1") != "0" and "KFB_WGRAD_BLOCKS" not in os.environ
+_WGRAD_CANDIDATES = (384, 512, 768, 1024)
+_wgrad_tuned = {}
+
+
+def _tune_wgrad(dy, x, dw, geo):
+    key = (str(x.device), x.dtype) + geo
+    best = _wgrad_tuned.get(key)
+    if best is not None:
+        return best
+    if torch.cuda.is_current_stream_capturing():
+        return _WGRAD_TARGET_BLOCKS
+    scratch = torch.zeros_like(dw)
+    times = {}
+    for t in _WGRAD_CANDIDATES:
+        _wgrad_launch(dy, x, scratch, geo, t)  # warm
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        for _ in range(3):
+            _wgrad_launch(dy, x, scratch, geo, t)
+        ev1.record()
+        ev1.synchronize()
+        times[t] = ev0.elapsed_time(ev1)
+    best = min(times, key=times.get)
+    _wgrad_tuned[key] = best
+    return best
+
+
 def conv_wgrad(dy, x, w_shape, stride, pads, out=None):
     """Accumulates dW into ``out`` (fp32 [Cout,KH,KW,C], e.g. the parameter's
     view of the zeroed flat gradient buffer) or into a fresh zeroed tensor."""
@@ -170,8 +219,9 @@ def conv_wgrad(dy, x, w_shape, stride, pads, out=None):
     pt, pb, pl, pr = pads
     dw = out if out is not None else torch.zeros((cout, KH, KW, C), dtype=torch.float32,
                                                  device=x.device)
-    N.call("kfb_conv_wgrad", N.dt(x), dy.data_ptr(), x.data_ptr(), dw.data_ptr(), n, H, W, C, OH,
-           OW, KH, KW, sh, sw, pt, pl, cout, _WGRAD_TARGET_BLOCKS, N.stream(x.device))
+    geo = (n, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, cout)
+    target = _tune_wgrad(dy, x, dw, geo) if _AUTOTUNE else _WGRAD_TARGET_BLOCKS
+    _wgrad_launch(dy, x, dw, geo, target)
     return dw
 
 
