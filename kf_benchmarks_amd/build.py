@@ -86,8 +86,22 @@ def build_hip(force=False, jobs=None, verbose=False):
     if todo or force or not os.path.exists(HIP_LIB):
         tmp = HIP_LIB + ".tmp"
         _run([HIPCC, "-shared", "-fPIC", "--offload-arch=%s" % ARCH, "-o", tmp] + objs)
+        _check_no_missing_stubs(tmp)
         os.replace(tmp, HIP_LIB)
     return HIP_LIB
+
+
+def _check_no_missing_stubs(lib):
+    """A kernel template the host pass silently dropped leaves its launch
+    stub undefined: the link succeeds and only dlopen fails (on the GPU box).
+    Catch it here instead."""
+    nm = shutil.which("nm")
+    if nm is None:
+        return
+    out = subprocess.run([nm, "-u", lib], stdout=subprocess.PIPE, text=True).stdout
+    missing = [l.split()[-1] for l in out.splitlines() if "__device_stub__" in l]
+    if missing:
+        raise RuntimeError("undefined kernel launch stubs in %s: %s" % (lib, missing))
 
 
 def build_rt(force=False):

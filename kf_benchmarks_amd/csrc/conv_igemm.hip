@@ -95,169 +95,16 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 typedef __attribute__((ext_vector_type(4))) unsigned int v4u;
 
-// FAST (forward / stride-1 gather, C % 64 == 0, operands < 2 GiB): every
-// 64-deep K step lies inside one filter tap, so the tap (kh, kw) and the
-// channel offset advance as wave-uniform scalars; each pixel row carries a
-// bitmask of its in-bounds taps, and operands are read with range-checked
-// buffer loads (an out-of-range offset returns zeros), so the loads need no
-// per-lane branches and no 64-bit address math.
-template <typename T, int BM, int BN, bool TRANS, bool FAST>
-__global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
-  constexpr int XC = BM / 32;  // 16-byte X chunks per thread per K step
-  constexpr int WC = BN / 32;  // 16-byte W chunks per thread per K step
-  constexpr int TM = BM / 32;  // 16-wide pixel subtiles per wave
-  constexpr int TN = BN / 32;  // 16-wide channel subtiles per wave
-  __shared__ __attribute__((aligned(16))) T smem[2 * (BM + BN) * IG_BK];
-
-  const T* __restrict__ x = (const T*)a.x;
-  const T* __restrict__ w = (const T*)a.w;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int mtiles = (a.M + BM - 1) / BM, ntiles = (a.Ncol + BN - 1) / BN;
-  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles);
-  const int m0 = (bid / ntiles) * BM, n0 = (bid % ntiles) * BN;
-  const int kc = tid & 7;  // this thread's 16-byte chunk within a 64-wide K step
+// Shared epilogue of the implicit-GEMM kernels: acc[i][j] holds channels
+// n..n+3 of pixel m for each (i, j) 16x16 subtile of the wave's
+// (BM/WGM) x (BN/WGN) block; NT threads; smem must hold BM*BN elements (and
+// NT*16 floats for the statistics fold).
+template <typename T, int BM, int BN, int NT, int WGM, int WGN>
+__device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN / 16][BM / WGM / 16],
+                                            T* smem, int m0, int n0, int wm, int wn) {
+  constexpr int TN = BN / WGN / 16, TM = BM / WGM / 16;
+  const int tid = threadIdx.x, lane = tid & 63;
   const int OHW = a.OH * a.OW;
-
-  // Per-thread pixel rows of the X tile.
-  int xbase[XC], xh[XC], xw[XC];
-  bool xok[XC];
-#pragma unroll
-  for (int i = 0; i < XC; ++i) {
-    const int m = m0 + (tid >> 3) + i * 32;
-    xok[i] = m < a.M;
-    const int mm = xok[i] ? m : 0;
-    const int img = mm / OHW, rem = mm - img * OHW;
-    const int oh = rem / a.OW, ow = rem - oh * a.OW;
-    xbase[i] = img * a.H * a.W * a.C;
-    if (TRANS) { xh[i] = oh + a.pt; xw[i] = ow + a.pl; }
-    else { xh[i] = oh * a.sh - a.pt; xw[i] = ow * a.sw - a.pl; }
-  }
-  const T* wrow[WC];
-  bool wok[WC];
-#pragma unroll
-  for (int i = 0; i < WC; ++i) {
-    const int n = n0 + (tid >> 3) + i * 32;
-    wok[i] = n < a.Ncol;
-    wrow[i] = w + (long)(wok[i] ? n : 0) * a.Ktot;
-  }
-
-  uint4 xr[XC], wr[WC];
-  // ---- FAST-path state
-  const __amdgpu_buffer_rsrc_t xrs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, a.xbytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wrs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, a.wbytes, 0x00020000);
-  unsigned long long tapmask[XC];
-  int xoff[XC], woff[WC];
-  int s_cc = 0, s_kh = 0, s_kw = 0, s_tap = 0, s_tapi = 0, s_k = 0;
-  if constexpr (FAST) {
-#pragma unroll
-    for (int i = 0; i < XC; ++i) {
-      unsigned long long mk = 0;
-      for (int kh = 0; kh < a.KH; ++kh)
-        for (int kw = 0; kw < a.KW; ++kw) {
-          const bool in = (unsigned)(xh[i] + kh) < (unsigned)a.H &&
-                          (unsigned)(xw[i] + kw) < (unsigned)a.W;
-          mk |= (unsigned long long)(in && xok[i]) << (kh * a.KW + kw);
-        }
-      tapmask[i] = mk;
-      xoff[i] = xbase[i] + (xh[i] * a.W + xw[i]) * a.C + kc * 8;
-    }
-#pragma unroll
-    for (int i = 0; i < WC; ++i) woff[i] = (n0 + (tid >> 3) + i * 32) * a.Ktot + kc * 8;
-  }
-  auto load_fast = [&]() {
-#pragma unroll
-    for (int i = 0; i < XC; ++i) {
-      const bool ok = (tapmask[i] >> s_tapi) & 1ull;
-      const int off = ok ? (xoff[i] + s_tap + s_cc) * (int)sizeof(T) : -1;
-      xr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
-    }
-#pragma unroll
-    for (int i = 0; i < WC; ++i)
-      wr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                           wrs, (woff[i] + s_k) * (int)sizeof(T), 0, 0));
-    s_k += IG_BK;
-    s_cc += IG_BK;
-    if (s_cc == a.C) {
-      s_cc = 0;
-      ++s_tapi;
-      if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
-      s_tap = (s_kh * a.W + s_kw) * a.C;
-    }
-  };
-  auto load = [&](int kt) {
-    const int k = kt * IG_BK + kc * 8;
-    const bool kok = k < a.Ktot;
-    const int tap = k / a.C, cc = k - tap * a.C;
-    const int kh = tap / a.KW, kw = tap - kh * a.KW;
-#pragma unroll
-    for (int i = 0; i < XC; ++i) {
-      bool ok = kok && xok[i];
-      int hi, wi;
-      if (TRANS) {
-        const int hh = xh[i] - kh, ww = xw[i] - kw;
-        ok = ok && hh >= 0 && ww >= 0;
-        hi = hh / a.sh; wi = ww / a.sw;
-        ok = ok && hi * a.sh == hh && wi * a.sw == ww && hi < a.H && wi < a.W;
-      } else {
-        hi = xh[i] + kh; wi = xw[i] + kw;
-        ok = ok && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-      }
-      xr[i] = ok ? *(const uint4*)(x + xbase[i] + (hi * a.W + wi) * a.C + cc)
-                 : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < WC; ++i)
-      wr[i] = (kok && wok[i]) ? *(const uint4*)(wrow[i] + k) : make_uint4(0, 0, 0, 0);
-  };
-  auto store = [&](int buf) {
-    T* xs = smem + buf * (BM + BN) * IG_BK;
-    T* ws = xs + BM * IG_BK;
-#pragma unroll
-    for (int i = 0; i < XC; ++i) *(uint4*)(xs + swz_off((tid >> 3) + i * 32, kc)) = xr[i];
-#pragma unroll
-    for (int i = 0; i < WC; ++i) *(uint4*)(ws + swz_off((tid >> 3) + i * 32, kc)) = wr[i];
-  };
-
-  v4f acc[TN][TM];
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-  const int wn = wid >> 1, wm = wid & 1;
-  const int nk = (a.Ktot + IG_BK - 1) / IG_BK;
-  if constexpr (FAST) load_fast(); else load(0);
-  store(0);
-  __syncthreads();
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) {
-      if constexpr (FAST) load_fast(); else load(kt + 1);
-    }
-    const T* xs = smem + cur * (BM + BN) * IG_BK;
-    const T* ws = xs + BM * IG_BK;
-#pragma unroll
-    for (int ks = 0; ks < IG_BK / 32; ++ks) {
-      const int chunk = ks * 4 + (lane >> 4);
-      v8s af[TN], bfr[TM];
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-        af[i] = *(const v8s*)(ws + swz_off(wn * (BN / 2) + i * 16 + (lane & 15), chunk));
-#pragma unroll
-      for (int j = 0; j < TM; ++j)
-        bfr[j] = *(const v8s*)(xs + swz_off(wm * (BM / 2) + j * 16 + (lane & 15), chunk));
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-#pragma unroll
-        for (int j = 0; j < TM; ++j) acc[i][j] = Mfma<T>::run(af[i], bfr[j], acc[i][j]);
-    }
-    if (kt + 1 < nk) store(cur ^ 1);
-    __syncthreads();
-    cur ^= 1;
-  }
-
   // Epilogue: lane holds channels n..n+3 of pixel m for each (i, j) subtile.
   // Stage the BM x BN tile through LDS (rows = pixels, 16-byte chunks
   // XOR-swizzled by row) so every global store is a full 16-byte lane write
@@ -267,10 +114,10 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
   constexpr int CPR = BN / 8;  // 16-byte chunks per staged row
 #pragma unroll
   for (int j = 0; j < TM; ++j) {
-    const int ml = wm * (BM / 2) + j * 16 + (lane & 15);
+    const int ml = wm * (BM / WGM) + j * 16 + (lane & 15);
 #pragma unroll
     for (int i = 0; i < TN; ++i) {
-      const int nl = wn * (BN / 2) + i * 16 + (lane >> 4) * 4;
+      const int nl = wn * (BN / WGN) + i * 16 + (lane >> 4) * 4;
       Vec<T, 4> o;
 #pragma unroll
       for (int r = 0; r < 4; ++r) o.v[r] = (T)acc[i][j][r];
@@ -284,7 +131,7 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
   const bool fused = a.stats || a.addend;
-  constexpr int NPASS = BM * CPR / 256;
+  constexpr int NPASS = BM * CPR / NT;
   constexpr int PB = NPASS >= 2 ? 2 : 1;  // passes whose global loads are issued together
 #pragma unroll
   for (int p0 = 0; p0 < NPASS; p0 += PB) {
@@ -294,7 +141,7 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
     int nq[PB];
 #pragma unroll
     for (int q = 0; q < PB; ++q) {
-      const int t = tid + (p0 + q) * 256;
+      const int t = tid + (p0 + q) * NT;
       const int ml = t / CPR, ch = t % CPR;
       const int m = m0 + ml, n = n0 + ch * 8;
       nq[q] = n;
@@ -368,7 +215,7 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
     // Fold the per-thread sums of threads sharing a chunk column, then one
     // atomic add per channel per workgroup into a spread slot.
     __syncthreads();
-    float* red = (float*)smem;  // [256/CPR][CPR][16]
+    float* red = (float*)smem;  // [NT/CPR][CPR][16]
     const int ch = tid % CPR, rg = tid / CPR;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -376,7 +223,7 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
       red[(rg * CPR + ch) * 16 + 8 + k] = s2[k];
     }
     __syncthreads();
-    constexpr int RG = 256 / CPR;
+    constexpr int RG = NT / CPR;
     if (tid < CPR * 16) {
       const int c = tid / 16, k = tid % 16;
       float acc2 = 0.f;
@@ -388,6 +235,355 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
       }
     }
   }
+}
+
+// FAST (forward / stride-1 gather, C % 64 == 0, operands < 2 GiB): every
+// 64-deep K step lies inside one filter tap, so the tap (kh, kw) and the
+// channel offset advance as wave-uniform scalars; each pixel row carries a
+// bitmask of its in-bounds taps, and operands are read with range-checked
+// buffer loads (an out-of-range offset returns zeros), so the loads need no
+// per-lane branches and no 64-bit address math.
+template <typename T, int BM, int BN, bool TRANS, bool FAST>
+__global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
+  constexpr int XC = BM / 32;  // 16-byte X chunks per thread per K step
+  constexpr int WC = BN / 32;  // 16-byte W chunks per thread per K step
+  constexpr int TM = BM / 32;  // 16-wide pixel subtiles per wave
+  constexpr int TN = BN / 32;  // 16-wide channel subtiles per wave
+  __shared__ __attribute__((aligned(16))) T smem[2 * (BM + BN) * IG_BK];
+
+  const T* __restrict__ x = (const T*)a.x;
+  const T* __restrict__ w = (const T*)a.w;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int mtiles = (a.M + BM - 1) / BM, ntiles = (a.Ncol + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int m0 = (bid / ntiles) * BM, n0 = (bid % ntiles) * BN;
+  const int kc = tid & 7;  // this thread's 16-byte chunk within a 64-wide K step
+  const int OHW = a.OH * a.OW;
+
+  // Per-thread pixel rows of the X tile.
+  int xbase[XC], xh[XC], xw[XC];
+  bool xok[XC];
+#pragma unroll
+  for (int i = 0; i < XC; ++i) {
+    const int m = m0 + (tid >> 3) + i * 32;
+    xok[i] = m < a.M;
+    const int mm = xok[i] ? m : 0;
+    const int img = mm / OHW, rem = mm - img * OHW;
+    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+    xbase[i] = img * a.H * a.W * a.C;
+    if (TRANS) { xh[i] = oh + a.pt; xw[i] = ow + a.pl; }
+    else { xh[i] = oh * a.sh - a.pt; xw[i] = ow * a.sw - a.pl; }
+  }
+  const T* wrow[WC];
+  bool wok[WC];
+#pragma unroll
+  for (int i = 0; i < WC; ++i) {
+    const int n = n0 + (tid >> 3) + i * 32;
+    wok[i] = n < a.Ncol;
+    wrow[i] = w + (long)(wok[i] ? n : 0) * a.Ktot;
+  }
+
+  // X staging registers come in two sets: the X loads of K step t+2 are
+  // issued at the top of step t and written to LDS at the bottom of step
+  // t+1, so each has two steps of MFMA work (not one) to cover its latency.
+  uint4 xr0[XC], wr0[WC], xr1[XC];
+  // ---- FAST-path state
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, a.wbytes, 0x00020000);
+  unsigned long long tapmask[XC];
+  int xoff[XC], woff[WC];
+  int s_cc = 0, s_kh = 0, s_kw = 0, s_tap = 0, s_tapi = 0, s_k = 0;
+  if constexpr (FAST) {
+#pragma unroll
+    for (int i = 0; i < XC; ++i) {
+      unsigned long long mk = 0;
+      for (int kh = 0; kh < a.KH; ++kh)
+        for (int kw = 0; kw < a.KW; ++kw) {
+          const bool in = (unsigned)(xh[i] + kh) < (unsigned)a.H &&
+                          (unsigned)(xw[i] + kw) < (unsigned)a.W;
+          mk |= (unsigned long long)(in && xok[i]) << (kh * a.KW + kw);
+        }
+      tapmask[i] = mk;
+      xoff[i] = xbase[i] + (xh[i] * a.W + xw[i]) * a.C + kc * 8;
+    }
+#pragma unroll
+    for (int i = 0; i < WC; ++i) woff[i] = (n0 + (tid >> 3) + i * 32) * a.Ktot + kc * 8;
+  }
+  // X and W have separate step counters: X runs one K step ahead of W.
+  auto load_x = [&](uint4 (&xr)[XC], int kt) {
+    if constexpr (FAST) {
+#pragma unroll
+      for (int i = 0; i < XC; ++i) {
+        const bool ok = (tapmask[i] >> s_tapi) & 1ull;
+        const int off = ok ? (xoff[i] + s_tap + s_cc) * (int)sizeof(T) : -1;
+        xr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+      }
+      s_cc += IG_BK;
+      if (s_cc == a.C) {
+        s_cc = 0;
+        ++s_tapi;
+        if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
+        s_tap = (s_kh * a.W + s_kw) * a.C;
+      }
+    } else {
+      const int k = kt * IG_BK + kc * 8;
+      const bool kok = k < a.Ktot;
+      const int tap = k / a.C, cc = k - tap * a.C;
+      const int kh = tap / a.KW, kw = tap - kh * a.KW;
+#pragma unroll
+      for (int i = 0; i < XC; ++i) {
+        bool ok = kok && xok[i];
+        int hi, wi;
+        if (TRANS) {
+          const int hh = xh[i] - kh, ww = xw[i] - kw;
+          ok = ok && hh >= 0 && ww >= 0;
+          hi = hh / a.sh; wi = ww / a.sw;
+          ok = ok && hi * a.sh == hh && wi * a.sw == ww && hi < a.H && wi < a.W;
+        } else {
+          hi = xh[i] + kh; wi = xw[i] + kw;
+          ok = ok && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+        }
+        xr[i] = ok ? *(const uint4*)(x + xbase[i] + (hi * a.W + wi) * a.C + cc)
+                   : make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto load_w = [&](uint4 (&wr)[WC], int kt) {
+    if constexpr (FAST) {
+#pragma unroll
+      for (int i = 0; i < WC; ++i)
+        wr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             wrs, (woff[i] + s_k) * (int)sizeof(T), 0, 0));
+      s_k += IG_BK;
+    } else {
+      const int k = kt * IG_BK + kc * 8;
+      const bool kok = k < a.Ktot;
+#pragma unroll
+      for (int i = 0; i < WC; ++i)
+        wr[i] = (kok && wok[i]) ? *(const uint4*)(wrow[i] + k) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store = [&](const uint4 (&xr)[XC], const uint4 (&wr)[WC], int buf) {
+    T* xs = smem + buf * (BM + BN) * IG_BK;
+    T* ws = xs + BM * IG_BK;
+#pragma unroll
+    for (int i = 0; i < XC; ++i) *(uint4*)(xs + swz_off((tid >> 3) + i * 32, kc)) = xr[i];
+#pragma unroll
+    for (int i = 0; i < WC; ++i) *(uint4*)(ws + swz_off((tid >> 3) + i * 32, kc)) = wr[i];
+  };
+
+  v4f acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int wn = wid >> 1, wm = wid & 1;
+  const int nk = (a.Ktot + IG_BK - 1) / IG_BK;
+  auto compute = [&](int buf) {
+    const T* xs = smem + buf * (BM + BN) * IG_BK;
+    const T* ws = xs + BM * IG_BK;
+#pragma unroll
+    for (int ks = 0; ks < IG_BK / 32; ++ks) {
+      const int chunk = ks * 4 + (lane >> 4);
+      v8s af[TN], bfr[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+        af[i] = *(const v8s*)(ws + swz_off(wn * (BN / 2) + i * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+        bfr[j] = *(const v8s*)(xs + swz_off(wm * (BM / 2) + j * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = Mfma<T>::run(af[i], bfr[j], acc[i][j]);
+    }
+  };
+  // The pixel (X) operand is loaded two K steps ahead through two register
+  // sets; the weight operand (small, L2-resident) one step ahead through a
+  // single set (a second set would spill at 128x128).
+  load_x(xr0, 0);
+  load_w(wr0, 0);
+  store(xr0, wr0, 0);
+  // Only the FAST 128x128 kernel takes the second X set: the generic gather
+  // would spill, and at 128x64 the extra registers cost a workgroup per CU
+  // (measured slower).
+  constexpr bool DEEP = FAST && BN > 64;
+  if constexpr (!DEEP) {
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) { load_x(xr0, kt + 1); load_w(wr0, kt + 1); }
+      compute(kt & 1);
+      if (kt + 1 < nk) store(xr0, wr0, (kt + 1) & 1);
+      __syncthreads();
+    }
+  }
+  if (DEEP && nk > 1) load_x(xr1, 1);
+  if constexpr (DEEP) __syncthreads();
+  // LDS buffer (kt & 1) holds step kt; X set 1 holds step kt+1 for even kt, set 0 for odd kt.
+  for (int kt = 0; DEEP && kt < nk; kt += 2) {
+    if (kt + 1 < nk) load_w(wr0, kt + 1);
+    if (kt + 2 < nk) load_x(xr0, kt + 2);
+    compute(0);
+    if (kt + 1 < nk) store(xr1, wr0, 1);
+    __syncthreads();
+    if (kt + 1 >= nk) break;
+    if (kt + 2 < nk) load_w(wr0, kt + 2);
+    if (kt + 3 < nk) load_x(xr1, kt + 3);
+    compute(1);
+    if (kt + 2 < nk) store(xr0, wr0, 0);
+    __syncthreads();
+  }
+
+  ig_epilogue<T, BM, BN, 256, 2, 2>(a, acc, smem, m0, n0, wm, wn);
+}
+
+// ------------------------------------------------------------ LDS-DMA igemm
+// FAST-geometry implicit GEMM whose operand tiles go global -> LDS by
+// LDS-DMA (buffer_load_dwordx4 ... lds): no staging registers, no ds_write
+// pass, and a 3-stage LDS ring so the loads of K step t+2 are in flight
+// while step t computes (counted vmcnt + raw barrier; never vmcnt(0) in the
+// loop).  512 threads = 8 waves as WGM (pixels) x WGN (channels); tile
+// BM pixels x BN channels; one workgroup per CU (the ring is up to 144 KB).
+//
+// An LDS-DMA wave-instruction writes 1 KB linearly (lane l -> base + 16 l),
+// i.e. 8 rows of the 128-byte-row image; the XOR swizzle of the fragment
+// reads (swz_off) is applied on the SOURCE side instead: lane l fetches the
+// logical 16-byte chunk (l & 7) ^ ((row >> 1) & 7) of its row.  Out-of-range
+// offsets (padding taps, rows past M or Ncol) make the range-checked load
+// write zeros into LDS (probed: scripts/probes/glds_oob.hip).
+constexpr int GL_STAGES = 3;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  // s_waitcnt simm16: vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt_hi[15:14]
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
+}
+
+// One LDS-DMA piece: 16 bytes per lane from buffer offset `off` (bytes) to
+// LDS base `lds` + 16 * lane.  A plain (non-template) device function: the
+// host compilation pass drops a kernel template that names this builtin.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, int off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
+                                           off, 0, 0, 0);
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  // raw barrier: __syncthreads() would also drain vmcnt (the ring's DMAs)
+  asm volatile("s_barrier" ::: "memory");
+}
+
+template <typename T, int BM, int BN, int WGM, int WGN>
+__global__ void __launch_bounds__(512, 1) igemm_glds_k(IgArgs a) {
+  constexpr int NT = 512;
+  static_assert(WGM * WGN == NT / 64, "wave grid");
+  constexpr int TM = BM / WGM / 16, TN = BN / WGN / 16;
+  constexpr int XI = BM / 64, WI = BN / 64;  // DMA instructions per thread per K step
+  constexpr int STAGE = (BM + BN) * IG_BK;   // elements per ring stage
+  static_assert(BM * BN <= GL_STAGES * STAGE, "epilogue staging exceeds the ring");
+  __shared__ __attribute__((aligned(16))) T smem[GL_STAGES * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mtiles = (a.M + BM - 1) / BM, ntiles = (a.Ncol + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int m0 = (bid / ntiles) * BM, n0 = (bid % ntiles) * BN;
+  const int OHW = a.OH * a.OW;
+  const int rr = tid >> 3;                       // DMA row within each 64-row slab
+  const int kc = (lane & 7) ^ ((rr >> 1) & 7);   // logical chunk this lane fetches
+
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.wbytes, 0x00020000);
+  unsigned long long tapmask[XI];
+  int xoff[XI], woff[WI];
+#pragma unroll
+  for (int i = 0; i < XI; ++i) {
+    const int m = m0 + i * 64 + rr;
+    const bool ok = m < a.M;
+    const int mm = ok ? m : 0;
+    const int img = mm / OHW, rem = mm - img * OHW;
+    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+    const int xh = oh * a.sh - a.pt, xw = ow * a.sw - a.pl;
+    unsigned long long mk = 0;
+    for (int kh = 0; kh < a.KH; ++kh)
+      for (int kw = 0; kw < a.KW; ++kw) {
+        const bool in = (unsigned)(xh + kh) < (unsigned)a.H && (unsigned)(xw + kw) < (unsigned)a.W;
+        mk |= (unsigned long long)(in && ok) << (kh * a.KW + kw);
+      }
+    tapmask[i] = mk;
+    xoff[i] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + kc * 8;
+  }
+#pragma unroll
+  for (int j = 0; j < WI; ++j) woff[j] = (n0 + j * 64 + rr) * a.Ktot + kc * 8;
+
+  int s_cc = 0, s_kh = 0, s_kw = 0, s_tap = 0, s_tapi = 0, s_k = 0;
+  auto issue = [&](int stage) {
+    T* xs = smem + stage * STAGE;
+    T* ws = xs + BM * IG_BK;
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const bool ok = (tapmask[i] >> s_tapi) & 1ull;
+      const int off = ok ? (xoff[i] + s_tap + s_cc) * (int)sizeof(T) : -1;
+      dma16(xrs, xs + (i * 64 + wid * 8) * IG_BK, off);
+    }
+#pragma unroll
+    for (int j = 0; j < WI; ++j)
+      dma16(wrs, ws + (j * 64 + wid * 8) * IG_BK, (woff[j] + s_k) * (int)sizeof(T));
+    s_k += IG_BK;
+    s_cc += IG_BK;
+    if (s_cc == a.C) {
+      s_cc = 0;
+      ++s_tapi;
+      if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
+      s_tap = (s_kh * a.W + s_kw) * a.C;
+    }
+  };
+
+  v4f acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int wm = wid % WGM, wn = wid / WGM;
+  auto compute = [&](int stage) {
+    const T* xs = smem + stage * STAGE;
+    const T* ws = xs + BM * IG_BK;
+#pragma unroll
+    for (int ks = 0; ks < IG_BK / 32; ++ks) {
+      const int chunk = ks * 4 + (lane >> 4);
+      v8s af[TN], bfr[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+        af[i] = *(const v8s*)(ws + swz_off(wn * (BN / WGN) + i * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+        bfr[j] = *(const v8s*)(xs + swz_off(wm * (BM / WGM) + j * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = Mfma<T>::run(af[i], bfr[j], acc[i][j]);
+    }
+  };
+
+  const int nk = a.Ktot / IG_BK;  // FAST geometry: C % 64 == 0
+  issue(0);
+  if (nk > 1) issue(1);
+  int st = 0;  // stage of step kt
+  for (int kt = 0; kt < nk; ++kt) {
+    // retire step kt's DMAs (step kt+1's, issued later, may stay in flight)
+    if (kt + 1 < nk) wait_vmcnt<XI + WI>(); else wait_vmcnt<0>();
+    lds_barrier();  // every wave's DMAs of step kt landed; stage (kt+2)%3 fully read
+    if (kt + 2 < nk) issue(st == 0 ? 2 : st - 1);
+    compute(st);  // (s_setprio(1) around it measured no faster)
+    st = st == 2 ? 0 : st + 1;
+  }
+  __syncthreads();  // all fragment reads done before the epilogue reuses the ring
+  ig_epilogue<T, BM, BN, NT, WGM, WGN>(a, acc, smem, m0, n0, wm, wn);
 }
 
 // ------------------------------------------------------------------ wgrad
@@ -713,6 +909,17 @@ static bool igemm_fast_disabled() {
   return off;
 }
 
+template <typename T>
+static void launch_glds(const IgArgs& a, hipStream_t s) {
+  const int mt = (a.M + 255) / 256;
+  if (a.Ncol <= 64)
+    hipLaunchKernelGGL((igemm_glds_k<T, 256, 64, 8, 1>), dim3(mt * ((a.Ncol + 63) / 64)), dim3(512),
+                       0, s, a);
+  else
+    hipLaunchKernelGGL((igemm_glds_k<T, 256, 128, 4, 2>), dim3(mt * ((a.Ncol + 127) / 128)),
+                       dim3(512), 0, s, a);
+}
+
 template <typename T, int BM, int BN>
 static void launch_ig(const IgArgs& a, bool trans, bool fast, hipStream_t s) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
@@ -752,13 +959,23 @@ static void launch_wg(const WgArgs& a, int mode, dim3 grid, hipStream_t s) {
 
 using namespace kfb;
 
+// Kernel choice (algo): IG_ALGO_CLASSIC = register-staged 128-tile igemm_k,
+// IG_ALGO_GLDS = LDS-DMA ring igemm_glds_k (FAST geometry only; others fall
+// back to igemm_k).  ops/conv_hip.py times both per geometry.
+enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2 };
+
+KFB_API int kfb_conv_igemm_fast(int C, int KH, int KW, int trans) {
+  return !trans && C % IG_BK == 0 && KH * KW <= 64 && !igemm_fast_disabled();
+}
+
 // Forward conv or dgrad (trans=1) or scattered 1x1 GEMM (ys>1).
 // Requirements: C % 8 == 0, Ncol % 4 == 0, 16-byte aligned pointers.
 KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void* y, int N, int H,
                                   int W, int C, int OH, int OW, int KH, int KW, int sh, int sw,
                                   int pt, int pl, int Ncol, int YH, int YW, int ys, int ldy,
                                   int trans, float* stats, const void* mask, const void* xbn,
-                                  const float* mean, const void* addend, hipStream_t stream) {
+                                  const float* mean, const void* addend, int algo,
+                                  hipStream_t stream) {
   if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
   const long xbytes = (long)N * H * W * C * 2, wbytes = (long)Ncol * KH * KW * C * 2;
   IgArgs a{x, w, y, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
@@ -767,6 +984,12 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
   const bool t = trans != 0;
   const bool fast = !t && C % IG_BK == 0 && KH * KW <= 64 && xbytes < (1L << 31) &&
                     wbytes < (1L << 31) && !igemm_fast_disabled();
+  if (algo == IG_ALGO_GLDS && fast) {
+    if (dtype == BF16) launch_glds<bf16>(a, stream);
+    else if (dtype == F16) launch_glds<f16>(a, stream);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   if (dtype == BF16) {
     if (Ncol <= 64) launch_ig<bf16, 128, 64>(a, t, fast, stream);
     else launch_ig<bf16, 128, 128>(a, t, fast, stream);

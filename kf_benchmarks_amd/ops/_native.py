@@ -67,7 +67,8 @@ class NativeError(RuntimeError):
 
 
 def lib_path() -> str:
-    return _build.HIP_LIB
+    # KFB_HIP_LIB: load an alternative build (kernel A/B experiments)
+    return os.environ.get("KFB_HIP_LIB") or _build.HIP_LIB
 
 
 def available() -> bool:

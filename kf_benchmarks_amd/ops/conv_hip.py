@@ -20,8 +20,15 @@ import torch
 
 from . import _native as N
 
-_SIG = [N.I, N.P, N.P, N.P] + [N.I] * 17 + [N.I, N.P, N.P, N.P, N.P, N.P, N.P]
+_SIG = [N.I, N.P, N.P, N.P] + [N.I] * 17 + [N.I, N.P, N.P, N.P, N.P, N.P, N.I, N.P]
 N.register_optional("kfb_conv_igemm", _SIG)
+N.register_optional("kfb_conv_igemm_fast", [N.I] * 4, N.c_int)
+
+# igemm kernel choice (csrc/conv_igemm.hip): 1 = register-staged 128-tile
+# igemm_k, 2 = LDS-DMA ring igemm_glds_k (FAST geometries only).
+IG_CLASSIC, IG_GLDS = 1, 2
+_IG_FORCE = {"classic": IG_CLASSIC, "glds": IG_GLDS}.get(os.environ.get("KFB_IGEMM_ALGO", ""))
+_ig_tuned = {}
 N.register_optional("kfb_conv_stats_spread", [], N.c_int)
 N.register_optional("kfb_conv_wgrad", [N.I, N.P, N.P, N.P] + [N.I] * 12 + [N.I, N.I, N.P, N.L, N.P])
 N.register_optional("kfb_conv_wgrad_splits", [N.I] * 8, N.c_int)
@@ -94,11 +101,48 @@ def stats_buffer(channels, device):
     return STATS_ARENA.take(2 * STATS_SPREAD * channels, device)[:2 * STATS_SPREAD * channels]
 
 
+def _igemm_call(algo, x, wmat, y, geo, stats=None, mask=None, xbn=None, mean=None, addend=None):
+    N.call("kfb_conv_igemm", N.dt(x), x.data_ptr(), wmat.data_ptr(), y.data_ptr(), *geo,
+           N.ptr(stats), N.ptr(mask), N.ptr(xbn), N.ptr(mean), N.ptr(addend), algo,
+           N.stream(x.device))
+
+
+def _igemm_algo(x, wmat, y, geo):
+    """Per-geometry kernel choice, timed once on the real operands (the
+    role cuDNN's algorithm autotune plays for the reference): both kernels
+    run the same K order, so the choice does not change the numerics."""
+    if _IG_FORCE is not None:
+        return _IG_FORCE
+    C, KH, KW, trans = geo[3], geo[6], geo[7], geo[17]
+    if not N.load().kfb_conv_igemm_fast(C, KH, KW, trans):
+        return IG_CLASSIC
+    key = (str(x.device), x.dtype) + tuple(geo)
+    best = _ig_tuned.get(key)
+    if best is not None:
+        return best
+    if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
+        return IG_GLDS
+    scratch = torch.empty_like(y)
+    times = {}
+    for algo in (IG_CLASSIC, IG_GLDS):
+        _igemm_call(algo, x, wmat, scratch, geo)  # warm
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        for _ in range(3):
+            _igemm_call(algo, x, wmat, scratch, geo)
+        ev1.record()
+        ev1.synchronize()
+        times[algo] = ev0.elapsed_time(ev1)
+    best = min(times, key=times.get)
+    _ig_tuned[key] = best
+    return best
+
+
 def _igemm(x, wmat, y, N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy,
            trans, stats=None, mask=None, xbn=None, mean=None, addend=None):
-    N.call("kfb_conv_igemm", N.dt(x), x.data_ptr(), wmat.data_ptr(), y.data_ptr(), N_, H, W, C,
-           OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy, int(trans), N.ptr(stats),
-           N.ptr(mask), N.ptr(xbn), N.ptr(mean), N.ptr(addend), N.stream(x.device))
+    geo = (N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy, int(trans))
+    algo = _igemm_algo(x, wmat, y, geo)
+    _igemm_call(algo, x, wmat, y, geo, stats, mask, xbn, mean, addend)
 
 
 def conv_fwd(x, wl, stride, pads, stats=None):

@@ -24,12 +24,23 @@ SHAPES = [
     (2, 8, 8, 20, 36, 3, 3, 1, "SAME"),           # Cin, Cout not multiples of 8
     (9, 2, 2, 64, 64, 3, 3, 1, "SAME"),           # rows wrap several images per K step
     (40, 1, 1, 256, 128, 1, 1, 1, "SAME"),        # 1x1 spatial (FC-like)
+    (3, 19, 21, 128, 192, 3, 3, 1, "SAME_RESNET"),  # M = 1197: several 256-row tiles + remainder
+    (2, 23, 23, 64, 320, 1, 1, 1, "SAME"),        # Ncol not a multiple of 128
 ]
+
+
+@pytest.fixture(params=["classic", "glds"])
+def ig_algo(request, monkeypatch):
+    """Runs a test once per igemm kernel (register-staged / LDS-DMA ring)."""
+    from kf_benchmarks_amd.ops import conv_hip
+    monkeypatch.setattr(conv_hip, "_IG_FORCE",
+                        {"classic": conv_hip.IG_CLASSIC, "glds": conv_hip.IG_GLDS}[request.param])
+    return request.param
 
 
 @pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-def test_conv_fwd_bwd(cuda, shape, dt):
+def test_conv_fwd_bwd(cuda, shape, dt, ig_algo):
     n, H, W, cin, cout, kh, kw, s, mode = shape
     torch.manual_seed(0)
     x = torch.randn(n, H, W, cin).to(dt).float()
@@ -84,12 +95,13 @@ FUSED_SHAPES = [
     (3, 9, 9, 64, 96, 3, 3, 2, "SAME_RESNET"),       # transposed gather
     (4, 2, 2, 512, 2048, 1, 1, 1, "SAME"),           # M=16
     (2, 13, 13, 64, 128, 1, 1, 2, "SAME"),           # scatter (addend only)
+    (2, 20, 20, 128, 192, 3, 3, 1, "SAME_RESNET"),   # M = 800: 256-row tiles + remainder
 ]
 
 
 @pytest.mark.parametrize("shape", FUSED_SHAPES, ids=[str(s) for s in FUSED_SHAPES])
 @pytest.mark.parametrize("with_addend", [False, True])
-def test_dgrad_fused_epilogue(cuda, shape, with_addend):
+def test_dgrad_fused_epilogue(cuda, shape, with_addend, ig_algo):
     """dgrad epilogue: dX = (conv^T(dY) + addend) * [x > 0] and the producer
     BN's backward partials sum(dX), sum(dX * (x_bn - mean)) per channel."""
     from kf_benchmarks_amd.ops import conv_hip
@@ -130,7 +142,7 @@ def test_dgrad_fused_epilogue(cuda, shape, with_addend):
 
 
 @pytest.mark.parametrize("shape", FUSED_SHAPES[:4], ids=[str(s) for s in FUSED_SHAPES[:4]])
-def test_fwd_stats_epilogue(cuda, shape):
+def test_fwd_stats_epilogue(cuda, shape, ig_algo):
     from kf_benchmarks_amd.ops import conv_hip
     n, H, W, cin, cout, kh, kw, s, mode = shape
     g = torch.Generator().manual_seed(2)
