@@ -74,7 +74,9 @@ def init_world(device_type: str = "cuda", all_reduce_spec: Optional[str] = None,
     if size <= 1:
         _WORLD = World(0, 1, local_rank, None)
         return _WORLD
-    backend = "nccl" if device_type == "cuda" else "gloo"
+    # KFB_DIST_BACKEND=gloo: ranks that share one GPU (RCCL refuses two ranks
+    # on one device) - the 2-rank GPU rehearsal on a 1-GPU box
+    backend = os.environ.get("KFB_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
     if backend == "nccl" and all_reduce_spec:
         from .allreduce import rccl_env_for_spec
         for k, v in rccl_env_for_spec(all_reduce_spec).items():
