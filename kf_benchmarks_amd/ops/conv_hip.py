@@ -165,11 +165,13 @@ def is_scatter_dgrad(w_shape, stride, pads):
     return KH == 1 and KW == 1 and pads[0] == 0 and pads[2] == 0 and stride != (1, 1)
 
 
-def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None, addend=None, wt=None):
+def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None, addend=None, wt=None,
+               addend_inplace=False):
     """``fuse`` = (stats, mask, xbn, mean): also apply the producer BN's ReLU
     mask to dX and accumulate its backward partial sums (see BNLink).
     ``addend``: gradient already produced by other consumers, added to dX
-    (not combined with ``fuse`` on the strided-1x1 scatter path)."""
+    (not combined with ``fuse`` on the strided-1x1 scatter path, where
+    ``addend_inplace`` lets dX accumulate into the addend's own buffer)."""
     n, H, W, C = x_shape
     fz = tuple(fuse if fuse is not None else (None, None, None, None)) + (addend,)
     cout, KH, KW, _ = wl.shape
@@ -183,7 +185,7 @@ def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None, addend=None, wt=None):
         elif addend is not None:
             # unsampled pixels keep the addend; sampled ones accumulate in place
             assert fuse is None
-            dx = addend.clone()
+            dx = addend if addend_inplace else addend.clone()
             fz = (None, None, None, None, dx)
         else:
             dx = torch.zeros((n, H, W, C), dtype=dy.dtype, device=dy.device)
@@ -269,6 +271,26 @@ def conv_wgrad(dy, x, w_shape, stride, pads, out=None):
     return dw
 
 
+_PAD_CACHE = {}
+
+
+def _padded_input(x, cin_p):
+    """Channel-padded copy of a network input (the RGB stem's 3 -> 8): the
+    synthetic batch is the same unmodified tensor every step, so its padded
+    copy is kept (one entry, keyed by storage and version counter) instead of
+    re-padded each step."""
+    if x.requires_grad:
+        return torch.nn.functional.pad(x, (0, cin_p - x.shape[-1]))
+    hit = _PAD_CACHE.get("in")
+    # identity (the entry keeps x alive, so its storage cannot be recycled
+    # under the key) plus the version counter (no in-place edit since)
+    if hit is not None and hit[0] is x and hit[1] == (x._version, cin_p):
+        return hit[2]
+    xp = torch.nn.functional.pad(x, (0, cin_p - x.shape[-1]))
+    _PAD_CACHE["in"] = (x, (x._version, cin_p), xp)
+    return xp
+
+
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, wl, stride, pads, stats, wt):
@@ -280,7 +302,7 @@ class _Conv2d(torch.autograd.Function):
         cin_p, cout_p = _pad8(cin), _pad8(cout)
         xp, wp = x, wl
         if cin_p != cin:
-            xp = torch.nn.functional.pad(x, (0, cin_p - cin))
+            xp = _padded_input(x, cin_p)
             wp = torch.nn.functional.pad(wp, (0, cin_p - cin))
         if cout_p != cout:
             wp = torch.nn.functional.pad(wp, (0, 0, 0, 0, 0, 0, 0, cout_p - cout))
@@ -311,7 +333,7 @@ class _Conv2d(torch.autograd.Function):
             padded = wp.shape[-1] != cin
             if link is not None and link.fusable:
                 if link.arrive():
-                    pend = link.pending
+                    pend, owned = link.pending, link.pending_owned
                     link.pending = None
                     if padded:
                         dx = conv_dgrad(dy, wp, xp.shape, stride, pads)[..., :cin]
@@ -322,7 +344,7 @@ class _Conv2d(torch.autograd.Function):
                             parts = stats_buffer(cin, dy.device)
                             fuse = (parts, xp if link.relu else None, link.x_bn, link.mean)
                         dx = conv_dgrad(dy, wp, xp.shape, stride, pads, fuse, addend=pend,
-                                        wt=ctx.wt)
+                                        wt=ctx.wt, addend_inplace=owned)
                         if fuse is not None:
                             link.partials = fuse[0]
                 else:

@@ -98,12 +98,13 @@ class BNLink:
     """
 
     __slots__ = ("x_bn", "mean", "relu", "convs", "resid", "other", "partials", "pending",
-                 "arrived")
+                 "pending_owned", "arrived")
 
     def __init__(self, x_bn, mean, relu):
         self.x_bn, self.mean, self.relu = x_bn, mean, relu
         self.convs, self.resid, self.other = 0, 0, False
         self.partials, self.pending, self.arrived = None, None, 0
+        self.pending_owned = False
 
     @property
     def fusable(self):
@@ -118,8 +119,13 @@ class BNLink:
         self.arrived += 1
         return self.arrived >= self.total
 
-    def deposit(self, g):
-        self.pending = g if self.pending is None else self.pending + g
+    def deposit(self, g, owned=True):
+        """``owned``: g is a fresh buffer nothing else reads, so the last
+        contributor may accumulate into it in place."""
+        if self.pending is None:
+            self.pending, self.pending_owned = g, owned
+        else:
+            self.pending, self.pending_owned = self.pending + g, True
 
 
 def _grad_sink(p):
@@ -216,7 +222,7 @@ class _BatchNormTrain(torch.autograd.Function):
                     dres = dres + rl.pending
                     rl.pending = None
             else:
-                rl.deposit(dres)
+                rl.deposit(dres, owned=dres is not dy)
                 dres = None
         if direct:
             _grad_ready(ctx.gamma)

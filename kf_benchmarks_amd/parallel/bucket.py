@@ -76,6 +76,7 @@ class BucketReducer:
                       for b in range(len(self.buckets))]
         self._pending = list(self.sizes)
         self._ready = [False] * len(self.buckets)
+        self._arrived = set()
         self._next = 0
         self._works = []
         self._active = False
@@ -93,6 +94,7 @@ class BucketReducer:
 
     def begin(self):
         """Arm the hooks for one backward pass."""
+        self._arrived = set()
         self._pending = list(self.sizes)
         self._ready = [False] * len(self.buckets)
         self._next = 0
@@ -105,6 +107,13 @@ class BucketReducer:
         b = self.param_bucket.get(id(p))
         if b is None:
             return
+        # A parameter whose kernel writes the flat gradient directly reports
+        # through _kfb_ready_cb, and autograd then still runs its (empty)
+        # AccumulateGrad post-hook: count each parameter once per backward, or
+        # a bucket would launch while half its gradients are still unwritten.
+        if id(p) in self._arrived:
+            return
+        self._arrived.add(id(p))
         self._pending[b] -= 1
         if self._pending[b] == 0:
             self._ready[b] = True

@@ -21,10 +21,37 @@ def main():
     from kf_benchmarks_amd.benchmark import BenchmarkCNN
     from kf_benchmarks_amd.parallel import comm
     p = P.make_params(**kw)
+    trace = []
+    if os.environ.get("KFB_TEST_TRACE_BUCKETS"):
+        from kf_benchmarks_amd.parallel import bucket
+        oh, ol = bucket.BucketReducer._hook, bucket.BucketReducer._launch
+
+        def hook(self, q):
+            trace.append(("hook", getattr(q, "_kfb_name", "?"), self.param_bucket.get(id(q)),
+                          self._active))
+            oh(self, q)
+
+        def launch(self, b, src=None):
+            trace.append(("launch", b, list(self._pending)))
+            ol(self, b, src)
+        bucket.BucketReducer._hook, bucket.BucketReducer._launch = hook, launch
     bench = BenchmarkCNN(p)
     bench.build()
+    for name, q, _, _ in bench.flat.segments():
+        q._kfb_name = name
     bench.strategy.broadcast_initial_model(bench.optimizer.slot_tensors().values())
     w0 = bench.flat.flat.detach().double().sum().item()
+    gsegs = []
+    if os.environ.get("KFB_TEST_GRAD_SEGS"):
+        orig = bench.strategy.after_backward
+
+        def after_backward(step):
+            orig(step)
+            torch.cuda.synchronize()
+            g = bench.flat.grad
+            gsegs.append({name: g[off:off + n].double().sum().item()
+                          for name, _, off, n in bench.flat.segments()})
+        bench.strategy.after_backward = after_backward
     losses = []
     for _ in range(steps):
         loss, _ = bench.train_step(need_loss=True)
@@ -34,6 +61,9 @@ def main():
     res = {"losses": losses, "w0": w0, "wsum": flat.double().sum().item(),
            "wabs": flat.double().abs().sum().item(), "head": flat[:64].cpu().tolist(),
            "tail": flat[-64:].cpu().tolist(), "rank": comm.get_world().rank,
+           "gsegs": gsegs, "trace": trace,
+           "segs": {name: flat[off:off + n].double().sum().item()
+                    for name, _, off, n in bench.flat.segments()},
            "size": comm.get_world().size}
     with open(out, "w") as f:
         json.dump(res, f)

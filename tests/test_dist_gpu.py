@@ -30,6 +30,7 @@ def _run(kw, steps, tmp_path, n=2):
     for r in range(n):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KFB_DIST_BACKEND="gloo",
+                   KFB_TEST_GRAD_SEGS="1",
                    PYTHONPATH=ROOT)
         out = tmp_path / ("rank%d.json" % r)
         cmd = [sys.executable, os.path.join(ROOT, "tests", "dist_gpu_worker.py"), str(out),
@@ -61,6 +62,13 @@ def test_two_ranks_stay_in_lock_step(cuda, tmp_path, extra):
     r0, r1 = _run(kw, 3, tmp_path)
     assert r0["size"] == r1["size"] == 2
     assert r0["w0"] == r1["w0"]  # broadcast initial model
+    for step, (g0, g1) in enumerate(zip(r0["gsegs"], r1["gsegs"])):
+        gd = [k for k in g0 if g0[k] != g1[k]]
+        assert not gd, "step %d: reduced gradients differ in %d variables, e.g. %s" % (
+            step, len(gd), [(k, g0[k], g1[k]) for k in gd[:4]])
+    diff = [k for k in r0["segs"] if r0["segs"][k] != r1["segs"][k]]
+    assert not diff, "replicas differ in %d of %d variables, e.g. %s" % (
+        len(diff), len(r0["segs"]), diff[:8])
     assert r0["wsum"] == r1["wsum"] and r0["wabs"] == r1["wabs"]
     assert r0["head"] == r1["head"] and r0["tail"] == r1["tail"]
     assert r0["wsum"] != r0["w0"]  # the step changed the weights
