@@ -28,7 +28,7 @@ step() {  # step <name> <timeout> <cmd...>
 
 step smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
 fi
 if [ "${CONV_BENCH:-0}" = "1" ]; then
   step conv_bench 600 python scripts/bench_conv.py --json "$OUT/conv_bench.json"
