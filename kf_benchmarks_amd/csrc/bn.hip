@@ -306,6 +306,279 @@ bn_bwd_apply_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __res
   }
 }
 
+// --------------------------------------------- BN + ReLU + max-pool (stem)
+// The ResNet stem tail relu(bn(conv1)) -> maxpool 3x3/2 as one op
+// (tcb/models/resnet_model.py:306-312): the forward never materializes the
+// 112x112 BN output (it normalizes each window tap on the fly and keeps the
+// argmax byte), and the backward never materializes the max-pool gradient
+// (each input pixel gathers the pooled gradients that routed to it, ReLU
+// masked by the pooled value, in both the partial-sum and the apply pass).
+struct BPGeo {
+  int N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl;
+};
+
+template <typename T, int V>
+__global__ void __launch_bounds__(256)
+bn_relu_maxpool_fwd_k(const T* __restrict__ x, T* __restrict__ z, uint8_t* __restrict__ idx,
+                      const float* __restrict__ scale, const float* __restrict__ shift, BPGeo g) {
+  // 32-bit index math (the host checks the element counts < 2^31)
+  const unsigned cv = (unsigned)(g.C / V);
+  const unsigned total = (unsigned)g.N * g.OH * g.OW * cv;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    const int c = (int)(i % cv) * V;
+    unsigned p = i / cv;
+    const int ow = (int)(p % (unsigned)g.OW); p /= (unsigned)g.OW;
+    const int oh = (int)(p % (unsigned)g.OH);
+    const int n = (int)(p / (unsigned)g.OH);
+    float sc[V], sf[V], best[V];
+    int bi[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      sc[k] = scale[c + k]; sf[k] = shift[c + k]; best[k] = -INFINITY; bi[k] = 0;
+    }
+    const int h0 = oh * g.sh - g.pt, w0 = ow * g.sw - g.pl;
+    for (int a = 0; a < g.kh; ++a) {
+      const int h = h0 + a;
+      if (h < 0 || h >= g.H) continue;
+      for (int b = 0; b < g.kw; ++b) {
+        const int w = w0 + b;
+        if (w < 0 || w >= g.W) continue;
+        float v[V];
+        load_vec<T, V>(x + (((long)n * g.H + h) * g.W + w) * g.C + c, v);
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+          // same bf16 rounding as the unfused BN output the pool would read
+          const float o = (float)from_f32<T>(fmaxf(v[k] * sc[k] + sf[k], 0.f));
+          if (o > best[k]) { best[k] = o; bi[k] = a * g.kw + b; }
+        }
+      }
+    }
+    const long o = (((long)n * g.OH + oh) * g.OW + ow) * g.C + c;
+    store_vec<T, V>(z + o, best);
+    Vec<uint8_t, V> iv;
+#pragma unroll
+    for (int k = 0; k < V; ++k) iv.v[k] = (uint8_t)bi[k];
+    *reinterpret_cast<Vec<uint8_t, V>*>(idx + o) = iv;
+  }
+}
+
+// Gradient reaching BN-output pixel (n, h, w), channels c..c+V-1: the sum of
+// the pooled gradients whose argmax is this pixel, where the pooled value is
+// > 0 (ReLU mask: the pooled value IS the ReLU output at the argmax).
+template <typename T, int V>
+__device__ __forceinline__ void pool_route_grad(const T* __restrict__ dz, const T* __restrict__ z,
+                                                const uint8_t* __restrict__ idx, const BPGeo& g,
+                                                int n, int h, int w, int c, float (&acc)[V]) {
+#pragma unroll
+  for (int k = 0; k < V; ++k) acc[k] = 0.f;
+  int oh_lo = h + g.pt - g.kh + 1;
+  oh_lo = oh_lo <= 0 ? 0 : (oh_lo + g.sh - 1) / g.sh;
+  int oh_hi = (h + g.pt) / g.sh;
+  if (oh_hi >= g.OH) oh_hi = g.OH - 1;
+  int ow_lo = w + g.pl - g.kw + 1;
+  ow_lo = ow_lo <= 0 ? 0 : (ow_lo + g.sw - 1) / g.sw;
+  int ow_hi = (w + g.pl) / g.sw;
+  if (ow_hi >= g.OW) ow_hi = g.OW - 1;
+  for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+    const int a = h - (oh * g.sh - g.pt);
+    for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+      const int pos = a * g.kw + (w - (ow * g.sw - g.pl));
+      const long o = (((long)n * g.OH + oh) * g.OW + ow) * g.C + c;
+      float d[V], zv[V];
+      load_vec<T, V>(dz + o, d);
+      load_vec<T, V>(z + o, zv);
+      const Vec<uint8_t, V> iv = *reinterpret_cast<const Vec<uint8_t, V>*>(idx + o);
+#pragma unroll
+      for (int k = 0; k < V; ++k)
+        if (iv.v[k] == pos && zv[k] > 0.f) acc[k] += d[k];
+    }
+  }
+}
+
+// Pass 1: per-slab sums of g and g*(x - mean) (g = routed, masked gradient).
+template <typename T, int V>
+__global__ void __launch_bounds__(BN_THREADS)
+bn_pool_partial_grad_k(const T* __restrict__ dz, const T* __restrict__ z,
+                       const uint8_t* __restrict__ idx, const T* __restrict__ x,
+                       const float* __restrict__ mean, BPGeo g, long rows, int cw, int tpr,
+                       int rpi, long slab_rows, float* __restrict__ pdy, float* __restrict__ pdyx) {
+  extern __shared__ float lds[];
+  const int C = g.C;
+  const int tid = threadIdx.x;
+  const int t = tid % tpr, r = tid / tpr;
+  const int c0 = blockIdx.y * cw + t * V;
+  const bool cok = (c0 < C) && (r < rpi);
+  float s[V], q[V], m[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) { s[i] = 0.f; q[i] = 0.f; m[i] = cok ? mean[c0 + i] : 0.f; }
+  const long rbeg = (long)blockIdx.x * slab_rows;
+  long rend = rbeg + slab_rows;
+  if (rend > rows) rend = rows;
+  if (cok) {
+    for (long row = rbeg + r; row < rend; row += rpi) {
+      const unsigned ur = (unsigned)row;
+      const int w = (int)(ur % (unsigned)g.W);
+      const unsigned hn = ur / (unsigned)g.W;
+      const int h = (int)(hn % (unsigned)g.H), n = (int)(hn / (unsigned)g.H);
+      float gr[V], xv[V];
+      pool_route_grad<T, V>(dz, z, idx, g, n, h, w, c0, gr);
+      load_vec<T, V>(x + row * C + c0, xv);
+#pragma unroll
+      for (int i = 0; i < V; ++i) { s[i] += gr[i]; q[i] += gr[i] * (xv[i] - m[i]); }
+    }
+  }
+  block_row_reduce<V>(s, q, lds, t, r, tpr, rpi);
+  if (r == 0 && c0 < C) {
+    float* ps = pdy + (long)blockIdx.x * C + c0;
+    float* pq = pdyx + (long)blockIdx.x * C + c0;
+#pragma unroll
+    for (int i = 0; i < V; ++i) { ps[i] = s[i]; pq[i] = q[i]; }
+  }
+}
+
+// Pass 2: dx = g*A + x*B + Cc for every BN input pixel.
+template <typename T, int V>
+__global__ void __launch_bounds__(256)
+bn_pool_bwd_apply_k(const T* __restrict__ dz, const T* __restrict__ z,
+                    const uint8_t* __restrict__ idx, const T* __restrict__ x, T* __restrict__ dx,
+                    BPGeo g, const float* __restrict__ A, const float* __restrict__ B,
+                    const float* __restrict__ Cc) {
+  const unsigned cv = (unsigned)(g.C / V);
+  const unsigned total = (unsigned)g.N * g.H * g.W * cv;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    const int c = (int)(i % cv) * V;
+    const unsigned row = i / cv;
+    const int w = (int)(row % (unsigned)g.W);
+    const unsigned hn = row / (unsigned)g.W;
+    const int h = (int)(hn % (unsigned)g.H), n = (int)(hn / (unsigned)g.H);
+    float gr[V], xv[V], o[V];
+    pool_route_grad<T, V>(dz, z, idx, g, n, h, w, c, gr);
+    load_vec<T, V>(x + row * g.C + c, xv);
+#pragma unroll
+    for (int k = 0; k < V; ++k) o[k] = gr[k] * A[c + k] + xv[k] * B[c + k] + Cc[c + k];
+    store_vec<T, V>(dx + row * g.C + c, o);
+  }
+}
+
+// 3x3 / stride-2 specialization (the ResNet stem pool).  A thread owns the
+// 2x2 block of BN-output pixels (2*oy - pt + a, 2*ox - pl + b), a, b in {0,1},
+// for 8 channels: exactly the windows (oy-1|oy, ox-1|ox) can route gradient
+// into it, so the thread reads those <= 4 windows once for 4 pixels (the
+// generic gather above reads up to 4 windows per pixel) and needs no
+// per-window index arithmetic.
+template <typename T>
+__device__ __forceinline__ void route_block_3s2(const T* __restrict__ dz, const T* __restrict__ z,
+                                                const uint8_t* __restrict__ idx, const BPGeo& g,
+                                                int n, int oy, int ox, int c,
+                                                float (&gr)[2][2][8]) {
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gr[a][b][k] = 0.f;
+#pragma unroll
+  for (int dy = -1; dy <= 0; ++dy) {
+    const int oh = oy + dy;
+    if ((unsigned)oh >= (unsigned)g.OH) continue;
+#pragma unroll
+    for (int dx = -1; dx <= 0; ++dx) {
+      const int ow = ox + dx;
+      if ((unsigned)ow >= (unsigned)g.OW) continue;
+      const long o = (((long)n * g.OH + oh) * g.OW + ow) * g.C + c;
+      float d[8], zv[8];
+      load_vec<T, 8>(dz + o, d);
+      load_vec<T, 8>(z + o, zv);
+      const Vec<uint8_t, 8> iv = *reinterpret_cast<const Vec<uint8_t, 8>*>(idx + o);
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int rh = a - 2 * dy;  // row of pixel a inside window oh: 0..3
+        if (rh > 2) continue;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int rw = b - 2 * dx;
+          if (rw > 2) continue;
+          const int pos = rh * 3 + rw;
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (iv.v[k] == pos && zv[k] > 0.f) gr[a][b][k] += d[k];
+        }
+      }
+    }
+  }
+}
+
+// PASS 0: per-block partial sums of g and g*(x-mean) -> slab blockIdx.x
+// (threads of a block share a channel group iff C/8 divides 256).
+// PASS 1: dx = g*A + x*B + Cc.
+template <typename T, int PASS>
+__global__ void __launch_bounds__(256)
+bn_pool3s2_k(const T* __restrict__ dz, const T* __restrict__ z, const uint8_t* __restrict__ idx,
+             const T* __restrict__ x, T* __restrict__ dx, BPGeo g, int OHo, int OWo,
+             const float* __restrict__ mean, float* __restrict__ pdy, float* __restrict__ pdyx,
+             const float* __restrict__ A, const float* __restrict__ B,
+             const float* __restrict__ Cc) {
+  const unsigned cv = (unsigned)(g.C / 8);
+  const unsigned total = (unsigned)g.N * OHo * OWo * cv;
+  const int c = (int)(threadIdx.x % cv) * 8;  // fixed: the grid stride is a multiple of cv
+  float cA[8], cB[8], cC[8], m[8], s[8], q[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (PASS == 0) { m[k] = mean[c + k]; s[k] = 0.f; q[k] = 0.f; }
+    else { cA[k] = A[c + k]; cB[k] = B[c + k]; cC[k] = Cc[c + k]; }
+  }
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    unsigned p = i / cv;
+    const int ox = (int)(p % (unsigned)OWo); p /= (unsigned)OWo;
+    const int oy = (int)(p % (unsigned)OHo);
+    const int n = (int)(p / (unsigned)OHo);
+    float gr[2][2][8];
+    route_block_3s2<T>(dz, z, idx, g, n, oy, ox, c, gr);
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int h = 2 * oy - g.pt + a;
+      if ((unsigned)h >= (unsigned)g.H) continue;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int w = 2 * ox - g.pl + b;
+        if ((unsigned)w >= (unsigned)g.W) continue;
+        const long e = (((long)n * g.H + h) * g.W + w) * g.C + c;
+        float xv[8];
+        load_vec<T, 8>(x + e, xv);
+        if (PASS == 0) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { s[k] += gr[a][b][k]; q[k] += gr[a][b][k] * (xv[k] - m[k]); }
+        } else {
+          float o[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = gr[a][b][k] * cA[k] + xv[k] * cB[k] + cC[k];
+          store_vec<T, 8>(dx + e, o);
+        }
+      }
+    }
+  }
+  if (PASS == 0) {
+    // fold the 256/cv threads of each channel group: LDS [256][16]
+    __shared__ float red[256 * 17];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[threadIdx.x * 17 + k] = s[k];
+      red[threadIdx.x * 17 + 8 + k] = q[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < cv * 16) {
+      const int grp = threadIdx.x / 16, k = threadIdx.x % 16;
+      float acc = 0.f;
+      for (int t = grp; t < 256; t += cv) acc += red[t * 17 + k];
+      float* dst = (k < 8 ? pdy : pdyx) + (long)blockIdx.x * g.C + grp * 8 + (k & 7);
+      *dst = acc;
+    }
+  }
+}
+
 static int stream_grid(long nvec) {
   long b = (nvec + 255) / 256;
   if (b > 256L * 16) b = 256L * 16;  // grid-stride beyond 16 blocks per CU
@@ -462,4 +735,87 @@ KFB_API hipError_t kfb_bn_bwd(int dtype, const void* dy, const void* y, const vo
     });
   });
   return hipGetLastError();
+}
+
+// Fused stem tail, forward (training): BN statistics come from the producing
+// conv's epilogue (psum/psq [nslab][C]); z = maxpool(relu(bn(x))) and the
+// per-element argmax bytes idx.  V = 8 (C % 8 == 0) only.
+KFB_API hipError_t kfb_bn_relu_maxpool_fwd(int dtype, const void* x, void* z, uint8_t* idx, int N,
+                                           int H, int W, int C, int OH, int OW, int kh, int kw,
+                                           int sh, int sw, int pt, int pl, const float* gamma,
+                                           const float* beta, float decay, float eps,
+                                           float* run_mean, float* run_var, float* save_mean,
+                                           float* save_invstd, float* scale, float* shift,
+                                           float* psum, float* psq, int nslab,
+                                           hipStream_t stream) {
+  if (C % 8 || kh * kw > 255 || (long)N * H * W * C >= (1L << 31)) return hipErrorInvalidValue;
+  const BPGeo g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
+  const long rows = (long)N * H * W;
+  hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, 4), 0, stream, psum, psq,
+                     nslab, C, rows, gamma, beta, decay, eps, run_mean, run_var, save_mean,
+                     save_invstd, scale, shift);
+  const long total = (long)N * OH * OW * (C / 8);
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((bn_relu_maxpool_fwd_k<T, 8>), dim3(stream_grid(total)), dim3(256), 0,
+                       stream, (const T*)x, (T*)z, idx, scale, shift, g);
+  });
+  return hipGetLastError();
+}
+
+// Fused stem tail, backward: dx (gradient of the BN input) from the pooled
+// gradient dz; dgamma/dbeta written (accumulate=0) or added (accumulate=1).
+// pdy/pdyx: [kfb_bn_num_slabs(N*H*W, C)][C] scratch; coef*: [C] scratch.
+KFB_API hipError_t kfb_bn_relu_maxpool_bwd(int dtype, const void* dz, const void* z,
+                                           const uint8_t* idx, const void* x, void* dx, int N,
+                                           int H, int W, int C, int OH, int OW, int kh, int kw,
+                                           int sh, int sw, int pt, int pl, const float* gamma,
+                                           const float* save_mean, const float* save_invstd,
+                                           float* dgamma, float* dbeta, float* pdy, float* pdyx,
+                                           int nslab, float* coefA, float* coefB, float* coefC,
+                                           int accumulate, hipStream_t stream) {
+  if (C % 8 || (long)N * H * W * C >= (1L << 31)) return hipErrorInvalidValue;
+  const BPGeo g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
+  const long rows = (long)N * H * W;
+  const int cv = C / 8;
+  if (kh == 3 && kw == 3 && sh == 2 && sw == 2 && 256 % cv == 0) {
+    // 3x3/2 block kernels: nslab blocks for the partial pass (the caller
+    // sizes the slabs with kfb_bn_pool_num_slabs)
+    const int OHo = (H + pt + 1) / 2, OWo = (W + pl + 1) / 2;
+    const long total = (long)N * OHo * OWo * cv;
+    if (total >= (1L << 31)) return hipErrorInvalidValue;
+    KFB_DISPATCH_DTYPE(dtype, T, {
+      hipLaunchKernelGGL((bn_pool3s2_k<T, 0>), dim3(nslab), dim3(256), 0, stream, (const T*)dz,
+                         (const T*)z, idx, (const T*)x, (T*)dx, g, OHo, OWo, save_mean, pdy, pdyx,
+                         nullptr, nullptr, nullptr);
+      hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, 4), 0, stream, pdy,
+                         pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta, coefA,
+                         coefB, coefC, accumulate);
+      hipLaunchKernelGGL((bn_pool3s2_k<T, 1>), dim3(stream_grid(total)), dim3(256), 0, stream,
+                         (const T*)dz, (const T*)z, idx, (const T*)x, (T*)dx, g, OHo, OWo, nullptr,
+                         nullptr, nullptr, coefA, coefB, coefC);
+    });
+    return hipGetLastError();
+  }
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    Geo gg = make_geo<8>(C);
+    const long slab_rows = (rows + nslab - 1) / nslab;
+    const size_t lds = 2 * (size_t)gg.rpi * gg.tpr * 8 * sizeof(float);
+    hipLaunchKernelGGL((bn_pool_partial_grad_k<T, 8>), dim3(nslab, gg.nchunk), dim3(BN_THREADS),
+                       lds, stream, (const T*)dz, (const T*)z, idx, (const T*)x, save_mean, g,
+                       rows, gg.cw, gg.tpr, gg.rpi, slab_rows, pdy, pdyx);
+    hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, 4), 0, stream, pdy,
+                       pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta, coefA,
+                       coefB, coefC, accumulate);
+    hipLaunchKernelGGL((bn_pool_bwd_apply_k<T, 8>), dim3(stream_grid(rows * C / 8)), dim3(256), 0,
+                       stream, (const T*)dz, (const T*)z, idx, (const T*)x, (T*)dx, g, coefA,
+                       coefB, coefC);
+  });
+  return hipGetLastError();
+}
+
+// Slab count kfb_bn_relu_maxpool_bwd uses (pdy/pdyx need nslab * C floats).
+KFB_API int kfb_bn_pool_num_slabs(int N, int H, int W, int C, int kh, int kw, int sh, int sw) {
+  if (kh == 3 && kw == 3 && sh == 2 && sw == 2 && C % 8 == 0 && 256 % (C / 8) == 0)
+    return 1024;  // 4 blocks per CU of the latency-bound gather pass
+  return kfb_bn_num_slabs((long)N * H * W, C);
 }

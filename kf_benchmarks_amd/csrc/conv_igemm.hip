@@ -243,13 +243,21 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
 // bitmask of its in-bounds taps, and operands are read with range-checked
 // buffer loads (an out-of-range offset returns zeros), so the loads need no
 // per-lane branches and no 64-bit address math.
-template <typename T, int BM, int BN, bool TRANS, bool FAST>
-__global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
+//
+// NBUF = 1: one LDS stage (the tile of step kt+1 waits in registers while
+// step kt computes).  Half the LDS and <= 128 VGPRs give 4 workgroups per CU
+// instead of 2; for the short-K layers (K = 64..128, e.g. the 56x56 1x1
+// convs, one or two K steps) the kernel is latency/epilogue bound and the
+// doubled occupancy is what hides it.
+template <typename T, int BM, int BN, bool TRANS, bool FAST, int NBUF = 2>
+__global__ void __launch_bounds__(256, NBUF == 1 ? 4 : 2) igemm_k(IgArgs a) {
   constexpr int XC = BM / 32;  // 16-byte X chunks per thread per K step
   constexpr int WC = BN / 32;  // 16-byte W chunks per thread per K step
   constexpr int TM = BM / 32;  // 16-wide pixel subtiles per wave
   constexpr int TN = BN / 32;  // 16-wide channel subtiles per wave
-  __shared__ __attribute__((aligned(16))) T smem[2 * (BM + BN) * IG_BK];
+  static_assert(NBUF == 1 || NBUF == 2, "stages");
+  static_assert(NBUF * (BM + BN) * IG_BK >= BM * BN, "epilogue staging exceeds LDS");
+  __shared__ __attribute__((aligned(16))) T smem[NBUF * (BM + BN) * IG_BK];
 
   const T* __restrict__ x = (const T*)a.x;
   const T* __restrict__ w = (const T*)a.w;
@@ -366,6 +374,7 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
     }
   };
   auto store = [&](const uint4 (&xr)[XC], const uint4 (&wr)[WC], int buf) {
+    if constexpr (NBUF == 1) buf = 0;
     T* xs = smem + buf * (BM + BN) * IG_BK;
     T* ws = xs + BM * IG_BK;
 #pragma unroll
@@ -383,6 +392,7 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
   const int wn = wid >> 1, wm = wid & 1;
   const int nk = (a.Ktot + IG_BK - 1) / IG_BK;
   auto compute = [&](int buf) {
+    if constexpr (NBUF == 1) buf = 0;
     const T* xs = smem + buf * (BM + BN) * IG_BK;
     const T* ws = xs + BM * IG_BK;
 #pragma unroll
@@ -410,13 +420,16 @@ __global__ void __launch_bounds__(256, 2) igemm_k(IgArgs a) {
   // Only the FAST 128x128 kernel takes the second X set: the generic gather
   // would spill, and at 128x64 the extra registers cost a workgroup per CU
   // (measured slower).
-  constexpr bool DEEP = FAST && BN > 64;
+  constexpr bool DEEP = FAST && BN > 64 && NBUF == 2;
   if constexpr (!DEEP) {
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + 1 < nk) { load_x(xr0, kt + 1); load_w(wr0, kt + 1); }
       compute(kt & 1);
-      if (kt + 1 < nk) store(xr0, wr0, (kt + 1) & 1);
+      if (kt + 1 < nk) {
+        if constexpr (NBUF == 1) __syncthreads();  // every wave done reading the stage
+        store(xr0, wr0, (kt + 1) & 1);
+      }
       __syncthreads();
     }
   }
@@ -910,9 +923,9 @@ static bool igemm_fast_disabled() {
 }
 
 template <typename T>
-static void launch_glds(const IgArgs& a, hipStream_t s) {
+static void launch_glds(const IgArgs& a, bool narrow, hipStream_t s) {
   const int mt = (a.M + 255) / 256;
-  if (a.Ncol <= 64)
+  if (a.Ncol <= 64 || narrow)
     hipLaunchKernelGGL((igemm_glds_k<T, 256, 64, 8, 1>), dim3(mt * ((a.Ncol + 63) / 64)), dim3(512),
                        0, s, a);
   else
@@ -921,9 +934,11 @@ static void launch_glds(const IgArgs& a, hipStream_t s) {
 }
 
 template <typename T, int BM, int BN>
-static void launch_ig(const IgArgs& a, bool trans, bool fast, hipStream_t s) {
+static void launch_ig(const IgArgs& a, bool trans, bool fast, hipStream_t s, bool onebuf = false) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
-  if (trans)
+  if (onebuf && fast)
+    hipLaunchKernelGGL((igemm_k<T, BM, BN, false, true, 1>), dim3(nwg), dim3(256), 0, s, a);
+  else if (trans)
     hipLaunchKernelGGL((igemm_k<T, BM, BN, true, false>), dim3(nwg), dim3(256), 0, s, a);
   else if (fast)
     hipLaunchKernelGGL((igemm_k<T, BM, BN, false, true>), dim3(nwg), dim3(256), 0, s, a);
@@ -961,8 +976,14 @@ using namespace kfb;
 
 // Kernel choice (algo): IG_ALGO_CLASSIC = register-staged 128-tile igemm_k,
 // IG_ALGO_GLDS = LDS-DMA ring igemm_glds_k (FAST geometry only; others fall
-// back to igemm_k).  ops/conv_hip.py times both per geometry.
-enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2 };
+// back to igemm_k).  The _N64 variants force the 64-channel-wide tile for
+// Ncol > 64: twice the workgroups, which pays where 128-wide tiles leave the
+// last wave of workgroups mostly empty (small-M stage-4/5 layers: 784 tiles
+// on 512 slots is 1.5 waves).  ops/conv_hip.py times the candidates per
+// geometry.
+//   IG_ALGO_ONEBUF(_N64): FAST igemm_k with one LDS stage (4 workgroups/CU).
+enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_GLDS_N64 = 4,
+       IG_ALGO_ONEBUF = 5, IG_ALGO_ONEBUF_N64 = 6 };
 
 KFB_API int kfb_conv_igemm_fast(int C, int KH, int KW, int trans) {
   return !trans && C % IG_BK == 0 && KH * KW <= 64 && !igemm_fast_disabled();
@@ -984,18 +1005,21 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
   const bool t = trans != 0;
   const bool fast = !t && C % IG_BK == 0 && KH * KW <= 64 && xbytes < (1L << 31) &&
                     wbytes < (1L << 31) && !igemm_fast_disabled();
-  if (algo == IG_ALGO_GLDS && fast) {
-    if (dtype == BF16) launch_glds<bf16>(a, stream);
-    else if (dtype == F16) launch_glds<f16>(a, stream);
+  const bool narrow = algo == IG_ALGO_CLASSIC_N64 || algo == IG_ALGO_GLDS_N64 ||
+                      algo == IG_ALGO_ONEBUF_N64;
+  const bool onebuf = algo == IG_ALGO_ONEBUF || algo == IG_ALGO_ONEBUF_N64;
+  if ((algo == IG_ALGO_GLDS || algo == IG_ALGO_GLDS_N64) && fast) {
+    if (dtype == BF16) launch_glds<bf16>(a, narrow, stream);
+    else if (dtype == F16) launch_glds<f16>(a, narrow, stream);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }
   if (dtype == BF16) {
-    if (Ncol <= 64) launch_ig<bf16, 128, 64>(a, t, fast, stream);
-    else launch_ig<bf16, 128, 128>(a, t, fast, stream);
+    if (Ncol <= 64 || narrow) launch_ig<bf16, 128, 64>(a, t, fast, stream, onebuf);
+    else launch_ig<bf16, 128, 128>(a, t, fast, stream, onebuf);
   } else if (dtype == F16) {
-    if (Ncol <= 64) launch_ig<f16, 128, 64>(a, t, fast, stream);
-    else launch_ig<f16, 128, 128>(a, t, fast, stream);
+    if (Ncol <= 64 || narrow) launch_ig<f16, 128, 64>(a, t, fast, stream, onebuf);
+    else launch_ig<f16, 128, 128>(a, t, fast, stream, onebuf);
   } else {
     return hipErrorInvalidValue;
   }

@@ -1,0 +1,91 @@
+// Space-to-depth repack for stride-2 convolutions over few-channel inputs
+// (the RGB stem: 7x7/2, 3 -> 64, tcb/models/resnet_model.py:311 with the
+// SAME_RESNET padding of tcb/convnet_builder.py:159-183).
+//
+// A 3-channel NHWC image gives an implicit GEMM only 3 useful elements per
+// tap, so the generic kernel pads C to 8 and walks 49 taps of 8 (K = 392 for
+// 147 useful).  Instead, for each output row oh and each column pair j the
+// repack writes one 64-element "pixel":
+//
+//   X2[n][oh][j][kh*8 + t*4 + c] = x[n][2*oh - pt + kh][2*j + t - pl][c]
+//
+// (zero outside the image, for c >= C and for kh >= KH).  The strided conv
+// then becomes a stride-1, KW2 = ceil(KW/2)-tap, 64-channel conv over X2 with
+// no padding: K = 4*64 = 256 for the 7x7 stem, and the FAST implicit-GEMM
+// kernels (C % 64 == 0, wave-uniform tap stepping, LDS-DMA) apply unchanged.
+// The weight is repacked to [Cout][1][KW2][64] the same way (host side,
+// ops/conv_hip.py), and the weight gradient of the X2 conv maps back by the
+// inverse permutation.
+#include "common.h"
+
+namespace kfb {
+
+// One workgroup per output row (n, oh): its KH input rows are read with
+// dword loads (all issued before any LDS write: 8 rows x 4 per thread in
+// flight) into an LDS copy raw[kh][W*C] (zeros for rows outside the image or
+// kh >= KH); every 16-byte output chunk (j, kh) is then gathered from LDS and
+// written with one 16-byte store.
+constexpr int S2D_ROW_DW = 1024;  // max dwords per input row (host-checked)
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+s2d_stem_k(const T* __restrict__ x, T* __restrict__ x2, int H, int W, int C, int OH, int OW2,
+           int KH, int pt, int pl) {
+  __shared__ uint32_t raw[8 * S2D_ROW_DW];
+  const int row = blockIdx.x;  // n * OH + oh
+  const int n = row / OH, oh = row - n * OH;
+  const int rdw = W * C * (int)sizeof(T) / 4;
+  const int tid = threadIdx.x;
+  uint32_t v[8][4];
+#pragma unroll
+  for (int kh = 0; kh < 8; ++kh) {
+    const int h = 2 * oh - pt + kh;
+    const bool ok = kh < KH && (unsigned)h < (unsigned)H;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(x + ((long)n * H + (ok ? h : 0)) * W * C);
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int d = tid + it * 256;
+      v[kh][it] = (ok && d < rdw) ? src[d] : 0u;
+    }
+  }
+#pragma unroll
+  for (int kh = 0; kh < 8; ++kh)
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int d = tid + it * 256;
+      if (d < rdw) raw[kh * rdw + d] = v[kh][it];
+    }
+  __syncthreads();
+  const T* rt = reinterpret_cast<const T*>(raw);
+  const int rel = rdw * 4 / (int)sizeof(T);  // elements per LDS row (= W*C)
+  T* dst = x2 + (long)row * OW2 * 64;
+  for (int q = tid; q < OW2 * 8; q += 256) {
+    const int j = q >> 3, kh = q & 7;
+    Vec<T, 8> o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int t = e >> 2, c = e & 3;
+      const int w = 2 * j + t - pl;
+      o.v[e] = (c < C && (unsigned)w < (unsigned)W) ? rt[kh * rel + w * C + c] : (T)0.f;
+    }
+    *reinterpret_cast<Vec<T, 8>*>(dst + (long)j * 64 + kh * 8) = o;
+  }
+}
+
+}  // namespace kfb
+
+using namespace kfb;
+
+// x [N,H,W,C] (C <= 4) -> x2 [N,OH,OW2,64]; requires KH <= 8.
+KFB_API hipError_t kfb_s2d_stem(int dtype, const void* x, void* x2, int N, int H, int W, int C,
+                                int OH, int OW2, int KH, int pt, int pl, hipStream_t stream) {
+  const int esz = dtype == F32 ? 4 : 2;
+  if (C > 4 || KH > 8 || (W * C * esz) % 4 || W * C * esz > 4 * S2D_ROW_DW ||
+      ((uintptr_t)x & 3))
+    return hipErrorInvalidValue;
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((s2d_stem_k<T>), dim3(N * OH), dim3(256), 0, stream, (const T*)x, (T*)x2,
+                       H, W, C, OH, OW2, KH, pt, pl);
+  });
+  return hipGetLastError();
+}

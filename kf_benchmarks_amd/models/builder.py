@@ -93,7 +93,10 @@ class ConvNetBuilder:
     # ------------------------------------------------------------------ conv
     def conv(self, num_out_channels, k_height, k_width, d_height=1, d_width=1, mode="SAME",
              input_layer=None, num_channels_in=None, use_batch_norm=None, stddev=None,
-             activation="relu", bias=0.0, kernel_initializer=None, residual=None):
+             activation="relu", bias=0.0, kernel_initializer=None, residual=None, pool=None):
+        """``pool`` = (k_h, k_w, d_h, d_w, mode): a max-pool applied to the
+        (BN + ReLU) output, i.e. conv(...) then mpool(*pool); with BN in
+        training on the GPU the BN apply, ReLU and pool run as one fused op."""
         x = self.top_layer if input_layer is None else input_layer
         cin = self.top_size if num_channels_in is None else num_channels_in
         name = "conv%d" % self.counts["conv"]
@@ -120,6 +123,14 @@ class ConvNetBuilder:
         y = F.conv2d(x, w, None if self.meta else layer.weight_lp, (d_height, d_width), pads,
                      self.impl, stats, None if self.meta else layer.weight_t)
         relu = activation == "relu"
+        if pool is not None:
+            if use_batch_norm and relu and residual is None and not self.meta and \
+                    F.bn_relu_max_pool_fusable(y, stats, self.phase_train):
+                with self.scope(name):
+                    self.top_layer, self.top_size = y, num_out_channels
+                    y = self._bn_relu_max_pool(y, stats, pool, **self.batch_norm_config)
+                self.top_layer, self.top_size = y, num_out_channels
+                return y
         if use_batch_norm:
             with self.scope(name):
                 self.top_layer, self.top_size = y, num_out_channels
@@ -134,6 +145,8 @@ class ConvNetBuilder:
             if activation not in ("relu", None, "linear"):
                 y = F.activation(y, activation)
         self.top_layer, self.top_size = y, num_out_channels
+        if pool is not None:
+            return self.mpool(*pool)
         return y
 
     def depthwise_conv(self, k_height, k_width, d_height=1, d_width=1, mode="SAME",
@@ -299,16 +312,30 @@ class ConvNetBuilder:
         return self._batch_norm(x, decay=decay, scale=scale, epsilon=epsilon, relu=relu,
                                 residual=residual)
 
+    def _bn_layer(self, C, scale, decay, epsilon):
+        name = "batchnorm%d" % self.counts["batchnorm"]
+        self.counts["batchnorm"] += 1
+        scope = self._scoped(name)
+        return self._layer(scope, lambda: BatchNormLayer(scope, C, scale, decay, epsilon,
+                                                         self.net.param_device))
+
+    def _bn_relu_max_pool(self, x, stats, pool, decay=0.999, scale=False, epsilon=0.001):
+        """relu(batch_norm(x)) then mpool(*pool), fused (training, GPU); the
+        layer names and counts are those of _batch_norm + mpool."""
+        self._use(x)
+        layer = self._bn_layer(x.shape[-1], scale, decay, epsilon)
+        kh, kw, sh, sw, mode = (tuple(pool) + ("VALID",))[:5]
+        self.counts["mpool"] += 1
+        return F.bn_relu_max_pool(x, layer.gamma, layer.beta, layer.moving_mean,
+                                  layer.moving_variance, layer.decay, layer.eps, stats,
+                                  kh, kw, sh, sw, mode)
+
     def _batch_norm(self, x, decay=0.999, scale=False, epsilon=0.001, relu=False,
                     residual=None, stats=None):
         self._use(x)
         self._use(residual, resid=True)
-        name = "batchnorm%d" % self.counts["batchnorm"]
-        self.counts["batchnorm"] += 1
-        scope = self._scoped(name)
         C = x.shape[-1]
-        layer = self._layer(scope, lambda: BatchNormLayer(scope, C, scale, decay, epsilon,
-                                                          self.net.param_device))
+        layer = self._bn_layer(C, scale, decay, epsilon)
         training = self.phase_train and not self.meta
         if self.meta:
             y = F.batch_norm(x, self._p(layer.gamma), self._p(layer.beta),

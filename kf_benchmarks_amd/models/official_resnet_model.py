@@ -49,12 +49,12 @@ class ImagenetResnetModel(model_lib.CNNModel):
 
     # --------------------------------------------------------------- blocks
     def _conv(self, cnn, filters, k, stride, bn, relu, input_layer=None, cin=None,
-              residual=None):
+              residual=None, pool=None):
         cin = cnn.top_size if cin is None else cin
         return cnn.conv(filters, k, k, stride, stride, mode="SAME_RESNET", input_layer=input_layer,
                         num_channels_in=cin, use_batch_norm=bn, bias=None,
                         stddev=_he(cin, k), activation="relu" if relu else None,
-                        residual=residual)
+                        residual=residual, pool=pool)
 
     def _block_v1(self, cnn, filters, stride, project, bottleneck):
         x, cin = cnn.top_layer, cnn.top_size
@@ -95,8 +95,7 @@ class ImagenetResnetModel(model_lib.CNNModel):
         cnn.batch_norm_config = {"decay": 0.997, "epsilon": 1e-5, "scale": True}
         v1 = self.version == 1
         with cnn.scope("resnet_model"):
-            self._conv(cnn, 64, 7, 2, v1, v1)
-            cnn.mpool(3, 3, 2, 2, mode="SAME")
+            self._conv(cnn, 64, 7, 2, v1, v1, pool=(3, 3, 2, 2, "SAME"))
             filters = 64
             for li, n in enumerate(layers):
                 stride = 1 if li == 0 else 2

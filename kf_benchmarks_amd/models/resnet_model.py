@@ -139,8 +139,9 @@ class ResnetModel(model_lib.CNNModel):
             raise ValueError("Layer counts not specified for %s" % self.get_model_name())
         cnn.use_batch_norm = True
         cnn.batch_norm_config = {"decay": 0.9, "epsilon": 1e-5, "scale": True}
-        cnn.conv(64, 7, 7, 2, 2, mode="SAME_RESNET", use_batch_norm=True)
-        cnn.mpool(3, 3, 2, 2, mode="SAME")
+        # conv -> BN -> ReLU -> 3x3/2 max-pool (fused on the GPU in training)
+        cnn.conv(64, 7, 7, 2, 2, mode="SAME_RESNET", use_batch_norm=True,
+                 pool=(3, 3, 2, 2, "SAME"))
         for _ in range(self.layer_counts[0]):
             bottleneck_block(cnn, 256, 64, 1, self.version)
         for i in range(self.layer_counts[1]):

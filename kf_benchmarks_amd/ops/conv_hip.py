@@ -26,8 +26,10 @@ N.register_optional("kfb_conv_igemm_fast", [N.I] * 4, N.c_int)
 
 # igemm kernel choice (csrc/conv_igemm.hip): 1 = register-staged 128-tile
 # igemm_k, 2 = LDS-DMA ring igemm_glds_k (FAST geometries only).
-IG_CLASSIC, IG_GLDS = 1, 2
-_IG_FORCE = {"classic": IG_CLASSIC, "glds": IG_GLDS}.get(os.environ.get("KFB_IGEMM_ALGO", ""))
+IG_CLASSIC, IG_GLDS, IG_CLASSIC_N64, IG_GLDS_N64, IG_ONEBUF, IG_ONEBUF_N64 = 1, 2, 3, 4, 5, 6
+IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N64,
+            "glds_n64": IG_GLDS_N64, "onebuf": IG_ONEBUF, "onebuf_n64": IG_ONEBUF_N64}
+_IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 N.register_optional("kfb_conv_stats_spread", [], N.c_int)
 N.register_optional("kfb_conv_wgrad", [N.I, N.P, N.P, N.P] + [N.I] * 12 + [N.I, N.I, N.P, N.L, N.P])
@@ -107,29 +109,41 @@ def _igemm_call(algo, x, wmat, y, geo, stats=None, mask=None, xbn=None, mean=Non
            N.stream(x.device))
 
 
-def _igemm_algo(x, wmat, y, geo):
-    """Per-geometry kernel choice, timed once on the real operands (the
-    role cuDNN's algorithm autotune plays for the reference): both kernels
-    run the same K order, so the choice does not change the numerics."""
+def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None)):
+    """Per-geometry kernel choice, timed once on the real operands with the
+    real fused epilogue (the role cuDNN's algorithm autotune plays for the
+    reference): all kernels run the same K order, so the choice does not
+    change the numerics.  ``fused`` = (stats, mask, xbn, mean, addend); the
+    timing runs write a scratch output and scratch statistics."""
     if _IG_FORCE is not None:
         return _IG_FORCE
-    C, KH, KW, trans = geo[3], geo[6], geo[7], geo[17]
-    if not N.load().kfb_conv_igemm_fast(C, KH, KW, trans):
-        return IG_CLASSIC
-    key = (str(x.device), x.dtype) + tuple(geo)
+    C, KH, KW, ncol, trans = geo[3], geo[6], geo[7], geo[12], geo[17]
+    fast = N.load().kfb_conv_igemm_fast(C, KH, KW, trans)
+    cands = (IG_CLASSIC, IG_GLDS, IG_ONEBUF) if fast else (IG_CLASSIC,)
+    if ncol > 64:  # 64-wide tiles: more workgroups for small-M layers
+        cands += (IG_CLASSIC_N64, IG_GLDS_N64, IG_ONEBUF_N64) if fast else (IG_CLASSIC_N64,)
+    if len(cands) == 1:
+        return cands[0]
+    stats, mask, xbn, mean, addend = fused
+    key = (str(x.device), x.dtype, stats is not None, mask is not None, xbn is not None,
+           addend is not None) + tuple(geo)
     best = _ig_tuned.get(key)
     if best is not None:
         return best
     if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
-        return IG_GLDS
+        return IG_GLDS if fast else IG_CLASSIC
     scratch = torch.empty_like(y)
+    if addend is not None and addend.data_ptr() == y.data_ptr():
+        addend = addend.clone()  # in-place accumulation target: time on a copy
+    sstats = torch.zeros_like(stats) if stats is not None else None
     times = {}
-    for algo in (IG_CLASSIC, IG_GLDS):
-        _igemm_call(algo, x, wmat, scratch, geo)  # warm
+    for algo in cands:
+        args = (x, wmat, scratch, geo, sstats, mask, xbn, mean, addend)
+        _igemm_call(algo, *args)  # warm
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
         for _ in range(3):
-            _igemm_call(algo, x, wmat, scratch, geo)
+            _igemm_call(algo, *args)
         ev1.record()
         ev1.synchronize()
         times[algo] = ev0.elapsed_time(ev1)
@@ -141,7 +155,7 @@ def _igemm_algo(x, wmat, y, geo):
 def _igemm(x, wmat, y, N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy,
            trans, stats=None, mask=None, xbn=None, mean=None, addend=None):
     geo = (N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy, int(trans))
-    algo = _igemm_algo(x, wmat, y, geo)
+    algo = _igemm_algo(x, wmat, y, geo, (stats, mask, xbn, mean, addend))
     _igemm_call(algo, x, wmat, y, geo, stats, mask, xbn, mean, addend)
 
 
@@ -291,6 +305,63 @@ def _padded_input(x, cin_p):
     return xp
 
 
+N.register_optional("kfb_s2d_stem", [N.I, N.P, N.P] + [N.I] * 9 + [N.P])
+_STEM_S2D = os.environ.get("KFB_STEM_S2D", "1") != "0"
+
+
+def use_s2d(x, wl_shape, stride, needs_dx, pads) -> bool:
+    """Stride-2 conv over a <=4-channel input with a big kernel (the RGB
+    stem) and no input gradient: run it as a 64-channel stride-1 conv over a
+    space-to-depth repack (csrc/stem.hip)."""
+    cout, KH, KW, cin = wl_shape
+    if not (_STEM_S2D and not needs_dx and tuple(stride) == (2, 2) and cin <= 4
+            and KH <= 8 and KW <= 8 and KH * KW >= 25 and cout % 8 == 0
+            and hasattr(N.load(), "kfb_s2d_stem")):
+        return False
+    OH, _, _, OW2 = s2d_geometry(x.shape, wl_shape, pads)
+    row_bytes = x.shape[2] * cin * x.element_size()
+    return (x.shape[0] * OH * OW2 * 64 < (1 << 31) and row_bytes % 4 == 0
+            and row_bytes <= 4096 and x.data_ptr() % 4 == 0)
+
+
+def s2d_geometry(x_shape, wl_shape, pads):
+    n, H, W, _ = x_shape
+    _, KH, KW, _ = wl_shape
+    pt, pb, pl, pr = pads
+    OH = (H + pt + pb - KH) // 2 + 1
+    OW = (W + pl + pr - KW) // 2 + 1
+    kw2 = (KW + 1) // 2
+    return OH, OW, kw2, OW + kw2 - 1
+
+
+def s2d_input(x, wl_shape, pads):
+    """x [N,H,W,C<=4] -> X2 [N,OH,OW+KW2-1,64] (see csrc/stem.hip)."""
+    n, H, W, cin = x.shape
+    KH = wl_shape[1]
+    OH, _, _, OW2 = s2d_geometry(x.shape, wl_shape, pads)
+    x2 = torch.empty((n, OH, OW2, 64), dtype=x.dtype, device=x.device)
+    N.call("kfb_s2d_stem", N.dt(x), x.data_ptr(), x2.data_ptr(), n, H, W, cin, OH, OW2, KH,
+           pads[0], pads[2], N.stream(x.device))
+    return x2
+
+
+def s2d_weight(wl):
+    """[Cout,KH,KW,C] -> [Cout,1,KW2,64] with channel = kh*8 + t*4 + c for
+    tap column kw = 2*j + t (zeros where kh >= KH, kw >= KW, c >= C)."""
+    cout, KH, KW, cin = wl.shape
+    kw2 = (KW + 1) // 2
+    wp = torch.nn.functional.pad(wl, (0, 4 - cin, 0, 2 * kw2 - KW, 0, 8 - KH))
+    return wp.view(cout, 8, kw2, 2, 4).permute(0, 2, 1, 3, 4).reshape(cout, 1, kw2, 64)
+
+
+def s2d_weight_grad(dw2, wl_shape):
+    """Inverse of s2d_weight for the fp32 weight gradient."""
+    cout, KH, KW, cin = wl_shape
+    kw2 = dw2.shape[2]
+    g = dw2.view(cout, kw2, 8, 2, 4).permute(0, 2, 1, 3, 4).reshape(cout, 8, 2 * kw2, 4)
+    return g[:, :KH, :KW, :cin]
+
+
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, wl, stride, pads, stats, wt):
@@ -299,6 +370,15 @@ class _Conv2d(torch.autograd.Function):
             wl = w.detach().to(x.dtype)
         cin = x.shape[-1]
         cout = wl.shape[0]
+        ctx.s2d = None
+        if use_s2d(x, wl.shape, stride, ctx.needs_input_grad[0], pads):
+            x2 = s2d_input(x, wl.shape, pads)
+            w2 = s2d_weight(wl).contiguous()
+            y = conv_fwd(x2, w2, (1, 1), (0, 0, 0, 0), stats)
+            ctx.save_for_backward(x2, w2)
+            ctx.s2d = tuple(wl.shape)
+            ctx.w = w
+            return y
         cin_p, cout_p = _pad8(cin), _pad8(cout)
         xp, wp = x, wl
         if cin_p != cin:
@@ -321,6 +401,8 @@ class _Conv2d(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        if ctx.s2d is not None:
+            return _Conv2d._backward_s2d(ctx, dy)
         xp, wp = ctx.saved_tensors
         stride, pads, cin, cout, x_shape = ctx.meta
         dy = dy.contiguous()
@@ -369,6 +451,26 @@ class _Conv2d(torch.autograd.Function):
             elif dw.shape[0] != cout or dw.shape[-1] != cin:
                 dw = dw[:cout, :, :, :cin].contiguous()
         return dx, dw, None, None, None, None, None
+
+
+    @staticmethod
+    def _backward_s2d(ctx, dy):
+        x2, w2 = ctx.saved_tensors
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw2 = conv_wgrad(dy.contiguous(), x2, w2.shape, (1, 1), (0, 0, 0, 0))
+            dw = s2d_weight_grad(dw2, ctx.s2d)
+            w = ctx.w
+            sink = getattr(w, "_kfb_grad_sink", None)
+            if sink is not None and _fuse_enabled():
+                sink.add_(dw)
+                cb = getattr(w, "_kfb_ready_cb", None)
+                if cb is not None:
+                    cb(w)
+                dw = None
+            else:
+                dw = dw.contiguous()
+        return None, dw, None, None, None, None, None
 
 
 def conv2d(x, w, wl, stride, pads, stats=None, wt=None):

@@ -424,6 +424,85 @@ class _AvgPool(torch.autograd.Function):
         return dx, None, None, None, None, None, None, None
 
 
+N.register_optional("kfb_bn_relu_maxpool_fwd", [N.I, N.P, N.P, N.P] + [N.I] * 12 +
+                    [N.P, N.P, N.F, N.F] + [N.P] * 8 + [N.I, N.P])
+N.register_optional("kfb_bn_pool_num_slabs", [N.I] * 8, N.c_int)
+N.register_optional("kfb_bn_relu_maxpool_bwd", [N.I, N.P, N.P, N.P, N.P, N.P] + [N.I] * 12 +
+                    [N.P] * 7 + [N.I] + [N.P] * 3 + [N.I, N.P])
+
+
+class _BNReluMaxPool(torch.autograd.Function):
+    """maxpool(relu(bn_train(x))) with the BN statistics already summed by
+    the producing conv (the ResNet stem tail, csrc/bn.hip): neither the BN
+    output nor the max-pool input gradient is ever materialized."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, rm, rv, decay, eps, stats, kh, kw, sh, sw, pads, OH, OW):
+        x = x.contiguous()
+        n, H, W, C = x.shape
+        dev = x.device
+        nslab = stats.numel() // (2 * C)
+        st = torch.empty((4, C), dtype=torch.float32, device=dev)  # mean, invstd, scale, shift
+        z = torch.empty((n, OH, OW, C), dtype=x.dtype, device=dev)
+        idx = torch.empty((n, OH, OW, C), dtype=torch.uint8, device=dev)
+        geo = (n, H, W, C, OH, OW, kh, kw, sh, sw, pads[0], pads[2])
+        N.call("kfb_bn_relu_maxpool_fwd", N.dt(x), x.data_ptr(), z.data_ptr(), idx.data_ptr(),
+               *geo, N.ptr(gamma), N.ptr(beta), float(decay), float(eps), N.ptr(rm), N.ptr(rv),
+               st[0].data_ptr(), st[1].data_ptr(), st[2].data_ptr(), st[3].data_ptr(),
+               stats[:nslab * C].data_ptr(), stats[nslab * C:].data_ptr(), nslab,
+               N.stream(dev))
+        ctx.save_for_backward(x, z, idx, gamma, st)
+        ctx.geo = geo
+        ctx.gamma, ctx.beta = gamma, beta
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        x, z, idx, gamma, st = ctx.saved_tensors
+        dz = dz.contiguous()
+        n, H, W, C = ctx.geo[:4]
+        dev = x.device
+        nslab = N.query("kfb_bn_pool_num_slabs", n, H, W, C, *ctx.geo[6:10])
+        ws = torch.empty((2 * nslab * C + 3 * C,), dtype=torch.float32, device=dev)
+        gsink, bsink = _grad_sink(ctx.gamma), _grad_sink(ctx.beta)
+        direct = bsink is not None and (ctx.gamma is None or gsink is not None) and \
+            _conv.FUSE_BN
+        if direct:
+            dgp, dbp = N.ptr(gsink), bsink.data_ptr()
+        else:
+            dparams = torch.empty((2, C), dtype=torch.float32, device=dev)
+            dgp, dbp = dparams[0].data_ptr(), dparams[1].data_ptr()
+        dx = torch.empty_like(x)
+        o = 2 * nslab * C
+        N.call("kfb_bn_relu_maxpool_bwd", N.dt(x), dz.data_ptr(), z.data_ptr(), idx.data_ptr(),
+               x.data_ptr(), dx.data_ptr(), *ctx.geo, N.ptr(gamma), st[0].data_ptr(),
+               st[1].data_ptr(), dgp, dbp, ws[:nslab * C].data_ptr(),
+               ws[nslab * C:o].data_ptr(), nslab, ws[o:o + C].data_ptr(),
+               ws[o + C:o + 2 * C].data_ptr(), ws[o + 2 * C:].data_ptr(), int(direct),
+               N.stream(dev))
+        nones = (None,) * 12
+        if direct:
+            _grad_ready(ctx.gamma)
+            _grad_ready(ctx.beta)
+            return (dx, None, None) + nones
+        dgamma = dparams[0] if ctx.gamma is not None else None
+        return (dx, dgamma, dparams[1]) + nones
+
+
+def bn_relu_max_pool_fusable(x, stats, training) -> bool:
+    return (training and stats is not None and _on_gpu(x) and x.shape[-1] % 8 == 0
+            and _conv.FUSE_BN and hasattr(N.load(), "kfb_bn_relu_maxpool_fwd"))
+
+
+def bn_relu_max_pool(x, gamma, beta, running_mean, running_var, decay, eps, stats,
+                     kh, kw, sh, sw, mode="VALID"):
+    """maxpool(relu(batch_norm_train(x))) - see _BNReluMaxPool; the caller
+    checks bn_relu_max_pool_fusable first."""
+    pads, OH, OW = pool_geometry(x.shape, kh, kw, sh, sw, mode)
+    return _BNReluMaxPool.apply(x, gamma, beta, running_mean, running_var, decay, eps, stats,
+                                kh, kw, sh, sw, pads, OH, OW)
+
+
 def max_pool(x, kh, kw, sh, sw, mode="VALID"):
     pads, OH, OW = pool_geometry(x.shape, kh, kw, sh, sw, mode)
     if not _on_gpu(x):

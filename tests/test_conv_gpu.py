@@ -29,12 +29,12 @@ SHAPES = [
 ]
 
 
-@pytest.fixture(params=["classic", "glds"])
+@pytest.fixture(params=["classic", "glds", "classic_n64", "glds_n64", "onebuf", "onebuf_n64"])
 def ig_algo(request, monkeypatch):
-    """Runs a test once per igemm kernel (register-staged / LDS-DMA ring)."""
+    """Runs a test once per igemm kernel (register-staged / LDS-DMA ring /
+    single LDS stage, 128- or 64-channel-wide tiles)."""
     from kf_benchmarks_amd.ops import conv_hip
-    monkeypatch.setattr(conv_hip, "_IG_FORCE",
-                        {"classic": conv_hip.IG_CLASSIC, "glds": conv_hip.IG_GLDS}[request.param])
+    monkeypatch.setattr(conv_hip, "_IG_FORCE", conv_hip.IG_ALGOS[request.param])
     return request.param
 
 
