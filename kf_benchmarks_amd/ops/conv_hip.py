@@ -54,7 +54,7 @@ def _pad8(n):
     return (n + 7) // 8 * 8
 
 
-STATS_SPREAD = 32  # must match IG_SPREAD in csrc/conv_igemm.hip
+STATS_SPREAD = 32  # must match IG_SPREAD in csrc/conv_igemm.hip (checked at load)
 
 
 class _StatsArena:
@@ -98,8 +98,18 @@ class _StatsArena:
 STATS_ARENA = _StatsArena()
 
 
+_SPREAD_CHECKED = False
+
+
 def stats_buffer(channels, device):
     """Zeroed [2][STATS_SPREAD][C] fp32 buffer for fused BN partial sums."""
+    global _SPREAD_CHECKED
+    if not _SPREAD_CHECKED:
+        lib_spread = N.query("kfb_conv_stats_spread")
+        if lib_spread != STATS_SPREAD:
+            raise N.NativeError("stats spread mismatch: library %d, Python %d"
+                                % (lib_spread, STATS_SPREAD))
+        _SPREAD_CHECKED = True
     return STATS_ARENA.take(2 * STATS_SPREAD * channels, device)[:2 * STATS_SPREAD * channels]
 
 

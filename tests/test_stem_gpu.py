@@ -77,8 +77,8 @@ def test_bn_relu_maxpool_fused(cuda, shape):
     # the producing conv's epilogue statistics: [2][32][C] slabs of sum / sum^2
     stats = torch.zeros(2 * conv_hip.STATS_SPREAD * C, device=cuda)
     xf = xa.float().reshape(-1, C)
-    stats.view(2, 32, C)[0, 0] = xf.sum(0)
-    stats.view(2, 32, C)[1, 0] = (xf * xf).sum(0)
+    stats.view(2, conv_hip.STATS_SPREAD, C)[0, 0] = xf.sum(0)
+    stats.view(2, conv_hip.STATS_SPREAD, C)[1, 0] = (xf * xf).sum(0)
     ga = gamma.to(cuda).requires_grad_(True)
     ba = beta.to(cuda).requires_grad_(True)
     rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
