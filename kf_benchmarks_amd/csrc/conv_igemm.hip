@@ -78,6 +78,9 @@ struct IgArgs {
   const void* addend;
   // FAST path only: byte sizes of x and w (buffer-descriptor range checks)
   int xbytes, wbytes;
+  // byte size of the output layout (= that of addend / mask / xbn), or 0 if
+  // >= 2 GiB (the epilogue then uses plain loads instead of buffer loads)
+  int ybytes;
 };
 
 constexpr int IG_BK = 64;
@@ -94,6 +97,14 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }
 
 typedef __attribute__((ext_vector_type(4))) unsigned int v4u;
+
+// Workgroup barrier for LDS traffic only.  __syncthreads() also waits for
+// every outstanding global store of the wave (vmcnt(0)); in the epilogue the
+// statistics fold runs right after a tile's 16-32 KB of output stores, and
+// that wait cost ~2 us per workgroup round on the memory-bound layers.
+__device__ __forceinline__ void lds_only_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
 // Shared epilogue of the implicit-GEMM kernels: acc[i][j] holds channels
 // n..n+3 of pixel m for each (i, j) 16x16 subtile of the wave's
@@ -130,91 +141,137 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
   float s1[8], s2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
-  const bool fused = a.stats || a.addend;
+  const bool extras = a.addend || a.xbn;  // dgrad-style epilogue operands
+  // this thread's 8 output channels are fixed (column tid % CPR of every pass)
+  float mu[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int n = n0 + (tid % CPR) * 8 + k;
+    mu[k] = (a.xbn && n < a.Ncol) ? a.mean[n] : 0.f;
+  }
   constexpr int NPASS = BM * CPR / NT;
-  constexpr int PB = NPASS >= 2 ? 2 : 1;  // passes whose global loads are issued together
+  auto row_offset = [&](int m) -> long {
+    if (dense) return (long)m * a.ldy;
+    const int img = m / OHW, rem = m - img * OHW;
+    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+    return ((long)(img * a.YH + oh * a.ys) * a.YW + ow * a.ys) * a.ldy;
+  };
+  auto lds_chunk = [&](int t) -> uint4 {
+    const int ml = t / CPR, ch = t % CPR;
+    return *(const uint4*)(cs + ml * BN + ((ch ^ (ml & (CPR - 1))) * 8));
+  };
+  // Stores and loads share the in-order vmcnt counter: waiting for a load
+  // issued after a store also waits for that store.  So the epilogue issues
+  // no global load after its first store: the statistics-only path loads
+  // nothing, and the dgrad-style path issues every extra-operand load (as
+  // branch-free range-checked buffer loads) before any store.
+  if (!extras) {
 #pragma unroll
-  for (int p0 = 0; p0 < NPASS; p0 += PB) {
-    uint4 raw[PB], ad[PB], mk[PB], xb[PB];
-    long off[PB];
-    bool ok[PB];
-    int nq[PB];
+    for (int p = 0; p < NPASS; ++p) {
+      const int t = tid + p * NT;
+      const int m = m0 + t / CPR, n = n0 + (t % CPR) * 8;
+      const uint4 raw = lds_chunk(t);
+      if (m < a.M && n < a.Ncol) {
+        if (a.stats) {
+          const Vec<T, 8> tv = __builtin_bit_cast(Vec<T, 8>, raw);
 #pragma unroll
-    for (int q = 0; q < PB; ++q) {
-      const int t = tid + (p0 + q) * NT;
-      const int ml = t / CPR, ch = t % CPR;
-      const int m = m0 + ml, n = n0 + ch * 8;
-      nq[q] = n;
-      ok[q] = m < a.M && n < a.Ncol;
-      long rowoff = 0;
-      if (ok[q]) {
-        if (dense) {
-          rowoff = (long)m * a.ldy;
-        } else {
-          const int img = m / OHW, rem = m - img * OHW;
-          const int oh = rem / a.OW, ow = rem - oh * a.OW;
-          rowoff = ((long)(img * a.YH + oh * a.ys) * a.YW + ow * a.ys) * a.ldy;
+          for (int k = 0; k < 8; ++k) {
+            const float v = (float)tv.v[k];
+            s1[k] += v;
+            s2[k] += v * v;
+          }
         }
+        *(uint4*)(y + row_offset(m) + n) = raw;
       }
-      off[q] = rowoff + n;
-      raw[q] = *(const uint4*)(cs + ml * BN + ((ch ^ (ml & (CPR - 1))) * 8));
     }
-    if (!fused) {
+  } else if (a.ybytes > 0) {
+    const __amdgpu_buffer_rsrc_t rad = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.addend ? a.addend : a.y), (short)0, a.addend ? a.ybytes : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rmk = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.mask ? a.mask : a.y), (short)0, (a.mask && a.xbn) ? a.ybytes : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rxb = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.xbn ? a.xbn : a.y), (short)0, a.xbn ? a.ybytes : 0, 0x00020000);
+    int offb[NPASS];
+    uint4 ad[NPASS], mk[NPASS], xb[NPASS];
 #pragma unroll
-      for (int q = 0; q < PB; ++q)
-        if (ok[q]) *(uint4*)(y + off[q]) = raw[q];
-      continue;
+    for (int p = 0; p < NPASS; ++p) {
+      const int t = tid + p * NT;
+      const int m = m0 + t / CPR, n = n0 + (t % CPR) * 8;
+      offb[p] = (m < a.M && n < a.Ncol) ? (int)((row_offset(m) + n) * (long)sizeof(T)) : -1;
+      ad[p] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rad, offb[p], 0, 0));
+      mk[p] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rmk, offb[p], 0, 0));
+      xb[p] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rxb, offb[p], 0, 0));
     }
-    // issue every extra operand load of the batch before the first use
 #pragma unroll
-    for (int q = 0; q < PB; ++q) {
-      ad[q] = (ok[q] && a.addend) ? *(const uint4*)((const T*)a.addend + off[q]) : make_uint4(0, 0, 0, 0);
-      mk[q] = (ok[q] && a.xbn && a.mask) ? *(const uint4*)((const T*)a.mask + off[q]) : make_uint4(0, 0, 0, 0);
-      xb[q] = (ok[q] && a.xbn) ? *(const uint4*)((const T*)a.xbn + off[q]) : make_uint4(0, 0, 0, 0);
+    for (int p = 0; p < NPASS; ++p) {
+      const uint4 raw = lds_chunk(tid + p * NT);
+      const Vec<T, 8> tv = __builtin_bit_cast(Vec<T, 8>, raw);
+      const Vec<T, 8> av = __builtin_bit_cast(Vec<T, 8>, ad[p]);
+      const Vec<T, 8> mv = __builtin_bit_cast(Vec<T, 8>, mk[p]);
+      const Vec<T, 8> xv = __builtin_bit_cast(Vec<T, 8>, xb[p]);
+      Vec<T, 8> ov;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float v = (float)tv.v[k] + (float)av.v[k];  // zero addend when absent
+        if (a.xbn) {
+          if (a.mask) v = (float)mv.v[k] > 0.f ? v : 0.f;
+          s1[k] += v;
+          s2[k] += v * ((float)xv.v[k] - mu[k]);
+        } else if (a.stats) {
+          s1[k] += v;
+          s2[k] += v * v;
+        }
+        ov.v[k] = (T)v;
+      }
+      if (offb[p] >= 0) *(uint4*)((char*)y + offb[p]) = __builtin_bit_cast(uint4, ov);
     }
+  } else {
+    // outputs >= 2 GiB: plain loads interleaved with the stores
 #pragma unroll
-    for (int q = 0; q < PB; ++q) {
-      if (!ok[q]) continue;
-      const int n = nq[q];
+    for (int p = 0; p < NPASS; ++p) {
+      const int t = tid + p * NT;
+      const int m = m0 + t / CPR, n = n0 + (t % CPR) * 8;
+      if (m >= a.M || n >= a.Ncol) continue;
+      const long off = row_offset(m) + n;
+      const Vec<T, 8> tv = __builtin_bit_cast(Vec<T, 8>, lds_chunk(t));
       float v[8];
-      Vec<T, 8> tv = __builtin_bit_cast(Vec<T, 8>, raw[q]);
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = (float)tv.v[k];
       if (a.addend) {
-        Vec<T, 8> av = __builtin_bit_cast(Vec<T, 8>, ad[q]);
+        const Vec<T, 8> av = *(const Vec<T, 8>*)((const T*)a.addend + off);
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] += (float)av.v[k];
       }
       if (a.xbn) {
         if (a.mask) {
-          Vec<T, 8> mv = __builtin_bit_cast(Vec<T, 8>, mk[q]);
+          const Vec<T, 8> mv = *(const Vec<T, 8>*)((const T*)a.mask + off);
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[k] = (float)mv.v[k] > 0.f ? v[k] : 0.f;
         }
-        Vec<T, 8> xv = __builtin_bit_cast(Vec<T, 8>, xb[q]);
+        const Vec<T, 8> xv = *(const Vec<T, 8>*)((const T*)a.xbn + off);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           s1[k] += v[k];
-          s2[k] += v[k] * ((float)xv.v[k] - a.mean[n + k]);
+          s2[k] += v[k] * ((float)xv.v[k] - mu[k]);
         }
-        store_vec<T, 8>(y + off[q], v);
       } else if (a.stats) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           s1[k] += v[k];
           s2[k] += v[k] * v[k];
         }
-        if (a.addend) store_vec<T, 8>(y + off[q], v);
-        else *(uint4*)(y + off[q]) = raw[q];
-      } else {
-        store_vec<T, 8>(y + off[q], v);
       }
+      Vec<T, 8> ov;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ov.v[k] = (T)v[k];
+      *(uint4*)(y + off) = __builtin_bit_cast(uint4, ov);
     }
   }
   if (a.stats) {
     // Fold the per-thread sums of threads sharing a chunk column, then one
-    // atomic add per channel per workgroup into a spread slot.
-    __syncthreads();
+    // atomic add per channel per workgroup into a spread slot.  LDS-only
+    // barriers: the tile's global stores stay in flight.
+    lds_only_barrier();
     float* red = (float*)smem;  // [NT/CPR][CPR][16]
     const int ch = tid % CPR, rg = tid / CPR;
 #pragma unroll
@@ -222,7 +279,7 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
       red[(rg * CPR + ch) * 16 + k] = s1[k];
       red[(rg * CPR + ch) * 16 + 8 + k] = s2[k];
     }
-    __syncthreads();
+    lds_only_barrier();
     constexpr int RG = NT / CPR;
     if (tid < CPR * 16) {
       const int c = tid / 16, k = tid % 16;
@@ -999,9 +1056,11 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
                                   hipStream_t stream) {
   if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
   const long xbytes = (long)N * H * W * C * 2, wbytes = (long)Ncol * KH * KW * C * 2;
+  const long ybytes = (long)N * YH * YW * ldy * 2;
   IgArgs a{x, w, y, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
            N * OH * OW, YH, YW, ys, ldy, stats, mask, xbn, mean, addend,
-           (int)(xbytes < (1L << 31) ? xbytes : 0), (int)(wbytes < (1L << 31) ? wbytes : 0)};
+           (int)(xbytes < (1L << 31) ? xbytes : 0), (int)(wbytes < (1L << 31) ? wbytes : 0),
+           (int)(ybytes < (1L << 31) ? ybytes : 0)};
   const bool t = trans != 0;
   const bool fast = !t && C % IG_BK == 0 && KH * KW <= 64 && xbytes < (1L << 31) &&
                     wbytes < (1L << 31) && !igemm_fast_disabled();

@@ -49,6 +49,9 @@ def main():
         y = torch.empty(n, OH, OW, cout, device=dev, dtype=dt)
         stats = torch.zeros(2 * conv_hip.STATS_SPREAD * cout, device=dev)
         geo = (n, H, W, C, OH, OW, KH, KW, 1, 1, 0, 0, cout, OH, OW, 1, cout, 0)
+        # dgrad-style epilogue operands: ReLU mask, producer-BN input, mean, addend
+        mask, xbn, addend = (torch.randn_like(y) for _ in range(3))
+        mean = torch.zeros(cout, device=dev)
         ybytes = y.numel() * 2
         xbytes = x.numel() * 2
         tc = timeit(lambda: y.copy_(torch.empty_like(y)), a.iters) if False else \
@@ -59,8 +62,10 @@ def main():
             algo = conv_hip.IG_ALGOS[al]
             t0 = timeit(lambda: conv_hip._igemm_call(algo, x, w, y, geo), a.iters)
             t1 = timeit(lambda: conv_hip._igemm_call(algo, x, w, y, geo, stats), a.iters)
-            print("  %-11s plain %7.1f us (%.2f TB/s)   +stats %7.1f us"
-                  % (al, t0, (ybytes + xbytes) / t0 / 1e6, t1))
+            t2 = timeit(lambda: conv_hip._igemm_call(algo, x, w, y, geo, stats, mask, xbn, mean,
+                                                     addend), a.iters)
+            print("  %-11s plain %7.1f us (%.2f TB/s)   +stats %7.1f us   dgrad-fused %7.1f us"
+                  % (al, t0, (ybytes + xbytes) / t0 / 1e6, t1, t2))
 
 
 if __name__ == "__main__":
