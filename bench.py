@@ -36,7 +36,7 @@ def main(argv=None):
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--kernel_impl", default="hip")
     ap.add_argument("--optimizer", default="momentum")
-    ap.add_argument("--bucket_size_mb", type=float, default=64.0)
+    ap.add_argument("--bucket_size_mb", type=float, default=25.0)
     ap.add_argument("--wire_dtype", default="fp32")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--variable_update", default="kungfu",

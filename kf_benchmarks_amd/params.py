@@ -195,8 +195,11 @@ D.DEFINE_string("benchmark_test_id", None, "Test id recorded in the benchmark lo
 # Flags that only exist on this stack (MI355X-specific). Kept after the 129
 # reference flags so the reference surface is a prefix of ours.
 D.DEFINE_boolean("use_bf16", False, "Compute in bfloat16 (fp32 master weights). MI355X native.")
-D.DEFINE_float("bucket_size_mb", 64.0,
-               "Gradient bucket size for overlapped all-reduce (MB of fp32 gradient).")
+D.DEFINE_float("bucket_size_mb", 25.0,
+               "Gradient bucket size for overlapped all-reduce (MB of fp32 gradient). "
+               "Small enough that the last bucket (launched after backward, not "
+               "overlapped) is short on an 8-GPU xGMI ring; large enough that each "
+               "RCCL launch moves MBs.")
 D.DEFINE_boolean("overlap_gradient_allreduce", True,
                  "Launch bucket all-reduces from backward hooks (overlap with compute).")
 D.DEFINE_enum("gradient_wire_dtype", "auto", ("auto", "fp32", "bf16", "fp16"),
