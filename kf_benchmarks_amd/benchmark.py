@@ -574,6 +574,12 @@ class BenchmarkCNN:
             from .utils.summary import SummaryWriter
             self.summary_writer = SummaryWriter(p.train_dir)
         timer = _EventTimer(self.device)
+        # asynchronous PS: the run is timed by the shared global step
+        watcher = None
+        if getattr(self.strategy, "state", None) is not None and \
+                p.variable_update == "parameter_server" and not p.cross_replica_sync:
+            from .parallel.async_ps import GlobalStepWatcher
+            watcher = GlobalStepWatcher(self.strategy.state)
         step_train_times: List[float] = []
         forward_only = p.forward_only
         num_warmup = self.num_warmup_batches
@@ -603,6 +609,8 @@ class BenchmarkCNN:
                     torch.cuda.synchronize(self.device)
                 self.world.barrier(self.device if self.device_type == "cuda" else None)
                 loop_start = time.perf_counter()
+                if watcher is not None:
+                    watcher.start()
                 step_train_times = []
                 timer.reset()
                 timer.mark()
@@ -647,6 +655,9 @@ class BenchmarkCNN:
         num_steps = local_step
         images_per_sec = (self.num_workers * num_steps * self.batch_size / elapsed
                           if elapsed > 0 else 0.0)
+        if watcher is not None and watcher.start_step is not None:
+            watcher.stop()
+            images_per_sec = watcher.steps_per_second() * self.batch_size
         log_fn("-" * 64)
         log_fn("total images/sec: %.2f" % images_per_sec)
         log_fn("-" * 64)
@@ -672,6 +683,8 @@ class BenchmarkCNN:
                  "images_per_sec": images_per_sec}
         if last_loss is not None:
             stats["last_average_loss"] = last_loss
+        if watcher is not None and watcher.end_step is not None:
+            stats["ps_global_step"] = watcher.end_step
         if eval_hook is not None:
             stats.update(eval_hook.stats())
         if p.print_json_result and self.world.is_chief:

@@ -221,6 +221,10 @@ def make_strategy(params, world, flat, tower_mode=False, num_gpus=1):
             from .kungfu import PairAveraging
             return PairAveraging(params, world, flat, **kw)
         raise ValueError('KungFu distributed option "%s" was not recognized' % opt)
+    if vu == "parameter_server" and not params.cross_replica_sync and world.size > 1 \
+            and not tower_mode:
+        from .async_ps import AsyncParameterServer
+        return AsyncParameterServer(params, world, flat, **kw)
     if vu in ("parameter_server", "replicated", "distributed_replicated", "collective_all_reduce",
               "distributed_all_reduce", "horovod"):
         return SumAllReduceStrategy(vu, params, world, flat, **kw)

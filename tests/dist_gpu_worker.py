@@ -65,6 +65,11 @@ def main():
            "segs": {name: flat[off:off + n].double().sum().item()
                     for name, _, off, n in bench.flat.segments()},
            "size": comm.get_world().size}
+    state = getattr(bench.strategy, "state", None)
+    if state is not None:  # asynchronous parameter server
+        comm.get_world().barrier()
+        res["ps_global_step"] = state.global_step
+        bench.strategy.close()
     with open(out, "w") as f:
         json.dump(res, f)
     comm.get_world().shutdown()

@@ -22,7 +22,7 @@ def main():
     # the last bench is reachable through the world only; recompute vars via a fresh read
     import kf_benchmarks_amd.benchmark as bm  # noqa: F401
     with open(out, "w") as f:
-        json.dump({"losses": losses, "vars": tu.LAST_VARS}, f)
+        json.dump({"losses": losses, "vars": tu.LAST_VARS, "stats": tu.LAST_STATS}, f)
     comm.get_world().shutdown()
 
 

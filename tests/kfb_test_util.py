@@ -198,11 +198,13 @@ def run_test_model(params, inputs=None, digits=15):
     with capture_logs() as logs, monkey_patch(benchmark, LOSS_AND_ACCURACY_DIGITS_TO_SHOW=digits):
         bench = benchmark.BenchmarkCNN(params, dataset=TestDataSet(), model=TestCNNModel(params))
         bench.set_fake_data(inputs, np.ones(inputs.shape[0], dtype=np.int64))
-        bench.run()
-    global LAST_VARS
+        stats = bench.run()
+    global LAST_VARS, LAST_STATS
+    LAST_STATS = stats
     LAST_VARS = [float(p.detach().float().sum()) for _, p in bench.net.trainable_variables()]
     outs = get_training_outputs_from_logs(logs, params.print_training_accuracy)
     return [o.loss for o in outs], logs
 
 
 LAST_VARS = None
+LAST_STATS = None

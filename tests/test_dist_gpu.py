@@ -74,3 +74,17 @@ def test_two_ranks_stay_in_lock_step(cuda, tmp_path, extra):
     assert r0["wsum"] != r0["w0"]  # the step changed the weights
     for l0, l1 in zip(r0["losses"], r1["losses"]):
         assert l0 == l0 and l1 == l1 and abs(l0) < 1e3
+
+
+def test_two_ranks_async_parameter_server(cuda, tmp_path):
+    """--cross_replica_sync=False: the shared model lives in rank 0's device
+    memory (HIP IPC); every rank applies its gradients to it under the PS
+    lock, and the shared global step counts every apply."""
+    kw = dict(model="resnet50", batch_size=8, num_gpus=1, use_bf16=True, optimizer="momentum",
+              data_format="NHWC", variable_update="parameter_server", cross_replica_sync=False)
+    r0, r1 = _run(kw, 3, tmp_path)
+    assert r0["ps_global_step"] == r1["ps_global_step"] == 6
+    assert r0["w0"] == r1["w0"]
+    for r in (r0, r1):
+        assert r["wsum"] != r["w0"] and r["wsum"] == r["wsum"]
+        assert all(l == l and abs(l) < 1e3 for l in r["losses"])

@@ -119,6 +119,27 @@ def test_two_workers_async_pair_averaging(tmp_path):
         assert all(np.isfinite(r["losses"]))
 
 
+def test_two_workers_async_parameter_server(tmp_path):
+    """--variable_update=parameter_server --cross_replica_sync=False: each
+    worker applies its own (possibly stale) gradient to the shared model under
+    the PS lock; every apply is counted in the shared global step that times
+    the run (GlobalStepWatcher), and the first step of each worker sees the
+    initial model."""
+    kw = dict(variable_update="parameter_server", cross_replica_sync=False, num_batches=6,
+              loss_type_to_report="base_loss")
+    res = run_workers(2, kw, tmp_path)
+    params = tu.get_var_update_params(**kw)
+    expected = tu.manually_compute_losses(tu.get_fake_var_update_inputs(), 2, params, "none")
+    for r in range(2):
+        assert len(res[r]["losses"]) == 6
+        np.testing.assert_allclose(res[r]["losses"][0], expected[r][0], rtol=1e-6)
+        assert res[r]["stats"]["ps_global_step"] >= 6
+    assert max(r["stats"]["ps_global_step"] for r in res) == 12
+    # the workers trained one shared model, not two independent ones
+    ind = run_workers(2, dict(variable_update="independent", num_batches=6), tmp_path)
+    assert res[0]["vars"] != ind[0]["vars"]
+
+
 def _tower_oracle(inputs, ntowers, params, mean):
     """One worker with ``ntowers`` towers (tower t reads the data rolled by
     t/ntowers): tower gradients averaged (parameter_server) or summed
