@@ -175,3 +175,18 @@ def test_engine_trains_and_evals_on_tfrecords(tmp_path):
     with tu.capture_logs() as logs:
         benchmark.BenchmarkCNN(benchmark.make_params(**base)).run()
     assert any("Accuracy @ 1" in line for line in logs)
+
+
+def test_get_imagenet_probe(tmp_path):
+    """tools.get_imagenet (role of tcb/get_imagenet.py) finds the shards of
+    an ImageNet-layout directory and decodes their records natively."""
+    from kf_benchmarks_amd.tools import get_imagenet
+    test_data.write_black_and_white_tfrecord_data(str(tmp_path), 11, num_train_images=16,
+                                                  num_validation_images=8, train_shards=2,
+                                                  validation_shards=1)
+    res = get_imagenet.probe(str(tmp_path), sample_shards=2)
+    assert res["subsets"]["train"]["shards"] == 2
+    assert res["subsets"]["train"]["sampled_records"] == 16
+    assert res["subsets"]["validation"]["sampled_records"] == 8
+    assert res["subsets"]["train"]["first_example"]["image/encoded"] > 0
+    assert get_imagenet.main(["--data_dir", str(tmp_path)]) == 0
