@@ -163,9 +163,17 @@ class CNNModel(Model):
         return {"top_1_accuracy": top1, "top_5_accuracy": top5}
 
 
+_SANITIZED = {}
+
+
 def _sanitize(scope: str) -> str:
-    return re.sub(r"[^0-9A-Za-z_]", lambda m: {"/": "__", ".": "_d_"}.get(m.group(0), "_"),
-                  scope)
+    # memoized: every forward looks up every layer by scope (host launch path)
+    key = _SANITIZED.get(scope)
+    if key is None:
+        key = re.sub(r"[^0-9A-Za-z_]", lambda m: {"/": "__", ".": "_d_"}.get(m.group(0), "_"),
+                     scope)
+        _SANITIZED[scope] = key
+    return key
 
 
 class Network(nn.Module):

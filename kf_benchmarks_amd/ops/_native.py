@@ -111,9 +111,14 @@ def register_optional(name, argtypes, restype=c_int):
         fn.restype = restype
 
 
+_FN = {}
+
+
 def call(name, *args):
     """Calls a kernel entry point and raises on a non-zero hipError_t."""
-    fn = getattr(load(), name)
+    fn = _FN.get(name)
+    if fn is None:
+        fn = _FN[name] = getattr(load(), name)
     err = fn(*args)
     if err != 0:
         raise NativeError("%s failed with hipError %d" % (name, err))
@@ -135,7 +140,21 @@ def ptr(t):
     return None if t is None else t.data_ptr()
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream(device=None) -> int:
+    """hipStream_t of the current torch stream of ``device``.  The raw C
+    accessor skips torch.cuda.current_stream's Stream-object construction
+    (~5 us per kernel launch on the host, which the forward pass is bound by)."""
+    if _RAW_STREAM is not None:
+        if device is None:
+            idx = torch.cuda.current_device()
+        elif isinstance(device, int):
+            idx = device
+        else:
+            idx = device.index if device.index is not None else torch.cuda.current_device()
+        return _RAW_STREAM(idx)
     return torch.cuda.current_stream(device).cuda_stream
 
 
