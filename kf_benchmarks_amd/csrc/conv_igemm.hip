@@ -76,6 +76,10 @@ struct IgArgs {
   // mask / statistics - the gradient other consumers of the conv input
   // already produced (residual / second-branch accumulation).
   const void* addend;
+  // mcoef != null (with xbn, mask == null): the producer BN's ReLU mask is
+  // recomputed as xbn * scale + shift > 0 (mcoef = [scale | shift], [2][Ncol])
+  // instead of read from its output - BNs without a residual add.
+  const float* mcoef;
   // FAST path only: byte sizes of x and w (buffer-descriptor range checks)
   int xbytes, wbytes;
   // byte size of the output layout (= that of addend / mask / xbn), or 0 if
@@ -143,11 +147,15 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
   for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
   const bool extras = a.addend || a.xbn;  // dgrad-style epilogue operands
   // this thread's 8 output channels are fixed (column tid % CPR of every pass)
-  float mu[8];
+  float mu[8], msc[8], msh[8];
+  const bool mrec = a.xbn && !a.mask && a.mcoef;  // recompute the ReLU mask from xbn
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int n = n0 + (tid % CPR) * 8 + k;
-    mu[k] = (a.xbn && n < a.Ncol) ? a.mean[n] : 0.f;
+    const bool nok = n < a.Ncol;
+    mu[k] = (a.xbn && nok) ? a.mean[n] : 0.f;
+    msc[k] = (mrec && nok) ? a.mcoef[n] : 0.f;
+    msh[k] = (mrec && nok) ? a.mcoef[a.Ncol + n] : 0.f;
   }
   constexpr int NPASS = BM * CPR / NT;
   auto row_offset = [&](int m) -> long {
@@ -215,6 +223,8 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
         float v = (float)tv.v[k] + (float)av.v[k];  // zero addend when absent
         if (a.xbn) {
           if (a.mask) v = (float)mv.v[k] > 0.f ? v : 0.f;
+          // same expression as the BN apply (bn_apply_k), so the same sign
+          else if (mrec) v = (float)xv.v[k] * msc[k] + msh[k] > 0.f ? v : 0.f;
           s1[k] += v;
           s2[k] += v * ((float)xv.v[k] - mu[k]);
         } else if (a.stats) {
@@ -249,6 +259,10 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
           for (int k = 0; k < 8; ++k) v[k] = (float)mv.v[k] > 0.f ? v[k] : 0.f;
         }
         const Vec<T, 8> xv = *(const Vec<T, 8>*)((const T*)a.xbn + off);
+        if (mrec) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = (float)xv.v[k] * msc[k] + msh[k] > 0.f ? v[k] : 0.f;
+        }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           s1[k] += v[k];
@@ -1052,13 +1066,13 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
                                   int W, int C, int OH, int OW, int KH, int KW, int sh, int sw,
                                   int pt, int pl, int Ncol, int YH, int YW, int ys, int ldy,
                                   int trans, float* stats, const void* mask, const void* xbn,
-                                  const float* mean, const void* addend, int algo,
-                                  hipStream_t stream) {
+                                  const float* mean, const void* addend, const float* mcoef,
+                                  int algo, hipStream_t stream) {
   if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
   const long xbytes = (long)N * H * W * C * 2, wbytes = (long)Ncol * KH * KW * C * 2;
   const long ybytes = (long)N * YH * YW * ldy * 2;
   IgArgs a{x, w, y, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
-           N * OH * OW, YH, YW, ys, ldy, stats, mask, xbn, mean, addend,
+           N * OH * OW, YH, YW, ys, ldy, stats, mask, xbn, mean, addend, mcoef,
            (int)(xbytes < (1L << 31) ? xbytes : 0), (int)(wbytes < (1L << 31) ? wbytes : 0),
            (int)(ybytes < (1L << 31) ? ybytes : 0)};
   const bool t = trans != 0;

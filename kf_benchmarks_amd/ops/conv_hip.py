@@ -20,7 +20,7 @@ import torch
 
 from . import _native as N
 
-_SIG = [N.I, N.P, N.P, N.P] + [N.I] * 17 + [N.I, N.P, N.P, N.P, N.P, N.P, N.I, N.P]
+_SIG = [N.I, N.P, N.P, N.P] + [N.I] * 17 + [N.I, N.P, N.P, N.P, N.P, N.P, N.P, N.I, N.P]
 N.register_optional("kfb_conv_igemm", _SIG)
 N.register_optional("kfb_conv_igemm_fast", [N.I] * 4, N.c_int)
 
@@ -113,17 +113,18 @@ def stats_buffer(channels, device):
     return STATS_ARENA.take(2 * STATS_SPREAD * channels, device)[:2 * STATS_SPREAD * channels]
 
 
-def _igemm_call(algo, x, wmat, y, geo, stats=None, mask=None, xbn=None, mean=None, addend=None):
+def _igemm_call(algo, x, wmat, y, geo, stats=None, mask=None, xbn=None, mean=None, addend=None,
+                mcoef=None):
     N.call("kfb_conv_igemm", N.dt(x), x.data_ptr(), wmat.data_ptr(), y.data_ptr(), *geo,
-           N.ptr(stats), N.ptr(mask), N.ptr(xbn), N.ptr(mean), N.ptr(addend), algo,
-           N.stream(x.device))
+           N.ptr(stats), N.ptr(mask), N.ptr(xbn), N.ptr(mean), N.ptr(addend), N.ptr(mcoef),
+           algo, N.stream(x.device))
 
 
-def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None)):
+def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None)):
     """Per-geometry kernel choice, timed once on the real operands with the
     real fused epilogue (the role cuDNN's algorithm autotune plays for the
     reference): all kernels run the same K order, so the choice does not
-    change the numerics.  ``fused`` = (stats, mask, xbn, mean, addend); the
+    change the numerics.  ``fused`` = (stats, mask, xbn, mean, addend, mcoef); the
     timing runs write a scratch output and scratch statistics."""
     if _IG_FORCE is not None:
         return _IG_FORCE
@@ -134,9 +135,9 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None)):
         cands += (IG_CLASSIC_N64, IG_GLDS_N64, IG_ONEBUF_N64) if fast else (IG_CLASSIC_N64,)
     if len(cands) == 1:
         return cands[0]
-    stats, mask, xbn, mean, addend = fused
+    stats, mask, xbn, mean, addend, mcoef = fused
     key = (str(x.device), x.dtype, stats is not None, mask is not None, xbn is not None,
-           addend is not None) + tuple(geo)
+           addend is not None, mcoef is not None) + tuple(geo)
     best = _ig_tuned.get(key)
     if best is not None:
         return best
@@ -148,7 +149,7 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None)):
     sstats = torch.zeros_like(stats) if stats is not None else None
     times = {}
     for algo in cands:
-        args = (x, wmat, scratch, geo, sstats, mask, xbn, mean, addend)
+        args = (x, wmat, scratch, geo, sstats, mask, xbn, mean, addend, mcoef)
         _igemm_call(algo, *args)  # warm
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
@@ -163,10 +164,10 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None)):
 
 
 def _igemm(x, wmat, y, N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy,
-           trans, stats=None, mask=None, xbn=None, mean=None, addend=None):
+           trans, stats=None, mask=None, xbn=None, mean=None, addend=None, mcoef=None):
     geo = (N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy, int(trans))
-    algo = _igemm_algo(x, wmat, y, geo, (stats, mask, xbn, mean, addend))
-    _igemm_call(algo, x, wmat, y, geo, stats, mask, xbn, mean, addend)
+    algo = _igemm_algo(x, wmat, y, geo, (stats, mask, xbn, mean, addend, mcoef))
+    _igemm_call(algo, x, wmat, y, geo, stats, mask, xbn, mean, addend, mcoef)
 
 
 def conv_fwd(x, wl, stride, pads, stats=None):
@@ -191,13 +192,17 @@ def is_scatter_dgrad(w_shape, stride, pads):
 
 def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None, addend=None, wt=None,
                addend_inplace=False):
-    """``fuse`` = (stats, mask, xbn, mean): also apply the producer BN's ReLU
-    mask to dX and accumulate its backward partial sums (see BNLink).
+    """``fuse`` = (stats, mask, xbn, mean[, mcoef]): also apply the producer
+    BN's ReLU mask (read from ``mask``, or recomputed from ``xbn`` with the BN's
+    [scale | shift] ``mcoef``) to dX and accumulate its backward partial sums
+    (see BNLink).
     ``addend``: gradient already produced by other consumers, added to dX
     (not combined with ``fuse`` on the strided-1x1 scatter path, where
     ``addend_inplace`` lets dX accumulate into the addend's own buffer)."""
     n, H, W, C = x_shape
-    fz = tuple(fuse if fuse is not None else (None, None, None, None)) + (addend,)
+    # _igemm's fused operands: stats, mask, xbn, mean, addend, mcoef
+    f5 = tuple(fuse) + (None,) * (5 - len(fuse)) if fuse is not None else (None,) * 5
+    fz = f5[:4] + (addend, f5[4])
     cout, KH, KW, _ = wl.shape
     _, OH, OW, _ = dy.shape
     sh, sw = stride
@@ -210,7 +215,7 @@ def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None, addend=None, wt=None,
             # unsampled pixels keep the addend; sampled ones accumulate in place
             assert fuse is None
             dx = addend if addend_inplace else addend.clone()
-            fz = (None, None, None, None, dx)
+            fz = (None, None, None, None, dx, None)
         else:
             dx = torch.zeros((n, H, W, C), dtype=dy.dtype, device=dy.device)
         # GEMM over dY pixels (1x1, stride 1 in dY space), scattered by ys.
@@ -434,7 +439,11 @@ class _Conv2d(torch.autograd.Function):
                         fuse = None
                         if not (pend is not None and is_scatter_dgrad(wp.shape, stride, pads)):
                             parts = stats_buffer(cin, dy.device)
-                            fuse = (parts, xp if link.relu else None, link.x_bn, link.mean)
+                            # ReLU mask: recomputed from x_bn when the BN has no
+                            # residual add (link.mcoef), else read from its output
+                            rec = link.relu and link.mcoef is not None
+                            fuse = (parts, xp if link.relu and not rec else None, link.x_bn,
+                                    link.mean, link.mcoef if rec else None)
                         dx = conv_dgrad(dy, wp, xp.shape, stride, pads, fuse, addend=pend,
                                         wt=ctx.wt, addend_inplace=owned)
                         if fuse is not None:

@@ -101,9 +101,12 @@ FUSED_SHAPES = [
 
 @pytest.mark.parametrize("shape", FUSED_SHAPES, ids=[str(s) for s in FUSED_SHAPES])
 @pytest.mark.parametrize("with_addend", [False, True])
-def test_dgrad_fused_epilogue(cuda, shape, with_addend, ig_algo):
+@pytest.mark.parametrize("mask_src", ["read", "recompute"])
+def test_dgrad_fused_epilogue(cuda, shape, with_addend, ig_algo, mask_src):
     """dgrad epilogue: dX = (conv^T(dY) + addend) * [x > 0] and the producer
-    BN's backward partials sum(dX), sum(dX * (x_bn - mean)) per channel."""
+    BN's backward partials sum(dX), sum(dX * (x_bn - mean)) per channel.  The
+    ReLU mask is read from x (the BN output) or recomputed as
+    x_bn * scale + shift > 0 (BNs without a residual add)."""
     from kf_benchmarks_amd.ops import conv_hip
     n, H, W, cin, cout, kh, kw, s, mode = shape
     scatter = kh == 1 and s > 1
@@ -118,6 +121,12 @@ def test_dgrad_fused_epilogue(cuda, shape, with_addend, ig_algo):
     dy = torch.randn(yb.shape, generator=g).to(dt)
     xb = torch.randn(n, H, W, cin, generator=g).to(dt)
     mean = torch.randn(cin, generator=g)
+    mcoef = None
+    if mask_src == "recompute":
+        # x = relu(xb * scale + shift) as the BN forward stores it
+        scale, shift = torch.rand(cin, generator=g) + 0.5, torch.randn(cin, generator=g) * 0.5
+        x = torch.relu(xb.float() * scale + shift).to(dt)
+        mcoef = torch.cat([scale, shift])
     add = torch.randn(n, H, W, cin, generator=g).to(dt) if with_addend else None
     xr = x.float().requires_grad_(True)
     conv_ops.conv2d_reference(xr, w.float(), (s, s), pads).backward(dy.float())
@@ -127,7 +136,10 @@ def test_dgrad_fused_epilogue(cuda, shape, with_addend, ig_algo):
     if not scatter:
         ref = ref * (x.float() > 0)
         parts = conv_hip.stats_buffer(cin, cuda).zero_()
-        fuse = (parts, x.to(cuda), xb.to(cuda), mean.to(cuda))
+        if mcoef is None:
+            fuse = (parts, x.to(cuda), xb.to(cuda), mean.to(cuda))
+        else:
+            fuse = (parts, None, xb.to(cuda), mean.to(cuda), mcoef.to(cuda))
     dx = conv_hip.conv_dgrad(dy.to(cuda), w.to(cuda), x.shape, (s, s), pads, fuse,
                              addend=add.to(cuda) if add is not None else None)
     torch.testing.assert_close(dx.float().cpu(), ref, rtol=3e-2, atol=3e-2)
