@@ -20,6 +20,7 @@
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <cmath>
 
 #define API extern "C" __attribute__((visibility("default")))
 
@@ -523,4 +524,49 @@ API long kfbrt_parse_example(const uint8_t* data, size_t n, uint8_t* out, size_t
   }
   if (!o.ok) return -2;
   return (long)o.n;
+}
+
+// ------------------------------------------------------------------ images
+// Saturation scale + hue shift of a float RGB image in place (the host
+// colour distortion of tcb/preprocessing.py:268-307, tf.image.adjust_saturation
+// / adjust_hue): one RGB -> HSV -> RGB pass per pixel, s <- clip(s * sat, 0, 1),
+// h <- (h + hue) mod 1.  Called through ctypes, which releases the GIL, so
+// the input pipeline's worker threads run it in parallel.
+API void kfbrt_adjust_sat_hue(float* img, long npix, float sat, float hue) {
+  for (long i = 0; i < npix; ++i) {
+    float* px = img + 3 * i;
+    const float r = px[0], g = px[1], b = px[2];
+    const float mx = std::max(r, std::max(g, b));
+    const float mn = std::min(r, std::min(g, b));
+    const float d = mx - mn;
+    const float v = mx;
+    float s = mx > 0.f ? d / std::max(mx, 1e-12f) : 0.f;
+    float h = 0.f;
+    if (d > 0.f) {
+      const float dd = std::max(d, 1e-12f);
+      if (mx == r) h = (g - b) / dd;
+      else if (mx == g) h = 2.f + (b - r) / dd;
+      else h = 4.f + (r - g) / dd;
+      h = h / 6.f;
+      h -= std::floor(h);
+    }
+    s = std::min(std::max(s * sat, 0.f), 1.f);
+    h += hue;
+    h -= std::floor(h);
+    const float h6 = h * 6.f;
+    const float fl = std::floor(h6);
+    const int sector = ((int)fl % 6 + 6) % 6;
+    const float f = h6 - fl;
+    const float p = v * (1.f - s), q = v * (1.f - s * f), t = v * (1.f - s * (1.f - f));
+    float ro, go, bo;
+    switch (sector) {
+      case 0: ro = v; go = t; bo = p; break;
+      case 1: ro = q; go = v; bo = p; break;
+      case 2: ro = p; go = v; bo = t; break;
+      case 3: ro = p; go = q; bo = v; break;
+      case 4: ro = t; go = p; bo = v; break;
+      default: ro = v; go = p; bo = q; break;
+    }
+    px[0] = ro; px[1] = go; px[2] = bo;
+  }
 }

@@ -203,6 +203,9 @@ def adjust_hue(img, delta):
     return _hsv_to_rgb((h + delta) % 1.0, s, v)
 
 
+_NATIVE_COLOR = os.environ.get("KFB_NATIVE_COLOR", "1") != "0"
+
+
 def distort_color(image, batch_position, rng: np.random.Generator, distort_color_in_yiq=False):
     """float image in [0, 1] -> colour-distorted, clipped to [0, 1].  Even
     batch positions: brightness, saturation/hue, contrast; odd: brightness,
@@ -210,11 +213,19 @@ def distort_color(image, batch_position, rng: np.random.Generator, distort_color
     img = adjust_brightness(image, rng.uniform(-32. / 255., 32. / 255.))
 
     def sat_hue(x):
+        # saturation and hue act on independent HSV components, so one native
+        # RGB->HSV->RGB pass applies both (the draw order stays the reference's)
         if distort_color_in_yiq:
-            x = adjust_hue(x, rng.uniform(-0.2, 0.2))
-            return adjust_saturation(x, rng.uniform(0.5, 1.5))
-        x = adjust_saturation(x, rng.uniform(0.5, 1.5))
-        return adjust_hue(x, rng.uniform(-0.2, 0.2))
+            hue = rng.uniform(-0.2, 0.2)
+            sat = rng.uniform(0.5, 1.5)
+        else:
+            sat = rng.uniform(0.5, 1.5)
+            hue = rng.uniform(-0.2, 0.2)
+        if _NATIVE_COLOR:
+            from .. import runtime
+            return runtime.adjust_saturation_hue(np.ascontiguousarray(x, dtype=np.float32),
+                                                 sat, hue)
+        return adjust_hue(adjust_saturation(x, sat), hue)
 
     if batch_position % 2 == 0:
         img = sat_hue(img)

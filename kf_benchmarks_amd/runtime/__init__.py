@@ -58,6 +58,9 @@ def _load():
         lib.kfbrt_table_entry.argtypes = [ctypes.c_void_p, ctypes.c_int, cpp, ctypes.POINTER(sz),
                                           cpp, ctypes.POINTER(sz)]
         lib.kfbrt_table_free.argtypes = [ctypes.c_void_p]
+        lib.kfbrt_adjust_sat_hue.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_float,
+                                             ctypes.c_float]
+        lib.kfbrt_adjust_sat_hue.restype = None
         lib.kfbrt_parse_example.argtypes = [ctypes.c_char_p, sz, ctypes.c_void_p, sz]
         lib.kfbrt_parse_example.restype = ctypes.c_long
         _LIB = lib
@@ -341,3 +344,12 @@ def table_read(path: str) -> List[Tuple[bytes, bytes]]:
         return out
     finally:
         lib.kfbrt_table_free(h)
+
+
+def adjust_saturation_hue(img, sat: float, hue: float):
+    """In place on a C-contiguous float32 [..., 3] RGB array (see
+    kfbrt_adjust_sat_hue); returns the array."""
+    import numpy as np
+    assert img.dtype == np.float32 and img.flags["C_CONTIGUOUS"] and img.shape[-1] == 3
+    _load().kfbrt_adjust_sat_hue(img.ctypes.data, img.size // 3, float(sat), float(hue))
+    return img

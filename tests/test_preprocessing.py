@@ -190,3 +190,19 @@ def test_get_imagenet_probe(tmp_path):
     assert res["subsets"]["validation"]["sampled_records"] == 8
     assert res["subsets"]["train"]["first_example"]["image/encoded"] > 0
     assert get_imagenet.main(["--data_dir", str(tmp_path)]) == 0
+
+
+def test_native_saturation_hue_matches_numpy():
+    """runtime.adjust_saturation_hue (one native HSV round trip) equals the
+    numpy adjust_saturation then adjust_hue of the colour distortion."""
+    from kf_benchmarks_amd import runtime
+    from kf_benchmarks_amd.data import preprocessing as pp
+    rng = np.random.default_rng(7)
+    img = rng.random((37, 41, 3), dtype=np.float32)
+    img[0, 0] = [0.5, 0.5, 0.5]   # grey: no hue
+    img[0, 1] = [0.0, 0.0, 0.0]   # black
+    img[0, 2] = [1.0, 0.0, 1.0]   # magenta: max shared by r and b
+    for sat, hue in [(0.5, 0.0), (1.5, 0.2), (1.0, -0.2), (0.73, 0.11)]:
+        ref = pp.adjust_hue(pp.adjust_saturation(img, sat), hue)
+        out = runtime.adjust_saturation_hue(img.copy(), sat, hue)
+        np.testing.assert_allclose(out, ref, rtol=1e-5, atol=2e-6)
