@@ -213,9 +213,10 @@ def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None, addend=None, wt=None,
             dx = torch.empty((n, H, W, C), dtype=dy.dtype, device=dy.device)
         elif addend is not None:
             # unsampled pixels keep the addend; sampled ones accumulate in place
-            assert fuse is None
+            # (with ``fuse`` the caller guarantees the addend is zero at every
+            # unsampled pixel, so the BN partials over sampled pixels are complete)
             dx = addend if addend_inplace else addend.clone()
-            fz = (None, None, None, None, dx, None)
+            fz = f5[:4] + (dx, f5[4])
         else:
             dx = torch.zeros((n, H, W, C), dtype=dy.dtype, device=dy.device)
         # GEMM over dY pixels (1x1, stride 1 in dY space), scattered by ys.
@@ -322,6 +323,9 @@ def _padded_input(x, cin_p):
 
 N.register_optional("kfb_s2d_stem", [N.I, N.P, N.P] + [N.I] * 9 + [N.P])
 _STEM_S2D = os.environ.get("KFB_STEM_S2D", "1") != "0"
+# BN backward partials in the epilogue of strided-1x1 (scatter) dgrads whose
+# pending gradient is sparse on the same grid (A/B and test switch)
+_SCATTER_BN_FUSE = os.environ.get("KFB_SCATTER_BN_FUSE", "1") != "0"
 
 
 def use_s2d(x, wl_shape, stride, needs_dx, pads) -> bool:
@@ -437,7 +441,15 @@ class _Conv2d(torch.autograd.Function):
                         dx = (dx + pend if pend is not None else dx).contiguous()
                     else:
                         fuse = None
-                        if not (pend is not None and is_scatter_dgrad(wp.shape, stride, pads)):
+                        scatter = is_scatter_dgrad(wp.shape, stride, pads)
+                        # A strided-1x1 (scatter) dgrad writes only every s-th
+                        # pixel, so it can finish the BN backward work only when
+                        # the pending gradient is zero elsewhere too (every other
+                        # contributor was a scatter of the same stride, as the
+                        # projection shortcut + conv a of a ResNet v1 block).
+                        sparse_ok = scatter and _SCATTER_BN_FUSE and stride[0] == stride[1] \
+                            and link.pending_sparse == stride[0]
+                        if not (pend is not None and scatter) or sparse_ok:
                             parts = stats_buffer(cin, dy.device)
                             # ReLU mask: recomputed from x_bn when the BN has no
                             # residual add (link.mcoef), else read from its output
@@ -450,7 +462,9 @@ class _Conv2d(torch.autograd.Function):
                             link.partials = fuse[0]
                 else:
                     g = conv_dgrad(dy, wp, xp.shape, stride, pads, wt=ctx.wt)
-                    link.deposit(g[..., :cin].contiguous() if padded else g)
+                    sparse = (stride[0] if not padded and stride[0] == stride[1]
+                              and is_scatter_dgrad(wp.shape, stride, pads) else None)
+                    link.deposit(g[..., :cin].contiguous() if padded else g, sparse=sparse)
             else:
                 dx = conv_dgrad(dy, wp, xp.shape, stride, pads, wt=ctx.wt)
                 if dx is not None and padded:

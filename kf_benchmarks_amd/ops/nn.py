@@ -107,7 +107,7 @@ class BNLink:
     """
 
     __slots__ = ("x_bn", "mean", "relu", "convs", "resid", "other", "partials", "pending",
-                 "pending_owned", "arrived", "mcoef")
+                 "pending_owned", "arrived", "mcoef", "pending_sparse")
 
     def __init__(self, x_bn, mean, relu, mcoef=None):
         self.x_bn, self.mean, self.relu = x_bn, mean, relu
@@ -118,6 +118,9 @@ class BNLink:
         self.convs, self.resid, self.other = 0, 0, False
         self.partials, self.pending, self.arrived = None, None, 0
         self.pending_owned = False
+        # s when every deposited gradient is zero outside the stride-s pixel
+        # grid (strided 1x1 "scatter" dgrads), else None
+        self.pending_sparse = None
 
     @property
     def fusable(self):
@@ -132,13 +135,17 @@ class BNLink:
         self.arrived += 1
         return self.arrived >= self.total
 
-    def deposit(self, g, owned=True):
+    def deposit(self, g, owned=True, sparse=None):
         """``owned``: g is a fresh buffer nothing else reads, so the last
-        contributor may accumulate into it in place."""
+        contributor may accumulate into it in place.  ``sparse``: g is zero
+        outside the stride-``sparse`` pixel grid."""
         if self.pending is None:
             self.pending, self.pending_owned = g, owned
+            self.pending_sparse = sparse
         else:
             self.pending, self.pending_owned = self.pending + g, True
+            if sparse != self.pending_sparse:
+                self.pending_sparse = None
 
 
 def _grad_sink(p):

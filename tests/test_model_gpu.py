@@ -87,3 +87,21 @@ def test_fused_matches_unfused(cuda, name, ds, size, batch):
         conv_ops.FUSE_BN = True
     cos = sorted(_cos(fused[k], ref) for k, ref in plain.items() if ref.norm() > 0)
     assert cos[0] > 0.9 and cos[len(cos) // 2] > 0.97, (cos[0], cos[len(cos) // 2])
+
+
+def test_scatter_dgrad_bn_fusion_matches(cuda, monkeypatch):
+    """ResNet-50 v1 stage transitions: the block input feeds two strided 1x1
+    convs (conv a, projection shortcut), whose scatter dgrads now also apply
+    the producer BN's ReLU mask and accumulate its backward partials.  The
+    backward is identical up to the first such BN, so every gradient is
+    (nearly) unchanged against the unfused path; deeper ones drift only by
+    bf16 rounding order."""
+    from kf_benchmarks_amd.ops import conv_hip
+    monkeypatch.setattr(conv_hip, "_SCATTER_BN_FUSE", True)
+    _, new = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
+    monkeypatch.setattr(conv_hip, "_SCATTER_BN_FUSE", False)
+    _, old = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
+    cos = {k: _cos(new[k], ref) for k, ref in old.items() if ref.norm() > 0}
+    vals = sorted(cos.values())
+    print("scatter fusion cosines: min %.4f median %.4f" % (vals[0], vals[len(vals) // 2]))
+    assert vals[len(vals) // 2] > 0.99 and vals[0] > 0.9, (vals[0], vals[len(vals) // 2])
