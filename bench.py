@@ -44,6 +44,9 @@ def main(argv=None):
     ap.add_argument("--kungfu_option", default="sync_sgd",
                     help="sync_sgd (headline) | async_sgd (PairAveraging) | sma | ada_sgd")
     ap.add_argument("--data_name", default=None, help="dataset (coco for ssd300, ...)")
+    ap.add_argument("--reuse_synthetic", action="store_true",
+                    help="generate the synthetic batch once (tf_cnn_benchmarks' gpu_cached_images) "
+                         "instead of re-sampling it inside every timed step")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
@@ -61,7 +64,8 @@ def main(argv=None):
                       optimizer=a.optimizer, use_bf16=a.dtype == "bf16",
                       use_fp16=a.dtype == "fp16", data_format="NHWC",
                       kernel_impl=a.kernel_impl, bucket_size_mb=a.bucket_size_mb,
-                      gradient_wire_dtype=a.wire_dtype, display_every=10**9)
+                      gradient_wire_dtype=a.wire_dtype, display_every=10**9,
+                      synthetic_resample=not a.reuse_synthetic)
     bench = BenchmarkCNN(p)
     bench.build()
     world = comm.get_world()
@@ -110,8 +114,10 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": round(value / base, 3) if base else None,
             "dtype": a.dtype,
-            "data": ("synthetic (%dx%dx3 ImageNet-shaped images, random-init weights)"
-                     % (bench.model.image_size, bench.model.image_size)
+            "data": ("synthetic (%dx%dx3 ImageNet-shaped images %s, random-init weights)"
+                     % (bench.model.image_size, bench.model.image_size,
+                        "generated once" if a.reuse_synthetic
+                        else "re-sampled on device every step")
                      if hasattr(bench.model, "image_size")
                      else "synthetic inputs of the model's shape, random-init weights"),
             "config": {"model": a.model, "global_batch": a.batch_size * n, "seq_len": None,

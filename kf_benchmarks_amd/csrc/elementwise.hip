@@ -134,6 +134,42 @@ synthetic_images_k(T* __restrict__ x, long n, float mean, float std, uint32_t se
   }
 }
 
+// 8 values per thread (one 16-byte store): both Box-Muller outputs of each
+// draw are used, rejected independently (|z| <= 2), with 32-bit indexing
+// and a per-thread hoisted seed hash - ~10x the per-element kernel above,
+// cheap enough to re-sample the synthetic batch every training step.
+__device__ __forceinline__ float u01h(uint32_t sh, uint32_t i) {
+  const uint32_t h = hash_u32(i ^ sh);
+  return ((h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+synthetic_images8_k(T* __restrict__ x, unsigned n8, float mean, float std, uint32_t seed) {
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += gridDim.x * blockDim.x) {
+    Vec<T, 8> o;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      float z0 = 0.f, z1 = 0.f;
+      bool ok0 = false, ok1 = false;
+      for (uint32_t k = 0; k < 8 && !(ok0 && ok1); ++k) {
+        const uint32_t sh1 = hash_u32(seed + 0x9e3779b9U * (2 * k + 1));
+        const uint32_t sh2 = hash_u32(seed + 0x9e3779b9U * (2 * k + 2));
+        const uint32_t j = i * 4 + p;
+        const float r = sqrtf(-2.f * __logf(u01h(sh1, j)));
+        float sn, cs;
+        __sincosf(6.28318530718f * u01h(sh2, j), &sn, &cs);
+        const float a = r * cs, b = r * sn;
+        if (!ok0 && fabsf(a) <= 2.f) { z0 = a; ok0 = true; }
+        if (!ok1 && fabsf(b) <= 2.f) { z1 = b; ok1 = true; }
+      }
+      o.v[2 * p] = from_f32<T>(mean + std * z0);
+      o.v[2 * p + 1] = from_f32<T>(mean + std * z1);
+    }
+    *reinterpret_cast<Vec<T, 8>*>(x + (long)i * 8) = o;
+  }
+}
+
 __global__ void __launch_bounds__(256)
 synthetic_labels_k(int* __restrict__ y, long n, int maxval, uint32_t seed) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -240,9 +276,14 @@ KFB_API hipError_t kfb_dropout(int dtype, const void* x, void* y, long n, float 
 
 KFB_API hipError_t kfb_synthetic_images(int dtype, void* x, long n, float mean, float std,
                                         uint32_t seed, hipStream_t stream) {
+  const bool vec8 = n % 8 == 0 && n / 8 < (1L << 31) && ((uintptr_t)x & 15) == 0;
   KFB_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL((synthetic_images_k<T>), dim3(egrid(n)), dim3(256), 0, stream, (T*)x, n,
-                       mean, std, seed);
+    if (vec8 && sizeof(T) == 2)
+      hipLaunchKernelGGL((synthetic_images8_k<T>), dim3(egrid(n / 8)), dim3(256), 0, stream,
+                         (T*)x, (unsigned)(n / 8), mean, std, seed);
+    else
+      hipLaunchKernelGGL((synthetic_images_k<T>), dim3(egrid(n)), dim3(256), 0, stream, (T*)x, n,
+                         mean, std, seed);
   });
   return hipGetLastError();
 }

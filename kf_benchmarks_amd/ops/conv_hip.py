@@ -301,24 +301,11 @@ def conv_wgrad(dy, x, w_shape, stride, pads, out=None):
     return dw
 
 
-_PAD_CACHE = {}
-
-
 def _padded_input(x, cin_p):
-    """Channel-padded copy of a network input (the RGB stem's 3 -> 8): the
-    synthetic batch is the same unmodified tensor every step, so its padded
-    copy is kept (one entry, keyed by storage and version counter) instead of
-    re-padded each step."""
-    if x.requires_grad:
-        return torch.nn.functional.pad(x, (0, cin_p - x.shape[-1]))
-    hit = _PAD_CACHE.get("in")
-    # identity (the entry keeps x alive, so its storage cannot be recycled
-    # under the key) plus the version counter (no in-place edit since)
-    if hit is not None and hit[0] is x and hit[1] == (x._version, cin_p):
-        return hit[2]
-    xp = torch.nn.functional.pad(x, (0, cin_p - x.shape[-1]))
-    _PAD_CACHE["in"] = (x, (x._version, cin_p), xp)
-    return xp
+    """Channel-padded copy of a few-channel network input (RGB 3 -> 8),
+    made every step (no cross-step caching, also for the constant synthetic
+    batch: the timed step does all of its work)."""
+    return torch.nn.functional.pad(x, (0, cin_p - x.shape[-1]))
 
 
 N.register_optional("kfb_s2d_stem", [N.I, N.P, N.P] + [N.I] * 9 + [N.P])

@@ -208,9 +208,10 @@ D.DEFINE_enum("gradient_wire_dtype", "auto", ("auto", "fp32", "bf16", "fp16"),
 D.DEFINE_float("kungfu_sma_alpha", 0.1, "SMA: pull factor toward the model average.")
 D.DEFINE_integer("kungfu_ada_switch_step", 100, "ada_sgd: step at which SMA switches to S-SGD.")
 D.DEFINE_integer("kungfu_peer_seed", 0, "Seed for PairAveraging peer selection.")
-D.DEFINE_boolean("use_hip_graph", False, "Capture the training step in a hipGraph and replay it.")
-D.DEFINE_boolean("synthetic_resample", False,
-                 "Re-sample synthetic inputs every step (the reference does; default reuses).")
+D.DEFINE_boolean("synthetic_resample", True,
+                 "Re-sample the synthetic batch on device every step, inside the timed step "
+                 "(as the fork's graph does; --nosynthetic_resample reuses one batch like "
+                 "the original tf_cnn_benchmarks' gpu_cached_images).")
 D.DEFINE_string("kernel_impl", "hip",
                 "Compute-op implementation on GPU: 'hip' (our kernels) or 'torch' "
                 "(stock PyTorch ops, for A/B comparison only).")

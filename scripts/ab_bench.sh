@@ -10,7 +10,9 @@ OUT="$ROOT/gpurun_out/$TAG"; mkdir -p "$OUT"
 for r in $(seq 1 "$R"); do
   for v in A B; do
     if [ "$v" = A ]; then E="$A"; else E="$B"; fi
-    env $E timeout -k 10 300 python bench.py --steps 30 --warmup 8 "$@" > "$OUT/$v$r.log" 2>&1 || exit $?
+    # "--..." variants are bench.py arguments, anything else environment assignments
+    if [ "${E#--}" != "$E" ]; then ARGS="$E"; ENVS=""; else ARGS=""; ENVS="$E"; fi
+    env $ENVS timeout -k 10 300 python bench.py --steps 30 --warmup 8 $ARGS "$@" > "$OUT/$v$r.log" 2>&1 || exit $?
     echo "$v ($E) round $r: $(grep -o '"value": [0-9.]*' "$OUT/$v$r.log")"
   done
 done
