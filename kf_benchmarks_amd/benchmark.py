@@ -449,6 +449,9 @@ class BenchmarkCNN:
         loss = self.model.loss_function(inputs, res)
         scaled = loss * self.loss_scale if self.loss_scale else loss
         scaled.backward()
+        if self.device_type == "cuda":
+            from .ops.conv_hip import join_wgrad_stream
+            join_wgrad_stream(self.device)
         acc = None
         if need_accuracy:
             acc = self.model.accuracy_function(inputs, res.logits.detach())

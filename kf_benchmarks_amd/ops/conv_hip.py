@@ -308,6 +308,52 @@ def _padded_input(x, cin_p):
     return torch.nn.functional.pad(x, (0, cin_p - x.shape[-1]))
 
 
+# Weight gradients on a side stream (KFB_WGRAD_STREAM=0: on the compute stream)
+_WGRAD_SIDE = os.environ.get("KFB_WGRAD_STREAM", "1") != "0"
+_SIDE_STREAMS = {}
+
+
+def wgrad_stream(device):
+    """The side stream weight gradients run on for ``device`` (None when
+    disabled or on the CPU)."""
+    if not _WGRAD_SIDE or device.type != "cuda":
+        return None
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _SIDE_STREAMS.get(idx)
+    if st is None:
+        st = _SIDE_STREAMS[idx] = torch.cuda.Stream(device=idx)
+    return st
+
+
+_JOIN_QUEUED = set()
+
+
+def _queue_join(device):
+    """Once per backward pass: join the side stream when the autograd graph
+    has finished, so every consumer of .grad (tests, optimizers) sees the
+    weight gradients without knowing about the side stream."""
+    idx = device.index
+    if idx in _JOIN_QUEUED:
+        return
+    _JOIN_QUEUED.add(idx)
+
+    def cb():
+        _JOIN_QUEUED.discard(idx)
+        join_wgrad_stream(torch.device("cuda", idx))
+    torch.autograd.Variable._execution_engine.queue_callback(cb)
+
+
+def join_wgrad_stream(device=None):
+    """Makes the current stream wait for every weight gradient enqueued so
+    far (before a gradient is read: all-reduce launch, optimizer step)."""
+    if not _SIDE_STREAMS:
+        return
+    cur = torch.cuda.current_stream(device)
+    st = _SIDE_STREAMS.get(cur.device.index)
+    if st is not None and st != cur:
+        cur.wait_stream(st)
+
+
 N.register_optional("kfb_s2d_stem", [N.I, N.P, N.P] + [N.I] * 9 + [N.P])
 _STEM_S2D = os.environ.get("KFB_STEM_S2D", "1") != "0"
 # BN backward partials in the epilogue of strided-1x1 (scatter) dgrads whose
@@ -462,6 +508,23 @@ class _Conv2d(torch.autograd.Function):
             sink = getattr(w, "_kfb_grad_sink", None)
             direct = (sink is not None and cout_p == cout and wp.shape[-1] == cin
                       and _fuse_enabled())
+            side = wgrad_stream(dy.device) if direct else None
+            if side is not None:
+                # weight gradient off the critical path: the dgrad chain
+                # continues on the compute stream while this runs beside it
+                # (backward of the small-grid stage-4/5 layers under-fills
+                # the chip).  Its inputs are kept alive for the side stream;
+                # gradient consumers join it (join_wgrad_stream).
+                side.wait_stream(torch.cuda.current_stream(dy.device))
+                _queue_join(dy.device)
+                with torch.cuda.stream(side):
+                    conv_wgrad(dy, xp, wp.shape, stride, pads, out=sink)
+                    dy.record_stream(side)
+                    xp.record_stream(side)
+                    cb = getattr(w, "_kfb_ready_cb", None)
+                    if cb is not None:
+                        cb(w)
+                return dx, None, None, None, None, None, None
             dw = conv_wgrad(dy, xp, wp.shape, stride, pads, out=sink if direct else None)
             if direct:
                 cb = getattr(w, "_kfb_ready_cb", None)

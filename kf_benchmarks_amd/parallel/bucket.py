@@ -122,6 +122,10 @@ class BucketReducer:
                 self._next += 1
 
     def _launch(self, b, src=None):
+        if self.flat.grad.is_cuda:
+            # gradients written on the weight-gradient side stream
+            from ..ops.conv_hip import join_wgrad_stream
+            join_wgrad_stream(self.flat.grad.device)
         s, e = self.buckets[b]
         view = (self.flat.grad if src is None else src)[s:e]
         buf = view.to(self.wire_dtype) if self.wire_dtype is not None else view
