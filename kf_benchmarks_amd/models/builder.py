@@ -18,6 +18,7 @@ from __future__ import annotations
 import collections
 import contextlib
 import math
+import os
 from typing import Optional
 
 import numpy as np
@@ -27,6 +28,22 @@ from .. import ops
 from ..ops import conv as conv_ops
 from ..ops import nn as F
 from .layers import AffineLayer, BatchNormLayer, ConvLayer, DepthwiseConvLayer
+
+
+# Independent branches (ResNet projection shortcuts) on a side stream with
+# KFB_SIDE_BRANCHES=1.  Off by default: interleaved A/B on ResNet-50 bs256
+# measured 12150 (off) vs 12115 img/s (on) - the four projection branches are
+# short next to the stream synchronization they add.
+_SIDE_BRANCHES = os.environ.get("KFB_SIDE_BRANCHES", "0") == "1"
+_BRANCH_STREAMS = {}
+
+
+def _branch_stream(device):
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _BRANCH_STREAMS.get(idx)
+    if st is None:
+        st = _BRANCH_STREAMS[idx] = torch.cuda.Stream(device=idx)
+    return st
 
 
 class ConvNetBuilder:
@@ -77,6 +94,35 @@ class ConvNetBuilder:
                 link.resid += 1
             else:
                 link.other = True
+
+    @contextlib.contextmanager
+    def side_branch(self, x):
+        """Runs the enclosed layers (an independent branch reading ``x``, e.g.
+        a projection shortcut) on a side HIP stream, concurrently with the
+        main branch that follows.  The branch output must be passed through
+        :meth:`join_branch` before the main stream uses it; autograd runs the
+        branch's backward on the same side stream.  No-op off the GPU."""
+        if (self.meta or not x.is_cuda or not _SIDE_BRANCHES):
+            yield
+            return
+        main = torch.cuda.current_stream(x.device)
+        side = _branch_stream(x.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            yield
+
+    @staticmethod
+    def join_branch(t):
+        """Makes the current stream wait for the side branch that produced
+        ``t`` (and keeps ``t``'s memory alive for it)."""
+        if t is None or not t.is_cuda or not _SIDE_BRANCHES:
+            return t
+        side = _BRANCH_STREAMS.get(t.device.index)
+        cur = torch.cuda.current_stream(t.device)
+        if side is not None and side != cur:
+            cur.wait_stream(side)
+            t.record_stream(cur)
+        return t
 
     @contextlib.contextmanager
     def switch_to_aux_top_layer(self):

@@ -24,15 +24,17 @@ def bottleneck_block_v1(cnn, depth, depth_bottleneck, stride):
             shortcut = input_layer if stride == 1 else cnn.apool(
                 1, 1, stride, stride, input_layer=input_layer, num_channels_in=in_size)
         else:
-            shortcut = cnn.conv(depth, 1, 1, stride, stride, activation=None,
-                                use_batch_norm=True, input_layer=input_layer,
-                                num_channels_in=in_size, bias=None)
+            # projection shortcut: independent of the a/b convs until the tail
+            with cnn.side_branch(input_layer):
+                shortcut = cnn.conv(depth, 1, 1, stride, stride, activation=None,
+                                    use_batch_norm=True, input_layer=input_layer,
+                                    num_channels_in=in_size, bias=None)
         cnn.conv(depth_bottleneck, 1, 1, stride, stride, input_layer=input_layer,
                  num_channels_in=in_size, use_batch_norm=True, bias=None)
         cnn.conv(depth_bottleneck, 3, 3, 1, 1, mode="SAME_RESNET", use_batch_norm=True,
                  bias=None)
         cnn.conv(depth, 1, 1, 1, 1, activation="relu", use_batch_norm=True, bias=None,
-                 residual=shortcut)
+                 residual=cnn.join_branch(shortcut))
         cnn.top_size = depth
 
 

@@ -467,6 +467,7 @@ class _Conv2d(torch.autograd.Function):
             padded = wp.shape[-1] != cin
             if link is not None and link.fusable:
                 if link.arrive():
+                    link.take_pending_stream()
                     pend, owned = link.pending, link.pending_owned
                     link.pending = None
                     if padded:

@@ -107,7 +107,7 @@ class BNLink:
     """
 
     __slots__ = ("x_bn", "mean", "relu", "convs", "resid", "other", "partials", "pending",
-                 "pending_owned", "arrived", "mcoef", "pending_sparse")
+                 "pending_owned", "arrived", "mcoef", "pending_sparse", "pending_event")
 
     def __init__(self, x_bn, mean, relu, mcoef=None):
         self.x_bn, self.mean, self.relu = x_bn, mean, relu
@@ -121,6 +121,9 @@ class BNLink:
         # s when every deposited gradient is zero outside the stride-s pixel
         # grid (strided 1x1 "scatter" dgrads), else None
         self.pending_sparse = None
+        # contributors may run on different streams (side branches): the
+        # pending gradient is complete once this event has fired
+        self.pending_event = None
 
     @property
     def fusable(self):
@@ -143,9 +146,22 @@ class BNLink:
             self.pending, self.pending_owned = g, owned
             self.pending_sparse = sparse
         else:
+            self.take_pending_stream()
             self.pending, self.pending_owned = self.pending + g, True
             if sparse != self.pending_sparse:
                 self.pending_sparse = None
+        if g.is_cuda:
+            self.pending_event = torch.cuda.Event()
+            self.pending_event.record()
+
+    def take_pending_stream(self):
+        """Makes the current stream wait for the pending gradient (written
+        on whatever stream its contributors ran on) before using it."""
+        if self.pending is not None and self.pending_event is not None:
+            cur = torch.cuda.current_stream(self.pending.device)
+            cur.wait_event(self.pending_event)
+            self.pending.record_stream(cur)
+            self.pending_event = None
 
 
 def _grad_sink(p):
@@ -240,6 +256,7 @@ class _BatchNormTrain(torch.autograd.Function):
         if res_fused:
             if rl.arrive():
                 if rl.pending is not None:
+                    rl.take_pending_stream()
                     dres = dres + rl.pending
                     rl.pending = None
             else:
