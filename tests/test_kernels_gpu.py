@@ -26,7 +26,9 @@ def _pair(x, dev, dt):
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("shape", [(4, 7, 7, 64), (2, 5, 6, 24), (3, 4, 4, 2048), (2, 3, 3, 20)])
+@pytest.mark.parametrize("shape", [(4, 7, 7, 64), (2, 5, 6, 24), (3, 4, 4, 2048), (2, 3, 3, 20),
+                                   # > 4 x the capped grid: the unrolled streaming loop + tail
+                                   (81, 32, 32, 256)])
 @pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
 def test_batch_norm_train(cuda, dt, shape, relu, res):
     torch.manual_seed(0)
@@ -46,11 +48,12 @@ def test_batch_norm_train(cuda, dt, shape, relu, res):
     torch.testing.assert_close(ya.float().cpu(), yb, **tol(dt))
     torch.testing.assert_close(rma.cpu(), rmb, rtol=1e-3, atol=1e-3)
     torch.testing.assert_close(rva.cpu(), rvb, rtol=1e-3, atol=1e-3)
-    dy = torch.randn(shape)
+    dy = torch.randn(shape).to(dt).float()  # both sides see the same rounded gradient
     ya.backward(dy.to(cuda, dt))
     yb.backward(dy)
     t = tol(dt)
-    torch.testing.assert_close(xa.grad.float().cpu(), xb.grad, rtol=t["rtol"] * 3, atol=t["atol"] * 3)
+    # bf16 output rounding: ~1 ulp of |dx| up to ~8 over 2e7 elements
+    torch.testing.assert_close(xa.grad.float().cpu(), xb.grad, rtol=t["rtol"] * 4, atol=t["atol"] * 4)
     torch.testing.assert_close(ga.grad.cpu(), gb.grad, rtol=5e-2 if dt != torch.float32 else 1e-3,
                                atol=0.5 if dt != torch.float32 else 1e-3)
     torch.testing.assert_close(ba.grad.cpu(), bb.grad, rtol=5e-2 if dt != torch.float32 else 1e-3,
