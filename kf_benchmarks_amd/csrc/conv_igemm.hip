@@ -560,15 +560,22 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_barrier" ::: "memory");
 }
 
-template <typename T, int BM, int BN, int WGM, int WGN>
-__global__ void __launch_bounds__(512, 1) igemm_glds_k(IgArgs a) {
-  constexpr int NT = 512;
-  static_assert(WGM * WGN == NT / 64, "wave grid");
+//
+// STAGES = 2 (the "tall" 64-channel tiles, 2 workgroups or one 144 KB
+// workgroup per CU): the DMAs of step t+1 are issued right after the barrier
+// that retires step t and fly during compute(t); the wait at the top of each
+// step is then vmcnt(0) (only that step's DMAs are outstanding).
+template <typename T, int BM, int BN, int WGM, int WGN, int STAGES = GL_STAGES>
+__global__ void __launch_bounds__(WGM * WGN * 64, 1) igemm_glds_k(IgArgs a) {
+  constexpr int NT = WGM * WGN * 64;
+  constexpr int SLAB = NT / 8;  // rows one DMA instruction of every wave covers
+  static_assert(STAGES == 2 || STAGES == 3, "ring depth");
+  static_assert(BM % SLAB == 0 && BN % SLAB == 0 && SLAB % 16 == 0, "DMA slabs");
   constexpr int TM = BM / WGM / 16, TN = BN / WGN / 16;
-  constexpr int XI = BM / 64, WI = BN / 64;  // DMA instructions per thread per K step
-  constexpr int STAGE = (BM + BN) * IG_BK;   // elements per ring stage
-  static_assert(BM * BN <= GL_STAGES * STAGE, "epilogue staging exceeds the ring");
-  __shared__ __attribute__((aligned(16))) T smem[GL_STAGES * STAGE];
+  constexpr int XI = BM / SLAB, WI = BN / SLAB;  // DMA instructions per thread per K step
+  constexpr int STAGE = (BM + BN) * IG_BK;       // elements per ring stage
+  static_assert(BM * BN <= STAGES * STAGE, "epilogue staging exceeds the ring");
+  __shared__ __attribute__((aligned(16))) T smem[STAGES * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -576,7 +583,7 @@ __global__ void __launch_bounds__(512, 1) igemm_glds_k(IgArgs a) {
   const int bid = xcd_remap(blockIdx.x, mtiles * ntiles);
   const int m0 = (bid / ntiles) * BM, n0 = (bid % ntiles) * BN;
   const int OHW = a.OH * a.OW;
-  const int rr = tid >> 3;                       // DMA row within each 64-row slab
+  const int rr = tid >> 3;                       // DMA row within each SLAB-row slab
   const int kc = (lane & 7) ^ ((rr >> 1) & 7);   // logical chunk this lane fetches
 
   const __amdgpu_buffer_rsrc_t xrs =
@@ -587,7 +594,7 @@ __global__ void __launch_bounds__(512, 1) igemm_glds_k(IgArgs a) {
   int xoff[XI], woff[WI];
 #pragma unroll
   for (int i = 0; i < XI; ++i) {
-    const int m = m0 + i * 64 + rr;
+    const int m = m0 + i * SLAB + rr;
     const bool ok = m < a.M;
     const int mm = ok ? m : 0;
     const int img = mm / OHW, rem = mm - img * OHW;
@@ -603,7 +610,7 @@ __global__ void __launch_bounds__(512, 1) igemm_glds_k(IgArgs a) {
     xoff[i] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + kc * 8;
   }
 #pragma unroll
-  for (int j = 0; j < WI; ++j) woff[j] = (n0 + j * 64 + rr) * a.Ktot + kc * 8;
+  for (int j = 0; j < WI; ++j) woff[j] = (n0 + j * SLAB + rr) * a.Ktot + kc * 8;
 
   int s_cc = 0, s_kh = 0, s_kw = 0, s_tap = 0, s_tapi = 0, s_k = 0;
   auto issue = [&](int stage) {
@@ -613,11 +620,11 @@ __global__ void __launch_bounds__(512, 1) igemm_glds_k(IgArgs a) {
     for (int i = 0; i < XI; ++i) {
       const bool ok = (tapmask[i] >> s_tapi) & 1ull;
       const int off = ok ? (xoff[i] + s_tap + s_cc) * (int)sizeof(T) : -1;
-      dma16(xrs, xs + (i * 64 + wid * 8) * IG_BK, off);
+      dma16(xrs, xs + (i * SLAB + wid * 8) * IG_BK, off);
     }
 #pragma unroll
     for (int j = 0; j < WI; ++j)
-      dma16(wrs, ws + (j * 64 + wid * 8) * IG_BK, (woff[j] + s_k) * (int)sizeof(T));
+      dma16(wrs, ws + (j * SLAB + wid * 8) * IG_BK, (woff[j] + s_k) * (int)sizeof(T));
     s_k += IG_BK;
     s_cc += IG_BK;
     if (s_cc == a.C) {
@@ -656,15 +663,23 @@ __global__ void __launch_bounds__(512, 1) igemm_glds_k(IgArgs a) {
 
   const int nk = a.Ktot / IG_BK;  // FAST geometry: C % 64 == 0
   issue(0);
-  if (nk > 1) issue(1);
+  if (STAGES == 3 && nk > 1) issue(1);
   int st = 0;  // stage of step kt
   for (int kt = 0; kt < nk; ++kt) {
-    // retire step kt's DMAs (step kt+1's, issued later, may stay in flight)
-    if (kt + 1 < nk) wait_vmcnt<XI + WI>(); else wait_vmcnt<0>();
-    lds_barrier();  // every wave's DMAs of step kt landed; stage (kt+2)%3 fully read
-    if (kt + 2 < nk) issue(st == 0 ? 2 : st - 1);
-    compute(st);  // (s_setprio(1) around it measured no faster)
-    st = st == 2 ? 0 : st + 1;
+    if constexpr (STAGES == 3) {
+      // retire step kt's DMAs (step kt+1's, issued later, may stay in flight)
+      if (kt + 1 < nk) wait_vmcnt<XI + WI>(); else wait_vmcnt<0>();
+      lds_barrier();  // every wave's DMAs of step kt landed; stage (kt+2)%3 fully read
+      if (kt + 2 < nk) issue(st == 0 ? 2 : st - 1);
+      compute(st);  // (s_setprio(1) around it measured no faster)
+      st = st == 2 ? 0 : st + 1;
+    } else {
+      wait_vmcnt<0>();  // step kt's DMAs (the only ones outstanding)
+      lds_barrier();    // ... of every wave landed; stage st^1 (step kt-1) fully read
+      if (kt + 1 < nk) issue(st ^ 1);
+      compute(st);
+      st ^= 1;
+    }
   }
   __syncthreads();  // all fragment reads done before the epilogue reuses the ring
   ig_epilogue<T, BM, BN, NT, WGM, WGN>(a, acc, smem, m0, n0, wm, wn);
@@ -994,6 +1009,19 @@ static bool igemm_fast_disabled() {
 }
 
 template <typename T>
+static void launch_glds_tall(const IgArgs& a, bool wide, hipStream_t s) {
+  // 64-channel tiles with 64x64 wave tiles and a 2-stage ring: 512 x 64 on 8
+  // waves (144 KB, one workgroup per CU) or 256 x 64 on 4 waves (80 KB, two)
+  const int nt = (a.Ncol + 63) / 64;
+  if (wide)
+    hipLaunchKernelGGL((igemm_glds_k<T, 512, 64, 8, 1, 2>), dim3(((a.M + 511) / 512) * nt),
+                       dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((igemm_glds_k<T, 256, 64, 4, 1, 2>), dim3(((a.M + 255) / 256) * nt),
+                       dim3(256), 0, s, a);
+}
+
+template <typename T>
 static void launch_glds(const IgArgs& a, bool narrow, hipStream_t s) {
   const int mt = (a.M + 255) / 256;
   if (a.Ncol <= 64 || narrow)
@@ -1053,8 +1081,10 @@ using namespace kfb;
 // on 512 slots is 1.5 waves).  ops/conv_hip.py times the candidates per
 // geometry.
 //   IG_ALGO_ONEBUF(_N64): FAST igemm_k with one LDS stage (4 workgroups/CU).
+//   IG_ALGO_TALL512 / TALL256: igemm_glds_k with 64-channel tiles and 64x64
+//   wave tiles (twice the MFMAs per fragment read of the 256x64 8-wave tile).
 enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_GLDS_N64 = 4,
-       IG_ALGO_ONEBUF = 5, IG_ALGO_ONEBUF_N64 = 6 };
+       IG_ALGO_ONEBUF = 5, IG_ALGO_ONEBUF_N64 = 6, IG_ALGO_TALL512 = 7, IG_ALGO_TALL256 = 8 };
 
 KFB_API int kfb_conv_igemm_fast(int C, int KH, int KW, int trans) {
   return !trans && C % IG_BK == 0 && KH * KW <= 64 && !igemm_fast_disabled();
@@ -1081,6 +1111,12 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
   const bool narrow = algo == IG_ALGO_CLASSIC_N64 || algo == IG_ALGO_GLDS_N64 ||
                       algo == IG_ALGO_ONEBUF_N64;
   const bool onebuf = algo == IG_ALGO_ONEBUF || algo == IG_ALGO_ONEBUF_N64;
+  if ((algo == IG_ALGO_TALL512 || algo == IG_ALGO_TALL256) && fast) {
+    if (dtype == BF16) launch_glds_tall<bf16>(a, algo == IG_ALGO_TALL512, stream);
+    else if (dtype == F16) launch_glds_tall<f16>(a, algo == IG_ALGO_TALL512, stream);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   if ((algo == IG_ALGO_GLDS || algo == IG_ALGO_GLDS_N64) && fast) {
     if (dtype == BF16) launch_glds<bf16>(a, narrow, stream);
     else if (dtype == F16) launch_glds<f16>(a, narrow, stream);
