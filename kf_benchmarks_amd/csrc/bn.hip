@@ -209,6 +209,33 @@ bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y
   }
 }
 
+// y = relu?(x * scale + shift + xr * scale_r + shift_r): a BN whose residual
+// is itself a BN output with no ReLU (ResNet v1 projection shortcut,
+// tcb/models/resnet_model.py:60-75), applied from both raw inputs so the
+// shortcut BN output is never materialized.
+template <typename T, int V, bool RELU>
+__global__ void __launch_bounds__(256)
+bn_apply2_k(const T* __restrict__ x, const T* __restrict__ xr, T* __restrict__ y, long nvec, int C,
+            const float* __restrict__ scale, const float* __restrict__ shift,
+            const float* __restrict__ scale_r, const float* __restrict__ shift_r) {
+  const unsigned cv = (unsigned)(C / V);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)nvec;
+       i += gridDim.x * blockDim.x) {
+    const long e = (long)i * V;
+    const int c = (int)(i % cv) * V;
+    float v[V], r[V];
+    load_vec<T, V>(x + e, v);
+    load_vec<T, V>(xr + e, r);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      float o = v[k] * scale[c + k] + shift[c + k] + (r[k] * scale_r[c + k] + shift_r[c + k]);
+      if (RELU) o = fmaxf(o, 0.f);
+      v[k] = o;
+    }
+    store_vec<T, V>(y + e, v);
+  }
+}
+
 // ---------------------------------------------------------------- backward
 template <typename T, int V, bool MASK>
 __global__ void __launch_bounds__(BN_THREADS)
@@ -655,6 +682,41 @@ KFB_API hipError_t kfb_bn_fwd_train(int dtype, const void* x, const void* res, v
           hipLaunchKernelGGL((bn_apply_k<T, VV, false, false>), dim3(gb), dim3(256), 0, stream,
                              (const T*)x, (const T*)nullptr, (T*)y, nvec, C, scale, shift);
       }
+    });
+  });
+  return hipGetLastError();
+}
+
+// Forward, training mode, of y = relu?(bn(x) + bn_r(xr)) where both inputs'
+// partial sums [nslab][C] were accumulated by the producing convs' epilogues:
+// both finalizes (running statistics, scale/shift) and ONE apply pass.
+KFB_API hipError_t kfb_bn_fwd_train_dual(
+    int dtype, const void* x, const void* xr, void* y, long rows, int C, const float* gamma,
+    const float* beta, float decay, float eps, float* run_mean, float* run_var, float* save_mean,
+    float* save_invstd, float* scale, float* shift, const float* psum, const float* psq,
+    int nslab, const float* gamma_r, const float* beta_r, float decay_r, float eps_r,
+    float* run_mean_r, float* run_var_r, float* save_mean_r, float* save_invstd_r,
+    float* scale_r, float* shift_r, const float* psum_r, const float* psq_r, int nslab_r,
+    int relu, hipStream_t stream) {
+  const int V = vec_width(C);
+  hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, 4), 0, stream, psum_r,
+                     psq_r, nslab_r, C, rows, gamma_r, beta_r, decay_r, eps_r, run_mean_r,
+                     run_var_r, save_mean_r, save_invstd_r, scale_r, shift_r);
+  hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, 4), 0, stream, psum,
+                     psq, nslab, C, rows, gamma, beta, decay, eps, run_mean, run_var, save_mean,
+                     save_invstd, scale, shift);
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    KFB_DISPATCH_VEC(V, VV, {
+      const long nvec = rows * C / VV;
+      const int gb = stream_grid(nvec);
+      if (relu)
+        hipLaunchKernelGGL((bn_apply2_k<T, VV, true>), dim3(gb), dim3(256), 0, stream,
+                           (const T*)x, (const T*)xr, (T*)y, nvec, C, scale, shift, scale_r,
+                           shift_r);
+      else
+        hipLaunchKernelGGL((bn_apply2_k<T, VV, false>), dim3(gb), dim3(256), 0, stream,
+                           (const T*)x, (const T*)xr, (T*)y, nvec, C, scale, shift, scale_r,
+                           shift_r);
     });
   });
   return hipGetLastError();

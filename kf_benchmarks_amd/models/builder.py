@@ -35,6 +35,8 @@ from .layers import AffineLayer, BatchNormLayer, ConvLayer, DepthwiseConvLayer
 # measured 12150 (off) vs 12115 img/s (on) - the four projection branches are
 # short next to the stream synchronization they add.
 _SIDE_BRANCHES = os.environ.get("KFB_SIDE_BRANCHES", "0") == "1"
+# conv(defer_bn=True) returns the BN unapplied (KFB_DEFER_BN=0: always apply)
+_DEFER_BN = os.environ.get("KFB_DEFER_BN", "1") != "0"
 _BRANCH_STREAMS = {}
 
 
@@ -115,13 +117,14 @@ class ConvNetBuilder:
     def join_branch(t):
         """Makes the current stream wait for the side branch that produced
         ``t`` (and keeps ``t``'s memory alive for it)."""
-        if t is None or not t.is_cuda or not _SIDE_BRANCHES:
+        x = t.x if isinstance(t, F.DeferredBN) else t
+        if x is None or not x.is_cuda or not _SIDE_BRANCHES:
             return t
-        side = _BRANCH_STREAMS.get(t.device.index)
-        cur = torch.cuda.current_stream(t.device)
+        side = _BRANCH_STREAMS.get(x.device.index)
+        cur = torch.cuda.current_stream(x.device)
         if side is not None and side != cur:
             cur.wait_stream(side)
-            t.record_stream(cur)
+            x.record_stream(cur)
         return t
 
     @contextlib.contextmanager
@@ -139,10 +142,17 @@ class ConvNetBuilder:
     # ------------------------------------------------------------------ conv
     def conv(self, num_out_channels, k_height, k_width, d_height=1, d_width=1, mode="SAME",
              input_layer=None, num_channels_in=None, use_batch_norm=None, stddev=None,
-             activation="relu", bias=0.0, kernel_initializer=None, residual=None, pool=None):
+             activation="relu", bias=0.0, kernel_initializer=None, residual=None, pool=None,
+             defer_bn=False):
         """``pool`` = (k_h, k_w, d_h, d_w, mode): a max-pool applied to the
         (BN + ReLU) output, i.e. conv(...) then mpool(*pool); with BN in
-        training on the GPU the BN apply, ReLU and pool run as one fused op."""
+        training on the GPU the BN apply, ReLU and pool run as one fused op.
+
+        ``defer_bn``: for a conv + BN with no activation whose only consumer
+        is the ``residual`` of a later conv + BN (ResNet v1 projection
+        shortcut): in training on the GPU the BN is returned unapplied (an
+        ``ops.nn.DeferredBN``) and applied inside that later BN's apply pass;
+        top_layer is left unchanged.  Otherwise a normal tensor is returned."""
         x = self.top_layer if input_layer is None else input_layer
         cin = self.top_size if num_channels_in is None else num_channels_in
         name = "conv%d" % self.counts["conv"]
@@ -169,6 +179,14 @@ class ConvNetBuilder:
         y = F.conv2d(x, w, None if self.meta else layer.weight_lp, (d_height, d_width), pads,
                      self.impl, stats, None if self.meta else layer.weight_t)
         relu = activation == "relu"
+        if defer_bn and _DEFER_BN and use_batch_norm and activation is None and \
+                residual is None and pool is None and stats is not None and y.is_cuda:
+            with self.scope(name):
+                cfg = self.batch_norm_config
+                layer = self._bn_layer(num_out_channels, cfg.get("scale", False),
+                                       cfg.get("decay", 0.999), cfg.get("epsilon", 0.001))
+            return F.DeferredBN(y, layer.gamma, layer.beta, layer.moving_mean,
+                                layer.moving_variance, layer.decay, layer.eps, stats)
         if pool is not None:
             if use_batch_norm and relu and residual is None and not self.meta and \
                     F.bn_relu_max_pool_fusable(y, stats, self.phase_train):
@@ -379,10 +397,17 @@ class ConvNetBuilder:
     def _batch_norm(self, x, decay=0.999, scale=False, epsilon=0.001, relu=False,
                     residual=None, stats=None):
         self._use(x)
-        self._use(residual, resid=True)
+        deferred = isinstance(residual, F.DeferredBN)
+        self._use(None if deferred else residual, resid=True)
         C = x.shape[-1]
         layer = self._bn_layer(C, scale, decay, epsilon)
         training = self.phase_train and not self.meta
+        if deferred:
+            y = F.batch_norm_dual(x, layer.gamma, layer.beta, layer.moving_mean,
+                                  layer.moving_variance, layer.decay, layer.eps, relu,
+                                  stats if training else None, residual)
+            self.top_layer, self.top_size = y, C
+            return y
         if self.meta:
             y = F.batch_norm(x, self._p(layer.gamma), self._p(layer.beta),
                              self._p(layer.moving_mean), self._p(layer.moving_variance),

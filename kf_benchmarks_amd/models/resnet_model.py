@@ -25,10 +25,11 @@ def bottleneck_block_v1(cnn, depth, depth_bottleneck, stride):
                 1, 1, stride, stride, input_layer=input_layer, num_channels_in=in_size)
         else:
             # projection shortcut: independent of the a/b convs until the tail
+            # (its BN is applied inside the block-output BN: defer_bn)
             with cnn.side_branch(input_layer):
                 shortcut = cnn.conv(depth, 1, 1, stride, stride, activation=None,
                                     use_batch_norm=True, input_layer=input_layer,
-                                    num_channels_in=in_size, bias=None)
+                                    num_channels_in=in_size, bias=None, defer_bn=True)
         cnn.conv(depth_bottleneck, 1, 1, stride, stride, input_layer=input_layer,
                  num_channels_in=in_size, use_batch_norm=True, bias=None)
         cnn.conv(depth_bottleneck, 3, 3, 1, 1, mode="SAME_RESNET", use_batch_norm=True,

@@ -215,59 +215,139 @@ class _BatchNormTrain(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, y, gamma, st = ctx.saved_tensors
-        dy = dy.contiguous()
+        dx, dgamma, dbeta, dres = _bn_backward(x, y, gamma, st, dy, ctx.relu, ctx.has_res,
+                                               ctx.link, ctx.res_link, ctx.gamma, ctx.beta)
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None
+
+
+def _bn_backward(x, y, gamma, st, dy, relu, has_res, link, res_link, gamma_p, beta_p):
+    """BN backward (kfb_bn_bwd): returns (dx, dgamma, dbeta, dres); dgamma and
+    dbeta are None when they went straight into the flat gradient buffer."""
+    dy = dy.contiguous()
+    C = x.shape[-1]
+    rows = x.numel() // C
+    dev = x.device
+    pre = link is not None and link.partials is not None
+    if pre:
+        parts = link.partials
+        nslab = parts.numel() // (2 * C)
+        pdy, pdyx = parts[:nslab * C], parts[nslab * C:]
+        coef = torch.empty((3 * C,), dtype=torch.float32, device=dev)
+        link.partials = None
+    else:
+        nslab = N.query("kfb_bn_num_slabs", rows, C)
+        ws = torch.empty((2 * nslab * C + 3 * C,), dtype=torch.float32, device=dev)
+        pdy, pdyx = ws[:nslab * C], ws[nslab * C:2 * nslab * C]
+        coef = ws[2 * nslab * C:]
+    gsink, bsink = _grad_sink(gamma_p), _grad_sink(beta_p)
+    direct = bsink is not None and (gamma_p is None or gsink is not None) and _conv.FUSE_BN
+    if direct:
+        dgp, dbp = N.ptr(gsink), bsink.data_ptr()
+    else:
+        dparams = torch.empty((2, C), dtype=torch.float32, device=dev)
+        dgp, dbp = dparams[0].data_ptr(), dparams[1].data_ptr()
+    dx = torch.empty_like(x)
+    rl = res_link
+    res_fused = has_res and rl is not None and rl.fusable
+    # the residual's gradient is dy' (masked dy): with a pre-masked dy it
+    # is dy itself, no kernel write needed
+    dres = torch.empty_like(x) if has_res and not (pre and res_fused) else None
+    N.call("kfb_bn_bwd", N.dt(x), dy.data_ptr(), N.ptr(y), x.data_ptr(), dx.data_ptr(),
+           N.ptr(dres), rows, C, N.ptr(gamma), st[0].data_ptr(), st[1].data_ptr(),
+           dgp, dbp, pdy.data_ptr(), pdyx.data_ptr(),
+           nslab, coef[:C].data_ptr(), coef[C:2 * C].data_ptr(), coef[2 * C:].data_ptr(),
+           int(relu), int(direct), int(pre), N.stream(dev))
+    if has_res and dres is None:
+        dres = dy
+    if res_fused:
+        if rl.arrive():
+            if rl.pending is not None:
+                rl.take_pending_stream()
+                dres = dres + rl.pending
+                rl.pending = None
+        else:
+            rl.deposit(dres, owned=dres is not dy)
+            dres = None
+    if direct:
+        _grad_ready(gamma_p)
+        _grad_ready(beta_p)
+        return dx, None, None, dres
+    dgamma = dparams[0] if gamma_p is not None else None
+    return dx, dgamma, dparams[1], dres
+
+
+class DeferredBN:
+    """A training-mode BN (no ReLU, no residual) not applied yet: its raw
+    input ``x`` (a conv output whose epilogue accumulated ``stats``) and the
+    BN's parameters.  As the ``residual`` of another BN it is applied inside
+    that BN's apply pass (:func:`batch_norm_dual`), so its output is never
+    materialized; any other use calls :meth:`materialize`."""
+
+    __slots__ = ("x", "gamma", "beta", "rm", "rv", "decay", "eps", "stats")
+
+    def __init__(self, x, gamma, beta, rm, rv, decay, eps, stats):
+        self.x, self.gamma, self.beta, self.rm, self.rv = x, gamma, beta, rm, rv
+        self.decay, self.eps, self.stats = decay, eps, stats
+
+    def materialize(self):
+        return _BatchNormTrain.apply(self.x, self.gamma, self.beta, None, self.rm, self.rv,
+                                     self.decay, self.eps, False, self.stats)
+
+
+class _BatchNormTrainDual(torch.autograd.Function):
+    """y = relu?(bn(x) + bn_r(xr)), both BNs in training mode with conv-epilogue
+    statistics (kfb_bn_fwd_train_dual: one apply pass over x and xr).  The
+    backward is that of the two separate BNs: bn_r's output gradient is the
+    ReLU-masked dy, which the first BN backward writes as its residual
+    gradient."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, xr, gamma_r, beta_r, rm, rv, rm_r, rv_r, decay, eps,
+                decay_r, eps_r, relu, stats, stats_r):
+        x, xr = x.contiguous(), xr.contiguous()
         C = x.shape[-1]
         rows = x.numel() // C
         dev = x.device
-        link = ctx.link
-        pre = link is not None and link.partials is not None
-        if pre:
-            parts = link.partials
-            nslab = parts.numel() // (2 * C)
-            pdy, pdyx = parts[:nslab * C], parts[nslab * C:]
-            coef = torch.empty((3 * C,), dtype=torch.float32, device=dev)
-            link.partials = None
-        else:
-            nslab = N.query("kfb_bn_num_slabs", rows, C)
-            ws = torch.empty((2 * nslab * C + 3 * C,), dtype=torch.float32, device=dev)
-            pdy, pdyx = ws[:nslab * C], ws[nslab * C:2 * nslab * C]
-            coef = ws[2 * nslab * C:]
-        gsink, bsink = _grad_sink(ctx.gamma), _grad_sink(ctx.beta)
-        direct = bsink is not None and (ctx.gamma is None or gsink is not None) and \
-            _conv.FUSE_BN
-        if direct:
-            dgp, dbp = N.ptr(gsink), bsink.data_ptr()
-        else:
-            dparams = torch.empty((2, C), dtype=torch.float32, device=dev)
-            dgp, dbp = dparams[0].data_ptr(), dparams[1].data_ptr()
-        dx = torch.empty_like(x)
-        rl = ctx.res_link
-        res_fused = ctx.has_res and rl is not None and rl.fusable
-        # the residual's gradient is dy' (masked dy): with a pre-masked dy it
-        # is dy itself, no kernel write needed
-        dres = torch.empty_like(x) if ctx.has_res and not (pre and res_fused) else None
-        N.call("kfb_bn_bwd", N.dt(x), dy.data_ptr(), N.ptr(y), x.data_ptr(), dx.data_ptr(),
-               N.ptr(dres), rows, C, N.ptr(gamma), st[0].data_ptr(), st[1].data_ptr(),
-               dgp, dbp, pdy.data_ptr(), pdyx.data_ptr(),
-               nslab, coef[:C].data_ptr(), coef[C:2 * C].data_ptr(), coef[2 * C:].data_ptr(),
-               int(ctx.relu), int(direct), int(pre), N.stream(dev))
-        if ctx.has_res and dres is None:
-            dres = dy
-        if res_fused:
-            if rl.arrive():
-                if rl.pending is not None:
-                    rl.take_pending_stream()
-                    dres = dres + rl.pending
-                    rl.pending = None
-            else:
-                rl.deposit(dres, owned=dres is not dy)
-                dres = None
-        if direct:
-            _grad_ready(ctx.gamma)
-            _grad_ready(ctx.beta)
-            return dx, None, None, dres, None, None, None, None, None, None
-        dgamma = dparams[0] if ctx.gamma is not None else None
-        return dx, dgamma, dparams[1], dres, None, None, None, None, None, None
+        nslab, nslab_r = stats.numel() // (2 * C), stats_r.numel() // (2 * C)
+        ws = torch.empty((2, 4, C), dtype=torch.float32, device=dev)  # [bn][mean|invstd|scale|shift]
+        y = torch.empty_like(x)
+        N.call("kfb_bn_fwd_train_dual", N.dt(x), x.data_ptr(), xr.data_ptr(), y.data_ptr(),
+               rows, C, N.ptr(gamma), N.ptr(beta), float(decay), float(eps), N.ptr(rm),
+               N.ptr(rv), ws[0, 0].data_ptr(), ws[0, 1].data_ptr(), ws[0, 2].data_ptr(),
+               ws[0, 3].data_ptr(), stats[:nslab * C].data_ptr(), stats[nslab * C:].data_ptr(),
+               nslab, N.ptr(gamma_r), N.ptr(beta_r), float(decay_r), float(eps_r), N.ptr(rm_r),
+               N.ptr(rv_r), ws[1, 0].data_ptr(), ws[1, 1].data_ptr(), ws[1, 2].data_ptr(),
+               ws[1, 3].data_ptr(), stats_r[:nslab_r * C].data_ptr(),
+               stats_r[nslab_r * C:].data_ptr(), nslab_r, int(relu), N.stream(dev))
+        st, st_r = ws[0, :2], ws[1, :2]
+        ctx.save_for_backward(x, y if relu else None, gamma, st, xr, gamma_r, st_r)
+        ctx.relu = relu
+        ctx.params = (gamma, beta, gamma_r, beta_r)
+        link = BNLink(x, st[0], relu)
+        y._kfb_bn_link = link
+        ctx.link = link
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, gamma, st, xr, gamma_r, st_r = ctx.saved_tensors
+        gp, bp, gp_r, bp_r = ctx.params
+        dx, dg, db, g = _bn_backward(x, y, gamma, st, dy, ctx.relu, True, ctx.link, None, gp, bp)
+        dxr, dg_r, db_r, _ = _bn_backward(xr, None, gamma_r, st_r, g, False, False, None, None,
+                                          gp_r, bp_r)
+        return (dx, dg, db, dxr, dg_r, db_r) + (None,) * 11
+
+
+def batch_norm_dual(x, gamma, beta, running_mean, running_var, decay, eps, relu, stats,
+                    r: "DeferredBN"):
+    """relu?(bn(x) + r) for a deferred BN ``r`` (training mode, GPU, both
+    inputs with conv-epilogue statistics); otherwise r is materialized first."""
+    if stats is None or r.stats is None or not _on_gpu(x) or x.shape != r.x.shape:
+        return batch_norm(x, gamma, beta, running_mean, running_var, decay, eps, True, relu,
+                          r.materialize(), stats=stats)
+    return _BatchNormTrainDual.apply(x, gamma, beta, r.x, r.gamma, r.beta, running_mean,
+                                     running_var, r.rm, r.rv, decay, eps, r.decay, r.eps, relu,
+                                     stats, r.stats)
 
 
 def batch_norm(x, gamma: Optional[torch.Tensor], beta: torch.Tensor,

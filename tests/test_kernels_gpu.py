@@ -189,3 +189,50 @@ def test_fused_optimizer(cuda, kind):
     a, b = res["cpu"], res[str(cuda)]
     torch.testing.assert_close(b[0], a[0], rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(b[1], a[1], rtol=1e-2, atol=1e-2)
+
+
+def _epilogue_stats(x):
+    """[2][32][C] partial sums as a conv epilogue leaves them (slot 0 only)."""
+    from kf_benchmarks_amd.ops import conv_hip
+    C = x.shape[-1]
+    xf = x.float().reshape(-1, C)
+    st = torch.zeros(2, conv_hip.STATS_SPREAD, C, device=x.device)
+    st[0, 0] = xf.sum(0)
+    st[1, 0] = (xf * xf).sum(0)
+    return st.reshape(-1)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(4, 7, 7, 64), (2, 5, 6, 256)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_batch_norm_dual(cuda, dt, shape, relu):
+    """relu?(bn(x) + bn_r(xr)) in one apply pass (kfb_bn_fwd_train_dual,
+    DeferredBN) vs the fp32 reference of two BNs and the add."""
+    from kf_benchmarks_amd.ops import nn as KF
+    torch.manual_seed(2)
+    C = shape[-1]
+    x, xr = torch.randn(shape) * 2 + 0.5, torch.randn(shape) * 0.5 - 1
+    g0, b0, g1, b1 = torch.rand(C) + 0.5, torch.randn(C), torch.rand(C) + 0.5, torch.randn(C)
+    xa, xb = _pair(x, cuda, dt)
+    ra, rb = _pair(xr, cuda, dt)
+    pa = [t.clone().to(cuda).requires_grad_(True) for t in (g0, b0, g1, b1)]
+    pb = [t.clone().requires_grad_(True) for t in (g0, b0, g1, b1)]
+    rms = [torch.zeros(C, device=cuda), torch.ones(C, device=cuda),
+           torch.zeros(C, device=cuda), torch.ones(C, device=cuda)]
+    d = KF.DeferredBN(ra, pa[2], pa[3], rms[2], rms[3], 0.9, 1e-5, _epilogue_stats(ra.detach()))
+    ya = KF.batch_norm_dual(xa, pa[0], pa[1], rms[0], rms[1], 0.9, 1e-5, relu,
+                            _epilogue_stats(xa.detach()), d)
+    rm_b = [torch.zeros(C), torch.ones(C), torch.zeros(C), torch.ones(C)]
+    yr = F.batch_norm(rb, pb[2], pb[3], rm_b[2], rm_b[3], 0.9, 1e-5, True, False)
+    yb = F.batch_norm(xb, pb[0], pb[1], rm_b[0], rm_b[1], 0.9, 1e-5, True, relu, yr)
+    t = dict(rtol=2e-2, atol=2e-2) if dt == torch.bfloat16 else dict(rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(ya.float().cpu(), yb, rtol=t["rtol"] * 2, atol=t["atol"] * 2)
+    for a, b in zip(rms, rm_b):
+        torch.testing.assert_close(a.cpu(), b, rtol=1e-3, atol=1e-3)
+    dy = torch.randn(shape).to(dt).float()
+    ya.backward(dy.to(cuda, dt))
+    yb.backward(dy)
+    torch.testing.assert_close(xa.grad.float().cpu(), xb.grad, rtol=t["rtol"] * 4, atol=t["atol"] * 4)
+    torch.testing.assert_close(ra.grad.float().cpu(), rb.grad, rtol=t["rtol"] * 4, atol=t["atol"] * 4)
+    for a, b in zip(pa, pb):
+        torch.testing.assert_close(a.grad.cpu(), b.grad, rtol=5e-2, atol=0.5)

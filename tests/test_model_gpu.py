@@ -105,3 +105,26 @@ def test_scatter_dgrad_bn_fusion_matches(cuda, monkeypatch):
     vals = sorted(cos.values())
     print("scatter fusion cosines: min %.4f median %.4f" % (vals[0], vals[len(vals) // 2]))
     assert vals[len(vals) // 2] > 0.99 and vals[0] > 0.9, (vals[0], vals[len(vals) // 2])
+
+
+def test_deferred_shortcut_bn_network(cuda, monkeypatch):
+    """ResNet-50 v1 projection shortcuts take the deferred-BN path (the
+    shortcut BN applied inside the block-output BN's apply pass) on the GPU:
+    4 dual BNs, the same loss as the materialized path up to the bf16
+    rounding of the shortcut BN output, finite gradients for every variable
+    (numerics of the dual op: test_kernels_gpu.py::test_batch_norm_dual)."""
+    from kf_benchmarks_amd.models import builder
+    from kf_benchmarks_amd.ops import nn as F
+    calls = []
+    orig = F._BatchNormTrainDual.apply
+    monkeypatch.setattr(F._BatchNormTrainDual, "apply",
+                        lambda *a: calls.append(1) or orig(*a))
+    monkeypatch.setattr(builder, "_DEFER_BN", True)
+    loss_new, new = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
+    assert len(calls) == 4
+    monkeypatch.setattr(builder, "_DEFER_BN", False)
+    loss_old, old = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
+    assert len(calls) == 4
+    assert set(new) == set(old)
+    assert abs(loss_new - loss_old) < 2e-2 * abs(loss_old), (loss_new, loss_old)
+    assert all(torch.isfinite(g).all() for g in new.values())
