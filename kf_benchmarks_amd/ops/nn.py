@@ -220,9 +220,11 @@ class _BatchNormTrain(torch.autograd.Function):
         return dx, dgamma, dbeta, dres, None, None, None, None, None, None
 
 
-def _bn_backward(x, y, gamma, st, dy, relu, has_res, link, res_link, gamma_p, beta_p):
+def _bn_backward(x, y, gamma, st, dy, relu, has_res, link, res_link, gamma_p, beta_p,
+                 alias_res=False):
     """BN backward (kfb_bn_bwd): returns (dx, dgamma, dbeta, dres); dgamma and
-    dbeta are None when they went straight into the flat gradient buffer."""
+    dbeta are None when they went straight into the flat gradient buffer.
+    ``alias_res``: the caller only reads dres, so it may be dy itself."""
     dy = dy.contiguous()
     C = x.shape[-1]
     rows = x.numel() // C
@@ -251,7 +253,7 @@ def _bn_backward(x, y, gamma, st, dy, relu, has_res, link, res_link, gamma_p, be
     res_fused = has_res and rl is not None and rl.fusable
     # the residual's gradient is dy' (masked dy): with a pre-masked dy it
     # is dy itself, no kernel write needed
-    dres = torch.empty_like(x) if has_res and not (pre and res_fused) else None
+    dres = torch.empty_like(x) if has_res and not (pre and (res_fused or alias_res)) else None
     N.call("kfb_bn_bwd", N.dt(x), dy.data_ptr(), N.ptr(y), x.data_ptr(), dx.data_ptr(),
            N.ptr(dres), rows, C, N.ptr(gamma), st[0].data_ptr(), st[1].data_ptr(),
            dgp, dbp, pdy.data_ptr(), pdyx.data_ptr(),
@@ -294,6 +296,10 @@ class DeferredBN:
                                      self.decay, self.eps, False, self.stats)
 
 
+# the dual BN backward hands a pre-masked dy to bn_r as is (no copy)
+_DUAL_ALIAS_RES = True
+
+
 class _BatchNormTrainDual(torch.autograd.Function):
     """y = relu?(bn(x) + bn_r(xr)), both BNs in training mode with conv-epilogue
     statistics (kfb_bn_fwd_train_dual: one apply pass over x and xr).  The
@@ -332,7 +338,8 @@ class _BatchNormTrainDual(torch.autograd.Function):
     def backward(ctx, dy):
         x, y, gamma, st, xr, gamma_r, st_r = ctx.saved_tensors
         gp, bp, gp_r, bp_r = ctx.params
-        dx, dg, db, g = _bn_backward(x, y, gamma, st, dy, ctx.relu, True, ctx.link, None, gp, bp)
+        dx, dg, db, g = _bn_backward(x, y, gamma, st, dy, ctx.relu, True, ctx.link, None, gp, bp,
+                                     alias_res=_DUAL_ALIAS_RES)
         dxr, dg_r, db_r, _ = _bn_backward(xr, None, gamma_r, st_r, g, False, False, None, None,
                                           gp_r, bp_r)
         return (dx, dg, db, dxr, dg_r, db_r) + (None,) * 11
