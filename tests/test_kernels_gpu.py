@@ -59,7 +59,11 @@ def test_batch_norm_train(cuda, dt, shape, relu, res):
     torch.testing.assert_close(ba.grad.cpu(), bb.grad, rtol=5e-2 if dt != torch.float32 else 1e-3,
                                atol=0.5 if dt != torch.float32 else 1e-3)
     if res:
-        torch.testing.assert_close(ra.grad.float().cpu(), rb.grad, **tol(dt))
+        # the residual gradient is dy masked by the kernel's own output: a
+        # y within bf16 rounding of 0 may fall on either side of the fp32 mask
+        exp = dy * (ya.detach().float().cpu() > 0) if relu else dy
+        torch.testing.assert_close(ra.grad.float().cpu(), exp, **tol(dt))
+        assert (ra.grad.float().cpu() - rb.grad).abs().gt(0.05).float().mean() < 1e-5
 
 
 @pytest.mark.parametrize("dt", DT)
