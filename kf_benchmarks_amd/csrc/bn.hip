@@ -112,25 +112,28 @@ bn_partial_stats_k(const T* __restrict__ x, long rows, int C, int cw, int tpr, i
   }
 }
 
-// Slab partials -> per-channel totals.  Block = 64 channels x 4 slab lanes,
-// each lane sums every 4th slab with 4 independent accumulators (the slab
-// loop is latency-bound otherwise), lanes combine through LDS.
+// Slab partials -> per-channel totals.  Block = 64 channels x FOLD_Y slab
+// lanes, each lane sums every FOLD_Y-th slab with 4 independent accumulators
+// (the fold is latency-bound: the 32 conv-epilogue slots take one round of
+// loads), lanes combine through LDS.
+constexpr int FOLD_Y = 16;  // slab lanes per channel (blockDim.y of the finalize kernels)
+
 __device__ __forceinline__ void fold_slabs(const float* __restrict__ pa,
                                            const float* __restrict__ pb, int nslab, int C,
                                            int c, double& sa, double& sb) {
-  __shared__ double red[2][4][64];
+  __shared__ double red[2][FOLD_Y][64];
   const int lane = threadIdx.y, cx = threadIdx.x;
   float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f};
   if (c < C) {
     int k = lane;
-    for (; k + 12 < nslab; k += 16) {
+    for (; k + 3 * FOLD_Y < nslab; k += 4 * FOLD_Y) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        a[u] += pa[(long)(k + 4 * u) * C + c];
-        b[u] += pb[(long)(k + 4 * u) * C + c];
+        a[u] += pa[(long)(k + FOLD_Y * u) * C + c];
+        b[u] += pb[(long)(k + FOLD_Y * u) * C + c];
       }
     }
-    for (; k < nslab; k += 4) {
+    for (; k < nslab; k += FOLD_Y) {
       a[0] += pa[(long)k * C + c];
       b[0] += pb[(long)k * C + c];
     }
@@ -138,11 +141,16 @@ __device__ __forceinline__ void fold_slabs(const float* __restrict__ pa,
   red[0][lane][cx] = (double)a[0] + a[1] + a[2] + a[3];
   red[1][lane][cx] = (double)b[0] + b[1] + b[2] + b[3];
   __syncthreads();
-  sa = red[0][0][cx] + red[0][1][cx] + red[0][2][cx] + red[0][3][cx];
-  sb = red[1][0][cx] + red[1][1][cx] + red[1][2][cx] + red[1][3][cx];
+  sa = 0.0;
+  sb = 0.0;
+#pragma unroll
+  for (int l = 0; l < FOLD_Y; ++l) {
+    sa += red[0][l][cx];
+    sb += red[1][l][cx];
+  }
 }
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(64 * FOLD_Y)
 bn_finalize_stats_k(const float* __restrict__ psum, const float* __restrict__ psq,
                     int nslab, int C, long rows, const float* __restrict__ gamma,
                     const float* __restrict__ beta, float decay, float eps,
@@ -281,7 +289,7 @@ bn_partial_grad_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __
 // dgamma = invstd * sum(dy'(x-mean)); dbeta = sum(dy').
 // dx = dy'*A + x*B + Cc  with A = g*invstd, B = -A*invstd^2*S2/n,
 // Cc = -A*S1/n - mean*B.
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(64 * FOLD_Y)
 bn_finalize_grad_k(const float* __restrict__ pdy, const float* __restrict__ pdyx,
                    int nslab, int C, long rows, const float* __restrict__ gamma,
                    const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -662,7 +670,7 @@ KFB_API hipError_t kfb_bn_fwd_train(int dtype, const void* x, const void* res, v
       if (!have_partials)  // else the producing conv's epilogue already summed y, y^2
         hipLaunchKernelGGL((bn_partial_stats_k<T, VV>), grid, dim3(BN_THREADS), lds, stream,
                            (const T*)x, rows, C, g.cw, g.tpr, g.rpi, slab_rows, psum, psq);
-      hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, 4), 0, stream, psum,
+      hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, psum,
                          psq, nslab, C, rows, gamma, beta, decay, eps, run_mean, run_var,
                          save_mean, save_invstd, scale, shift);
       const long nvec = rows * C / VV;
@@ -699,10 +707,10 @@ KFB_API hipError_t kfb_bn_fwd_train_dual(
     float* scale_r, float* shift_r, const float* psum_r, const float* psq_r, int nslab_r,
     int relu, hipStream_t stream) {
   const int V = vec_width(C);
-  hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, 4), 0, stream, psum_r,
+  hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, psum_r,
                      psq_r, nslab_r, C, rows, gamma_r, beta_r, decay_r, eps_r, run_mean_r,
                      run_var_r, save_mean_r, save_invstd_r, scale_r, shift_r);
-  hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, 4), 0, stream, psum,
+  hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, psum,
                      psq, nslab, C, rows, gamma, beta, decay, eps, run_mean, run_var, save_mean,
                      save_invstd, scale, shift);
   KFB_DISPATCH_DTYPE(dtype, T, {
@@ -782,7 +790,7 @@ KFB_API hipError_t kfb_bn_bwd(int dtype, const void* dy, const void* y, const vo
         hipLaunchKernelGGL((bn_partial_grad_k<T, VV, false>), grid, dim3(BN_THREADS), lds,
                            stream, (const T*)dy, (const T*)y, (const T*)x, save_mean, rows, C,
                            g.cw, g.tpr, g.rpi, slab_rows, pdy, pdyx);
-      hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, 4), 0, stream, pdy,
+      hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, pdy,
                          pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta,
                          coefA, coefB, coefC, accumulate);
       const long nvec = rows * C / VV;
@@ -813,7 +821,7 @@ KFB_API hipError_t kfb_bn_relu_maxpool_fwd(int dtype, const void* x, void* z, ui
   if (C % 8 || kh * kw > 255 || (long)N * H * W * C >= (1L << 31)) return hipErrorInvalidValue;
   const BPGeo g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
   const long rows = (long)N * H * W;
-  hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, 4), 0, stream, psum, psq,
+  hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, psum, psq,
                      nslab, C, rows, gamma, beta, decay, eps, run_mean, run_var, save_mean,
                      save_invstd, scale, shift);
   const long total = (long)N * OH * OW * (C / 8);
@@ -849,7 +857,7 @@ KFB_API hipError_t kfb_bn_relu_maxpool_bwd(int dtype, const void* dz, const void
       hipLaunchKernelGGL((bn_pool3s2_k<T, 0>), dim3(nslab), dim3(256), 0, stream, (const T*)dz,
                          (const T*)z, idx, (const T*)x, (T*)dx, g, OHo, OWo, save_mean, pdy, pdyx,
                          nullptr, nullptr, nullptr);
-      hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, 4), 0, stream, pdy,
+      hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, pdy,
                          pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta, coefA,
                          coefB, coefC, accumulate);
       hipLaunchKernelGGL((bn_pool3s2_k<T, 1>), dim3(stream_grid(total)), dim3(256), 0, stream,
@@ -865,7 +873,7 @@ KFB_API hipError_t kfb_bn_relu_maxpool_bwd(int dtype, const void* dz, const void
     hipLaunchKernelGGL((bn_pool_partial_grad_k<T, 8>), dim3(nslab, gg.nchunk), dim3(BN_THREADS),
                        lds, stream, (const T*)dz, (const T*)z, idx, (const T*)x, save_mean, g,
                        rows, gg.cw, gg.tpr, gg.rpi, slab_rows, pdy, pdyx);
-    hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, 4), 0, stream, pdy,
+    hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, pdy,
                        pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta, coefA,
                        coefB, coefC, accumulate);
     hipLaunchKernelGGL((bn_pool_bwd_apply_k<T, 8>), dim3(stream_grid(rows * C / 8)), dim3(256), 0,
