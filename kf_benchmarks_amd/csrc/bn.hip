@@ -341,6 +341,35 @@ bn_bwd_apply_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __res
   }
 }
 
+// Backward apply of y = relu(bn(x) + bn_r(xr)) with a pre-masked dy: both
+// input gradients from one read of dy (dx = dy*A + x*B + Cc, dxr likewise).
+template <typename T, int V>
+__global__ void __launch_bounds__(256)
+bn_bwd_apply2_k(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ xr,
+                T* __restrict__ dx, T* __restrict__ dxr, long nvec, int C,
+                const float* __restrict__ A, const float* __restrict__ B,
+                const float* __restrict__ Cc, const float* __restrict__ Ar,
+                const float* __restrict__ Br, const float* __restrict__ Cr) {
+  const unsigned cv = (unsigned)(C / V);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)nvec;
+       i += gridDim.x * blockDim.x) {
+    const long e = (long)i * V;
+    const int c = (int)(i % cv) * V;
+    float g[V], xv[V], rv[V];
+    load_vec<T, V>(dy + e, g);
+    load_vec<T, V>(x + e, xv);
+    load_vec<T, V>(xr + e, rv);
+    float o[V], orr[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      o[k] = g[k] * A[c + k] + xv[k] * B[c + k] + Cc[c + k];
+      orr[k] = g[k] * Ar[c + k] + rv[k] * Br[c + k] + Cr[c + k];
+    }
+    store_vec<T, V>(dx + e, o);
+    store_vec<T, V>(dxr + e, orr);
+  }
+}
+
 // --------------------------------------------- BN + ReLU + max-pool (stem)
 // The ResNet stem tail relu(bn(conv1)) -> maxpool 3x3/2 as one op
 // (tcb/models/resnet_model.py:306-312): the forward never materializes the
@@ -802,6 +831,43 @@ KFB_API hipError_t kfb_bn_bwd(int dtype, const void* dy, const void* y, const vo
         if (dres) launch_bwd_apply<T, VV, false, true>(gb, stream, dy, y, x, dx, dres, nvec, C, coefA, coefB, coefC);
         else launch_bwd_apply<T, VV, false, false>(gb, stream, dy, y, x, dx, dres, nvec, C, coefA, coefB, coefC);
       }
+    });
+  });
+  return hipGetLastError();
+}
+
+// Backward of y = relu(bn(x) + bn_r(xr)) (kfb_bn_fwd_train_dual) when dy
+// arrives ReLU-masked with bn's partial sums [nslab][C] already produced by
+// the consuming conv's dgrad epilogue: bn_r's partials (one pass over dy, xr),
+// both finalizes, and ONE apply pass writing dx and dxr.
+KFB_API hipError_t kfb_bn_bwd_dual(
+    int dtype, const void* dy, const void* x, const void* xr, void* dx, void* dxr, long rows,
+    int C, const float* gamma, const float* save_mean, const float* save_invstd, float* dgamma,
+    float* dbeta, const float* pdy, const float* pdyx, int nslab, float* coefA, float* coefB,
+    float* coefC, int accumulate, const float* gamma_r, const float* save_mean_r,
+    const float* save_invstd_r, float* dgamma_r, float* dbeta_r, float* pdy_r, float* pdyx_r,
+    int nslab_r, float* coefA_r, float* coefB_r, float* coefC_r, int accumulate_r,
+    hipStream_t stream) {
+  const int V = vec_width(C);
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    KFB_DISPATCH_VEC(V, VV, {
+      Geo g = make_geo<VV>(C);
+      const long slab_rows = (rows + nslab_r - 1) / nslab_r;
+      const size_t lds = 2 * (size_t)g.rpi * g.tpr * VV * sizeof(float);
+      hipLaunchKernelGGL((bn_partial_grad_k<T, VV, false>), dim3(nslab_r, g.nchunk),
+                         dim3(BN_THREADS), lds, stream, (const T*)dy, (const T*)nullptr,
+                         (const T*)xr, save_mean_r, rows, C, g.cw, g.tpr, g.rpi, slab_rows,
+                         pdy_r, pdyx_r);
+      hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,
+                         pdy, pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta,
+                         coefA, coefB, coefC, accumulate);
+      hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,
+                         pdy_r, pdyx_r, nslab_r, C, rows, gamma_r, save_mean_r, save_invstd_r,
+                         dgamma_r, dbeta_r, coefA_r, coefB_r, coefC_r, accumulate_r);
+      const long nvec = rows * C / VV;
+      hipLaunchKernelGGL((bn_bwd_apply2_k<T, VV>), dim3(stream_grid(nvec)), dim3(256), 0, stream,
+                         (const T*)dy, (const T*)x, (const T*)xr, (T*)dx, (T*)dxr, nvec, C, coefA,
+                         coefB, coefC, coefA_r, coefB_r, coefC_r);
     });
   });
   return hipGetLastError();

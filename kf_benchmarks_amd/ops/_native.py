@@ -36,6 +36,8 @@ _SIGS = {
     "kfb_bn_fwd_train": [I, P, P, P, L, I, P, P, F, F, P, P, P, P, P, P, P, P, I, I, I, P],
     "kfb_bn_fwd_train_dual": [I, P, P, P, L, I, P, P, F, F, P, P, P, P, P, P, P, P, I,
                               P, P, F, F, P, P, P, P, P, P, P, P, I, I, P],
+    "kfb_bn_bwd_dual": [I, P, P, P, P, P, L, I, P, P, P, P, P, P, P, I, P, P, P, I,
+                        P, P, P, P, P, P, P, I, P, P, P, I, P],
     "kfb_bn_fwd_infer": [I, P, P, P, L, I, P, P, P, P, F, P, P, I, P],
     "kfb_bn_bwd": [I, P, P, P, P, P, L, I, P, P, P, P, P, P, P, I, P, P, P, I, I, I, P],
     "kfb_opt_step": [I, P, P, P, P, P, I, P, L, F, F, F, F, F, F, F, F, F, I, P],

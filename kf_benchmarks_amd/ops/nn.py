@@ -220,6 +220,25 @@ class _BatchNormTrain(torch.autograd.Function):
         return dx, dgamma, dbeta, dres, None, None, None, None, None, None
 
 
+def _bn_grad_targets(gamma_p, beta_p, C, dev):
+    """Where a BN backward writes dgamma/dbeta: straight into the flat
+    gradient buffer (direct) or a fresh [2, C] tensor (dparams)."""
+    gsink, bsink = _grad_sink(gamma_p), _grad_sink(beta_p)
+    direct = bsink is not None and (gamma_p is None or gsink is not None) and _conv.FUSE_BN
+    if direct:
+        return True, N.ptr(gsink), bsink.data_ptr(), None
+    dparams = torch.empty((2, C), dtype=torch.float32, device=dev)
+    return False, dparams[0].data_ptr(), dparams[1].data_ptr(), dparams
+
+
+def _bn_grad_result(direct, dparams, gamma_p, beta_p):
+    if direct:
+        _grad_ready(gamma_p)
+        _grad_ready(beta_p)
+        return None, None
+    return (dparams[0] if gamma_p is not None else None), dparams[1]
+
+
 def _bn_backward(x, y, gamma, st, dy, relu, has_res, link, res_link, gamma_p, beta_p,
                  alias_res=False):
     """BN backward (kfb_bn_bwd): returns (dx, dgamma, dbeta, dres); dgamma and
@@ -241,13 +260,7 @@ def _bn_backward(x, y, gamma, st, dy, relu, has_res, link, res_link, gamma_p, be
         ws = torch.empty((2 * nslab * C + 3 * C,), dtype=torch.float32, device=dev)
         pdy, pdyx = ws[:nslab * C], ws[nslab * C:2 * nslab * C]
         coef = ws[2 * nslab * C:]
-    gsink, bsink = _grad_sink(gamma_p), _grad_sink(beta_p)
-    direct = bsink is not None and (gamma_p is None or gsink is not None) and _conv.FUSE_BN
-    if direct:
-        dgp, dbp = N.ptr(gsink), bsink.data_ptr()
-    else:
-        dparams = torch.empty((2, C), dtype=torch.float32, device=dev)
-        dgp, dbp = dparams[0].data_ptr(), dparams[1].data_ptr()
+    direct, dgp, dbp, dparams = _bn_grad_targets(gamma_p, beta_p, C, dev)
     dx = torch.empty_like(x)
     rl = res_link
     res_fused = has_res and rl is not None and rl.fusable
@@ -270,12 +283,8 @@ def _bn_backward(x, y, gamma, st, dy, relu, has_res, link, res_link, gamma_p, be
         else:
             rl.deposit(dres, owned=dres is not dy)
             dres = None
-    if direct:
-        _grad_ready(gamma_p)
-        _grad_ready(beta_p)
-        return dx, None, None, dres
-    dgamma = dparams[0] if gamma_p is not None else None
-    return dx, dgamma, dparams[1], dres
+    dgamma, dbeta = _bn_grad_result(direct, dparams, gamma_p, beta_p)
+    return dx, dgamma, dbeta, dres
 
 
 class DeferredBN:
@@ -298,6 +307,9 @@ class DeferredBN:
 
 # the dual BN backward hands a pre-masked dy to bn_r as is (no copy)
 _DUAL_ALIAS_RES = True
+# ... and with a pre-masked dy runs both BN backwards with one apply pass
+# (kfb_bn_bwd_dual; KFB_DUAL_BN_BWD=0: two separate BN backwards)
+_DUAL_BWD_FUSE = os.environ.get("KFB_DUAL_BN_BWD", "1") != "0"
 
 
 class _BatchNormTrainDual(torch.autograd.Function):
@@ -338,6 +350,33 @@ class _BatchNormTrainDual(torch.autograd.Function):
     def backward(ctx, dy):
         x, y, gamma, st, xr, gamma_r, st_r = ctx.saved_tensors
         gp, bp, gp_r, bp_r = ctx.params
+        link = ctx.link
+        if _DUAL_BWD_FUSE and link is not None and link.partials is not None:
+            dy = dy.contiguous()
+            C = x.shape[-1]
+            rows = x.numel() // C
+            dev = x.device
+            parts = link.partials
+            link.partials = None
+            nslab = parts.numel() // (2 * C)
+            nslab_r = N.query("kfb_bn_num_slabs", rows, C)
+            ws = torch.empty((2 * nslab_r * C + 6 * C,), dtype=torch.float32, device=dev)
+            pr = ws[:2 * nslab_r * C]
+            coef = ws[2 * nslab_r * C:].view(6, C)
+            t, tr = _bn_grad_targets(gp, bp, C, dev), _bn_grad_targets(gp_r, bp_r, C, dev)
+            dx, dxr = torch.empty_like(x), torch.empty_like(xr)
+            N.call("kfb_bn_bwd_dual", N.dt(x), dy.data_ptr(), x.data_ptr(), xr.data_ptr(),
+                   dx.data_ptr(), dxr.data_ptr(), rows, C, N.ptr(gamma), st[0].data_ptr(),
+                   st[1].data_ptr(), t[1], t[2], parts[:nslab * C].data_ptr(),
+                   parts[nslab * C:].data_ptr(), nslab, coef[0].data_ptr(),
+                   coef[1].data_ptr(), coef[2].data_ptr(), int(t[0]), N.ptr(gamma_r),
+                   st_r[0].data_ptr(), st_r[1].data_ptr(), tr[1], tr[2],
+                   pr[:nslab_r * C].data_ptr(), pr[nslab_r * C:].data_ptr(), nslab_r,
+                   coef[3].data_ptr(), coef[4].data_ptr(), coef[5].data_ptr(), int(tr[0]),
+                   N.stream(dev))
+            dg, db = _bn_grad_result(t[0], t[3], gp, bp)
+            dg_r, db_r = _bn_grad_result(tr[0], tr[3], gp_r, bp_r)
+            return (dx, dg, db, dxr, dg_r, db_r) + (None,) * 11
         dx, dg, db, g = _bn_backward(x, y, gamma, st, dy, ctx.relu, True, ctx.link, None, gp, bp,
                                      alias_res=_DUAL_ALIAS_RES)
         dxr, dg_r, db_r, _ = _bn_backward(xr, None, gamma_r, st_r, g, False, False, None, None,

@@ -130,11 +130,13 @@ def test_deferred_shortcut_bn_network(cuda, monkeypatch):
     assert all(torch.isfinite(g).all() for g in new.values())
     # (bf16 ResNet-50 gradients are chaotic under a forward rounding change,
     # see FP32_MODELS above, so the backward is pinned with the forward fixed:)
-    # handing the pre-masked dy to the shortcut BN as is == writing a copy
+    # the fused dual backward (one apply pass; kfb_bn_bwd_dual) == two
+    # separate BN backwards with the masked dy written out as a copy
     monkeypatch.setattr(builder, "_DEFER_BN", True)
     monkeypatch.setattr(F, "_DUAL_ALIAS_RES", False)
+    monkeypatch.setattr(F, "_DUAL_BWD_FUSE", False)
     loss_copy, copy = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
     assert loss_copy == loss_new
     cos = sorted(_cos(new[k], ref) for k, ref in copy.items() if ref.norm() > 0)
-    print("alias vs copy cosines: min %.4f median %.4f" % (cos[0], cos[len(cos) // 2]))
+    print("fused vs separate dual-BN backward cosines: min %.4f median %.4f" % (cos[0], cos[len(cos) // 2]))
     assert cos[len(cos) // 2] > 0.99 and cos[0] > 0.9, (cos[0], cos[len(cos) // 2])
