@@ -320,8 +320,13 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
 // instead of 2; for the short-K layers (K = 64..128, e.g. the 56x56 1x1
 // convs, one or two K steps) the kernel is latency/epilogue bound and the
 // doubled occupancy is what hides it.
+//
+// 64 x 64 tiles (NBUF = 1): <= 96 VGPRs and 16 KB of LDS staging for 5
+// workgroups (20 waves) per CU - more loads and stores in flight per CU, for
+// the short-K, write-heavy layers (e.g. 1x1 convs with K = 64).
 template <typename T, int BM, int BN, bool TRANS, bool FAST, int NBUF = 2>
-__global__ void __launch_bounds__(256, NBUF == 1 ? 4 : 2) igemm_k(IgArgs a) {
+__global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : (NBUF == 1 ? 4 : 2))
+    igemm_k(IgArgs a) {
   constexpr int XC = BM / 32;  // 16-byte X chunks per thread per K step
   constexpr int WC = BN / 32;  // 16-byte W chunks per thread per K step
   constexpr int TM = BM / 32;  // 16-wide pixel subtiles per wave
@@ -1083,8 +1088,10 @@ using namespace kfb;
 //   IG_ALGO_ONEBUF(_N64): FAST igemm_k with one LDS stage (4 workgroups/CU).
 //   IG_ALGO_TALL512 / TALL256: igemm_glds_k with 64-channel tiles and 64x64
 //   wave tiles (twice the MFMAs per fragment read of the 256x64 8-wave tile).
+//   IG_ALGO_SMALL: FAST igemm_k with 64x64 tiles, one LDS stage, 5 workgroups/CU.
 enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_GLDS_N64 = 4,
-       IG_ALGO_ONEBUF = 5, IG_ALGO_ONEBUF_N64 = 6, IG_ALGO_TALL512 = 7, IG_ALGO_TALL256 = 8 };
+       IG_ALGO_ONEBUF = 5, IG_ALGO_ONEBUF_N64 = 6, IG_ALGO_TALL512 = 7, IG_ALGO_TALL256 = 8,
+       IG_ALGO_SMALL = 9 };
 
 KFB_API int kfb_conv_igemm_fast(int C, int KH, int KW, int trans) {
   return !trans && C % IG_BK == 0 && KH * KW <= 64 && !igemm_fast_disabled();
@@ -1114,6 +1121,12 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
   if ((algo == IG_ALGO_TALL512 || algo == IG_ALGO_TALL256) && fast) {
     if (dtype == BF16) launch_glds_tall<bf16>(a, algo == IG_ALGO_TALL512, stream);
     else if (dtype == F16) launch_glds_tall<f16>(a, algo == IG_ALGO_TALL512, stream);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
+  if (algo == IG_ALGO_SMALL && fast) {
+    if (dtype == BF16) launch_ig<bf16, 64, 64>(a, false, true, stream, true);
+    else if (dtype == F16) launch_ig<f16, 64, 64>(a, false, true, stream, true);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }

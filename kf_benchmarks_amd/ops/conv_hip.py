@@ -27,10 +27,10 @@ N.register_optional("kfb_conv_igemm_fast", [N.I] * 4, N.c_int)
 # igemm kernel choice (csrc/conv_igemm.hip): 1 = register-staged 128-tile
 # igemm_k, 2 = LDS-DMA ring igemm_glds_k (FAST geometries only).
 IG_CLASSIC, IG_GLDS, IG_CLASSIC_N64, IG_GLDS_N64, IG_ONEBUF, IG_ONEBUF_N64 = 1, 2, 3, 4, 5, 6
-IG_TALL512, IG_TALL256 = 7, 8
+IG_TALL512, IG_TALL256, IG_SMALL = 7, 8, 9
 IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N64,
             "glds_n64": IG_GLDS_N64, "onebuf": IG_ONEBUF, "onebuf_n64": IG_ONEBUF_N64,
-            "tall512": IG_TALL512, "tall256": IG_TALL256}
+            "tall512": IG_TALL512, "tall256": IG_TALL256, "small": IG_SMALL}
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 N.register_optional("kfb_conv_stats_spread", [], N.c_int)
@@ -133,7 +133,7 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None)):
     C, KH, KW, ncol, trans = geo[3], geo[6], geo[7], geo[12], geo[17]
     fast = N.load().kfb_conv_igemm_fast(C, KH, KW, trans)
     # (IG_TALL512 is never the fastest on the ResNet-50 shapes: force-only)
-    cands = (IG_CLASSIC, IG_GLDS, IG_ONEBUF, IG_TALL256) if fast else (IG_CLASSIC,)
+    cands = (IG_CLASSIC, IG_GLDS, IG_ONEBUF, IG_TALL256, IG_SMALL) if fast else (IG_CLASSIC,)
     if ncol > 64:  # 64-wide tiles: more workgroups for small-M layers
         cands += (IG_CLASSIC_N64, IG_GLDS_N64, IG_ONEBUF_N64) if fast else (IG_CLASSIC_N64,)
     if len(cands) == 1:
