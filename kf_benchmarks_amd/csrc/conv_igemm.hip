@@ -66,8 +66,11 @@ struct IgArgs {
   //   stats != null, xbn != null  : BN backward partials of the *producer* BN
   //       of this conv's input: y' = y * (mask > 0) (mask may be null = no
   //       ReLU), stats[slot][0][n] += sum y', stats[slot][1][n] += sum y'(xbn - mean)
-  //   layout [2][IG_SPREAD][Ncol]; slot = workgroup % IG_SPREAD (spreads the
-  //   atomics over 32 copies; the BN finalize folds the 32 slots).
+  //   layout [2][IG_SPREAD][Ncol]; slot = pixel-tile index % IG_SPREAD (spreads
+  //   the atomics over 32 copies; the BN finalize folds the 32 slots).  Keyed
+  //   by the pixel tile, not the workgroup: the pixel tiles of one channel
+  //   tile land in distinct slots, so with <= 32 pixel tiles every slot takes
+  //   one add and the statistics are bitwise run-to-run deterministic.
   float* stats;
   const void* mask;
   const void* xbn;
@@ -301,7 +304,7 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
       for (int r = 0; r < RG; ++r) acc2 += red[(r * CPR + c) * 16 + k];
       const int n = n0 + c * 8 + (k & 7);
       if (n < a.Ncol) {
-        float* dst = a.stats + ((long)(k >> 3) * IG_SPREAD + blockIdx.x % IG_SPREAD) * a.Ncol + n;
+        float* dst = a.stats + ((long)(k >> 3) * IG_SPREAD + (m0 / BM) % IG_SPREAD) * a.Ncol + n;
         atomicAdd(dst, acc2);
       }
     }

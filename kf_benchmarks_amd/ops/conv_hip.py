@@ -33,6 +33,7 @@ IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N6
             "tall512": IG_TALL512, "tall256": IG_TALL256, "small": IG_SMALL}
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
+_NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
 N.register_optional("kfb_conv_stats_spread", [], N.c_int)
 N.register_optional("kfb_conv_wgrad", [N.I, N.P, N.P, N.P] + [N.I] * 12 + [N.I, N.I, N.P, N.L, N.P])
 N.register_optional("kfb_conv_wgrad_splits", [N.I] * 8, N.c_int)
@@ -133,7 +134,9 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None)):
     C, KH, KW, ncol, trans = geo[3], geo[6], geo[7], geo[12], geo[17]
     fast = N.load().kfb_conv_igemm_fast(C, KH, KW, trans)
     # (IG_TALL512 is never the fastest on the ResNet-50 shapes: force-only)
-    cands = (IG_CLASSIC, IG_GLDS, IG_ONEBUF, IG_TALL256, IG_SMALL) if fast else (IG_CLASSIC,)
+    cands = (IG_CLASSIC, IG_GLDS, IG_ONEBUF, IG_TALL256) if fast else (IG_CLASSIC,)
+    if fast and not _NO_SMALL:
+        cands += (IG_SMALL,)
     if ncol > 64:  # 64-wide tiles: more workgroups for small-M layers
         cands += (IG_CLASSIC_N64, IG_GLDS_N64, IG_ONEBUF_N64) if fast else (IG_CLASSIC_N64,)
     if len(cands) == 1:
