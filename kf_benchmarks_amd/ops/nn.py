@@ -729,8 +729,15 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, wl = ctx.saved_tensors
-        dx = torch.mm(dy, wl.t())
-        dw = torch.mm(x.t(), dy).float()
+        # (the first affine of a net on raw images needs no input gradient)
+        dx = torch.mm(dy, wl.t()) if ctx.needs_input_grad[0] else None
+        if dy.shape[1] < 16:
+            # narrow outputs (the trivial model's affine(1)): x^T @ dy with
+            # N < 16 takes an ~11 ms host-side slow path in torch.mm here
+            # (scripts/probes/r2l_mm_shapes.py); (dy^T @ x)^T is one GEMM launch
+            dw = torch.mm(dy.t(), x).t().float()
+        else:
+            dw = torch.mm(x.t(), dy).float()
         db = dy.float().sum(0) if ctx.has_b else None
         return dx, dw, db, None
 

@@ -21,11 +21,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch_size", type=int, default=256)
     a = ap.parse_args()
     import torch
     from kf_benchmarks_amd import params as P
     from kf_benchmarks_amd.benchmark import BenchmarkCNN
-    p = P.make_params(model="resnet50", batch_size=256, num_gpus=1, use_bf16=True,
+    p = P.make_params(model=a.model, batch_size=a.batch_size, num_gpus=1, use_bf16=True,
                       optimizer="momentum", data_format="NHWC", variable_update="kungfu")
     bench = BenchmarkCNN(p)
     bench.build()

@@ -240,3 +240,29 @@ def test_batch_norm_dual(cuda, dt, shape, relu):
     torch.testing.assert_close(ra.grad.float().cpu(), rb.grad, rtol=t["rtol"] * 4, atol=t["atol"] * 4)
     for a, b in zip(pa, pb):
         torch.testing.assert_close(a.grad.cpu(), b.grad, rtol=5e-2, atol=0.5)
+
+
+@pytest.mark.parametrize("cin,cout,x_grad", [(4099, 1, False), (512, 1000, True), (300, 7, True)])
+def test_linear_fwd_bwd(cuda, cin, cout, x_grad):
+    """F.linear (+bias, ReLU) vs fp32 PyTorch, including the narrow-output
+    dW path (Cout < 16) and the no-input-gradient first layer."""
+    g = torch.Generator().manual_seed(cin + cout)
+    x = torch.randn(33, cin, generator=g)
+    w = torch.randn(cin, cout, generator=g) / cin ** 0.5
+    b = torch.randn(cout, generator=g)
+    dy = torch.randn(33, cout, generator=g)
+    xd = x.to(cuda, torch.bfloat16).requires_grad_(x_grad)
+    wd, bd = w.to(cuda).requires_grad_(), b.to(cuda).requires_grad_()
+    y = F.linear(xd, wd, bd, relu=True)
+    y.backward(dy.to(cuda, torch.bfloat16))
+    xr = x.to(torch.bfloat16).float().requires_grad_(x_grad)
+    wr, br = w.to(torch.bfloat16).float().requires_grad_(), b.clone().requires_grad_()
+    yl = xr @ wr + br
+    assert torch.allclose(y.float().cpu(), torch.relu(yl), atol=3e-2, rtol=2e-2)
+    # ReLU mask from the kernel's own output (bf16 ties at y ~ 0)
+    yl.backward(dy.to(torch.bfloat16).float() * (y.float().cpu() > 0))
+    for got, ref in ((wd.grad, wr.grad), (bd.grad, br.grad)) + (((xd.grad, xr.grad),) if x_grad else ()):
+        err = float((got.float().cpu() - ref).abs().max() / (ref.abs().max() + 1e-6))
+        assert err < 2e-2, err
+    if not x_grad:
+        assert xd.grad is None
