@@ -47,48 +47,76 @@ def main(argv=None):
     ap.add_argument("--reuse_synthetic", action="store_true",
                     help="generate the synthetic batch once (tf_cnn_benchmarks' gpu_cached_images) "
                          "instead of re-sampling it inside every timed step")
+    ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
+                    help="cpu: plumbing rehearsal of the same step over gloo (tests)")
+    ap.add_argument("--rccl_channels", type=int, default=0,
+                    help="pin the RCCL channel count (0: RCCL's choice)")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
+
+    from kf_benchmarks_amd.parallel import comm
+
+    world_env = comm.env_world_size()
+    if a.gpus > 1 and world_env == 1 and os.environ.get("KFB_BENCH_NO_SELF_LAUNCH") != "1":
+        # no external launcher: start the N ranks ourselves (children, before
+        # anything touches the GPU in this process) and forward rank 0's line
+        return _self_launch(a, argv)
+    if world_env != a.gpus:
+        print("bench.py: --gpus=%d but the launcher started %d ranks" % (a.gpus, world_env),
+              file=sys.stderr)
+        return 2
 
     import torch
     from kf_benchmarks_amd import params as P
     from kf_benchmarks_amd.benchmark import BenchmarkCNN
-    from kf_benchmarks_amd.parallel import comm
 
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    if world_env != a.gpus:
-        print("warning: --gpus=%d but WORLD_SIZE=%d" % (a.gpus, world_env), file=sys.stderr)
+    cuda = a.device == "gpu"
+    if cuda and torch.cuda.device_count() < a.gpus:
+        print("bench.py: --gpus=%d but only %d GPU(s) visible" % (a.gpus, torch.cuda.device_count()),
+              file=sys.stderr)
+        return 2
     data_name = a.data_name or {"ssd300": "coco", "deepspeech2": "librispeech"}.get(a.model)
     p = P.make_params(model=a.model, batch_size=a.batch_size, num_gpus=1, data_name=data_name,
                       variable_update=a.variable_update, kungfu_option=a.kungfu_option,
                       optimizer=a.optimizer, use_bf16=a.dtype == "bf16",
-                      use_fp16=a.dtype == "fp16", data_format="NHWC",
+                      use_fp16=a.dtype == "fp16", data_format="NHWC", device=a.device,
+                      rccl_channels=a.rccl_channels,
                       kernel_impl=a.kernel_impl, bucket_size_mb=a.bucket_size_mb,
                       gradient_wire_dtype=a.wire_dtype, display_every=10**9,
                       synthetic_resample=not a.reuse_synthetic)
     bench = BenchmarkCNN(p)
     bench.build()
     world = comm.get_world()
+    if world.size != a.gpus:
+        print("bench.py: --gpus=%d but the world has %d ranks" % (a.gpus, world.size),
+              file=sys.stderr)
+        return 2
     dev = bench.device
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize(dev)
+
     bench.strategy.broadcast_initial_model(bench.optimizer.slot_tensors().values())
 
     t0 = time.time()
     for i in range(a.warmup):
         loss, _ = bench.train_step(need_loss=(i == a.warmup - 1))
-    torch.cuda.synchronize(dev)
+    sync()
     warm_loss = float(loss) if a.warmup > 0 else float("nan")
     if a.verbose and world.is_chief:
         print("warmup done in %.1fs, loss %.4f" % (time.time() - t0, warm_loss),
               file=sys.stderr)
 
-    world.barrier(dev)
-    torch.cuda.synchronize(dev)
+    bdev = dev if cuda else None
+    world.barrier(bdev)
+    sync()
     start = time.perf_counter()
     for _ in range(a.steps):
         loss, _ = bench.train_step()
-    torch.cuda.synchronize(dev)
-    world.barrier(dev)
-    torch.cuda.synchronize(dev)
+    sync()
+    world.barrier(bdev)
+    sync()
     elapsed = time.perf_counter() - start
     final_loss = float(loss)
 
@@ -114,6 +142,8 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": round(value / base, 3) if base else None,
             "dtype": a.dtype,
+            "ranks": world.size,
+            "backend": world.backend or "none",
             "data": ("synthetic (%dx%dx3 ImageNet-shaped images %s, random-init weights)"
                      % (bench.model.image_size, bench.model.image_size,
                         "generated once" if a.reuse_synthetic
@@ -132,7 +162,31 @@ def main(argv=None):
         print(json.dumps(out))
         sys.stdout.flush()
     world.shutdown()
+    return 0
+
+
+def _self_launch(a, argv) -> int:
+    """``bench.py --gpus N`` without a launcher: N ranks through kfb-run
+    (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* exported);
+    rank 0's output is echoed, the others go to per-rank logs."""
+    import subprocess
+    import tempfile
+    if a.device == "gpu":
+        import torch  # device_count() does not initialise the GPU on this image
+        n = torch.cuda.device_count()
+        if n < a.gpus:
+            print("bench.py: --gpus=%d but only %d GPU(s) visible" % (a.gpus, n), file=sys.stderr)
+            return 2
+    from kf_benchmarks_amd.parallel import launcher
+    root = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    logdir = tempfile.mkdtemp(prefix="kfb_bench_")
+    args = list(sys.argv[1:] if argv is None else argv)
+    cmd = [launcher.launcher_binary(), "-np", str(a.gpus), "-chief-only", "-logdir", logdir,
+           "--", sys.executable, os.path.abspath(__file__)] + args
+    return subprocess.call(cmd, env=env)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

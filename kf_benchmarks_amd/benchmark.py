@@ -276,7 +276,8 @@ class BenchmarkCNN:
                 self.benchmark_logger = None
                 return
             self.cluster_manager.setup_worker_env()
-        self.world = comm.init_world(self.device_type, params.all_reduce_spec)
+        self.world = comm.init_world(self.device_type, params.all_reduce_spec,
+                                     channels=params.rccl_channels)
         self.tower_mode = (os.environ.get("KFB_TOWER_GROUP") == "1" and self.num_gpus > 1
                            and self.world.size == self.num_gpus)
         self.task_index = self.world.rank
@@ -483,17 +484,21 @@ class BenchmarkCNN:
             skip = self._auto_loss_scale_check()
         if not skip:
             self.strategy.before_update(step)
-            wd = (p.weight_decay or 0.0) * self._l2_multiplier()
-            if self.strategy.update_is_empty:
-                wd = 0.0
-            if wd and self.l2_mask is not None:
-                # model-specific L2 subset (custom_l2_loss, e.g. SSD without
-                # batch-norm variables): add wd * w on the masked elements
-                # before the gradient scale the optimizer applies
-                self.flat.grad.addcmul_(self.l2_mask, self.flat.flat, value=wd / grad_scale)
-                wd = 0.0
-            self.optimizer.step(self.learning_rate(step), grad_scale=grad_scale,
-                                weight_decay=wd, clip=p.gradient_clip)
+            try:
+                wd = (p.weight_decay or 0.0) * self._l2_multiplier()
+                if self.strategy.update_is_empty:
+                    wd = 0.0
+                if wd and self.l2_mask is not None:
+                    # model-specific L2 subset (custom_l2_loss, e.g. SSD without
+                    # batch-norm variables): add wd * w on the masked elements
+                    # before the gradient scale the optimizer applies
+                    self.flat.grad.addcmul_(self.l2_mask, self.flat.flat, value=wd / grad_scale)
+                    wd = 0.0
+                self.optimizer.step(self.learning_rate(step), grad_scale=grad_scale,
+                                    weight_decay=wd, clip=p.gradient_clip)
+            except BaseException:
+                self.strategy.abort_update(step)
+                raise
             self.strategy.after_update(step)
         self.global_step += 1
         return loss, acc

@@ -93,6 +93,24 @@ bool port_free(int port) {
   return ok;
 }
 
+// An ephemeral port from the kernel (bind to port 0): concurrent launches
+// on one host never pick the same rendezvous port, unlike a scan upward
+// from the peer ports.
+int ephemeral_port() {
+  int s = socket(AF_INET, SOCK_STREAM, 0);
+  if (s < 0) return -1;
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = 0;
+  a.sin_addr.s_addr = inet_addr("127.0.0.1");
+  int port = -1;
+  socklen_t len = sizeof(a);
+  if (bind(s, (sockaddr*)&a, sizeof(a)) == 0 && getsockname(s, (sockaddr*)&a, &len) == 0)
+    port = ntohs(a.sin_port);
+  close(s);
+  return port;
+}
+
 bool g_chief_only = false;  // -chief-only: echo rank 0 verbatim, others to logs only
 
 void emit(Peer& p, Stream& s, const std::string& line, bool quiet, int color) {
@@ -223,6 +241,7 @@ int main(int argc, char** argv) {
     fprintf(stderr, "kfb-run: not enough free ports in %d-%d\n", port_lo, port_hi);
     return 2;
   }
+  if (master_port < 0) master_port = ephemeral_port();
   if (master_port < 0) {
     for (int p = ports.back() + 1; p < 65535; ++p)
       if (port_free(p)) {

@@ -76,11 +76,16 @@ class _SharedState:
         self._step_f = open(self.step_path, "r+b")
         self._step_m = mmap.mmap(self._step_f.fileno(), 64)
 
+    held = False
+
     def lock(self):
         fcntl.flock(self._lock_f, fcntl.LOCK_EX)
+        self.held = True
 
     def unlock(self):
-        fcntl.flock(self._lock_f, fcntl.LOCK_UN)
+        if self.held:
+            self.held = False
+            fcntl.flock(self._lock_f, fcntl.LOCK_UN)
 
     @property
     def global_step(self) -> int:
@@ -90,6 +95,7 @@ class _SharedState:
         struct.pack_into("<q", self._step_m, 0, self.global_step + 1)
 
     def close(self):
+        self.unlock()  # never leave the PS lock to a closed file
         self._step_m.close()
         self._step_f.close()
         self._lock_f.close()
@@ -134,6 +140,12 @@ class AsyncParameterServer(Strategy):
             torch.cuda.current_stream(self._local[0].device).synchronize()
         self.state.bump_step()
         self.state.unlock()
+
+    def abort_update(self, step):
+        """The update failed between before_update and after_update: release
+        the PS lock so the other workers do not block forever."""
+        if self.state is not None:
+            self.state.unlock()
 
     def close(self):
         if self.state is not None:

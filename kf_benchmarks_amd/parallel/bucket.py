@@ -81,6 +81,10 @@ class BucketReducer:
         self._works = []
         self._active = False
         self.overlap = overlap
+        # persistent wire-dtype staging (one per in-flight step: relaxed mode
+        # has the previous step's reduction outstanding while it launches)
+        self._wire = [None, None]
+        self.launch_count = 0  # collectives issued (tests, all_reduce_benchmark)
         self._handles = []
         if overlap:
             for _, p, _, _ in segs:
@@ -127,10 +131,19 @@ class BucketReducer:
             from ..ops.conv_hip import join_wgrad_stream
             join_wgrad_stream(self.flat.grad.device)
         s, e = self.buckets[b]
-        view = (self.flat.grad if src is None else src)[s:e]
-        buf = view.to(self.wire_dtype) if self.wire_dtype is not None else view
+        g = self.flat.grad if src is None else src
+        view = g[s:e]
+        if self.wire_dtype is not None:
+            k = self._relaxed_step % 2 if self.relaxed else 0
+            if self._wire[k] is None or self._wire[k].device != g.device:
+                self._wire[k] = torch.empty(g.numel(), dtype=self.wire_dtype, device=g.device)
+            buf = self._wire[k][s:e]
+            buf.copy_(view)
+        else:
+            buf = view
         pieces = torch.tensor_split(buf, self.shards) if self.shards > 1 else (buf,)
         for piece in pieces:
+            self.launch_count += 1
             work = comm.all_reduce(piece, op=self.op, async_op=True)
             self._works.append((work, None, None))
         self._works[-1] = (self._works[-1][0], buf, view)

@@ -20,16 +20,25 @@ import torch.distributed as dist
 
 
 class World:
-    def __init__(self, rank=0, size=1, local_rank=0, backend=None, initialized_here=False):
+    def __init__(self, rank=0, size=1, local_rank=0, backend=None, initialized_here=False,
+                 has_pg=None):
         self.rank = rank
         self.size = size
         self.local_rank = local_rank
         self.backend = backend
         self.initialized_here = initialized_here
+        # a process group exists (always for size > 1; at size 1 only with
+        # KFB_FORCE_PG=1, so the 1-GPU run exercises the real RCCL path)
+        self.has_pg = (size > 1) if has_pg is None else bool(has_pg)
 
     @property
     def distributed(self) -> bool:
         return self.size > 1
+
+    @property
+    def communicates(self) -> bool:
+        """Collectives are issued (size > 1, or a forced 1-rank group)."""
+        return self.has_pg
 
     @property
     def is_chief(self) -> bool:
@@ -39,7 +48,7 @@ class World:
         """All ranks block until all arrive (kungfu.run_barrier,
         tcb/tf_cnn_benchmarks.py:58-60).  On RCCL this is a 1-element
         all-reduce on the device, then a host wait."""
-        if not self.distributed:
+        if not self.has_pg:
             return
         if self.backend == "nccl" and device is not None:
             t = torch.zeros(1, device=device)
@@ -56,30 +65,84 @@ class World:
 _WORLD: Optional[World] = None
 
 
+def _env_int(names, default):
+    for n in names:
+        v = os.environ.get(n)
+        if v not in (None, ""):
+            return int(v)
+    return default
+
+
 def env_world_size() -> int:
-    return int(os.environ.get("WORLD_SIZE", "1"))
+    """WORLD_SIZE (torch.distributed.run / kfb-run), else the OpenMPI
+    variables that ``mpirun -np N`` exports (Horovod launch,
+    tcb/run_hv.sh:15-18, tcb/README.md:107-115)."""
+    return _env_int(("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE"), 1)
+
+
+def env_rank() -> int:
+    return _env_int(("RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK"), 0)
+
+
+def env_local_rank() -> int:
+    return _env_int(("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID"), env_rank())
+
+
+def force_pg() -> bool:
+    return os.environ.get("KFB_FORCE_PG") == "1"
+
+
+def _pg_options(backend: str):
+    """RCCL communicator options: the collective stream gets high priority
+    so bucket all-reduces are scheduled ahead of the compute kernels queued
+    beside them (SURVEY 2.4 / 7.4 #3).  KFB_RCCL_LOW_PRIORITY=1 opts out."""
+    if backend != "nccl" or os.environ.get("KFB_RCCL_LOW_PRIORITY") == "1":
+        return None
+    try:
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        return opts
+    except (AttributeError, RuntimeError):
+        return None
+
+
+def rccl_channel_env(channels: Optional[int]) -> dict:
+    """``--rccl_channels`` / KFB_RCCL_NCHANNELS: pin the RCCL channel count
+    (each channel is one ring over the xGMI links)."""
+    if not channels:
+        v = os.environ.get("KFB_RCCL_NCHANNELS")
+        channels = int(v) if v else 0
+    if not channels:
+        return {}
+    return {"NCCL_MIN_NCHANNELS": str(channels), "NCCL_MAX_NCHANNELS": str(channels)}
 
 
 def init_world(device_type: str = "cuda", all_reduce_spec: Optional[str] = None,
-               timeout_s: int = 1800) -> World:
+               timeout_s: int = 1800, channels: Optional[int] = None) -> World:
     """Initializes the default process group once (idempotent).
     ``all_reduce_spec`` picks RCCL's algorithm / channel count before the
-    communicator exists (parallel/allreduce.py:rccl_env_for_spec)."""
+    communicator exists (parallel/allreduce.py:rccl_env_for_spec).  At world
+    size 1 no group is created unless KFB_FORCE_PG=1."""
     global _WORLD
     if _WORLD is not None:
         return _WORLD
     size = env_world_size()
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
-    if size <= 1:
+    rank = env_rank()
+    local_rank = env_local_rank()
+    if size <= 1 and not force_pg():
         _WORLD = World(0, 1, local_rank, None)
         return _WORLD
+    if size <= 1:
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
     # KFB_DIST_BACKEND=gloo: ranks that share one GPU (RCCL refuses two ranks
     # on one device) - the 2-rank GPU rehearsal on a 1-GPU box
     backend = os.environ.get("KFB_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
-    if backend == "nccl" and all_reduce_spec:
-        from .allreduce import rccl_env_for_spec
-        for k, v in rccl_env_for_spec(all_reduce_spec).items():
+    if backend == "nccl":
+        env = dict(rccl_channel_env(channels))
+        if all_reduce_spec:
+            from .allreduce import rccl_env_for_spec
+            env.update(rccl_env_for_spec(all_reduce_spec))
+        for k, v in env.items():
             os.environ.setdefault(k, v)
     here = False
     if not dist.is_initialized():
@@ -88,10 +151,20 @@ def init_world(device_type: str = "cuda", all_reduce_spec: Optional[str] = None,
                       timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kwargs["device_id"] = torch.device("cuda", local_rank)
+            opts = _pg_options(backend)
+            if opts is not None:
+                kwargs["pg_options"] = opts
         dist.init_process_group(**kwargs)
         here = True
-    _WORLD = World(rank, size, local_rank, dist.get_backend(), here)
+    _WORLD = World(rank, size, local_rank, dist.get_backend(), here, has_pg=True)
     return _WORLD
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def get_world() -> World:
@@ -105,20 +178,20 @@ def reset_world():
 
 
 def all_reduce(t: torch.Tensor, op: str = "sum", async_op: bool = False):
-    if get_world().size <= 1:
+    if not get_world().has_pg:
         return None
     rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
     return dist.all_reduce(t, op=rop, async_op=async_op)
 
 
 def broadcast(t: torch.Tensor, src: int = 0, async_op: bool = False):
-    if get_world().size <= 1:
+    if not get_world().has_pg:
         return None
     return dist.broadcast(t, src=src, async_op=async_op)
 
 
 def all_gather_object(obj):
-    if get_world().size <= 1:
+    if not get_world().has_pg:
         return [obj]
     out = [None] * get_world().size
     dist.all_gather_object(out, obj)

@@ -10,17 +10,25 @@ spec in SURVEY.md Appendix A): every step each worker
   5. publishes its updated model for others.
 There is no global barrier per step.
 
-Model store: each rank owns a double-buffered model snapshot plus a version
-counter.  Publishing writes the slot the readers are NOT pointed at, then
-bumps the version (host shared memory, release ordering).  Readers copy the
-slot of the version they observed and re-check the version afterwards
-(retry on a concurrent double publish), so a pulled model is never torn.
+Model store: each rank owns two model slots plus a per-slot seqlock in a
+small /dev/shm header ``[seq0, seq1, latest]`` (int64 words, mapped by every
+rank).  Publish: pick the slot ``latest`` does NOT point at, make its
+sequence word odd (write in progress), copy the model into it, and once the
+copy has completed make the word even again and point ``latest`` at it.  A
+reader reads ``latest`` and that slot's (even) sequence word, copies the
+slot, and accepts the copy only if the word is unchanged afterwards; any
+overlap with a rewrite of that slot changes it, so a torn model is never
+accepted.  Retries are bounded and exhausting them raises.
 
 * GPU ranks: the two slots live in device memory and are shared with every
   peer through HIP IPC (torch CUDA-tensor sharing over dmabuf), so a pull is
-  a device-to-device copy over xGMI that the owner never sees.
+  a device-to-device copy over xGMI that the owner never sees.  Nothing
+  blocks the host inside the step: the peer pull is issued on a side stream
+  at the start of the step (overlapping forward/backward) and checked at the
+  update; the publish copy is enqueued after the update and committed
+  (sequence word made even) as soon as its event has completed - at the
+  latest at the next publish.
 * CPU ranks (tests, plumbing config): the slots live in /dev/shm.
-The version words always live in a small /dev/shm file per rank.
 """
 
 from __future__ import annotations
@@ -30,6 +38,7 @@ import os
 import random
 import struct
 import uuid
+import warnings
 
 import numpy as np
 import torch
@@ -38,8 +47,10 @@ from . import comm
 from .variable_mgr import Strategy
 
 
-class _Versions:
-    """One int64 version word per rank in /dev/shm (mapped by every rank)."""
+class _Header:
+    """Per-rank seqlock header ``[seq0, seq1, latest]`` in /dev/shm."""
+
+    WORDS = 3
 
     def __init__(self, job, rank, size):
         self.paths = ["/dev/shm/kfb_ver_%s_%d" % (job, r) for r in range(size)]
@@ -54,35 +65,47 @@ class _Versions:
             self._maps[r] = (f, mmap.mmap(f.fileno(), 64))
         return self._maps[r][1]
 
-    def get(self, r) -> int:
-        return struct.unpack_from("<q", self._map(r), 0)[0]
+    def read(self, r, word) -> int:
+        return struct.unpack_from("<q", self._map(r), 8 * word)[0]
 
-    def set(self, v: int):
-        struct.pack_into("<q", self._map(self.rank), 0, v)
+    def write(self, word, v: int):
+        # aligned 8-byte stores; x86-64 keeps store order, so a reader that
+        # sees the new ``latest`` also sees the sequence word written before it
+        struct.pack_into("<q", self._map(self.rank), 8 * word, v)
 
     def close(self):
         for f, m in self._maps.values():
             m.close()
             f.close()
+        self._maps = {}
         try:
             os.remove(self.paths[self.rank])
         except OSError:
             pass
 
 
+class TornReadError(RuntimeError):
+    pass
+
+
 class ModelStore:
+    SEQ0, SEQ1, LATEST = 0, 1, 2
+    MAX_TRIES = 64
+
     def __init__(self, flat: torch.Tensor, world: comm.World):
         self.world = world
         self.rank, self.size = world.rank, world.size
         job = comm.all_gather_object(uuid.uuid4().hex[:12] if world.rank == 0 else None)[0]
-        self.versions = _Versions(job, self.rank, self.size)
+        self.hdr = _Header(job, self.rank, self.size)
         n = flat.numel()
         self.n = n
         self.device = flat.device
-        if flat.is_cuda:
+        self.cuda = flat.is_cuda
+        if self.cuda:
             self.slots = torch.empty((2, n), dtype=flat.dtype, device=flat.device)
             self.slots[0].copy_(flat)
             self.slots[1].copy_(flat)
+            torch.cuda.synchronize(flat.device)
             from torch.multiprocessing.reductions import reduce_tensor
             handle = reduce_tensor(self.slots)
             handles = comm.all_gather_object(handle)
@@ -90,7 +113,7 @@ class ModelStore:
             for r, (fn, args) in enumerate(handles):
                 if r != self.rank:
                     self.peer_slots[r] = fn(*args)
-            self._files = []
+            self.pull_stream = torch.cuda.Stream(flat.device)
         else:
             self.path = "/dev/shm/kfb_model_%s_%d" % (job, self.rank)
             arr = np.memmap(self.path, dtype=np.float32, mode="w+", shape=(2, n))
@@ -104,33 +127,119 @@ class ModelStore:
             for r in range(self.size):
                 if r != self.rank:
                     p = "/dev/shm/kfb_model_%s_%d" % (job, r)
-                    self.peer_slots[r] = torch.from_numpy(
-                        np.memmap(p, dtype=np.float32, mode="r", shape=(2, n)))
-        self.version = 0
-        self.versions.set(0)
+                    with warnings.catch_warnings():  # read-only map, never written
+                        warnings.simplefilter("ignore", UserWarning)
+                        self.peer_slots[r] = torch.from_numpy(
+                            np.memmap(p, dtype=np.float32, mode="r", shape=(2, n)))
+            self.pull_stream = None
+        self.seq = [0, 0]
+        self.latest = 0
+        self.hdr.write(self.SEQ0, 0)
+        self.hdr.write(self.SEQ1, 0)
+        self.hdr.write(self.LATEST, 0)
+        self._pending = None  # (slot, event) of a publish not yet committed
+        self._inflight = None  # (peer, slot, seq, event, out) of a prefetch
+        self.publishes = 0
+        self.retries = 0
         comm.all_gather_object(True)
 
+    # ------------------------------------------------------------ writer
+    def _commit(self, wait: bool) -> bool:
+        if self._pending is None:
+            return True
+        slot, ev = self._pending
+        if ev is not None:
+            if wait:
+                ev.synchronize()
+            elif not ev.query():
+                return False
+        self.seq[slot] += 1  # even: slot complete
+        self.hdr.write(slot, self.seq[slot])
+        self.latest = slot
+        self.hdr.write(self.LATEST, slot)
+        self._pending = None
+        return True
+
+    def poll(self):
+        """Commit a completed publish without blocking."""
+        self._commit(wait=False)
+
     def publish(self, flat: torch.Tensor):
-        nxt = self.version + 1
-        self.slots[nxt % 2].copy_(flat)
-        if flat.is_cuda:
-            torch.cuda.current_stream(flat.device).synchronize()
-        self.version = nxt
-        self.versions.set(nxt)
+        """Enqueue a snapshot of ``flat`` (on the current stream, after the
+        update that produced it); committed once the copy has completed."""
+        self._commit(wait=True)
+        slot = 1 - self.latest
+        self.seq[slot] += 1  # odd: write in progress on this slot
+        self.hdr.write(slot, self.seq[slot])
+        self.slots[slot].copy_(flat)
+        ev = None
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(flat.device))
+        self._pending = (slot, ev)
+        self.publishes += 1
+        if ev is None:
+            self._commit(wait=True)
+
+    def flush(self):
+        self._commit(wait=True)
+
+    # ------------------------------------------------------------ reader
+    def _snapshot_header(self, peer):
+        for _ in range(self.MAX_TRIES):
+            slot = self.hdr.read(peer, self.LATEST)
+            v = self.hdr.read(peer, slot)
+            if v % 2 == 0:
+                return slot, v
+        raise TornReadError("peer %d's latest slot stayed mid-write" % peer)
+
+    def begin_pull(self, peer: int, out: torch.Tensor):
+        """Start copying ``peer``'s latest committed model into ``out``
+        (side stream on the GPU; the owner does not participate)."""
+        slot, v = self._snapshot_header(peer)
+        ev = None
+        if self.cuda:
+            cur = torch.cuda.current_stream(out.device)
+            self.pull_stream.wait_stream(cur)  # ``out`` is free to overwrite
+            with torch.cuda.stream(self.pull_stream):
+                out.copy_(self.peer_slots[peer][slot], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.pull_stream)
+        else:
+            out.copy_(self.peer_slots[peer][slot])
+        self._inflight = (peer, slot, v, ev, out)
+
+    def finish_pull(self) -> int:
+        """Wait for the prefetch, validate it against the seqlock (retrying
+        synchronously if the slot was rewritten meanwhile); returns the
+        accepted sequence number."""
+        peer, slot, v, ev, out = self._inflight
+        self._inflight = None
+        for _ in range(self.MAX_TRIES):
+            if ev is not None:
+                ev.synchronize()
+            if self.hdr.read(peer, slot) == v:
+                if self.cuda:
+                    torch.cuda.current_stream(out.device).wait_event(ev)
+                return v
+            self.retries += 1
+            self.begin_pull(peer, out)
+            peer, slot, v, ev, out = self._inflight
+            self._inflight = None
+        raise TornReadError("no untorn snapshot of peer %d after %d tries"
+                            % (peer, self.MAX_TRIES))
 
     def pull(self, peer: int, out: torch.Tensor) -> int:
-        for _ in range(8):
-            v = self.versions.get(peer)
-            out.copy_(self.peer_slots[peer][v % 2])
-            if out.is_cuda:
-                torch.cuda.current_stream(out.device).synchronize()
-            if self.versions.get(peer) - v < 2:  # slot v%2 not rewritten meanwhile
-                return v
-        return v
+        self.begin_pull(peer, out)
+        return self.finish_pull()
 
     def close(self):
-        self.versions.close()
-        if not self.slots.is_cuda:
+        if self._inflight is not None and self._inflight[3] is not None:
+            self._inflight[3].synchronize()
+        self._inflight = None
+        self.flush()
+        self.hdr.close()
+        if not self.cuda:
             try:
                 os.remove(self.path)
             except OSError:
@@ -152,13 +261,22 @@ class PairAveraging(Strategy):
             self.store = ModelStore(self.flat.flat, self.world)
             self._peer_buf = torch.empty_like(self.flat.flat)
 
+    def _pick_peer(self) -> int:
+        peer = self.rng.randrange(self.world.size - 1)
+        return peer + 1 if peer >= self.world.rank else peer
+
+    def before_backward(self, step):
+        super().before_backward(step)
+        if self.store is None:
+            return
+        self.store.poll()
+        # prefetch a random peer's model while forward/backward run
+        self.store.begin_pull(self._pick_peer(), self._peer_buf)
+
     def before_update(self, step):
         if self.store is None:
             return
-        peer = self.rng.randrange(self.world.size - 1)
-        if peer >= self.world.rank:
-            peer += 1
-        self.store.pull(peer, self._peer_buf)
+        self.store.finish_pull()
         w = self.flat.flat
         w.add_(self._peer_buf).mul_(0.5)
 
@@ -167,5 +285,10 @@ class PairAveraging(Strategy):
             self.store.publish(self.flat.flat)
 
     def close(self):
+        """Collective: every rank stops reading before any slot is freed."""
         if self.store is not None:
+            self.store.flush()
+            w = self.flat.flat
+            self.world.barrier(w.device if w.is_cuda else None)
             self.store.close()
+            self.store = None

@@ -49,7 +49,7 @@ class Strategy:
         self.flat = flat
         self.tower_scale = float(tower_scale)
         self.reducer: Optional[BucketReducer] = None
-        if self.reduces_gradients and world.size > 1:
+        if self.reduces_gradients and world.communicates:
             self.reducer = BucketReducer(flat, bucket_mb, wire_dtype, overlap=overlap,
                                          num_buckets=num_buckets, relaxed=relaxed,
                                          shards=shards)
@@ -62,7 +62,7 @@ class Strategy:
         """Rank-0 broadcast of every variable (+ optimizer slots, BN stats):
         what horovod.broadcast_global_variables(0) / kungfu broadcast do at
         init (tcb/benchmark_cnn.py:2094-2100)."""
-        if self.world.size <= 1:
+        if not self.world.communicates:
             return
         comm.broadcast(self.flat.flat, 0)
         for t in slots:
@@ -85,6 +85,9 @@ class Strategy:
 
     def after_update(self, step: int):
         pass
+
+    def abort_update(self, step: int):
+        """Called instead of after_update when the update raised."""
 
     @property
     def update_is_empty(self) -> bool:
@@ -135,7 +138,7 @@ class KungFuSMA(Strategy):
         self._avg = None
 
     def before_update(self, step):
-        if self.world.size <= 1:
+        if not self.world.communicates:
             return
         w = self.flat.flat
         if self._avg is None:

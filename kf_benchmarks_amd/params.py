@@ -205,6 +205,9 @@ D.DEFINE_boolean("overlap_gradient_allreduce", True,
 D.DEFINE_enum("gradient_wire_dtype", "auto", ("auto", "fp32", "bf16", "fp16"),
               "Dtype gradients travel in over RCCL; auto = fp16 under "
               "--compact_gradient_transfer with repacking, else fp32.")
+D.DEFINE_integer("rccl_channels", 0,
+                 "Pin the RCCL channel count (NCCL_MIN/MAX_NCHANNELS); 0 = RCCL's choice. "
+                 "Each channel is one ring over the xGMI links.", lower_bound=0)
 D.DEFINE_float("kungfu_sma_alpha", 0.1, "SMA: pull factor toward the model average.")
 D.DEFINE_integer("kungfu_ada_switch_step", 100, "ada_sgd: step at which SMA switches to S-SGD.")
 D.DEFINE_integer("kungfu_peer_seed", 0, "Seed for PairAveraging peer selection.")

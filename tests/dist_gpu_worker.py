@@ -57,19 +57,35 @@ def main():
         loss, _ = bench.train_step(need_loss=True)
         losses.append(float(loss))
     torch.cuda.synchronize()
+    reduce_identity = None
+    if os.environ.get("KFB_TEST_REDUCE_IDENTITY") and bench.strategy.reducer is not None:
+        # one more synchronous all-reduce of the last gradient over the group:
+        # at world size 1 RCCL must return it bit for bit
+        g0 = bench.flat.grad.detach().clone()
+        bench.strategy.reducer.reduce_now()
+        torch.cuda.synchronize()
+        reduce_identity = bool(torch.equal(g0, bench.flat.grad)) and bool(g0.abs().sum() > 0)
     flat = bench.flat.flat.detach()
-    res = {"losses": losses, "w0": w0, "wsum": flat.double().sum().item(),
+    res = {"reduce_identity": reduce_identity, "losses": losses, "w0": w0, "wsum": flat.double().sum().item(),
            "wabs": flat.double().abs().sum().item(), "head": flat[:64].cpu().tolist(),
            "tail": flat[-64:].cpu().tolist(), "rank": comm.get_world().rank,
            "gsegs": gsegs, "trace": trace,
            "segs": {name: flat[off:off + n].double().sum().item()
                     for name, _, off, n in bench.flat.segments()},
-           "size": comm.get_world().size}
+           "size": comm.get_world().size, "backend": comm.get_world().backend,
+           "bucket_launches": (bench.strategy.reducer.launch_count
+                               if bench.strategy.reducer is not None else 0),
+           "num_buckets": (bench.strategy.reducer.num_buckets
+                           if bench.strategy.reducer is not None else 0)}
     state = getattr(bench.strategy, "state", None)
     if state is not None:  # asynchronous parameter server
         comm.get_world().barrier()
         res["ps_global_step"] = state.global_step
         bench.strategy.close()
+    elif getattr(bench.strategy, "store", None) is not None:  # PairAveraging
+        res["pa_publishes"] = bench.strategy.store.publishes
+        res["pa_retries"] = bench.strategy.store.retries
+        bench.strategy.close()  # collective: no peer is still reading our slots
     with open(out, "w") as f:
         json.dump(res, f)
     comm.get_world().shutdown()

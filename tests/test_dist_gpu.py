@@ -24,7 +24,7 @@ def _port():
     return port
 
 
-def _run(kw, steps, tmp_path, n=2):
+def _run(kw, steps, tmp_path, n=2, env_extra=None, tag=""):
     port = _port()
     procs = []
     for r in range(n):
@@ -32,7 +32,10 @@ def _run(kw, steps, tmp_path, n=2):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KFB_DIST_BACKEND="gloo",
                    KFB_TEST_GRAD_SEGS="1",
                    PYTHONPATH=ROOT)
-        out = tmp_path / ("rank%d.json" % r)
+        env.update(env_extra or {})
+        for k in [k for k, v in env.items() if v is None]:
+            del env[k]
+        out = tmp_path / ("%srank%d.json" % (tag, r))
         cmd = [sys.executable, os.path.join(ROOT, "tests", "dist_gpu_worker.py"), str(out),
                json.dumps(kw), str(steps)]
         procs.append((subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE,
@@ -84,6 +87,79 @@ def test_two_ranks_async_parameter_server(cuda, tmp_path):
               data_format="NHWC", variable_update="parameter_server", cross_replica_sync=False)
     r0, r1 = _run(kw, 3, tmp_path)
     assert r0["ps_global_step"] == r1["ps_global_step"] == 6
+    assert r0["w0"] == r1["w0"]
+    for r in (r0, r1):
+        assert r["wsum"] != r["w0"] and r["wsum"] == r["wsum"]
+        assert all(l == l and abs(l) < 1e3 for l in r["losses"])
+
+
+# RCCL proper: a 1-rank "nccl" process group (KFB_FORCE_PG=1).  RCCL refuses
+# two ranks on one device, so on the 1-GPU box the real communicator runs at
+# size 1: same bucket hooks, same async all-reduce on RCCL's high-priority
+# stream, same broadcast; the result must match the run without any group.
+_RCCL = dict(KFB_FORCE_PG="1", KFB_DIST_BACKEND=None, WORLD_SIZE=None, RANK=None,
+             LOCAL_RANK=None)
+_NOCOMM = dict(KFB_DIST_BACKEND=None, WORLD_SIZE=None, RANK=None, LOCAL_RANK=None)
+
+
+def test_one_rank_rccl_is_identity(cuda, tmp_path):
+    """FC-only model through a real 1-rank RCCL group: every bucket launches
+    every step, a synchronous all-reduce of the gradient returns it bit for
+    bit, and training tracks the run without any process group."""
+    kw = dict(model="trivial", batch_size=16, num_gpus=1, use_bf16=True, optimizer="momentum",
+              data_format="NHWC", variable_update="kungfu", kungfu_option="sync_sgd",
+              bucket_size_mb=8.0)
+    env = dict(_RCCL, KFB_TEST_REDUCE_IDENTITY="1")
+    (a,) = _run(kw, 3, tmp_path, n=1, env_extra=env, tag="rccl")
+    (b,) = _run(kw, 3, tmp_path, n=1, env_extra=_NOCOMM, tag="nocomm")
+    assert a["backend"] == "nccl" and a["size"] == 1
+    assert a["bucket_launches"] == 3 * a["num_buckets"] > 0
+    assert b["bucket_launches"] == 0
+    assert a["reduce_identity"] is True
+    assert a["w0"] == b["w0"] and a["losses"][0] == b["losses"][0]
+    for la, lb in zip(a["losses"], b["losses"]):
+        assert abs(la - lb) <= 1e-4 * max(1.0, abs(lb)), (a["losses"], b["losses"])
+
+
+def test_one_rank_rccl_resnet50_overlap(cuda, tmp_path):
+    """ResNet-50 bs 8 through RCCL with backward-overlapped buckets and the
+    side-stream weight gradients: every bucket launches every step, and the
+    weights track the no-comm run (the BN statistics' fp32 atomics make
+    either run non-bitwise at these shapes, so the bound is a tolerance)."""
+    kw = dict(model="resnet50", batch_size=8, num_gpus=1, use_bf16=True, optimizer="momentum",
+              data_format="NHWC", variable_update="kungfu", kungfu_option="sync_sgd",
+              bucket_size_mb=4.0)
+    (a,) = _run(kw, 3, tmp_path, n=1, env_extra=_RCCL, tag="rccl")
+    (b,) = _run(kw, 3, tmp_path, n=1, env_extra=_NOCOMM, tag="nocomm")
+    assert a["backend"] == "nccl"
+    assert a["num_buckets"] >= 4 and a["bucket_launches"] == 3 * a["num_buckets"]
+    assert a["w0"] == b["w0"]
+    import math
+    for k in a["segs"]:
+        x, y = a["segs"][k], b["segs"][k]
+        assert math.isfinite(x) and abs(x - y) <= 2e-3 * max(1.0, abs(y)), (k, x, y)
+    for la, lb in zip(a["losses"], b["losses"]):
+        assert abs(la - lb) <= 0.05 * max(1.0, abs(lb)), (a["losses"], b["losses"])
+
+
+def test_pair_averaging_store_never_tears_over_hip_ipc(cuda, tmp_path):
+    """KungFu async_sgd's model store on device memory shared over HIP IPC
+    (both ranks on the box's one GPU): a publisher hammering constant-valued
+    snapshots, a reader pulling on its side stream; every accepted snapshot
+    is uniform."""
+    from test_variable_update import _hammer
+    pub, rd = _hammer(tmp_path, "cuda", 16 << 20, 4.0)
+    assert pub["publishes"] > 10 and rd["pulls"] > 10
+    assert rd["torn"] == 0, rd
+    assert rd["distinct"] > 2
+
+
+def test_two_ranks_pair_averaging_training(cuda, tmp_path):
+    """ResNet-50 bs 8 under --kungfu_option=async_sgd, two ranks on the GPU:
+    prefetched peer pulls and event-committed publishes; both ranks train."""
+    kw = dict(model="resnet50", batch_size=8, num_gpus=1, use_bf16=True, optimizer="momentum",
+              data_format="NHWC", variable_update="kungfu", kungfu_option="async_sgd")
+    r0, r1 = _run(kw, 4, tmp_path)
     assert r0["w0"] == r1["w0"]
     for r in (r0, r1):
         assert r["wsum"] != r["w0"] and r["wsum"] == r["wsum"]

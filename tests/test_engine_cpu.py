@@ -132,3 +132,34 @@ def test_benchmark_logger(tmp_path):
     with open(os.path.join(d, "metric.log")) as f:
         names = {json.loads(l)["name"] for l in f}
     assert "average_examples_per_sec" in names
+
+
+def test_failed_update_releases_strategy(tmp_path):
+    """An exception between before_update and after_update (optimizer,
+    non-finite check) reaches the strategy's abort_update, and the async
+    PS lock is released so the other workers do not block forever."""
+    import fcntl
+    from kf_benchmarks_amd.parallel import async_ps
+    b = benchmark.BenchmarkCNN(_params(num_batches=2))
+    b.set_fake_data(*_bw_data())
+    b.build()
+    calls = []
+    b.strategy.abort_update = lambda step: calls.append(step)
+
+    def boom(*a, **k):
+        raise FloatingPointError("injected")
+    b.optimizer.step = boom
+    with pytest.raises(FloatingPointError):
+        b.train_step()
+    assert calls == [0]
+    # the PS strategy's lock bookkeeping: abort releases a held lock
+    st = async_ps._SharedState.__new__(async_ps._SharedState)
+    st._lock_f = open(tmp_path / "ps.lock", "w")
+    strat = async_ps.AsyncParameterServer.__new__(async_ps.AsyncParameterServer)
+    strat.state = st
+    st.lock()
+    strat.abort_update(0)
+    with open(tmp_path / "ps.lock", "w") as f2:
+        fcntl.flock(f2, fcntl.LOCK_EX | fcntl.LOCK_NB)  # would raise if still held
+        fcntl.flock(f2, fcntl.LOCK_UN)
+    st._lock_f.close()

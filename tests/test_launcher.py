@@ -132,3 +132,73 @@ def test_ps_worker_cluster_flags(tmp_path):
                 p.kill()
     assert "total images/sec" in outs[1] and "total images/sec" in outs[2]
     assert "Running ps 0" in outs[0]
+
+
+def _bench_json(stdout):
+    import json
+    lines = [ln for ln in stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+def test_bench_self_launches_n_ranks():
+    """bench.py --gpus 2 without an external launcher starts 2 ranks itself
+    (kfb-run) and reports the whole 2-rank job; the driver contract."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+           "--model", "trivial", "--batch_size", "4", "--steps", "2", "--warmup", "1",
+           "--dtype", "fp32"]
+    r = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = _bench_json(r.stdout)
+    assert out["n_gpus"] == 2 and out["ranks"] == 2 and out["backend"] == "gloo"
+    assert out["config"]["global_batch"] == 8 and out["config"]["parallelism"] == "dp2"
+
+
+def test_bench_refuses_mismatched_world():
+    """A launcher that started fewer ranks than --gpus is an error, never a
+    1-rank number labelled as N GPUs."""
+    env = _env()
+    env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    env["KFB_BENCH_NO_SELF_LAUNCH"] = "1"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+           "--model", "trivial", "--batch_size", "2", "--steps", "1", "--warmup", "0"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and not r.stdout.strip(), (r.stdout, r.stderr)
+
+
+def test_bench_forced_one_rank_group():
+    """KFB_FORCE_PG=1: a 1-rank process group is created, so the bucketed
+    all-reduce and the broadcast run (gloo here; RCCL on the GPU box)."""
+    env = _env()
+    env["KFB_FORCE_PG"] = "1"
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--model",
+           "trivial", "--batch_size", "2", "--steps", "2", "--warmup", "1", "--dtype", "fp32"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = _bench_json(r.stdout)
+    assert out["ranks"] == 1 and out["backend"] == "gloo"
+
+
+def test_openmpi_environment_gives_one_rank_per_process(tmp_path):
+    """mpirun -np N exports OMPI_COMM_WORLD_{RANK,SIZE,LOCAL_RANK} only
+    (tcb/run_hv.sh:15-18): the world is read from them (horovod mode)."""
+    port = 23450
+    code = ("from kf_benchmarks_amd.parallel import comm; import torch;"
+            "w=comm.init_world('cpu'); t=torch.ones(1); comm.all_reduce(t);"
+            "print('W', w.rank, w.size, w.local_rank, int(t.item()))")
+    procs = []
+    for r in range(2):
+        env = _env()
+        for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+            env.pop(k, None)
+        env.update(OMPI_COMM_WORLD_RANK=str(r), OMPI_COMM_WORLD_SIZE="2",
+                   OMPI_COMM_WORLD_LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", code], env=env, text=True,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE))
+    outs = [p.communicate(timeout=120) for p in procs]
+    for r, (o, e) in enumerate(outs):
+        assert procs[r].returncode == 0, e
+        assert ("W %d 2 %d 2" % (r, r)) in o

@@ -219,3 +219,40 @@ def test_two_workers_relaxed_consistency(tmp_path):
         prev = cur
     for r in range(2):
         np.testing.assert_allclose(res[r]["losses"], exp[r], rtol=1e-5, atol=0)
+
+
+def _hammer(tmp_path, device, numel, seconds):
+    import json
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONPATH=root)
+        out = tmp_path / ("hammer%d.json" % r)
+        procs.append((subprocess.Popen(
+            [sys.executable, os.path.join(root, "tests", "pairavg_hammer.py"), str(out),
+             device, str(numel), str(seconds)], env=env, stdout=subprocess.PIPE,
+            stderr=subprocess.STDOUT, text=True), out))
+    res = []
+    for p, out in procs:
+        log, _ = p.communicate(timeout=240)
+        assert p.returncode == 0, log[-3000:]
+        with open(out) as f:
+            res.append(json.load(f))
+    return res
+
+
+def test_pair_averaging_store_never_tears(tmp_path):
+    """The seqlock model store under a publisher hammering constant-valued
+    snapshots: every snapshot a reader accepts is uniform."""
+    pub, rd = _hammer(tmp_path, "cpu", 4 << 20, 3.0)
+    assert pub["publishes"] > 10 and rd["pulls"] > 10
+    assert rd["torn"] == 0, rd
+    assert rd["distinct"] > 2  # the reader saw the publisher advancing
