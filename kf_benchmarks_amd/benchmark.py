@@ -130,7 +130,8 @@ def validate_params_combinations(params):
             raise ValueError("Automatic loss scaling is not supported with staged_vars.")
     if p.debugger is not None and p.debugger != "cli" and ":" not in p.debugger:
         raise ValueError('--debugger must be "cli" or in the form host:port')
-    if p.hierarchical_copy and p.num_gpus <= 1:
+    if p.hierarchical_copy and p.num_gpus <= 1 and comm.env_world_size() <= 1:
+        # (one process per GPU: the ranks of the world are the devices)
         raise ValueError("--hierarchical_copy requires --num_gpus to be greater than 1")
     if p.save_model_secs and p.save_model_steps:
         raise ValueError("At most one of --save_model_secs and --save_model_steps can be "
@@ -397,6 +398,8 @@ class BenchmarkCNN:
                            kernel_impl=p.kernel_impl, seed=seed)
         lp = self.compute_dtype if self.compute_dtype != torch.float32 else None
         self.flat = optim.FlatParams(self.net, lp)
+        if p.staged_vars:
+            self.flat.enable_staging()
         if self.device_type == "cuda" and lp is not None and p.kernel_impl == "hip":
             from .ops.conv_hip import DgradWeights
             dgw = DgradWeights(self.net, self.flat)
@@ -493,6 +496,11 @@ class BenchmarkCNN:
                     # batch-norm variables): add wd * w on the masked elements
                     # before the gradient scale the optimizer applies
                     self.flat.grad.addcmul_(self.l2_mask, self.flat.flat, value=wd / grad_scale)
+                    wd = 0.0
+                elif wd and self.flat.master is not None:
+                    # staged_vars: the L2 loss is over the staged (read) values,
+                    # so its gradient uses them, not the master being updated
+                    self.flat.grad.add_(self.flat.flat, alpha=wd / grad_scale)
                     wd = 0.0
                 self.optimizer.step(self.learning_rate(step), grad_scale=grad_scale,
                                     weight_decay=wd, clip=p.gradient_clip)

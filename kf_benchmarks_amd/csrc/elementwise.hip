@@ -98,13 +98,35 @@ act_bwd_bias_k(const T* __restrict__ dy, const T* __restrict__ y, T* __restrict_
   }
 }
 
-__global__ void colsum_finalize_k(const float* __restrict__ p, int nslab, int C,
-                                  float* __restrict__ out, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0;
-  for (int k = 0; k < nslab; ++k) s += (double)p[(long)k * C + c];
-  out[c] = (accumulate ? out[c] : 0.f) + (float)s;
+// out[c] (+)= sum_k p[k][c].  16 channels x 16 slab groups per workgroup:
+// each thread strides over the slabs with four independent accumulators,
+// then the 16 groups fold through LDS (one thread per channel and slab
+// serially took ~0.3 ms per call at 1024 slabs: 4.7 ms of a VGG-16 step).
+__global__ void __launch_bounds__(256) colsum_finalize_k(const float* __restrict__ p, int nslab,
+                                                         int C, float* __restrict__ out,
+                                                         int accumulate) {
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (c < C) {
+    int k = grp;
+    for (; k + 48 < nslab; k += 64) {
+      a0 += p[(long)k * C + c];
+      a1 += p[(long)(k + 16) * C + c];
+      a2 += p[(long)(k + 32) * C + c];
+      a3 += p[(long)(k + 48) * C + c];
+    }
+    for (; k < nslab; k += 16) a0 += p[(long)k * C + c];
+  }
+  red[grp][cl] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (grp == 0 && c < C) {
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) s += red[g][cl];
+    out[c] = (accumulate ? out[c] : 0.f) + s;
+  }
 }
 
 template <typename T>
@@ -264,7 +286,7 @@ KFB_API hipError_t kfb_act_bwd_bias(int dtype, const void* dy, const void* y, vo
         hipLaunchKernelGGL((act_bwd_bias_k<T, VV, false>), grid, dim3(256), lds, stream,
                            (const T*)dy, (const T*)y, (T*)dx, rows, C, cw, tpr, rpi, slab_rows, pb);
       if (db)
-        hipLaunchKernelGGL(colsum_finalize_k, dim3(ceil_div(C, 256)), dim3(256), 0, stream,
+        hipLaunchKernelGGL(colsum_finalize_k, dim3(ceil_div(C, 16)), dim3(256), 0, stream,
                            pbias, nslab, C, db, accumulate);
     });
   });

@@ -76,30 +76,62 @@ class FakeDataInput:
 
 class PrefetchInput:
     """Pulls host batches from a preprocessor generator on a thread, copies
-    them to the device on a side stream, one batch ahead."""
+    them to the device on a side stream, one batch ahead.
 
-    def __init__(self, bench, batch_iter, depth: int = 2):
+    ``batch_group_size`` > 1 (--batch_group_size): the host side runs as the
+    reference's ImageProducer (tcb/cnn_util.py:118-198, wired at
+    tcb/benchmark_cnn.py:2139-2146): batches are staged in groups of that
+    many, at most two groups ahead of the consumer, which reports every
+    consumed batch."""
+
+    def __init__(self, bench, batch_iter, depth: int = 2, batch_group_size: int = 1):
         self.bench = bench
         self.device = bench.device
         self.dtype = bench.compute_dtype
-        self._q: "queue.Queue" = queue.Queue(maxsize=max(depth, 1))
         self._it = batch_iter
         self._stop = threading.Event()
         self._err: Optional[BaseException] = None
-        self._thread = threading.Thread(target=self._run, daemon=True)
-        self._thread.start()
         self._stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         self._next = None
+        self.producer = None
+        if batch_group_size > 1:
+            from ..cnn_util import ImageProducer
+            self._q: "queue.Queue" = queue.Queue()  # bounded by the producer
+            self._ended = False
+            self.producer = ImageProducer(self._put_one, batch_group_size)
+            self.producer.start()
+        else:
+            self._q = queue.Queue(maxsize=max(depth, 1))
+            self._thread = threading.Thread(target=self._run, daemon=True)
+            self._thread.start()
+
+    def _host(self, batch):
+        ts = [torch.from_numpy(np.ascontiguousarray(x)) for x in batch]
+        if self.device.type == "cuda":
+            ts = [t.pin_memory() for t in ts]
+        return ts
+
+    def _put_one(self):
+        """ImageProducer put_fn: stage one batch (or the end marker)."""
+        if self._ended:
+            self._stop.wait(0.05)
+            return
+        try:
+            self._q.put(self._host(next(self._it)))
+        except StopIteration:
+            self._ended = True
+            self._q.put(None)
+        except BaseException as e:
+            self._ended = True
+            self._err = e
+            self._q.put(None)
 
     def _run(self):
         try:
             for batch in self._it:
                 if self._stop.is_set():
                     return
-                ts = [torch.from_numpy(np.ascontiguousarray(x)) for x in batch]
-                if self.device.type == "cuda":
-                    ts = [t.pin_memory() for t in ts]
-                self._q.put(ts)
+                self._q.put(self._host(batch))
             self._q.put(None)
         except BaseException as e:
             self._err = e
@@ -118,6 +150,8 @@ class PrefetchInput:
 
     def _fetch(self):
         item = self._q.get()
+        if self.producer is not None and item is not None:
+            self.producer.notify_image_consumption()
         if item is None:
             if self._err is not None:
                 raise RuntimeError("input pipeline failed") from self._err
@@ -148,6 +182,8 @@ class PrefetchInput:
 
     def close(self):
         self._stop.set()
+        if self.producer is not None:
+            self.producer.done()
 
 
 def make_input_source(bench, subset="train"):
@@ -158,4 +194,5 @@ def make_input_source(bench, subset="train"):
         return SyntheticInput(bench, subset)
     from . import preprocessing
     it = preprocessing.make_batch_iterator(bench, subset)
-    return PrefetchInput(bench, it, depth=max(bench.params.datasets_prefetch_buffer_size, 1) + 1)
+    return PrefetchInput(bench, it, depth=max(bench.params.datasets_prefetch_buffer_size, 1) + 1,
+                         batch_group_size=max(int(bench.params.batch_group_size or 1), 1))

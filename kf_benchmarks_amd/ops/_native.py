@@ -60,8 +60,13 @@ _SIGS = {
     "kfb_synthetic_images": [I, P, L, F, F, c_uint32, P],
     "kfb_synthetic_labels": [P, L, I, c_uint32, P],
     "kfb_add": [I, P, P, P, L, I, P],
+    "kfb_gemm": [I, I, P, I, P, I, I, I, I, P, I, P, I, I, P, L, I, P],
+    "kfb_gemm_splits": [I, I, I, I],
+    "kfb_lrn_fwd": [I, P, P, L, I, I, F, F, F, P],
+    "kfb_lrn_bwd": [I, P, P, P, L, I, I, F, F, F, P],
 }
-_RESTYPES = {"kfb_bn_num_slabs": c_int, "kfb_colsum_num_slabs": c_int}
+_RESTYPES = {"kfb_bn_num_slabs": c_int, "kfb_colsum_num_slabs": c_int,
+             "kfb_gemm_splits": c_int}
 # Optional symbols (added by later kernel files); bound if present.
 _OPTIONAL = {}
 

@@ -714,32 +714,89 @@ def spatial_mean(x, keep_dims=False):
 
 
 # ---------------------------------------------------------------------- affine
+_GEMM_FWD, _GEMM_DGRAD, _GEMM_WGRAD = 0, 1, 2
+
+
+def _gemm(mode, p, ldp, q, ldq, rows, cols, red, out, ldc, bias=None, relu=False,
+          accumulate=False):
+    """csrc/gemm.hip, out [rows][cols]: mode 0 out = p . q (q [red][cols]),
+    mode 1 out = p . q^T (q [cols][red]), mode 2 out (+)= p^T . q
+    (p [red][rows], q [red][cols], fp32 out)."""
+    dev = p.device
+    nsplit, slab = 1, None
+    if mode != _GEMM_WGRAD:
+        nsplit = N.query("kfb_gemm_splits", N.dt(p), rows, cols, red)
+        if nsplit > 1:
+            slab = torch.empty((nsplit * rows * ((cols + 3) // 4 * 4),), dtype=torch.float32,
+                               device=dev)
+    N.call("kfb_gemm", N.dt(p), mode, p.data_ptr(), ldp, q.data_ptr(), ldq, rows, cols, red,
+           out.data_ptr(), ldc, N.ptr(bias), int(relu), int(accumulate), N.ptr(slab),
+           slab.numel() if slab is not None else 0, nsplit, N.stream(dev))
+
+
 class _Linear(torch.autograd.Function):
-    """y = x @ W + b with W the fp32 master [Cin, Cout] and W_lp its compute
-    copy.  Plain GEMMs: these go to the vendor BLAS (hipBLASLt)."""
+    """y = act(x @ W + b) with W the fp32 master [Cin, Cout] (TF layout) and
+    W_lp its compute copy, on the MFMA GEMM (csrc/gemm.hip): the forward
+    reads W as is (K-strided operand), the input gradient is dy . W^T
+    (K-contiguous W), and the weight gradient x^T . dy is written in fp32
+    straight into the flat gradient buffer; bias and ReLU ride in the
+    forward's epilogue and one fused ReLU-backward + bias-column-sum pass
+    (tcb/convnet_builder.py:311-345)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, w_lp):
-        wl = w_lp if w_lp is not None else w.to(x.dtype)
-        y = torch.mm(x, wl)
-        ctx.save_for_backward(x, wl)
-        ctx.has_b = b is not None
+    def forward(ctx, x, w, b, w_lp, relu):
+        x = x.contiguous()
+        wl = (w_lp if w_lp is not None else w.to(x.dtype)).contiguous()
+        M, K = x.shape
+        Nout = wl.shape[1]
+        y = torch.empty((M, Nout), dtype=x.dtype, device=x.device)
+        _gemm(_GEMM_FWD, x, K, wl, Nout, M, Nout, K, y, Nout, bias=b, relu=relu)
+        ctx.save_for_backward(x, wl, y if relu else None)
+        ctx.relu, ctx.has_b = relu, b is not None
+        ctx.w, ctx.b = w, b
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, wl = ctx.saved_tensors
-        # (the first affine of a net on raw images needs no input gradient)
-        dx = torch.mm(dy, wl.t()) if ctx.needs_input_grad[0] else None
-        if dy.shape[1] < 16:
-            # narrow outputs (the trivial model's affine(1)): x^T @ dy with
-            # N < 16 takes an ~11 ms host-side slow path in torch.mm here
-            # (scripts/probes/r2l_mm_shapes.py); (dy^T @ x)^T is one GEMM launch
-            dw = torch.mm(dy.t(), x).t().float()
+        x, wl, y = ctx.saved_tensors
+        dy = dy.contiguous()
+        M, K = x.shape
+        Nout = wl.shape[1]
+        dev = dy.device
+        db = None
+        if ctx.relu or ctx.has_b:
+            g = torch.empty_like(dy) if ctx.relu else dy
+            pb = dbuf = None
+            nslab = 1
+            if ctx.has_b:
+                nslab = N.query("kfb_colsum_num_slabs", M, Nout)
+                pb = torch.empty((nslab * Nout,), dtype=torch.float32, device=dev)
+                bsink = _grad_sink(ctx.b)
+                dbuf = bsink if bsink is not None else torch.empty(
+                    (Nout,), dtype=torch.float32, device=dev)
+            N.call("kfb_act_bwd_bias", N.dt(dy), dy.data_ptr(), N.ptr(y), g.data_ptr(), M, Nout,
+                   int(ctx.relu), N.ptr(pb), nslab, N.ptr(dbuf),
+                   int(ctx.has_b and _grad_sink(ctx.b) is not None), N.stream(dev))
+            if ctx.has_b:
+                if _grad_sink(ctx.b) is not None:
+                    _grad_ready(ctx.b)
+                else:
+                    db = dbuf
+            dy = g
+        dx = None
+        if ctx.needs_input_grad[0]:
+            # (the first affine of a net on raw images needs no input gradient)
+            dx = torch.empty((M, K), dtype=dy.dtype, device=dev)
+            _gemm(_GEMM_DGRAD, dy, Nout, wl, Nout, M, K, Nout, dx, K)
+        wsink = _grad_sink(ctx.w)
+        dw = None
+        if wsink is not None:
+            _gemm(_GEMM_WGRAD, x, K, dy, Nout, K, Nout, M, wsink, Nout, accumulate=True)
+            _grad_ready(ctx.w)
         else:
-            dw = torch.mm(x.t(), dy).float()
-        db = dy.float().sum(0) if ctx.has_b else None
-        return dx, dw, db, None
+            dw = torch.empty((K, Nout), dtype=torch.float32, device=dev)
+            _gemm(_GEMM_WGRAD, x, K, dy, Nout, K, Nout, M, dw, Nout)
+        return dx, dw, db, None, None
 
 
 def linear(x, w, b, w_lp=None, relu=False):
@@ -750,8 +807,7 @@ def linear(x, w, b, w_lp=None, relu=False):
         if relu:
             y = torch.relu(y)
         return y.to(x.dtype)
-    y = _Linear.apply(x, w, None, w_lp)
-    return bias_act(y, b, relu)
+    return _Linear.apply(x, w, b, w_lp, relu)
 
 
 # --------------------------------------------------------------------- dropout
@@ -783,8 +839,35 @@ def dropout(x, keep_prob: float, training: bool, seed: int):
 
 
 # ------------------------------------------------------------------------- LRN
+class _LRN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, depth_radius, bias, alpha, beta):
+        x = x.contiguous()
+        C = x.shape[-1]
+        y = torch.empty_like(x)
+        N.call("kfb_lrn_fwd", N.dt(x), x.data_ptr(), y.data_ptr(), x.numel() // C, C,
+               int(depth_radius), float(bias), float(alpha), float(beta), N.stream(x.device))
+        ctx.save_for_backward(x)
+        ctx.args = (int(depth_radius), float(bias), float(alpha), float(beta))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        C = x.shape[-1]
+        dx = torch.empty_like(x)
+        r, bias, alpha, beta = ctx.args
+        N.call("kfb_lrn_bwd", N.dt(x), x.data_ptr(), dy.data_ptr(), dx.data_ptr(),
+               x.numel() // C, C, r, bias, alpha, beta, N.stream(x.device))
+        return dx, None, None, None, None
+
+
 def lrn(x, depth_radius, bias, alpha, beta):
-    """tf.nn.lrn over the channel dim of NHWC x (sum over 2r+1 channels)."""
+    """tf.nn.lrn over the channel dim of NHWC x (sum over 2r+1 channels;
+    tcb/convnet_builder.py:463-469).  GPU: csrc/lrn.hip."""
+    if _on_gpu(x):
+        return _LRN.apply(x, depth_radius, bias, alpha, beta)
     xf = x.float()
     sq = (xf * xf).permute(0, 3, 1, 2).unsqueeze(1)  # N,1,C,H,W
     k = 2 * depth_radius + 1

@@ -56,6 +56,13 @@ class FlatParams:
         if self.lp_dtype is not None:
             self.lp = self.flat.to(self.lp_dtype)
             self._attach_lp_views()
+        # --staged_vars: the optimizer updates ``master``; the layers read
+        # ``flat`` (and its low-precision shadow), which is refreshed from the
+        # master just BEFORE each update, so step t's forward/backward reads
+        # the variables as they were one update earlier (the StagingArea
+        # reads of tcb/variable_mgr_util.py:236-393, VariableMgrLocalFetch-
+        # FromStagedPS tcb/variable_mgr.py:246-274)
+        self.master: Optional[torch.Tensor] = None
 
     def _attach_lp_views(self):
         index = {id(p): (o, p) for p, o in zip(self.params, self.offsets)}
@@ -66,12 +73,47 @@ class FlatParams:
                     o, _ = index[id(p)]
                     setattr(layer, lp_attr, self.lp[o:o + p.numel()].view(p.shape))
 
+    def enable_staging(self):
+        self.master = self.flat.clone()
+
+    @property
+    def update_target(self) -> torch.Tensor:
+        """The fp32 buffer the optimizer updates."""
+        return self.master if self.master is not None else self.flat
+
+    def stage_reads(self):
+        """Staged mode: publish the current master as the values the next
+        step reads (called right before the update)."""
+        self.flat.copy_(self.master)
+        if self.lp is not None:
+            self.lp.copy_(self.master)
+
     def refresh_lp(self):
         """Re-derive the low-precision shadow from the fp32 master (after a
         checkpoint restore or a model broadcast)."""
+        if self.master is not None:
+            self.master.copy_(self.flat)
         if self.lp is not None:
             self.lp.copy_(self.flat)
         self.after_update()
+
+    def real_values(self):
+        """Context manager: the layer-visible buffer holds the real (master)
+        variables inside (checkpoint save of a staged run)."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def swap():
+            if self.master is None:
+                yield
+                return
+            keep = self.flat.clone()
+            self.flat.copy_(self.master)
+            try:
+                yield
+            finally:
+                self.flat.copy_(keep)
+        return swap()
 
     def add_update_hook(self, fn):
         """fn() runs after every write of the weights (optimizer step, restore)."""
@@ -137,10 +179,15 @@ class FusedOptimizer:
             b1, b2, eps = self.adam
             lr_t = lr * math.sqrt(1 - b2 ** self.t) / (1 - b1 ** self.t)
         clipv = float(clip) if clip else 0.0
+        staged = f.master is not None
+        if staged:
+            f.stage_reads()
+        w = f.update_target
+        lp = None if staged else f.lp
         if f.device.type == "cuda":
-            N.call("kfb_opt_step", _KINDS[self.kind], f.flat.data_ptr(), g.data_ptr(),
-                   N.ptr(self.s1), N.ptr(self.s2), N.ptr(f.lp),
-                   N.dt(f.lp) if f.lp is not None else 0, None, f.numel, float(lr),
+            N.call("kfb_opt_step", _KINDS[self.kind], w.data_ptr(), g.data_ptr(),
+                   N.ptr(self.s1), N.ptr(self.s2), N.ptr(lp),
+                   N.dt(lp) if lp is not None else 0, None, f.numel, float(lr),
                    float(grad_scale), float(weight_decay), clipv, float(mom), float(b1),
                    float(b2), float(eps), float(lr_t), int(self.nesterov), N.stream(f.device))
             f.after_update()
@@ -150,7 +197,7 @@ class FusedOptimizer:
 
     @torch.no_grad()
     def _step_torch(self, g, lr, grad_scale, wd, clip, mom, b1, b2, eps, lr_t):
-        w = self.flat.flat
+        w = self.flat.update_target
         gk = g * grad_scale
         if wd:
             gk = gk + wd * w
@@ -172,7 +219,7 @@ class FusedOptimizer:
             self.s1.add_((gk - self.s1) * (1 - b1))
             self.s2.add_((gk * gk - self.s2) * (1 - b2))
             w.sub_(lr_t * self.s1 / (self.s2.sqrt() + eps))
-        if self.flat.lp is not None:
+        if self.flat.lp is not None and self.flat.master is None:
             self.flat.lp.copy_(w)
 
 

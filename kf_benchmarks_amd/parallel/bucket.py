@@ -19,9 +19,10 @@ the links busy while leaving enough buckets (ResNet-50: 102 MB fp32 -> 4 at
 the bytes on the wire (the reference's --compact_gradient_transfer).
 
 ``num_buckets`` (``--gradient_repacking=k``) splits the flat gradient into k
-equal buckets instead of size-capped ones; ``shards`` (``alg#shards`` in
-``--all_reduce_spec``) issues each bucket as that many concurrent
-collectives; ``relaxed`` (``--variable_consistency=relaxed``) defers the
+equal buckets instead of size-capped ones; ``spec`` (the parsed
+``--all_reduce_spec``) picks per bucket size the collective algorithm and
+the number of concurrent pieces (``alg#shards``), see
+:mod:`kf_benchmarks_amd.parallel.allreduce`; ``relaxed`` (``--variable_consistency=relaxed``) defers the
 gradients by one step: step t's reduction runs while step t+1 computes, and
 step t applies step t-1's result (zeros at the first step), as the
 StagingArea deferral of tcb/batch_allreduce.py:353-389.
@@ -33,18 +34,21 @@ from typing import List, Optional
 
 import torch
 
-from . import comm
+from . import allreduce, comm
 
 
 class BucketReducer:
     def __init__(self, flat, bucket_mb: float = 25.0, wire_dtype: Optional[torch.dtype] = None,
                  overlap: bool = True, op: str = "sum", group=None, num_buckets: int = 0,
-                 relaxed: bool = False, shards: int = 1):
+                 relaxed: bool = False, shards: int = 1, spec=None, hierarchical=None):
         self.flat = flat
         self.wire_dtype = wire_dtype if wire_dtype not in (None, torch.float32) else None
         self.op = op
         self.group = group
         self.shards = max(int(shards), 1)
+        self.spec = spec  # [AllReduceSpecTuple] or None
+        self.world_size = comm.get_world().size
+        self.hierarchical = hierarchical  # allreduce.Hierarchical or None
         self.relaxed = bool(relaxed)
         self._stash = None
         self._stash_works = None
@@ -141,11 +145,17 @@ class BucketReducer:
             buf.copy_(view)
         else:
             buf = view
-        pieces = torch.tensor_split(buf, self.shards) if self.shards > 1 else (buf,)
+        if self.spec:
+            alg = allreduce.algorithm_for(self.spec, e - s)
+            name, shards = alg.alg, max(alg.shards, 1)
+        else:
+            name, shards = "nccl", self.shards
+        pieces = torch.tensor_split(buf, shards) if shards > 1 else (buf,)
         for piece in pieces:
             self.launch_count += 1
-            work = comm.all_reduce(piece, op=self.op, async_op=True)
-            self._works.append((work, None, None))
+            works = allreduce.launch_collective(comm, piece, name, b, self.world_size, self.op,
+                                                self.hierarchical)
+            self._works.append((works, None, None))
         self._works[-1] = (self._works[-1][0], buf, view)
 
     def _finish_relaxed(self):
@@ -165,8 +175,8 @@ class BucketReducer:
         if prev_works is None:
             g.zero_()  # first step: nothing reduced yet
         else:
-            for work, buf, view in prev_works:
-                if work is not None:
+            for works, buf, view in prev_works:
+                for work in works:
                     work.wait()
                 if buf is not None and buf is not view:
                     view.copy_(buf)
@@ -183,8 +193,8 @@ class BucketReducer:
         while self._next < len(self.buckets):
             self._launch(self._next)
             self._next += 1
-        for work, buf, view in self._works:
-            if work is not None:
+        for works, buf, view in self._works:
+            for work in works:
                 work.wait()
             if buf is not None and buf is not view:
                 view.copy_(buf)

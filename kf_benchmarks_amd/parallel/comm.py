@@ -184,6 +184,13 @@ def all_reduce(t: torch.Tensor, op: str = "sum", async_op: bool = False):
     return dist.all_reduce(t, op=rop, async_op=async_op)
 
 
+def reduce(t: torch.Tensor, dst: int = 0, op: str = "sum", async_op: bool = False):
+    if not get_world().has_pg:
+        return None
+    rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+    return dist.reduce(t, dst=dst, op=rop, async_op=async_op)
+
+
 def broadcast(t: torch.Tensor, src: int = 0, async_op: bool = False):
     if not get_world().has_pg:
         return None

@@ -43,16 +43,22 @@ class Strategy:
     each_tower_has_variables = True
 
     def __init__(self, params, world: comm.World, flat, bucket_mb=64.0, wire_dtype=None,
-                 overlap=True, tower_scale=1.0, num_buckets=0, relaxed=False, shards=1):
+                 overlap=True, tower_scale=1.0, num_buckets=0, relaxed=False, shards=1,
+                 spec=None, hierarchical=False):
         self.params = params
         self.world = world
         self.flat = flat
         self.tower_scale = float(tower_scale)
         self.reducer: Optional[BucketReducer] = None
         if self.reduces_gradients and world.communicates:
+            hier = None
+            if hierarchical and world.size > 1:
+                from .allreduce import Hierarchical
+                hier = Hierarchical(world.size, world.rank,
+                                    str(getattr(params, "network_topology", "dgx1")))
             self.reducer = BucketReducer(flat, bucket_mb, wire_dtype, overlap=overlap,
                                          num_buckets=num_buckets, relaxed=relaxed,
-                                         shards=shards)
+                                         shards=shards, spec=spec, hierarchical=hier)
 
     @property
     def grad_scale(self) -> float:
@@ -201,14 +207,15 @@ def make_strategy(params, world, flat, tower_mode=False, num_gpus=1):
         tower_scale = 1.0 if vu in MEAN_OVER_TOWERS else float(num_gpus)
     else:
         tower_scale = 1.0
-    shards = 1
+    spec = None
     if params.all_reduce_spec:
         from .allreduce import parse_all_reduce_spec
-        shards = max(s.shards for s in parse_all_reduce_spec(params.all_reduce_spec))
+        spec = parse_all_reduce_spec(params.all_reduce_spec)
     kw = dict(bucket_mb=params.bucket_size_mb, wire_dtype=wire,
               overlap=params.overlap_gradient_allreduce, tower_scale=tower_scale,
               num_buckets=params.gradient_repacking,
-              relaxed=params.variable_consistency == "relaxed", shards=shards)
+              relaxed=params.variable_consistency == "relaxed", spec=spec,
+              hierarchical=bool(params.hierarchical_copy))
     if vu == "independent":
         return IndependentStrategy(params, world, flat, **kw)
     if vu == "kungfu":

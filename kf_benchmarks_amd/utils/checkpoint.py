@@ -267,7 +267,9 @@ class Saver:
     # -- tensors
     def _collect(self) -> Dict[str, object]:
         b = self.bench
-        out = dict(b.net.tf_variables(prefix=self.prefix))
+        with b.flat.real_values():  # staged_vars: save the real variables
+            out = {k: (v.detach().cpu().clone() if torch.is_tensor(v) else v)
+                   for k, v in b.net.tf_variables(prefix=self.prefix).items()}
         out["global_step"] = np.array(b.global_step, dtype=np.int64)
         opt = b.optimizer
         s1n, s2n = _SLOT_NAMES[opt.kind]

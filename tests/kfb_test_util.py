@@ -125,12 +125,14 @@ def get_fake_var_update_inputs():
     return np.resize(127.5 * np.array(range(16)), (16, 1, 1, 1))
 
 
-def manually_compute_losses(inputs, num_workers, params, aggregation):
+def manually_compute_losses(inputs, num_workers, params, aggregation, staged=False):
     """Simulates ``num_workers`` workers on the analytic model.
 
     aggregation: 'sum' (parameter_server/replicated/... all-reduce SUM),
     'mean' (kungfu sync_sgd), 'none' (independent).  Returns losses[w][step]
-    as reported with loss_type_to_report.
+    as reported with loss_type_to_report.  ``staged``: --staged_vars, the
+    loss and gradients of step t use the variables as they were before the
+    previous update (tcb/variable_mgr_util.py:236-393).
     """
     bs = params.batch_size
     n_batches = inputs.shape[0] // bs
@@ -146,16 +148,17 @@ def manually_compute_losses(inputs, num_workers, params, aggregation):
     B = [TestCNNModel.VAR_B_INITIAL_VALUE] * num_workers
     acc = [[0.0, 0.0] for _ in range(num_workers)]
     losses = [[] for _ in range(num_workers)]
+    RA, RB = list(A), list(B)  # staged reads
     for step in range(params.num_batches):
         grads = []
         for w in range(num_workers):
             xb = workers[w][step % n_batches]
             m = xb.mean()
-            a, b = A[w], B[w]
+            a, b = (RA[w], RB[w]) if staged else (A[w], B[w])
             base = m * a * b
             total = base + wd * (a * a + b * b) / 2
             losses[w].append(base if params.loss_type_to_report == "base_loss" else total)
-            grads.append((m * b, m * a))  # data gradient; wd added at update
+            grads.append((m * b, m * a, a, b))  # data gradient; wd added at update
         if aggregation == "sum":
             # every worker's gradient carries its own wd * w term (the
             # reference oracle applies each worker's total-loss gradient,
@@ -168,8 +171,10 @@ def manually_compute_losses(inputs, num_workers, params, aggregation):
         else:
             agg = grads
         for w in range(num_workers):
-            ga = agg[w][0] + wd * A[w]
-            gb = agg[w][1] + wd * B[w]
+            wa, wb = (grads[w][2], grads[w][3]) if staged else (A[w], B[w])
+            ga = agg[w][0] + wd * wa
+            gb = agg[w][1] + wd * wb
+            RA[w], RB[w] = A[w], B[w]
             if params.optimizer == "sgd":
                 A[w] -= lr * ga
                 B[w] -= lr * gb

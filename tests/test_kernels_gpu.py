@@ -266,3 +266,71 @@ def test_linear_fwd_bwd(cuda, cin, cout, x_grad):
         assert err < 2e-2, err
     if not x_grad:
         assert xd.grad is None
+
+
+def _rel_err(got, ref):
+    return float((got.double() - ref.double()).abs().max() / (ref.double().abs().max() + 1e-6))
+
+
+@pytest.mark.parametrize("B,cin,cout", [
+    (128, 25088, 4096),   # VGG-16 fc6 at bs 128 (split-K forward, KS weight operand)
+    (128, 4096, 4096),    # fc7
+    (128, 4096, 1001),    # logits: Cout % 8 != 0 (per-element loads / stores)
+    (512, 9216, 4096),    # AlexNet fc6 at bs 512
+    (37, 203, 77),        # ragged everything
+])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_linear_production_shapes(cuda, B, cin, cout, dt):
+    """The affine op's three GEMMs (csrc/gemm.hip) at the zoo's FC shapes
+    against an fp32 oracle on the same bf16-rounded inputs (torch fp32 on
+    the GPU: this is the reference, not the op under test)."""
+    g = torch.Generator(device="cpu").manual_seed(B + cin + cout)
+    x = torch.randn(B, cin, generator=g).to(cuda, dt)
+    w = (torch.randn(cin, cout, generator=g) / cin ** 0.5).to(cuda)
+    b = torch.randn(cout, generator=g).to(cuda)
+    dy = torch.randn(B, cout, generator=g).to(cuda, dt)
+    wl = w.to(dt)
+    xd = x.clone().requires_grad_(True)
+    wd, bd = w.clone().requires_grad_(), b.clone().requires_grad_()
+    y = F.linear(xd, wd, bd, w_lp=wl, relu=False)
+    y.backward(dy)
+    xf, wf, dyf = x.double(), wl.double(), dy.double()
+    yr = xf @ wf + b.double()
+    lim = 1e-2 if dt == torch.bfloat16 else 1e-5
+    assert _rel_err(y, yr) < lim
+    assert _rel_err(xd.grad, dyf @ wf.t()) < lim
+    assert _rel_err(wd.grad, xf.t() @ dyf) < lim
+    assert _rel_err(bd.grad, dyf.sum(0)) < lim
+
+
+def test_linear_grad_sink_accumulates(cuda):
+    """A FlatParams-managed weight: dW is accumulated in place in the flat
+    gradient view (no autograd tensor returned) and the ready callback fires."""
+    torch.manual_seed(3)
+    x = torch.randn(64, 256, device=cuda).to(torch.bfloat16)
+    w = torch.nn.Parameter(torch.randn(256, 128, device=cuda) / 16)
+    sink = torch.full((256, 128), 0.5, device=cuda)
+    w._kfb_grad_sink = sink
+    fired = []
+    w._kfb_ready_cb = lambda p: fired.append(p)
+    dy = torch.randn(64, 128, device=cuda).to(torch.bfloat16)
+    y = F.linear(x, w, None, w_lp=w.detach().to(torch.bfloat16), relu=False)
+    y.backward(dy)
+    ref = x.float().t() @ dy.float() + 0.5
+    assert _rel_err(sink, ref) < 1e-2 and fired == [w] and w.grad is None
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("shape,r", [((4, 8, 8, 64), 4), ((2, 5, 5, 20), 2), ((3, 3, 3, 96), 5)])
+def test_lrn(cuda, dt, shape, r):
+    torch.manual_seed(1)
+    x = torch.randn(shape) * 2
+    bias, alpha, beta = 1.0, 0.001 / 9.0, 0.75
+    xa, xb = _pair(x, cuda, dt)
+    ya = F.lrn(xa, r, bias, alpha, beta)
+    yb = F.lrn(xb, r, bias, alpha, beta)
+    torch.testing.assert_close(ya.float().cpu(), yb.float(), **tol(dt))
+    dy = torch.randn(shape).to(dt).float()
+    ya.backward(dy.to(cuda, dt))
+    yb.float().backward(dy)
+    torch.testing.assert_close(xa.grad.float().cpu(), xb.grad, **tol(dt))

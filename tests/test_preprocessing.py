@@ -10,7 +10,7 @@ from kf_benchmarks_amd import params as P, runtime
 from kf_benchmarks_amd.data import preprocessing as pre
 from kf_benchmarks_amd.data import test_data
 
-REF_DATA = "/root/reference/scripts/tf_cnn_benchmarks/test_data"
+REF_DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")  # vendored (data/README.md)
 
 
 def _jpeg(value, h=20, w=30):
@@ -76,8 +76,6 @@ def test_color_distortion_identity_and_clip():
     assert out.min() >= 0 and out.max() <= 1
 
 
-@pytest.mark.skipif(not os.path.isdir(os.path.join(REF_DATA, "fake_tf_record_data")),
-                    reason="reference fixtures not present")
 def test_reference_fake_tfrecords_parse():
     """The reference's checked-in fixture shards read through our TFRecord +
     Example parser: 10 classes, each image a flat gray of level
@@ -94,7 +92,7 @@ def test_reference_fake_tfrecords_parse():
             assert 30 <= img.shape[0] <= 299 and 30 <= img.shape[1] <= 299
             assert abs(float(img.mean()) - label * 25.5) < 3
             n += 1
-    assert n == 512 + 128
+    assert n == 64 + 64  # one train + one validation shard
 
 
 def test_generated_fixture_and_batches(tmp_path):
@@ -206,3 +204,38 @@ def test_native_saturation_hue_matches_numpy():
         ref = pp.adjust_hue(pp.adjust_saturation(img, sat), hue)
         out = runtime.adjust_saturation_hue(img.copy(), sat, hue)
         np.testing.assert_allclose(out, ref, rtol=1e-5, atol=2e-6)
+
+
+def test_batch_group_size_stages_groups(tmp_path):
+    """--batch_group_size=3 on the real-data path: batches are staged by the
+    ImageProducer in groups of 3, at most two groups ahead of the consumer
+    (tcb/cnn_util.py:118-198), and training consumes them all."""
+    import kfb_test_util as tu
+    from kf_benchmarks_amd import benchmark
+    from kf_benchmarks_amd.data import input_pipeline
+    data = tmp_path / "data"
+    test_data.write_black_and_white_tfrecord_data(str(data), 2, 48, 16, 2, 1)
+    params = benchmark.make_params(model="trivial", data_name="imagenet", data_dir=str(data),
+                                   batch_size=4, num_warmup_batches=0, device="cpu",
+                                   data_format="NHWC", optimizer="sgd", num_batches=6,
+                                   distortions=False, batch_group_size=3)
+    seen = []
+    orig = input_pipeline.PrefetchInput.__init__
+
+    def init(self, *a, **k):
+        orig(self, *a, **k)
+        seen.append(self)
+    input_pipeline.PrefetchInput.__init__ = init
+    try:
+        with tu.capture_logs() as logs:
+            b = benchmark.BenchmarkCNN(params)
+            b.print_info()
+            stats = b.run()
+    finally:
+        input_pipeline.PrefetchInput.__init__ = orig
+    assert stats["num_steps"] == 6
+    assert any("3 batches per prepocessing group" in line for line in logs)
+    prod = seen[0].producer
+    assert prod is not None and prod.batch_group_size == 3
+    assert prod._consumed >= 6 and prod._produced % 3 == 0
+    assert prod._produced - prod._consumed <= 2 * 3 + 3

@@ -13,7 +13,8 @@ from kf_benchmarks_amd import runtime as rt
 from kf_benchmarks_amd.utils import checkpoint as ck
 from kf_benchmarks_amd.utils import summary as sm
 
-REF_DATA = "/root/reference/scripts/tf_cnn_benchmarks/test_data/fake_tf_record_data"
+REF_DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data",
+                        "fake_tf_record_data")  # vendored reference fixture (data/README.md)
 
 
 def test_crc32c_known_vectors():
@@ -38,7 +39,6 @@ def test_tfrecord_roundtrip(tmp_path):
         list(rt.tf_record_iterator(p))
 
 
-@pytest.mark.skipif(not os.path.isdir(REF_DATA), reason="reference fixtures not mounted")
 def test_reads_reference_tf_written_records():
     n = 0
     labels = set()

@@ -256,3 +256,45 @@ def test_pair_averaging_store_never_tears(tmp_path):
     assert pub["publishes"] > 10 and rd["pulls"] > 10
     assert rd["torn"] == 0, rd
     assert rd["distinct"] > 2  # the reader saw the publisher advancing
+
+
+@pytest.mark.parametrize("opt", ["sgd", "momentum"])
+def test_staged_vars_parameter_server(opt):
+    """--staged_vars (PS mode): step t's loss and gradients use the variables
+    as read one update earlier, checked against the analytic oracle
+    (tcb/benchmark_cnn_test.py:197 _testVariables('parameter_server',
+    staged_vars=True))."""
+    params = tu.get_var_update_params(variable_update="parameter_server", staged_vars=True,
+                                      optimizer=opt, num_batches=6)
+    losses, _ = tu.run_test_model(params)
+    expected = tu.manually_compute_losses(tu.get_fake_var_update_inputs(), 1, params, "sum",
+                                          staged=True)[0]
+    np.testing.assert_allclose(losses, expected, rtol=1e-5, atol=0)
+    plain = tu.manually_compute_losses(tu.get_fake_var_update_inputs(), 1, params, "sum")[0]
+    assert not np.allclose(plain, expected)  # staging changes the trajectory
+
+
+@pytest.mark.parametrize("spec", ["psgpu#2", "pscpu/pscpu", "nccl/xring:64:psgpu"])
+def test_two_workers_all_reduce_specs(spec, tmp_path):
+    """--all_reduce_spec algorithms as process-level collectives (RCCL on the
+    GPU, gloo here): parameter-server reduce+broadcast with rotating roots,
+    sharded pieces, size-ranged choice; same sums as the plain all-reduce."""
+    kw = dict(variable_update="replicated", num_batches=4, all_reduce_spec=spec)
+    res = run_workers(2, kw, tmp_path)
+    params = tu.get_var_update_params(**kw)
+    expected = tu.manually_compute_losses(tu.get_fake_var_update_inputs(), 2, params, "sum")
+    for r in range(2):
+        np.testing.assert_allclose(res[r]["losses"], expected[r], rtol=1e-5, atol=0)
+
+
+def test_hierarchical_copy_eight_workers(tmp_path):
+    """--hierarchical_copy with the DGX-1 topology over 8 ranks: reduce inside
+    {0-3} / {4-7}, all-reduce between the two leaders, broadcast back
+    (tcb/batch_allreduce.py:173-267); same sums as the flat all-reduce."""
+    kw = dict(variable_update="replicated", num_batches=3, hierarchical_copy=True,
+              network_topology="dgx1", bucket_size_mb=1e-5)
+    res = run_workers(8, kw, tmp_path)
+    params = tu.get_var_update_params(**kw)
+    expected = tu.manually_compute_losses(tu.get_fake_var_update_inputs(), 8, params, "sum")
+    for r in range(8):
+        np.testing.assert_allclose(res[r]["losses"], expected[r], rtol=1e-5, atol=0)
