@@ -6,10 +6,13 @@ K-contiguous: an activation row of K is a run of Cin channels per tap, a
 weight column of K is contiguous.
 
 Implementations:
-  * ``hip``   - our gfx950 implicit-GEMM kernels (csrc/conv*.hip) when the
-                shape is supported by them;
-  * ``torch`` - PyTorch/MIOpen on channels-last views (A/B reference only);
-  * CPU       - PyTorch reference (plumbing config and test oracle).
+  * GPU: our gfx950 implicit-GEMM kernels - bf16/fp16 in csrc/conv_igemm.hip
+    (ops/conv_hip.py, with the fused BN epilogues), fp32 in csrc/conv_f32.hip
+    (ops/conv_f32.py).  There is no vendor fallback: a GPU tensor either runs
+    one of these kernels or raises.
+  * ``impl="torch"`` - PyTorch/MIOpen on channels-last views, reachable only
+    from tests as an A/B oracle (the CLI accepts --kernel_impl=hip only).
+  * CPU - PyTorch reference (plumbing config and test oracle).
 """
 
 from __future__ import annotations
@@ -78,11 +81,15 @@ def conv2d(x, w, w_lp, stride, pads, impl="hip", stats=None, w_t=None):
     if not x.is_cuda:
         y = _torch_conv(x.float(), w, stride, pads)
         return y.to(x.dtype).contiguous()
-    if impl == "hip" and _hip_supported(x, w, stride, pads):
+    if impl == "torch":
+        # test oracle only: torch/MIOpen on channels-last views; autograd
+        # routes the weight gradient through the cast back to the fp32 master
+        return _torch_conv(x, w.to(x.dtype), stride, pads).contiguous()
+    if x.dtype == torch.float32:
+        from . import conv_f32
+        return conv_f32.conv2d(x, w, stride, pads)
+    if _hip_supported(x, w, stride, pads):
         from . import conv_hip
         return conv_hip.conv2d(x, w, w_lp, stride, pads, stats, w_t)
-    # torch/MIOpen path on channels-last views; autograd routes the weight
-    # gradient through the cast back to the fp32 master.
-    wl = w.to(x.dtype)
-    y = _torch_conv(x, wl, stride, pads)
-    return y.contiguous()
+    raise N.NativeError("no HIP convolution kernel for a %s tensor of shape %s"
+                        % (x.dtype, tuple(x.shape)))

@@ -3,8 +3,8 @@ NASNet separable convs (role of slim.separable_conv2d / tf.nn.depthwise_conv2d
 in tcb/models/mobilenet_conv_blocks.py and tcb/models/nasnet_utils.py).
 
 Weights are [KH, KW, C] fp32 masters (TF layout [KH, KW, C, 1] on export).
-GPU bf16/fp16: csrc/depthwise.hip (fwd / dgrad / wgrad straight into the
-flat gradient sink).  CPU and fp32: PyTorch grouped conv on NCHW views.
+GPU (bf16 / fp16 / fp32): csrc/depthwise.hip (fwd / dgrad / wgrad straight
+into the flat gradient sink).  CPU: PyTorch grouped conv on NCHW views.
 """
 
 from __future__ import annotations
@@ -90,8 +90,8 @@ class _DepthwiseHip(torch.autograd.Function):
 
 def depthwise_conv2d(x, w, w_lp, stride, pads, impl="hip"):
     """x [N,H,W,C], w [KH,KW,C] -> [N,OH,OW,C]."""
-    if x.is_cuda and impl == "hip" and x.dtype in (torch.bfloat16, torch.float16):
-        return _DepthwiseHip.apply(x, w, w_lp, tuple(stride), tuple(pads))
     if not x.is_cuda:
         return _torch_dw(x.float(), w, stride, pads).to(x.dtype).contiguous()
-    return _torch_dw(x, w.to(x.dtype), stride, pads).contiguous()
+    if impl == "torch":  # test oracle only
+        return _torch_dw(x, w.to(x.dtype), stride, pads).contiguous()
+    return _DepthwiseHip.apply(x, w, w_lp, tuple(stride), tuple(pads))

@@ -202,3 +202,28 @@ def test_depthwise_fwd_bwd(cuda, shape):
     torch.testing.assert_close(xa.grad.float().cpu(), xb.grad, rtol=3e-2, atol=3e-2)
     torch.testing.assert_close(wa.grad.cpu(), wb.grad, rtol=3e-2,
                                atol=2e-2 * wb.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+def test_conv_fp32_fwd_bwd(cuda, shape):
+    """fp32 convs (csrc/conv_f32.hip, exact fp32 MFMA products) vs the CPU
+    fp32 reference: forward, data and weight gradients."""
+    n, H, W, cin, cout, kh, kw, s, mode = shape
+    torch.manual_seed(0)
+    x = torch.randn(n, H, W, cin)
+    w = torch.randn(cout, kh, kw, cin) / (kh * kw * cin) ** 0.5
+    pads = F.resolve_pads(mode, H, W, kh, kw, s, s)
+    xa = x.to(cuda).requires_grad_(True)
+    wa = w.to(cuda).requires_grad_(True)
+    ya = conv_ops.conv2d(xa, wa, None, (s, s), pads, "hip")
+    xb = x.clone().double().requires_grad_(True)
+    wb = w.clone().double().requires_grad_(True)
+    yb = conv_ops._torch_conv(xb, wb, (s, s), pads)
+    assert ya.dtype == torch.float32 and ya.shape == yb.shape
+    dy = torch.randn(yb.shape)
+    ya.backward(dy.to(cuda))
+    yb.backward(dy.double())
+    for got, ref in ((ya, yb), (xa.grad, xb.grad), (wa.grad, wb.grad)):
+        err = float((got.detach().cpu().double() - ref.detach()).abs().max()
+                    / (ref.detach().abs().max() + 1e-12))
+        assert err < 1e-5, err

@@ -149,7 +149,7 @@ def test_pair_averaging_store_never_tears_over_hip_ipc(cuda, tmp_path):
     snapshots, a reader pulling on its side stream; every accepted snapshot
     is uniform."""
     from test_variable_update import _hammer
-    pub, rd = _hammer(tmp_path, "cuda", 16 << 20, 4.0)
+    pub, rd = _hammer(tmp_path, "cuda", 16 << 20, 4.0, pace_us=100)
     assert pub["publishes"] > 10 and rd["pulls"] > 10
     assert rd["torn"] == 0, rd
     assert rd["distinct"] > 2

@@ -140,3 +140,23 @@ def test_deferred_shortcut_bn_network(cuda, monkeypatch):
     cos = sorted(_cos(new[k], ref) for k, ref in copy.items() if ref.norm() > 0)
     print("fused vs separate dual-BN backward cosines: min %.4f median %.4f" % (cos[0], cos[len(cos) // 2]))
     assert cos[len(cos) // 2] > 0.99 and cos[0] > 0.9, (cos[0], cos[len(cos) // 2])
+
+
+def _kernel_names(fn):
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        fn()
+        torch.cuda.synchronize()
+    return {e.name for e in prof.events() if e.device_type.name == "CUDA"}
+
+
+@pytest.mark.parametrize("name,ds,size,batch", [("resnet20", "cifar10", None, 4),
+                                                ("googlenet", "imagenet", 224, 2)])
+def test_fp32_network_runs_only_our_kernels(cuda, name, ds, size, batch):
+    """One GPU path: an fp32 training step launches our HIP kernels (plus
+    torch's own fill/copy/elementwise helpers), never MIOpen or hipBLASLt."""
+    names = _kernel_names(lambda: _grads(name, ds, cuda, torch.float32, size, batch))
+    ours = [n for n in names if "kfb" in n]
+    foreign = [n for n in names if "kfb" not in n and "at::native" not in n
+               and not n.startswith("Memset") and not n.startswith("Memcpy")]
+    assert ours and not foreign, foreign[:10]

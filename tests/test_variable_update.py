@@ -221,7 +221,7 @@ def test_two_workers_relaxed_consistency(tmp_path):
         np.testing.assert_allclose(res[r]["losses"], exp[r], rtol=1e-5, atol=0)
 
 
-def _hammer(tmp_path, device, numel, seconds):
+def _hammer(tmp_path, device, numel, seconds, pace_us=0):
     import json
     import socket
     import subprocess
@@ -238,7 +238,7 @@ def _hammer(tmp_path, device, numel, seconds):
         out = tmp_path / ("hammer%d.json" % r)
         procs.append((subprocess.Popen(
             [sys.executable, os.path.join(root, "tests", "pairavg_hammer.py"), str(out),
-             device, str(numel), str(seconds)], env=env, stdout=subprocess.PIPE,
+             device, str(numel), str(seconds), str(pace_us)], env=env, stdout=subprocess.PIPE,
             stderr=subprocess.STDOUT, text=True), out))
     res = []
     for p, out in procs:
