@@ -130,12 +130,28 @@ class BucketReducer:
                 self._next += 1
 
     def _launch(self, b, src=None):
-        if self.flat.grad.is_cuda:
-            # gradients written on the weight-gradient side stream
-            from ..ops.conv_hip import join_wgrad_stream
-            join_wgrad_stream(self.flat.grad.device)
-        s, e = self.buckets[b]
         g = self.flat.grad if src is None else src
+        ctx = None
+        if g.is_cuda:
+            # A bucket holds gradients written on the compute stream (BN,
+            # affine) and on the weight-gradient side stream (convs).  The
+            # collective is issued FROM the side stream after it has caught
+            # up with the compute stream, so RCCL waits for both while the
+            # compute (dgrad) stream itself never waits for the side stream.
+            from ..ops.conv_hip import wgrad_stream
+            side = wgrad_stream(g.device)
+            cur = torch.cuda.current_stream(g.device)
+            if side is not None and side != cur:
+                side.wait_stream(cur)
+                ctx = torch.cuda.stream(side)
+        if ctx is None:
+            self._launch_on_current(b, g)
+        else:
+            with ctx:
+                self._launch_on_current(b, g)
+
+    def _launch_on_current(self, b, g):
+        s, e = self.buckets[b]
         view = g[s:e]
         if self.wire_dtype is not None:
             k = self._relaxed_step % 2 if self.relaxed else 0

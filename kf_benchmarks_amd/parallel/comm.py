@@ -145,6 +145,8 @@ def init_world(device_type: str = "cuda", all_reduce_spec: Optional[str] = None,
         for k, v in env.items():
             os.environ.setdefault(k, v)
     here = False
+    if backend == "nccl":
+        _reserve_compute_streams(local_rank)
     if not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kwargs = dict(backend=backend, init_method="env://", rank=rank, world_size=size,
@@ -158,6 +160,21 @@ def init_world(device_type: str = "cuda", all_reduce_spec: Optional[str] = None,
         here = True
     _WORLD = World(rank, size, local_rank, dist.get_backend(), here, has_pg=True)
     return _WORLD
+
+
+def _reserve_compute_streams(local_rank: int):
+    """Create the compute side streams (weight-gradient stream) BEFORE the
+    RCCL communicator: HIP maps streams onto a few hardware queues
+    (GPU_MAX_HW_QUEUES, 4 by default) in creation order, and a side stream
+    created after RCCL's streams can land on the compute stream's queue,
+    serializing the weight gradients behind the dgrad chain (measured: the
+    1-rank RCCL run lost the side-stream overlap, 22.5 vs 21.0 ms/step)."""
+    try:
+        torch.cuda.set_device(local_rank)
+        from ..ops import conv_hip
+        conv_hip.wgrad_stream(torch.device("cuda", local_rank))
+    except Exception:  # noqa: BLE001 - best effort; the streams are created lazily anyway
+        pass
 
 
 def _free_port() -> int:

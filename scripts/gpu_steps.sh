@@ -3,7 +3,7 @@
 # time limit; a fault / abort / timeout ends the script (no further GPU work).
 #   usage: scripts/gpu_steps.sh <tag> <step>...
 #   step:  pytest:<pytest args...> | bench:<bench.py args...> | prof:<bench.py args...>
-#          | py:<python args...>
+#          | py:<python args...> | smoke:   (env VAR=value pairs may prefix bench/prof args)
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"
@@ -19,7 +19,8 @@ for spec in "$@"; do
   echo "== step $n $kind: $args"
   case "$kind" in
     pytest) timeout -k 10 900 python -u -m pytest $args -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > "$log" 2>&1 ;;
-    bench) timeout -k 10 600 python bench.py $args > "$log" 2>&1 ;;
+    bench) env $(echo "$args" | tr ' ' '\n' | grep '=' | grep -v '^--') timeout -k 10 600 python bench.py $(echo "$args" | tr ' ' '\n' | grep -v '^[A-Z_]*=' ) > "$log" 2>&1 ;;
+    smoke) timeout -k 10 400 python -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1 ;;
     py) timeout -k 10 600 python $args > "$log" 2>&1 ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
