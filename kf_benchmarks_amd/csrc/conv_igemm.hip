@@ -83,6 +83,11 @@ struct IgArgs {
   // recomputed as xbn * scale + shift > 0 (mcoef = [scale | shift], [2][Ncol])
   // instead of read from its output - BNs without a residual add.
   const float* mcoef;
+  // Forward epilogue of a conv without BN (VGG / AlexNet / GoogLeNet
+  // style): y = act(conv + bias[n]), bias nullable, relu 0/1; never combined
+  // with the statistics or the dgrad-style operands.
+  const float* bias;
+  int relu;
   // FAST path only: byte sizes of x and w (buffer-descriptor range checks)
   int xbytes, wbytes;
   // byte size of the output layout (= that of addend / mask / xbn), or 0 if
@@ -177,11 +182,27 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
   // nothing, and the dgrad-style path issues every extra-operand load (as
   // branch-free range-checked buffer loads) before any store.
   if (!extras) {
+    const bool bact = a.bias || a.relu;
+    float bv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int n = n0 + (tid % CPR) * 8 + k;
+      bv[k] = (a.bias && n < a.Ncol) ? a.bias[n] : 0.f;
+    }
 #pragma unroll
     for (int p = 0; p < NPASS; ++p) {
       const int t = tid + p * NT;
       const int m = m0 + t / CPR, n = n0 + (t % CPR) * 8;
-      const uint4 raw = lds_chunk(t);
+      uint4 raw = lds_chunk(t);
+      if (bact) {
+        Vec<T, 8> tv = __builtin_bit_cast(Vec<T, 8>, raw);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float v = (float)tv.v[k] + bv[k];
+          tv.v[k] = (T)(a.relu ? fmaxf(v, 0.f) : v);
+        }
+        raw = __builtin_bit_cast(uint4, tv);
+      }
       if (m < a.M && n < a.Ncol) {
         if (a.stats) {
           const Vec<T, 8> tv = __builtin_bit_cast(Vec<T, 8>, raw);
@@ -1107,12 +1128,12 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
                                   int pt, int pl, int Ncol, int YH, int YW, int ys, int ldy,
                                   int trans, float* stats, const void* mask, const void* xbn,
                                   const float* mean, const void* addend, const float* mcoef,
-                                  int algo, hipStream_t stream) {
+                                  const float* bias, int relu, int algo, hipStream_t stream) {
   if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
   const long xbytes = (long)N * H * W * C * 2, wbytes = (long)Ncol * KH * KW * C * 2;
   const long ybytes = (long)N * YH * YW * ldy * 2;
   IgArgs a{x, w, y, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
-           N * OH * OW, YH, YW, ys, ldy, stats, mask, xbn, mean, addend, mcoef,
+           N * OH * OW, YH, YW, ys, ldy, stats, mask, xbn, mean, addend, mcoef, bias, relu,
            (int)(xbytes < (1L << 31) ? xbytes : 0), (int)(wbytes < (1L << 31) ? wbytes : 0),
            (int)(ybytes < (1L << 31) ? ybytes : 0)};
   const bool t = trans != 0;

@@ -176,9 +176,15 @@ class ConvNetBuilder:
             from ..ops import conv_hip
             stats = conv_hip.stats_buffer(num_out_channels, x.device)
         layer.stride = (d_height, d_width)
-        y = F.conv2d(x, w, None if self.meta else layer.weight_lp, (d_height, d_width), pads,
-                     self.impl, stats, None if self.meta else layer.weight_t)
         relu = activation == "relu"
+        # conv + bias (+ ReLU) without BN: applied in the conv's epilogue
+        fuse_bact = (not use_batch_norm and residual is None and not self.meta
+                     and activation in ("relu", None, "linear")
+                     and conv_ops.fuses_bias_act(x, self.impl))
+        y = F.conv2d(x, w, None if self.meta else layer.weight_lp, (d_height, d_width), pads,
+                     self.impl, stats, None if self.meta else layer.weight_t,
+                     bias=self._p(layer.bias) if fuse_bact else None,
+                     relu=relu and fuse_bact)
         if defer_bn and _DEFER_BN and use_batch_norm and activation is None and \
                 residual is None and pool is None and stats is not None and y.is_cuda:
             with self.scope(name):
@@ -203,7 +209,8 @@ class ConvNetBuilder:
             if activation not in ("relu", None, "linear"):
                 y = F.activation(y, activation)
         else:
-            y = F.bias_act(y, self._p(layer.bias), relu)
+            if not fuse_bact:
+                y = F.bias_act(y, self._p(layer.bias), relu)
             if residual is not None:
                 y = F.add(y, residual)
             if activation not in ("relu", None, "linear"):

@@ -75,9 +75,18 @@ def runs_hip_kernel(x, impl="hip") -> bool:
     return x.is_cuda and impl == "hip" and x.dtype in (torch.bfloat16, torch.float16)
 
 
-def conv2d(x, w, w_lp, stride, pads, impl="hip", stats=None, w_t=None):
+def fuses_bias_act(x, impl="hip") -> bool:
+    """True when conv2d(..., bias=, relu=) applies bias + ReLU in the conv's
+    own epilogue (the bf16/fp16 HIP kernels)."""
+    return FUSE_BN and runs_hip_kernel(x, impl)
+
+
+def conv2d(x, w, w_lp, stride, pads, impl="hip", stats=None, w_t=None, bias=None, relu=False):
     """NHWC conv.  ``stats``: see fills_bn_stats.  ``w_t``: optional
-    dgrad-ready weight copy (ops.conv_hip.DgradWeights)."""
+    dgrad-ready weight copy (ops.conv_hip.DgradWeights).  ``bias`` / ``relu``:
+    only where fuses_bias_act(x) (y = act(conv + bias) in the epilogue)."""
+    if (bias is not None or relu) and not fuses_bias_act(x, impl):
+        raise ValueError("bias/relu epilogue requested on a path without it")
     if not x.is_cuda:
         y = _torch_conv(x.float(), w, stride, pads)
         return y.to(x.dtype).contiguous()
@@ -90,6 +99,6 @@ def conv2d(x, w, w_lp, stride, pads, impl="hip", stats=None, w_t=None):
         return conv_f32.conv2d(x, w, stride, pads)
     if _hip_supported(x, w, stride, pads):
         from . import conv_hip
-        return conv_hip.conv2d(x, w, w_lp, stride, pads, stats, w_t)
+        return conv_hip.conv2d(x, w, w_lp, stride, pads, stats, w_t, bias, relu)
     raise N.NativeError("no HIP convolution kernel for a %s tensor of shape %s"
                         % (x.dtype, tuple(x.shape)))

@@ -20,7 +20,8 @@ import torch
 
 from . import _native as N
 
-_SIG = [N.I, N.P, N.P, N.P] + [N.I] * 17 + [N.I, N.P, N.P, N.P, N.P, N.P, N.P, N.I, N.P]
+_SIG = ([N.I, N.P, N.P, N.P] + [N.I] * 17 + [N.I, N.P, N.P, N.P, N.P, N.P, N.P]
+        + [N.P, N.I] + [N.I, N.P])  # ... mcoef, bias, relu, algo, stream
 N.register_optional("kfb_conv_igemm", _SIG)
 N.register_optional("kfb_conv_igemm_fast", [N.I] * 4, N.c_int)
 
@@ -117,13 +118,13 @@ def stats_buffer(channels, device):
 
 
 def _igemm_call(algo, x, wmat, y, geo, stats=None, mask=None, xbn=None, mean=None, addend=None,
-                mcoef=None):
+                mcoef=None, bias=None, relu=False):
     N.call("kfb_conv_igemm", N.dt(x), x.data_ptr(), wmat.data_ptr(), y.data_ptr(), *geo,
            N.ptr(stats), N.ptr(mask), N.ptr(xbn), N.ptr(mean), N.ptr(addend), N.ptr(mcoef),
-           algo, N.stream(x.device))
+           N.ptr(bias), int(relu), algo, N.stream(x.device))
 
 
-def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None)):
+def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bact=(None, False)):
     """Per-geometry kernel choice, timed once on the real operands with the
     real fused epilogue (the role cuDNN's algorithm autotune plays for the
     reference): all kernels run the same K order, so the choice does not
@@ -143,7 +144,7 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None)):
         return cands[0]
     stats, mask, xbn, mean, addend, mcoef = fused
     key = (str(x.device), x.dtype, stats is not None, mask is not None, xbn is not None,
-           addend is not None, mcoef is not None) + tuple(geo)
+           addend is not None, mcoef is not None, bact[0] is not None, bool(bact[1])) + tuple(geo)
     best = _ig_tuned.get(key)
     if best is not None:
         return best
@@ -155,7 +156,7 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None)):
     sstats = torch.zeros_like(stats) if stats is not None else None
     times = {}
     for algo in cands:
-        args = (x, wmat, scratch, geo, sstats, mask, xbn, mean, addend, mcoef)
+        args = (x, wmat, scratch, geo, sstats, mask, xbn, mean, addend, mcoef) + tuple(bact)
         _igemm_call(algo, *args)  # warm
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
@@ -170,15 +171,18 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None)):
 
 
 def _igemm(x, wmat, y, N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy,
-           trans, stats=None, mask=None, xbn=None, mean=None, addend=None, mcoef=None):
+           trans, stats=None, mask=None, xbn=None, mean=None, addend=None, mcoef=None,
+           bias=None, relu=False):
     geo = (N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy, int(trans))
-    algo = _igemm_algo(x, wmat, y, geo, (stats, mask, xbn, mean, addend, mcoef))
-    _igemm_call(algo, x, wmat, y, geo, stats, mask, xbn, mean, addend, mcoef)
+    algo = _igemm_algo(x, wmat, y, geo, (stats, mask, xbn, mean, addend, mcoef), (bias, relu))
+    _igemm_call(algo, x, wmat, y, geo, stats, mask, xbn, mean, addend, mcoef, bias, relu)
 
 
-def conv_fwd(x, wl, stride, pads, stats=None):
+def conv_fwd(x, wl, stride, pads, stats=None, bias=None, relu=False):
     """x [N,H,W,C] (C%8==0), wl [Cout,KH,KW,C] compute dtype -> y [N,OH,OW,Cout].
-    ``stats``: optional zeroed stats_buffer(Cout) receiving sum(y), sum(y^2)."""
+    ``stats``: optional zeroed stats_buffer(Cout) receiving sum(y), sum(y^2).
+    ``bias`` (fp32 [Cout], nullable) / ``relu``: y = act(conv + bias) in the
+    epilogue (convs without BN; not combined with ``stats``)."""
     n, H, W, C = x.shape
     cout, KH, KW, _ = wl.shape
     sh, sw = stride
@@ -187,7 +191,7 @@ def conv_fwd(x, wl, stride, pads, stats=None):
     OW = (W + pl + pr - KW) // sw + 1
     y = torch.empty((n, OH, OW, cout), dtype=x.dtype, device=x.device)
     _igemm(x, wl, y, n, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, cout, OH, OW, 1, cout, False,
-           stats)
+           stats, bias=bias, relu=relu)
     return y
 
 
@@ -422,18 +426,23 @@ def s2d_weight_grad(dw2, wl_shape):
 
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, wl, stride, pads, stats, wt):
+    def forward(ctx, x, w, wl, stride, pads, stats, wt, bias=None, relu=False):
         x = x.contiguous()
         if wl is None or wl.dtype != x.dtype:
             wl = w.detach().to(x.dtype)
         cin = x.shape[-1]
         cout = wl.shape[0]
         ctx.s2d = None
+        # bias + ReLU in the forward epilogue; their backward (ReLU mask and
+        # bias column sums) runs as one pass at the top of this backward
+        ctx.bact = bias is not None or relu
+        ctx.relu, ctx.bias = bool(relu), bias
+        bd = bias.detach() if bias is not None else None
         if use_s2d(x, wl.shape, stride, ctx.needs_input_grad[0], pads):
             x2 = s2d_input(x, wl.shape, pads)
             w2 = s2d_weight(wl).contiguous()
-            y = conv_fwd(x2, w2, (1, 1), (0, 0, 0, 0), stats)
-            ctx.save_for_backward(x2, w2)
+            y = conv_fwd(x2, w2, (1, 1), (0, 0, 0, 0), stats, bd, relu)
+            ctx.save_for_backward(x2, w2, y if relu else None)
             ctx.s2d = tuple(wl.shape)
             ctx.w = w
             return y
@@ -445,11 +454,13 @@ class _Conv2d(torch.autograd.Function):
         if cout_p != cout:
             wp = torch.nn.functional.pad(wp, (0, 0, 0, 0, 0, 0, 0, cout_p - cout))
             stats = None
+            if bd is not None:
+                bd = torch.nn.functional.pad(bd, (0, cout_p - cout))
         wp = wp.contiguous()
-        y = conv_fwd(xp, wp, stride, pads, stats)
+        y = conv_fwd(xp, wp, stride, pads, stats, bd, relu)
         if cout_p != cout:
             y = y[..., :cout].contiguous()
-        ctx.save_for_backward(xp, wp)
+        ctx.save_for_backward(xp, wp, y if relu else None)
         ctx.meta = (stride, pads, cin, cout, x.shape)
         ctx.x_needs_grad = ctx.needs_input_grad[0]
         ctx.w = w
@@ -459,9 +470,12 @@ class _Conv2d(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        db = None
+        if ctx.bact:
+            dy, db = _bias_act_backward(dy, ctx.saved_tensors[2], ctx.relu, ctx.bias)
         if ctx.s2d is not None:
-            return _Conv2d._backward_s2d(ctx, dy)
-        xp, wp = ctx.saved_tensors
+            return _Conv2d._backward_s2d(ctx, dy) + (db, None)
+        xp, wp = ctx.saved_tensors[:2]
         stride, pads, cin, cout, x_shape = ctx.meta
         dy = dy.contiguous()
         cout_p = wp.shape[0]
@@ -531,7 +545,7 @@ class _Conv2d(torch.autograd.Function):
                     cb = getattr(w, "_kfb_ready_cb", None)
                     if cb is not None:
                         cb(w)
-                return dx, None, None, None, None, None, None
+                return dx, None, None, None, None, None, None, db, None
             dw = conv_wgrad(dy, xp, wp.shape, stride, pads, out=sink if direct else None)
             if direct:
                 cb = getattr(w, "_kfb_ready_cb", None)
@@ -540,12 +554,12 @@ class _Conv2d(torch.autograd.Function):
                 dw = None
             elif dw.shape[0] != cout or dw.shape[-1] != cin:
                 dw = dw[:cout, :, :, :cin].contiguous()
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, db, None
 
 
     @staticmethod
     def _backward_s2d(ctx, dy):
-        x2, w2 = ctx.saved_tensors
+        x2, w2 = ctx.saved_tensors[:2]
         dw = None
         if ctx.needs_input_grad[1]:
             dw2 = conv_wgrad(dy.contiguous(), x2, w2.shape, (1, 1), (0, 0, 0, 0))
@@ -563,8 +577,34 @@ class _Conv2d(torch.autograd.Function):
         return None, dw, None, None, None, None, None
 
 
-def conv2d(x, w, wl, stride, pads, stats=None, wt=None):
-    return _Conv2d.apply(x, w, wl, tuple(stride), tuple(pads), stats, wt)
+def _bias_act_backward(dy, y, relu, bias):
+    """ReLU backward (mask from the saved output) and the bias gradient as
+    one pass (kfb_act_bwd_bias); the bias gradient accumulates straight into
+    the flat-gradient view when the bias has one."""
+    dy = dy.contiguous()
+    C = dy.shape[-1]
+    rows = dy.numel() // C
+    g = torch.empty_like(dy) if relu else dy
+    pb = dbuf = None
+    nslab = 1
+    sink = getattr(bias, "_kfb_grad_sink", None) if bias is not None else None
+    if bias is not None:
+        nslab = N.query("kfb_colsum_num_slabs", rows, C)
+        pb = torch.empty((nslab * C,), dtype=torch.float32, device=dy.device)
+        dbuf = sink if sink is not None else torch.empty((C,), dtype=torch.float32,
+                                                         device=dy.device)
+    N.call("kfb_act_bwd_bias", N.dt(dy), dy.data_ptr(), N.ptr(y), g.data_ptr(), rows, C,
+           int(relu), N.ptr(pb), nslab, N.ptr(dbuf), int(sink is not None), N.stream(dy.device))
+    if sink is not None:
+        cb = getattr(bias, "_kfb_ready_cb", None)
+        if cb is not None:
+            cb(bias)
+        return g, None
+    return g, dbuf
+
+
+def conv2d(x, w, wl, stride, pads, stats=None, wt=None, bias=None, relu=False):
+    return _Conv2d.apply(x, w, wl, tuple(stride), tuple(pads), stats, wt, bias, bool(relu))
 
 
 N.register_optional("kfb_wtrans_item_bytes", [], N.c_int)

@@ -61,11 +61,13 @@ def resolve_pads(mode: str, H: int, W: int, kh: int, kw: int, sh: int, sw: int) 
 
 # ------------------------------------------------------------------------ conv
 def conv2d(x, w, w_lp, stride: Tuple[int, int], pads: Pads, impl: str = "hip",
-           stats: Optional[torch.Tensor] = None, w_t: Optional[torch.Tensor] = None):
-    """NHWC convolution, no bias.  ``w_lp`` is the compute-dtype copy of the
-    fp32 master ``w`` (None -> cast on the fly).  ``stats`` (GPU): zeroed
-    [2*32*Cout] fp32 buffer that receives the BN statistics of the output."""
-    return _conv.conv2d(x, w, w_lp, stride, pads, impl, stats, w_t)
+           stats: Optional[torch.Tensor] = None, w_t: Optional[torch.Tensor] = None,
+           bias: Optional[torch.Tensor] = None, relu: bool = False):
+    """NHWC convolution.  ``w_lp`` is the compute-dtype copy of the fp32
+    master ``w`` (None -> cast on the fly).  ``stats`` (GPU): zeroed
+    [2*32*Cout] fp32 buffer that receives the BN statistics of the output.
+    ``bias`` / ``relu``: fused epilogue where ops.conv.fuses_bias_act(x)."""
+    return _conv.conv2d(x, w, w_lp, stride, pads, impl, stats, w_t, bias, relu)
 
 
 # ------------------------------------------------------------------ batch norm

@@ -227,3 +227,45 @@ def test_conv_fp32_fwd_bwd(cuda, shape):
         err = float((got.detach().cpu().double() - ref.detach()).abs().max()
                     / (ref.detach().abs().max() + 1e-12))
         assert err < 1e-5, err
+
+
+BACT_SHAPES = [
+    (2, 14, 14, 64, 256, 3, 3, 1, "SAME"),
+    (2, 17, 17, 3, 64, 3, 3, 1, "SAME"),          # RGB input (channel pad)
+    (2, 13, 13, 96, 36, 1, 1, 1, "SAME"),         # Cout not a multiple of 8
+    (2, 32, 32, 3, 64, 7, 7, 2, "SAME_RESNET"),   # s2d stem path
+]
+
+
+@pytest.mark.parametrize("shape", BACT_SHAPES, ids=[str(s) for s in BACT_SHAPES])
+@pytest.mark.parametrize("relu", [True, False])
+def test_conv_bias_relu_epilogue(cuda, shape, relu):
+    """conv + bias (+ ReLU) fused in the forward epilogue (VGG/AlexNet-style
+    layers without BN); backward = one mask + bias-sum pass, then dgrad /
+    wgrad; vs the fp32 CPU reference."""
+    n, H, W, cin, cout, kh, kw, s, mode = shape
+    torch.manual_seed(2)
+    dt = torch.bfloat16
+    x = torch.randn(n, H, W, cin).to(dt).float()
+    w = (torch.randn(cout, kh, kw, cin) / (kh * kw * cin) ** 0.5).to(dt).float()
+    b = torch.randn(cout) * 0.3
+    pads = F.resolve_pads(mode, H, W, kh, kw, s, s)
+    xa = x.to(cuda, dt).requires_grad_(True)
+    wa = w.to(cuda).requires_grad_(True)
+    ba = b.to(cuda).requires_grad_(True)
+    assert conv_ops.fuses_bias_act(xa)
+    ya = conv_ops.conv2d(xa, wa, wa.detach().to(dt), (s, s), pads, "hip", bias=ba, relu=relu)
+    xb, wb, bb = (t.clone().requires_grad_(True) for t in (x, w, b))
+    ylin = conv_ops.conv2d_reference(xb, wb, (s, s), pads) + bb
+    yb = torch.relu(ylin) if relu else ylin
+    torch.testing.assert_close(ya.float().cpu(), yb.detach(), rtol=2e-2, atol=2e-2)
+    dy = torch.randn(yb.shape).to(dt).float()
+    ya.backward(dy.to(cuda, dt))
+    # the ReLU mask of the kernel's own (bf16-rounded) output decides ties at 0
+    mask = (ya.detach().float().cpu() > 0).float() if relu else 1.0
+    ylin.backward(dy * mask)
+    scale = dy.abs().mean().item()
+    torch.testing.assert_close(xa.grad.float().cpu(), xb.grad, rtol=3e-2, atol=3e-2 * scale * 4)
+    torch.testing.assert_close(wa.grad.cpu(), wb.grad, rtol=3e-2,
+                               atol=2e-2 * wb.grad.abs().max().item())
+    torch.testing.assert_close(ba.grad.cpu(), bb.grad, rtol=2e-2, atol=2e-2 * scale * 50)
