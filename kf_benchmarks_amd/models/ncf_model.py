@@ -21,10 +21,20 @@ import math
 import torch
 from torch import nn
 
+from ..ops import nn as F_ops
 from . import model as model_lib
 
 NUM_USERS_20M = 138493
 NUM_ITEMS_20M = 26744
+
+
+class _Dense(nn.Module):
+    """Dense layer with the TF variable layout: kernel [in, out], bias [out]."""
+
+    def __init__(self, fan_in, fan_out, device):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(fan_in, fan_out, device=device))
+        self.bias = nn.Parameter(torch.zeros(fan_out, device=device))
 
 
 class NeuMF(nn.Module):
@@ -37,26 +47,31 @@ class NeuMF(nn.Module):
         self.mlp_user = nn.Embedding(num_users, half, device=device)
         self.mlp_item = nn.Embedding(num_items, half, device=device)
         dims = [layers[0]] + list(layers[1:])
-        self.mlp = nn.ModuleList(nn.Linear(a, b, device=device) for a, b in zip(dims[:-1], dims[1:]))
-        self.predict = nn.Linear(mf_dim + dims[-1], 1, device=device)
+        self.mlp = nn.ModuleList(_Dense(a, b, device) for a, b in zip(dims[:-1], dims[1:]))
+        self.predict = _Dense(mf_dim + dims[-1], 1, device)
         with torch.no_grad():
             for emb in (self.mf_user, self.mf_item, self.mlp_user, self.mlp_item):
                 emb.weight.copy_(torch.randn(emb.weight.shape, generator=gen) * 0.01)
             for lin in list(self.mlp) + [self.predict]:
                 # glorot uniform for the hidden layers, lecun uniform for the logit
-                fan_in, fan_out = lin.weight.shape[1], lin.weight.shape[0]
+                fan_in, fan_out = lin.weight.shape
                 lim = (math.sqrt(3.0 / fan_in) if lin is self.predict
                        else math.sqrt(6.0 / (fan_in + fan_out)))
                 lin.weight.copy_((torch.rand(lin.weight.shape, generator=gen) * 2 - 1) * lim)
                 lin.bias.zero_()
 
     def forward(self, inputs, phase_train=True):
-        users, items = inputs[0].long(), inputs[1].long()
-        gmf = self.mf_user(users) * self.mf_item(items)
-        h = torch.cat([self.mlp_user(users), self.mlp_item(items)], dim=1)
+        # embedding lookups, GMF product, dense layers and concats on our
+        # kernels (ops.nn); the tables are [rows, dim] like the official model
+        users, items = inputs[0], inputs[1]
+        emb = F_ops.embedding
+        gmf = emb(users, self.mf_user.weight) * emb(items, self.mf_item.weight)
+        h = F_ops.concat_channels([emb(users, self.mlp_user.weight),
+                                   emb(items, self.mlp_item.weight)])
         for lin in self.mlp:
-            h = torch.relu(lin(h))
-        logits = self.predict(torch.cat([gmf, h], dim=1))
+            h = F_ops.linear(h, lin.weight, lin.bias, relu=True)
+        logits = F_ops.linear(F_ops.concat_channels([gmf, h]), self.predict.weight,
+                              self.predict.bias)
         return model_lib.BuildNetworkResult(logits=logits, extra_info=None)
 
 
@@ -90,8 +105,8 @@ class NcfModel(model_lib.ModuleModel):
     def loss_function(self, inputs, build_network_result):
         logits = build_network_result.logits.float()
         # softmax over [1, logit] (kept as the official model does)
-        logits = torch.cat([torch.ones_like(logits), logits], dim=1)
-        return torch.nn.functional.cross_entropy(logits, inputs[2].long())
+        logits = F_ops.concat_channels([torch.ones_like(logits), logits])
+        return F_ops.softmax_cross_entropy(logits, inputs[2])
 
     def accuracy_function(self, inputs, logits):
         pred = (logits.float().reshape(-1) > 1.0).to(torch.int32)

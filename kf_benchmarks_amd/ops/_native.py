@@ -64,6 +64,9 @@ _SIGS = {
     "kfb_gemm_splits": [I, I, I, I],
     "kfb_lrn_fwd": [I, P, P, L, I, I, F, F, F, P],
     "kfb_lrn_bwd": [I, P, P, P, L, I, I, F, F, F, P],
+    "kfb_embedding_fwd": [I, P, L, P, P, L, I, P],
+    "kfb_embedding_bwd": [I, P, P, P, L, L, I, P],
+    "kfb_concat": [I, P, P, P, I, L, I, I, I, P],
 }
 _RESTYPES = {"kfb_bn_num_slabs": c_int, "kfb_colsum_num_slabs": c_int,
              "kfb_gemm_splits": c_int}

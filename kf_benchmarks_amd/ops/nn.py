@@ -954,5 +954,94 @@ def synthetic_labels(n, nclass, device, seed: int):
     return y
 
 
+class _Concat(torch.autograd.Function):
+    """Channel (last-dim) concat on the GPU (csrc/gather.hip): one launch
+    for all inputs; the backward splits the gradient in one launch."""
+
+    @staticmethod
+    def forward(ctx, *xs):
+        import ctypes
+        xs = [x.contiguous() for x in xs]
+        widths = [x.shape[-1] for x in xs]
+        offs = [0]
+        for w in widths:
+            offs.append(offs[-1] + w)
+        rows = xs[0].numel() // widths[0]
+        out = torch.empty(xs[0].shape[:-1] + (offs[-1],), dtype=xs[0].dtype, device=xs[0].device)
+        ctx.meta = (widths, offs, rows)
+        _concat_call(out, xs, offs, rows, split=False)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        widths, offs, rows = ctx.meta
+        dy = dy.contiguous()
+        dxs = [torch.empty(dy.shape[:-1] + (w,), dtype=dy.dtype, device=dy.device)
+               for w in widths]
+        _concat_call(dy, dxs, offs, rows, split=True)
+        return tuple(dxs)
+
+
+def _concat_call(out, parts, offs, rows, split):
+    import ctypes
+    k = len(parts)
+    esz = out.element_size()
+    epv = 16 // esz
+    vec = all(w % epv == 0 for w in (offs[j + 1] - offs[j] for j in range(k))) and \
+        all(t.data_ptr() % 16 == 0 for t in list(parts) + [out])
+    ptrs = (ctypes.c_void_p * k)(*[t.data_ptr() for t in parts])
+    offa = (ctypes.c_int * (k + 1))(*offs)
+    N.call("kfb_concat", N.dt(out), out.data_ptr(), ptrs, offa, k, rows, offs[-1], int(vec),
+           int(split), N.stream(out.device))
+
+
+_CAT_MAX = 16
+
+
 def concat_channels(xs: Sequence[torch.Tensor]):
-    return torch.cat(list(xs), dim=-1)
+    xs = list(xs)
+    if (xs[0].is_cuda and 1 < len(xs) <= _CAT_MAX
+            and all(x.dtype == xs[0].dtype and x.shape[:-1] == xs[0].shape[:-1] for x in xs)):
+        return _Concat.apply(*xs)
+    if len(xs) == 1:
+        return xs[0]
+    if xs[0].is_cuda:
+        raise N.NativeError("no HIP concat for %d inputs" % len(xs))
+    return torch.cat(xs, dim=-1)
+
+
+# ------------------------------------------------------------------ embedding
+class _Embedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, table):
+        idx = idx.to(torch.int32).contiguous()
+        rows, dim = table.shape
+        out = torch.empty((idx.numel(), dim), dtype=table.dtype, device=table.device)
+        N.call("kfb_embedding_fwd", N.dt(table), table.data_ptr(), rows, idx.data_ptr(),
+               out.data_ptr(), idx.numel(), dim, N.stream(table.device))
+        ctx.save_for_backward(idx)
+        ctx.table, ctx.shape = table, tuple(table.shape)
+        return out.view(tuple(idx.shape) + (dim,))
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        rows, dim = ctx.shape
+        dy = dy.contiguous()
+        sink = _grad_sink(ctx.table)
+        grad = sink if sink is not None else torch.zeros(ctx.shape, dtype=torch.float32,
+                                                         device=dy.device)
+        N.call("kfb_embedding_bwd", N.dt(dy), dy.data_ptr(), idx.data_ptr(), grad.data_ptr(),
+               rows, idx.numel(), dim, N.stream(dy.device))
+        if sink is not None:
+            _grad_ready(ctx.table)
+            return None, None
+        return None, grad
+
+
+def embedding(idx, table):
+    """tf.nn.embedding_lookup: rows of ``table`` [rows, dim] at ``idx``.  GPU:
+    csrc/gather.hip (gradient scatter-added into the flat-gradient view)."""
+    if table.is_cuda:
+        return _Embedding.apply(idx, table)
+    return F.embedding(idx.long(), table)

@@ -334,3 +334,38 @@ def test_lrn(cuda, dt, shape, r):
     ya.backward(dy.to(cuda, dt))
     yb.float().backward(dy)
     torch.testing.assert_close(xa.grad.float().cpu(), xb.grad, **tol(dt))
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("widths", [(64, 128, 32), (3, 5, 8, 1), (96, 96), (16,) * 16])
+def test_concat_channels(cuda, dt, widths):
+    """Channel concat (csrc/gather.hip) and its split backward vs torch.cat."""
+    torch.manual_seed(4)
+    xs = [torch.randn(3, 5, 7, w) for w in widths]
+    xa = [x.to(cuda, dt).requires_grad_(True) for x in xs]
+    y = F.concat_channels(xa)
+    ref = torch.cat([x.to(dt) for x in xs], dim=-1)
+    assert torch.equal(y.cpu(), ref)
+    dy = torch.randn(ref.shape).to(dt)
+    y.backward(dy.to(cuda))
+    off = 0
+    for x, w in zip(xa, widths):
+        assert torch.equal(x.grad.cpu(), dy[..., off:off + w])
+        off += w
+
+
+@pytest.mark.parametrize("dim", [64, 128, 5])
+def test_embedding_lookup_and_grad(cuda, dim):
+    """Embedding gather and the scatter-add gradient (repeated ids) vs torch."""
+    torch.manual_seed(5)
+    rows = 1000
+    table = torch.randn(rows, dim)
+    idx = torch.randint(0, rows, (4096,), dtype=torch.int32)
+    idx[:100] = 7  # many duplicates -> atomics on one row
+    ta = table.to(cuda).requires_grad_(True)
+    y = F.embedding(idx.to(cuda), ta)
+    assert torch.equal(y.cpu(), table[idx.long()])
+    dy = torch.randn(4096, dim)
+    y.backward(dy.to(cuda))
+    ref = torch.zeros(rows, dim).index_add_(0, idx.long(), dy)
+    torch.testing.assert_close(ta.grad.cpu(), ref, rtol=1e-5, atol=1e-4)
