@@ -1,7 +1,7 @@
 #!/bin/bash
 # Short 1-GPU training runs of the model zoo (bf16, synthetic data).  Each
 # model runs under its own time limit; a fault/timeout stops the script.
-#   usage: scripts/zoo_bench.sh <tag> [model:batch ...]
+#   usage: scripts/zoo_bench.sh <tag> [model:batch[:extra,bench,args] ...]
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"
@@ -11,9 +11,10 @@ mkdir -p "$OUT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 MODELS="${*:-mobilenet:128 nasnet:64 official_resnet50:128 resnet152:128 vgg16:128 inception3:128 googlenet:128 alexnet:512}"
 for mb in $MODELS; do
-  m="${mb%%:*}"; b="${mb##*:}"
-  echo "== $m bs $b"
-  timeout -k 10 300 python bench.py --model "$m" --batch_size "$b" --steps 10 --warmup 3 \
+  IFS=: read -r m b extra <<< "$mb"
+  extra="${extra//,/ }"
+  echo "== $m bs $b $extra"
+  timeout -k 10 300 python bench.py --model "$m" --batch_size "$b" --steps 10 --warmup 3 $extra \
       > "$OUT/$m.log" 2>&1
   rc=$?
   tail -n 1 "$OUT/$m.log"
