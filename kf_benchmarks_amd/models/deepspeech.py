@@ -20,6 +20,7 @@ import torch
 from torch import nn
 
 from .. import cnn_util
+from ..ops import nn as F_ops
 from . import model as model_lib
 
 SPEECH_LABELS = " abcdefghijklmnopqrstuvwxyz'-"
@@ -63,22 +64,45 @@ class DeepSpeechDecoder:
         return self.decode(list(np.argmax(logits, axis=1)))
 
 
+class _BN(nn.Module):
+    """Batch norm over the last (channel) dim of an NHWC-style tensor on our
+    kernels (ops.nn.batch_norm); decay / epsilon of the reference."""
+
+    def __init__(self, c, device, decay=0.997, eps=1e-5):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(c, device=device))
+        self.bias = nn.Parameter(torch.zeros(c, device=device))
+        self.register_buffer("running_mean", torch.zeros(c, device=device))
+        self.register_buffer("running_var", torch.ones(c, device=device))
+        self.decay, self.eps = decay, eps
+
+    def forward(self, x):
+        shape = x.shape
+        y = F_ops.batch_norm(x.reshape(-1, 1, 1, shape[-1]), self.weight, self.bias,
+                             self.running_mean, self.running_var, self.decay, self.eps,
+                             self.training)
+        return y.reshape(shape)
+
+
 class _ConvBN(nn.Module):
+    """conv (NHWC, our implicit-GEMM kernels) -> relu6 -> BN, as the reference
+    (tcb/models/experimental/deepspeech.py:155-170)."""
+
     def __init__(self, cin, cout, k, stride, pad, gen, device):
         super().__init__()
         self.pad = pad
         self.stride = stride
         fan_in, fan_out = cin * k[0] * k[1], cout * k[0] * k[1]
         lim = (6.0 / (fan_in + fan_out)) ** 0.5
-        w = (torch.rand((cout, cin, k[0], k[1]), generator=gen) * 2 - 1) * lim
-        self.weight = nn.Parameter(w.to(device))
-        self.bn = nn.BatchNorm2d(cout, eps=1e-5, momentum=1 - 0.997, device=device)
+        w = (torch.rand((cout, k[0], k[1], cin), generator=gen) * 2 - 1) * lim
+        self.weight = nn.Parameter(w.to(device))  # [Cout, KH, KW, Cin]
+        self.bn = _BN(cout, device)
 
-    def forward(self, x):  # x NCHW
-        y = torch.nn.functional.conv2d(x, self.weight.to(x.dtype), stride=self.stride,
-                                       padding=self.pad)
+    def forward(self, x):  # x NHWC [B, T, F, C]
+        ph, pw = self.pad
+        y = F_ops.conv2d(x, self.weight, None, self.stride, (ph, ph, pw, pw))
         y = torch.clamp(y, 0.0, 6.0)  # relu6 before BN, as the reference
-        return self.bn(y.float()).to(x.dtype)
+        return self.bn(y)
 
 
 class DeepSpeech2(nn.Module):
@@ -95,34 +119,31 @@ class DeepSpeech2(nn.Module):
         self.bns = nn.ModuleList()
         din = f * 32
         for i in range(num_rnn_layers):
-            self.bns.append(nn.BatchNorm1d(din, eps=1e-5, momentum=1 - 0.997, device=device)
-                            if i > 0 else nn.Identity())
+            self.bns.append(_BN(din, device) if i > 0 else nn.Identity())
             self.rnns.append(rnn_cls(din, hidden, batch_first=True, bidirectional=bidirectional,
                                      device=device))
             din = hidden * dirs
-        self.final_bn = nn.BatchNorm1d(din, eps=1e-5, momentum=1 - 0.997, device=device)
-        self.fc = nn.Linear(din, nclass, bias=use_bias, device=device)
-
-    @staticmethod
-    def _bn_seq(bn, x):
-        if isinstance(bn, nn.Identity):
-            return x
-        B, T, C = x.shape
-        return bn(x.reshape(B * T, C)).reshape(B, T, C)
+        self.final_bn = _BN(din, device)
+        # dense logits in the TF [in, out] layout, on the affine GEMM
+        self.fc_weight = nn.Parameter(
+            (torch.randn((din, nclass), generator=gen) / din ** 0.5).to(device))
+        self.fc_bias = nn.Parameter(torch.zeros(nclass, device=device)) if use_bias else None
 
     def forward(self, inputs, phase_train=True):
         self.train(phase_train)
         x = inputs[0]  # [B, T, F, 1] (NHWC)
-        x = x.permute(0, 3, 1, 2)  # NCHW [B, 1, T, F]
         x = self.conv2(self.conv1(x))
-        B, C, T, F = x.shape
-        x = x.permute(0, 2, 3, 1).reshape(B, T, F * C).float()
+        B, T, F, C = x.shape
+        # the reference flattens [F, C] per time step (channels-last)
+        x = x.reshape(B, T, F * C)
+        rnn_dtype = next(self.rnns[0].parameters()).dtype
         for bn, rnn in zip(self.bns, self.rnns):
-            x = self._bn_seq(bn, x)
-            x, _ = rnn(x)
-        x = self._bn_seq(self.final_bn, x)
-        logits = self.fc(x)
-        return model_lib.BuildNetworkResult(logits=logits, extra_info=None)
+            x = bn(x)
+            # the recurrent layers run through torch's LSTM (MIOpen on the GPU)
+            x, _ = rnn(x.to(rnn_dtype))
+        x = self.final_bn(x.to(inputs[0].dtype))
+        logits = F_ops.linear(x.reshape(B * T, -1), self.fc_weight, self.fc_bias)
+        return model_lib.BuildNetworkResult(logits=logits.reshape(B, T, -1), extra_info=None)
 
 
 class DeepSpeech2Model(model_lib.ModuleModel):

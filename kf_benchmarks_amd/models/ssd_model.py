@@ -19,6 +19,7 @@ import numpy as np
 import torch
 
 from .. import cnn_util, datasets
+from ..ops import nn as F_ops
 from . import model as model_lib
 from . import resnet_model
 from . import ssd_dataloader as sd
@@ -140,33 +141,14 @@ class SSD300Model(model_lib.CNNModel):
         return lr * 0.01
 
     def loss_function(self, inputs, build_network_result):
-        logits = build_network_result.logits.float()
-        pred_loc, pred_label = logits[..., :4], logits[..., 4:]
+        """Classification (softmax xent + 3:1 hard-negative mining) plus
+        smooth-L1 box loss, each normalised by the matched-box count and
+        averaged over the batch (tcb/models/ssd_model.py loss_function).  On
+        the GPU this is the fused kernel trio of csrc/ssd_loss.hip reading
+        the bf16 logits directly; ops.ssd_loss_reference is the tensor form."""
         _, gt_loc, gt_label, num_gt = inputs[:4]
-        gt_label = gt_label.reshape(gt_label.shape[0], -1).long()
-        num_gt = num_gt.float()
-        return (self._classification_loss(pred_label, gt_label, num_gt) +
-                self._localization_loss(pred_loc, gt_loc.float(), gt_label, num_gt))
-
-    @staticmethod
-    def _localization_loss(pred_loc, gt_loc, gt_label, num_matched):
-        mask = (gt_label > 0).float()
-        sl1 = torch.nn.functional.smooth_l1_loss(pred_loc, gt_loc, reduction="none",
-                                                 beta=1.0).sum(2)
-        return ((sl1 * mask).sum(1) / num_matched).mean()
-
-    @staticmethod
-    def _classification_loss(pred_label, gt_label, num_matched):
-        B, A, C = pred_label.shape
-        ce = torch.nn.functional.cross_entropy(pred_label.reshape(-1, C),
-                                               gt_label.reshape(-1).clamp(0, C - 1),
-                                               reduction="none").reshape(B, A)
-        pos = (gt_label > 0).float()
-        neg_ce = ce * (1 - pos)
-        rank = neg_ce.argsort(dim=1, descending=True).argsort(dim=1)
-        num_neg = torch.clamp(num_matched.long() * sd.NEGS_PER_POSITIVE, max=sd.NUM_SSD_BOXES)
-        neg = (rank < num_neg[:, None]).float()
-        return ((ce * (pos + neg)).sum(1) / num_matched).mean()
+        return F_ops.ssd_loss(build_network_result.logits, gt_loc, gt_label, num_gt,
+                              sd.NEGS_PER_POSITIVE)
 
     # -------------------------------------------------------------- eval
     def accuracy_function(self, inputs, logits):

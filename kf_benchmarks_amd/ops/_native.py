@@ -67,6 +67,8 @@ _SIGS = {
     "kfb_embedding_fwd": [I, P, L, P, P, L, I, P],
     "kfb_embedding_bwd": [I, P, P, P, L, L, I, P],
     "kfb_concat": [I, P, P, P, I, L, I, I, I, P],
+    "kfb_ssd_loss_fwd": [I, P, P, P, P, I, I, I, I, P, P, P],
+    "kfb_ssd_loss_bwd": [I, P, P, P, P, P, P, I, I, I, P, P],
 }
 _RESTYPES = {"kfb_bn_num_slabs": c_int, "kfb_colsum_num_slabs": c_int,
              "kfb_gemm_splits": c_int}

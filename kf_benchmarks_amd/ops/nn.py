@@ -912,6 +912,75 @@ def softmax_cross_entropy(logits, labels):
     return _SoftmaxXent.apply(logits, labels)
 
 
+def ssd_loss_reference(logits, gt_loc, gt_label, num_matched, negs_per_pos=3):
+    """Tensor form of the SSD300 loss (tcb/models/ssd_model.py loss_function:
+    softmax cross-entropy with hard-negative mining + smooth-L1 box loss).
+
+    logits [B, A, 4 + C]; gt_loc [B, A, 4]; gt_label [B, A] or [B, A, 1]
+    (float class ids, truncated); num_matched [B].  Hard negatives are the
+    k = min(negs_per_pos * floor(n_b), A) negatives with the largest
+    cross-entropy, equal values taken in anchor order (stable sort) -- the
+    exact selection rule of the fused kernel."""
+    B, A, R = logits.shape
+    C = R - 4
+    lf = logits.float()
+    lab = gt_label.reshape(B, A).float().long()
+    pos = lab > 0
+    ce = F.cross_entropy(lf[..., 4:].reshape(-1, C), lab.clamp(0, C - 1).reshape(-1),
+                         reduction="none").reshape(B, A)
+    nm = num_matched.float()
+    k = torch.clamp(nm.long() * negs_per_pos, 0, A)
+    key = torch.where(pos, torch.zeros_like(ce), ce.clamp(min=0))
+    order = torch.sort(key, dim=1, descending=True, stable=True).indices
+    rank = torch.empty_like(order)
+    rank.scatter_(1, order, torch.arange(A, device=order.device).expand(B, A).contiguous())
+    neg = (rank < k[:, None]) & ~pos
+    cls = (ce * (pos | neg).float()).sum(1)
+    sl1 = F.smooth_l1_loss(lf[..., :4], gt_loc.float(), reduction="none", beta=1.0).sum(2)
+    loc = (sl1 * pos.float()).sum(1)
+    return ((cls + loc) / nm).mean()
+
+
+class _SSDLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, gt_loc, gt_label, num_matched, negs_per_pos):
+        logits = logits.contiguous()
+        B, A, R = logits.shape
+        if A > 8960:
+            raise N.NativeError("ssd_loss: %d anchors exceed the kernel's LDS rows" % A)
+        gt_loc = gt_loc.float().contiguous()
+        gt_label = gt_label.float().reshape(B, A).contiguous()
+        num_matched = num_matched.float().reshape(B).contiguous()
+        if gt_loc.shape != (B, A, 4):
+            raise ValueError("ssd_loss: gt_loc %s != %s" % (tuple(gt_loc.shape), (B, A, 4)))
+        work = torch.empty((B + 3 * B * A,), dtype=torch.float32, device=logits.device)
+        out = torch.empty((1,), dtype=torch.float32, device=logits.device)
+        N.call("kfb_ssd_loss_fwd", N.dt(logits), logits.data_ptr(), gt_loc.data_ptr(),
+               gt_label.data_ptr(), num_matched.data_ptr(), B, A, R - 4, int(negs_per_pos),
+               work.data_ptr(), out.data_ptr(), N.stream(logits.device))
+        ctx.save_for_backward(logits, gt_loc, gt_label, num_matched, work)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, gt_loc, gt_label, num_matched, work = ctx.saved_tensors
+        B, A, R = logits.shape
+        g = g.float().reshape(1).contiguous()
+        dl = torch.empty_like(logits)
+        N.call("kfb_ssd_loss_bwd", N.dt(logits), logits.data_ptr(), gt_loc.data_ptr(),
+               gt_label.data_ptr(), num_matched.data_ptr(), work.data_ptr(), g.data_ptr(), B, A,
+               R - 4, dl.data_ptr(), N.stream(logits.device))
+        return dl, None, None, None, None
+
+
+def ssd_loss(logits, gt_loc, gt_label, num_matched, negs_per_pos=3):
+    """SSD300 training loss (fp32 scalar); fused HIP kernels on the GPU
+    (csrc/ssd_loss.hip), :func:`ssd_loss_reference` on the CPU."""
+    if not _on_gpu(logits):
+        return ssd_loss_reference(logits, gt_loc, gt_label, num_matched, negs_per_pos)
+    return _SSDLoss.apply(logits, gt_loc, gt_label, num_matched, negs_per_pos)
+
+
 def in_top_k(logits, labels):
     """(#top-1 correct, #top-5 correct) as fp32 device scalars."""
     if not _on_gpu(logits):

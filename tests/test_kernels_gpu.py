@@ -369,3 +369,33 @@ def test_embedding_lookup_and_grad(cuda, dim):
     y.backward(dy.to(cuda))
     ref = torch.zeros(rows, dim).index_add_(0, idx.long(), dy)
     torch.testing.assert_close(ta.grad.cpu(), ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("case", ["mixed", "all_negative", "many_matched"])
+def test_ssd_loss(cuda, dt, case):
+    """Fused SSD loss (csrc/ssd_loss.hip: per-row lse + per-image radix
+    select of the hard negatives) vs the stable-sort tensor form in fp32."""
+    B, A, C = 4, 8732, 81
+    g = torch.Generator().manual_seed(7)
+    logits = torch.randn(B, A, 4 + C, generator=g) * 2
+    gt_loc = torch.randn(B, A, 4, generator=g)
+    if case == "all_negative":  # the synthetic-data configuration: every label 0
+        label = torch.zeros(B, A, 1)
+        nm = torch.rand(B, generator=g) * 9 + 1
+    else:
+        frac = 0.02 if case == "mixed" else 0.2
+        pos = torch.rand(B, A, 1, generator=g) < frac
+        label = torch.where(pos, torch.randint(1, C, (B, A, 1), generator=g).float(),
+                            torch.zeros(B, A, 1)) + 0.3  # truncation like .long()
+        nm = pos.reshape(B, A).sum(1).float()
+        if case == "many_matched":  # k = 3 n exceeds A: every negative is mined
+            nm = nm * 2
+    a, b = _pair(logits, "cuda", dt)
+    got = F.ssd_loss(a, gt_loc.cuda(), label.cuda(), nm.cuda())
+    ref = F.ssd_loss_reference(b, gt_loc, label, nm)
+    torch.testing.assert_close(got.cpu(), ref, rtol=1e-4, atol=1e-4)
+    (got * 1.7).backward()
+    (ref * 1.7).backward()
+    t = dict(rtol=2e-2, atol=1e-6) if dt == torch.bfloat16 else dict(rtol=1e-4, atol=1e-8)
+    torch.testing.assert_close(a.grad.float().cpu(), b.grad, **t)

@@ -76,8 +76,11 @@ def test_network_grads_bf16(cuda, name, ds, size, batch):
     assert cos[0] > 0.85 and cos[len(cos) // 2] > 0.95, (cos[0], cos[len(cos) // 2])
 
 
-@pytest.mark.parametrize("name,ds,size,batch", BF16_MODELS[:1])
+@pytest.mark.parametrize("name,ds,size,batch", BF16_MODELS[:1] + [("resnet20", "cifar10", None, 64)])
 def test_fused_matches_unfused(cuda, name, ds, size, batch):
+    """(The batch-64 case has 512 pixel tiles per 32x32 layer, far more than
+    the 32 statistics slots: the conv-epilogue BN statistics then depend on
+    the order of their fp32 atomics, and the tolerance must hold anyway.)"""
     conv_ops.FUSE_BN = True
     _, fused = _grads(name, ds, cuda, torch.bfloat16, size, batch)
     conv_ops.FUSE_BN = False
