@@ -1,0 +1,365 @@
+// Recurrent layers of DeepSpeech2 on gfx950: TF BasicLSTMCell (gates i, j,
+// f, o; forget bias 1.0) and the basic tanh RNN cell, one or two directions
+// (tcb/models/experimental/deepspeech.py:121-125, :231-270).
+//
+// The layer is split the way its FLOPs split:
+//   * the input projection x . Wx + b of every time step is ONE big GEMM
+//     (ops/nn.linear, csrc/gemm.hip) producing gx [T][B][dirs*G*H];
+//   * the recurrence runs one launch per time step (both directions in the
+//     same launch, blockIdx.z = direction) of a kernel that multiplies the
+//     16-unit x (16*NB)-row tile of h_{t-1} . Wh on MFMA and applies the cell
+//     in its epilogue (gates, c, h never round-trip through a separate
+//     elementwise kernel);
+//   * the backward step kernel does dh = dout + dG_{t+1} . Wh^T on MFMA with
+//     the cell's backward in the epilogue, writing dG_t = d(gx) in place for
+//     the input-projection backward; dWh = sum_t h_{t-1}^T dG_t is one GEMM
+//     over all steps afterwards (ops/rnn.py).
+// The host loops over time steps in C++ (kfb_rnn_fwd / kfb_rnn_bwd), so a
+// layer costs one ctypes call, not T.
+//
+// Layouts (time-major; direction d processes time t = s or T-1-s at step s):
+//   gx   [T][B][ldg]  (T)  columns d*G*H + g*H + u        (ldg = dirs*G*H)
+//   whT  [dirs][G*H][H] (T)  forward operand (K = H contiguous)
+//   wh   [dirs][H][G*H] (T)  backward operand (K = G*H contiguous; TF layout)
+//   out  [T][B][dirs*H] (T)  h_t, directions concatenated
+//   hp   [dirs][T][B][H] (T) h entering the step at time t (0 for the first)
+//   act  [dirs][T][B][G*H] fp32  activated gates (LSTM) / h_t (RNN)
+//   cell [dirs][T][B][H] fp32    c_t (LSTM)
+//   dc   [2][dirs][B][H] fp32    cell gradient carried between backward steps
+#include "common.h"
+
+namespace kfb {
+namespace rnn {
+
+typedef __attribute__((ext_vector_type(4))) float v4f;
+typedef __attribute__((ext_vector_type(8))) short v8s;
+
+enum Kind : int { LSTM = 0, TANH = 1 };
+
+// acc[nb][r] += sum_{k in [kb, ke)} A[i][k] * B[nb*16 + j][k] with
+// i = 4*(lane/16) + r, j = lane % 16 (the 16x16 MFMA accumulator layout).
+// A: 16 rows (lda), B: up to 16*NB rows (ldb), rows >= brows read as zero.
+// Each lane loads one contiguous k-chunk per row per MFMA step: the k order
+// inside a step is a permutation, identical for A and B, so the sum is the
+// plain dot product.  kb, ke multiples of 8 (16-bit) / 4 (fp32).
+template <typename T, int NB>
+__device__ __forceinline__ void dot_rows(const T* __restrict__ A, long lda,
+                                         const T* __restrict__ Bm, long ldb, int brows, int kb,
+                                         int ke, v4f (&acc)[NB]) {
+  const int lane = threadIdx.x & 63, r16 = lane & 15, kq = lane >> 4;
+  const T* pa = A + r16 * lda;
+  const T* pb[NB];
+  bool bok[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    bok[nb] = nb * 16 + r16 < brows;
+    pb[nb] = Bm + (long)(bok[nb] ? nb * 16 + r16 : 0) * ldb;
+  }
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll 4
+    for (int k = kb; k < ke; k += 32) {
+      const int kk = k + kq * 8;
+      const bool kok = kk < ke;
+      const v8s a = kok ? *(const v8s*)(pa + kk) : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const v8s b = (kok && bok[nb]) ? *(const v8s*)(pb[nb] + kk) : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+        if constexpr (__is_same(T, bf16))
+          acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[nb], 0, 0, 0);
+        else {
+          typedef __attribute__((ext_vector_type(8))) _Float16 v8h;
+          acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(v8h, a),
+                                                           __builtin_bit_cast(v8h, b), acc[nb],
+                                                           0, 0, 0);
+        }
+      }
+    }
+  } else {
+#pragma unroll 4
+    for (int k = kb; k < ke; k += 16) {
+      const int kk = k + kq * 4;
+      const bool kok = kk < ke;
+      const float4 a = kok ? *(const float4*)(pa + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const float4 b =
+            (kok && bok[nb]) ? *(const float4*)(pb[nb] + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc[nb], 0, 0, 0);
+        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc[nb], 0, 0, 0);
+        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc[nb], 0, 0, 0);
+        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc[nb], 0, 0, 0);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+struct Args {
+  const void* gx;
+  const void* w;  // forward: whT; backward: wh
+  void* out;
+  void* hp;
+  float* act;
+  float* cell;
+  const void* dout;
+  void* dgx;
+  float* dc;
+  int T, B, H, dirs, ldg;
+};
+
+constexpr int NB = 2;         // 16-row batch blocks per workgroup (32 rows)
+constexpr int BT = 16 * NB;   // batch rows per workgroup
+constexpr int RED_LD = BT + 1;
+
+// The 4 waves of a workgroup share G gate blocks x (4/G) K parts; wave w
+// takes gate w % G over K part w / G.  Partial tiles go through LDS
+// red[w][u][b] and the epilogue thread of (b, u) sums its gate's parts.
+__device__ __forceinline__ void kpart(int K, int parts, int p, int& kb, int& ke) {
+  const int per = ((K / parts) + 7) / 8 * 8;
+  kb = min(K, p * per);
+  ke = min(K, kb + per);
+}
+
+template <typename T, int G>
+__global__ void __launch_bounds__(256) rnn_fwd_step_k(Args a, int s) {
+  __shared__ float red[4][16][RED_LD];
+  const int d = blockIdx.z, u0 = blockIdx.x * 16, b0 = blockIdx.y * BT;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int T_ = a.T, B = a.B, H = a.H, GH = G * H;
+  const int t = d ? T_ - 1 - s : s;
+  const int tprev = d ? t + 1 : t - 1, tnext = d ? t - 1 : t + 1;
+  const T* __restrict__ hp = (const T*)a.hp;
+  v4f acc[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = v4f{0.f, 0.f, 0.f, 0.f};
+  if (s > 0) {
+    constexpr int P = 4 / G;
+    const int g = w % G, p = w / G;
+    int kb, ke;
+    kpart(H, P, p, kb, ke);
+    const T* A = (const T*)a.w + ((long)d * GH + g * H + u0) * H;
+    const T* Bm = hp + (((long)d * T_ + t) * B + b0) * H;
+    dot_rows<T, NB>(A, H, Bm, H, B - b0, kb, ke, acc);
+  }
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][4 * (lane >> 4) + r][nb * 16 + (lane & 15)] = acc[nb][r];
+  __syncthreads();
+  const T* __restrict__ gx = (const T*)a.gx;
+#pragma unroll
+  for (int pass = 0; pass < BT * 16 / 256; ++pass) {
+    const int e = tid + pass * 256;
+    const int ul = e & 15, bl = e >> 4;
+    const int b = b0 + bl, u = u0 + ul;
+    if (b >= B) continue;
+    const long grow = ((long)t * B + b) * a.ldg + (long)d * GH;
+    const long srow = ((long)d * T_ + t) * B + b;  // [dirs][T][B] row
+    float pre[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float v = (float)gx[grow + g * H + u];
+#pragma unroll
+      for (int q = g; q < 4; q += G) v += red[q][ul][bl];
+      pre[g] = v;
+    }
+    float h;
+    if constexpr (G == 4) {
+      const float ig = sigm(pre[0]), jg = tanhf(pre[1]), fg = sigm(pre[2] + 1.0f),
+                  og = sigm(pre[3]);
+      const float cp = s > 0 ? a.cell[((long)d * T_ + tprev) * B * H + (long)b * H + u] : 0.f;
+      const float c = cp * fg + ig * jg;
+      h = tanhf(c) * og;
+      float* ap = a.act + srow * GH + u;
+      ap[0] = ig; ap[H] = jg; ap[2 * H] = fg; ap[3 * H] = og;
+      a.cell[srow * H + u] = c;
+    } else {
+      h = tanhf(pre[0]);
+      a.act[srow * GH + u] = h;
+    }
+    const T hv = (T)h;
+    ((T*)a.out)[((long)t * B + b) * a.dirs * H + (long)d * H + u] = hv;
+    T* hpw = (T*)a.hp;
+    if (s == 0) hpw[srow * H + u] = (T)0.f;  // h_{-1} = 0 (read by the dWh GEMM)
+    if (s + 1 < T_) hpw[(((long)d * T_ + tnext) * B + b) * H + u] = hv;
+  }
+}
+
+template <typename T, int G>
+__global__ void __launch_bounds__(256) rnn_bwd_step_k(Args a, int s) {
+  __shared__ float red[4][16][RED_LD];
+  const int d = blockIdx.z, u0 = blockIdx.x * 16, b0 = blockIdx.y * BT;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int T_ = a.T, B = a.B, H = a.H, GH = G * H;
+  const int t = d ? s : T_ - 1 - s;  // reverse of the forward order
+  const int tnext = d ? t - 1 : t + 1, tprev = d ? t + 1 : t - 1;
+  const bool has_prev = d ? t < T_ - 1 : t > 0;
+  v4f acc[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = v4f{0.f, 0.f, 0.f, 0.f};
+  if (s > 0) {
+    // dh_rec[u][b] = sum_n wh[d][u][n] * dG(tnext)[b][n], K = G*H in 4 parts
+    int kb, ke;
+    kpart(GH, 4, w, kb, ke);
+    const T* A = (const T*)a.w + ((long)d * H + u0) * GH;
+    const T* Bm = (const T*)a.dgx + ((long)tnext * B + b0) * a.ldg + (long)d * GH;
+    dot_rows<T, NB>(A, GH, Bm, a.ldg, B - b0, kb, ke, acc);
+  }
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][4 * (lane >> 4) + r][nb * 16 + (lane & 15)] = acc[nb][r];
+  __syncthreads();
+  const T* __restrict__ dout = (const T*)a.dout;
+  T* __restrict__ dgx = (T*)a.dgx;
+#pragma unroll
+  for (int pass = 0; pass < BT * 16 / 256; ++pass) {
+    const int e = tid + pass * 256;
+    const int ul = e & 15, bl = e >> 4;
+    const int b = b0 + bl, u = u0 + ul;
+    if (b >= B) continue;
+    const long srow = ((long)d * T_ + t) * B + b;
+    float dh = (float)dout[((long)t * B + b) * a.dirs * H + (long)d * H + u] +
+               ((red[0][ul][bl] + red[1][ul][bl]) + (red[2][ul][bl] + red[3][ul][bl]));
+    const long grow = ((long)t * B + b) * a.ldg + (long)d * GH;
+    if constexpr (G == 4) {
+      const float* ap = a.act + srow * GH + u;
+      const float ig = ap[0], jg = ap[H], fg = ap[2 * H], og = ap[3 * H];
+      const float c = a.cell[srow * H + u];
+      const float cp = has_prev ? a.cell[((long)d * T_ + tprev) * B * H + (long)b * H + u] : 0.f;
+      const float tc = tanhf(c);
+      const long dci = ((long)d * B + b) * H + u, dcn = (long)a.dirs * B * H;
+      float dcv = dh * og * (1.f - tc * tc);
+      if (s > 0) dcv += a.dc[(s & 1) * dcn + dci];
+      a.dc[((s + 1) & 1) * dcn + dci] = dcv * fg;
+      dgx[grow + u] = (T)(dcv * jg * ig * (1.f - ig));
+      dgx[grow + H + u] = (T)(dcv * ig * (1.f - jg * jg));
+      dgx[grow + 2 * H + u] = (T)(dcv * cp * fg * (1.f - fg));
+      dgx[grow + 3 * H + u] = (T)(dh * tc * og * (1.f - og));
+    } else {
+      const float h = a.act[srow * GH + u];
+      dgx[grow + u] = (T)(dh * (1.f - h * h));
+    }
+  }
+}
+
+// out[n][c][r] = (T) in[n][r][c]   (batched transpose with cast, 32x32 tiles)
+template <typename T>
+__global__ void __launch_bounds__(256) transpose_cast_k(const float* __restrict__ in,
+                                                        T* __restrict__ out, int R, int C) {
+  __shared__ float tile[32][33];
+  const long base = (long)blockIdx.z * R * C;
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+#pragma unroll
+  for (int i = 0; i < 32; i += 8) {
+    const int r = r0 + ty + i, c = c0 + tx;
+    tile[ty + i][tx] = (r < R && c < C) ? in[base + (long)r * C + c] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 32; i += 8) {
+    const int c = c0 + ty + i, r = r0 + tx;
+    if (r < R && c < C) out[base + (long)c * R + r] = (T)tile[tx][ty + i];
+  }
+}
+
+// out[j][i][:] = in[i][j][:]  ([A][Bd][R] -> [Bd][A][R]); R % V == 0
+template <typename T, int V>
+__global__ void __launch_bounds__(256) permute01_k(const T* __restrict__ in, T* __restrict__ out,
+                                                   int A, int Bd, int R) {
+  const int rv = R / V;
+  const long n = (long)A * Bd * rv;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int c = (int)(e % rv);
+    const long row = e / rv;  // output row j*A + i
+    const int i = (int)(row % A), j = (int)(row / A);
+    *(Vec<T, V>*)(out + row * R + c * V) = *(const Vec<T, V>*)(in + ((long)i * Bd + j) * R + c * V);
+  }
+}
+
+template <typename T>
+static hipError_t fwd(int kind, const Args& a, hipStream_t st) {
+  const dim3 grid(a.H / 16, (a.B + BT - 1) / BT, a.dirs);
+  for (int s = 0; s < a.T; ++s) {
+    if (kind == LSTM) hipLaunchKernelGGL((rnn_fwd_step_k<T, 4>), grid, dim3(256), 0, st, a, s);
+    else hipLaunchKernelGGL((rnn_fwd_step_k<T, 1>), grid, dim3(256), 0, st, a, s);
+  }
+  return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t bwd(int kind, const Args& a, hipStream_t st) {
+  const dim3 grid(a.H / 16, (a.B + BT - 1) / BT, a.dirs);
+  for (int s = 0; s < a.T; ++s) {
+    if (kind == LSTM) hipLaunchKernelGGL((rnn_bwd_step_k<T, 4>), grid, dim3(256), 0, st, a, s);
+    else hipLaunchKernelGGL((rnn_bwd_step_k<T, 1>), grid, dim3(256), 0, st, a, s);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace rnn
+}  // namespace kfb
+
+using namespace kfb;
+
+static bool rnn_shape_ok(int kind, int T, int B, int H, int dirs) {
+  return (kind == rnn::LSTM || kind == rnn::TANH) && T > 0 && B > 0 && H > 0 && H % 16 == 0 &&
+         (dirs == 1 || dirs == 2);
+}
+
+// Forward recurrence over all T steps (see the layout block at the top).
+KFB_API hipError_t kfb_rnn_fwd(int dtype, int kind, const void* gx, const void* whT, void* out,
+                               void* hp, float* act, float* cell, int T, int B, int H, int dirs,
+                               hipStream_t stream) {
+  if (!rnn_shape_ok(kind, T, B, H, dirs) || (kind == rnn::LSTM && !cell))
+    return hipErrorInvalidValue;
+  const int G = kind == rnn::LSTM ? 4 : 1;
+  rnn::Args a{gx, whT, out, hp, act, cell, nullptr, nullptr, nullptr, T, B, H, dirs,
+              dirs * G * H};
+  KFB_DISPATCH_DTYPE(dtype, T_, return rnn::fwd<T_>(kind, a, stream));
+  return hipSuccess;
+}
+
+// Backward recurrence: dgx [T][B][dirs*G*H] (T) receives d(gx); dc is a
+// [2][dirs][B][H] fp32 workspace.
+KFB_API hipError_t kfb_rnn_bwd(int dtype, int kind, const void* dout, const void* wh,
+                               const float* act, const float* cell, void* dgx, float* dc, int T,
+                               int B, int H, int dirs, hipStream_t stream) {
+  if (!rnn_shape_ok(kind, T, B, H, dirs) || (kind == rnn::LSTM && (!cell || !dc)))
+    return hipErrorInvalidValue;
+  const int G = kind == rnn::LSTM ? 4 : 1;
+  rnn::Args a{nullptr, wh, nullptr, nullptr, (float*)act, (float*)cell, dout, dgx, dc, T, B, H,
+              dirs, dirs * G * H};
+  KFB_DISPATCH_DTYPE(dtype, T_, return rnn::bwd<T_>(kind, a, stream));
+  return hipSuccess;
+}
+
+// out[n] = cast(in[n]^T): in fp32 [nb][R][C] -> out [nb][C][R] in dtype.
+KFB_API hipError_t kfb_transpose_cast(int dtype, const float* in, void* out, int nb, int R, int C,
+                                      hipStream_t stream) {
+  const dim3 grid((C + 31) / 32, (R + 31) / 32, nb);
+  KFB_DISPATCH_DTYPE(dtype, T_,
+                     hipLaunchKernelGGL(rnn::transpose_cast_k<T_>, grid, dim3(256), 0, stream,
+                                        in, (T_*)out, R, C));
+  return hipGetLastError();
+}
+
+// [A][Bd][R] -> [Bd][A][R] (swap the two leading dims; R contiguous).
+KFB_API hipError_t kfb_permute01(int dtype, const void* in, void* out, int A, int Bd, int R,
+                                 hipStream_t stream) {
+  const int es = dtype == F32 ? 4 : 2;
+  const int vw = vec_width(R) * es > 16 ? 16 / es : vec_width(R);
+  const long n = (long)A * Bd * (R / vw);
+  long blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  KFB_DISPATCH_DTYPE(dtype, T_,
+                     KFB_DISPATCH_VEC(vw, V,
+                                      hipLaunchKernelGGL((rnn::permute01_k<T_, V>),
+                                                         dim3((unsigned)blocks), dim3(256), 0,
+                                                         stream, (const T_*)in, (T_*)out, A, Bd,
+                                                         R)));
+  return hipGetLastError();
+}

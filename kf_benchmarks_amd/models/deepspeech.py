@@ -4,10 +4,10 @@ Spectrogram [B, 3494, 161, 1] -> two conv+ReLU6+BN layers (41x11/2x2 pad
 20x5, 21x11/2x1 pad 10x5, 32 filters) -> 5 bidirectional LSTM(800) layers
 with BN on the inputs of layers 2..5 -> BN -> dense(29) -> CTC loss (blank =
 class 28) over length-scaled inputs (tcb/models/experimental/
-deepspeech.py:121-389).  Batch 128, LR 0.0005.  The LSTMs run in fp32 on
-MIOpen's fused RNN kernels; the greedy decoder and CER/WER (edit distance
-implemented here, no nltk) report eval quality like the reference's
-postprocess.
+deepspeech.py:121-389).  Batch 128, LR 0.0005.  The recurrent layers and
+the CTC loss run on our HIP kernels (ops/rnn.py: csrc/rnn.hip, csrc/ctc.hip);
+the greedy decoder and CER/WER (edit distance implemented here, no nltk)
+report eval quality like the reference's postprocess.
 """
 
 from __future__ import annotations
@@ -21,6 +21,7 @@ from torch import nn
 
 from .. import cnn_util
 from ..ops import nn as F_ops
+from ..ops import rnn as rnn_ops
 from . import model as model_lib
 
 SPEECH_LABELS = " abcdefghijklmnopqrstuvwxyz'-"
@@ -105,6 +106,28 @@ class _ConvBN(nn.Module):
         return self.bn(y)
 
 
+class _RNNLayer(nn.Module):
+    """One (bi)directional recurrent layer (TF BasicLSTMCell with forget bias
+    1.0, or the basic tanh cell) on ops.rnn: the [x, h] . W kernel of the
+    reference split into an input part wx [din, dirs*G*H] (one GEMM over all
+    steps) and a recurrent part wh [dirs, H, G*H]; glorot-uniform over the
+    reference's [din+H, G*H] fan, zero bias."""
+
+    def __init__(self, din, hidden, kind, dirs, gen, device):
+        super().__init__()
+        self.kind, self.dirs, self.hidden = kind, dirs, hidden
+        G = rnn_ops.GATES[kind]
+        lim = (6.0 / (din + hidden + G * hidden)) ** 0.5
+        wx = (torch.rand((din, dirs * G * hidden), generator=gen) * 2 - 1) * lim
+        wh = (torch.rand((dirs, hidden, G * hidden), generator=gen) * 2 - 1) * lim
+        self.wx = nn.Parameter(wx.to(device))
+        self.bx = nn.Parameter(torch.zeros(dirs * G * hidden, device=device))
+        self.wh = nn.Parameter(wh.to(device))
+
+    def forward(self, x):  # [T, B, din] -> [T, B, dirs*H]
+        return rnn_ops.rnn_layer(x, self.wx, self.bx, self.wh, self.kind, self.dirs, self.hidden)
+
+
 class DeepSpeech2(nn.Module):
     def __init__(self, nclass, num_rnn_layers, rnn_type, bidirectional, hidden, use_bias,
                  feature_bins, gen, device):
@@ -113,15 +136,14 @@ class DeepSpeech2(nn.Module):
         self.conv2 = _ConvBN(32, 32, (21, 11), (2, 1), (10, 5), gen, device)
         f = (feature_bins + 10 - 11) // 2 + 1
         f = (f + 10 - 11) // 1 + 1
-        rnn_cls = {"lstm": nn.LSTM, "gru": nn.GRU, "rnn": nn.RNN}[rnn_type]
+        kind = rnn_ops._KIND[rnn_type]
         dirs = 2 if bidirectional else 1
         self.rnns = nn.ModuleList()
         self.bns = nn.ModuleList()
         din = f * 32
         for i in range(num_rnn_layers):
             self.bns.append(_BN(din, device) if i > 0 else nn.Identity())
-            self.rnns.append(rnn_cls(din, hidden, batch_first=True, bidirectional=bidirectional,
-                                     device=device))
+            self.rnns.append(_RNNLayer(din, hidden, kind, dirs, gen, device))
             din = hidden * dirs
         self.final_bn = _BN(din, device)
         # dense logits in the TF [in, out] layout, on the affine GEMM
@@ -134,16 +156,16 @@ class DeepSpeech2(nn.Module):
         x = inputs[0]  # [B, T, F, 1] (NHWC)
         x = self.conv2(self.conv1(x))
         B, T, F, C = x.shape
-        # the reference flattens [F, C] per time step (channels-last)
-        x = x.reshape(B, T, F * C)
-        rnn_dtype = next(self.rnns[0].parameters()).dtype
+        # the reference flattens [F, C] per time step (channels-last); the
+        # recurrent stack runs time-major
+        x = rnn_ops.permute01(x.reshape(B, T, F * C))  # [T, B, F*C]
         for bn, rnn in zip(self.bns, self.rnns):
-            x = bn(x)
-            # the recurrent layers run through torch's LSTM (MIOpen on the GPU)
-            x, _ = rnn(x.to(rnn_dtype))
-        x = self.final_bn(x.to(inputs[0].dtype))
-        logits = F_ops.linear(x.reshape(B * T, -1), self.fc_weight, self.fc_bias)
-        return model_lib.BuildNetworkResult(logits=logits.reshape(B, T, -1), extra_info=None)
+            x = rnn(bn(x))
+        x = self.final_bn(x)
+        logits = F_ops.linear(x.reshape(T * B, -1), self.fc_weight, self.fc_bias)
+        # [B, T, C] view of the time-major logits
+        return model_lib.BuildNetworkResult(logits=logits.view(T, B, -1).transpose(0, 1),
+                                            extra_info=None)
 
 
 class DeepSpeech2Model(model_lib.ModuleModel):
@@ -192,15 +214,11 @@ class DeepSpeech2Model(model_lib.ModuleModel):
         return feats, labels, ilen, llen
 
     def loss_function(self, inputs, build_network_result):
-        logits = build_network_result.logits.float()  # [B, T', nclass]
+        logits = build_network_result.logits  # [B, T', nclass] (time-major storage)
         T = logits.shape[1]
+        # sequence lengths scaled to the logits' time axis, as the reference
         ctc_len = (inputs[2].reshape(-1).long() * T) // self.max_time_steps
-        log_probs = torch.log_softmax(logits, dim=-1).transpose(0, 1)  # [T', B, C]
-        blank = logits.shape[-1] - 1
-        labels = inputs[1].long()
-        llen = inputs[3].reshape(-1).long()
-        losses = torch.nn.functional.ctc_loss(log_probs, labels, ctc_len, llen, blank=blank,
-                                              reduction="none", zero_infinity=True)
+        losses = rnn_ops.ctc_loss(logits, inputs[1], ctc_len, inputs[3].reshape(-1))
         return losses.mean()
 
     def accuracy_function(self, inputs, logits):

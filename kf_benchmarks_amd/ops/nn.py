@@ -719,11 +719,35 @@ def spatial_mean(x, keep_dims=False):
 _GEMM_FWD, _GEMM_DGRAD, _GEMM_WGRAD = 0, 1, 2
 
 
+def _at(t, elems):
+    """A view of ``t``'s storage starting ``elems`` elements further on
+    (the GEMM entry point only reads the base pointer)."""
+    return t.as_strided((1,), (1,), t.storage_offset() + elems)
+
+
 def _gemm(mode, p, ldp, q, ldq, rows, cols, red, out, ldc, bias=None, relu=False,
           accumulate=False):
     """csrc/gemm.hip, out [rows][cols]: mode 0 out = p . q (q [red][cols]),
     mode 1 out = p . q^T (q [cols][red]), mode 2 out (+)= p^T . q
-    (p [red][rows], q [red][cols], fp32 out)."""
+    (p [red][rows], q [red][cols], fp32 out).  Operands of 2 GiB or more
+    (the kernel's buffer-descriptor range) are cut into row / reduction
+    chunks (DeepSpeech2's fp32 [T*B, 8H] gate tensors)."""
+    esz = p.element_size()
+    lim = (1 << 31) - (1 << 20)
+    if mode == _GEMM_WGRAD and (red * ldp * esz >= lim or red * ldq * esz >= lim):
+        step = max(1, lim // (max(ldp, ldq) * esz))
+        for r0 in range(0, red, step):
+            r1 = min(red, r0 + step)
+            _gemm(mode, _at(p, r0 * ldp), ldp, _at(q, r0 * ldq), ldq, rows, cols, r1 - r0, out, ldc,
+                  accumulate=accumulate or r0 > 0)
+        return
+    if mode != _GEMM_WGRAD and rows * ldp * esz >= lim:
+        step = max(1, lim // (ldp * esz))
+        for r0 in range(0, rows, step):
+            r1 = min(rows, r0 + step)
+            _gemm(mode, _at(p, r0 * ldp), ldp, q, ldq, r1 - r0, cols, red, _at(out, r0 * ldc), ldc,
+                  bias=bias, relu=relu, accumulate=accumulate)
+        return
     dev = p.device
     nsplit, slab = 1, None
     if mode != _GEMM_WGRAD:
