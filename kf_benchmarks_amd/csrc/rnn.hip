@@ -34,7 +34,7 @@ namespace rnn {
 typedef __attribute__((ext_vector_type(4))) float v4f;
 typedef __attribute__((ext_vector_type(8))) short v8s;
 
-enum Kind : int { LSTM = 0, TANH = 1 };
+enum Kind : int { LSTM = 0, TANH = 1, GRU = 2 };
 
 // acc[nb][r] += sum_{k in [kb, ke)} A[i][k] * B[nb*16 + j][k] with
 // i = 4*(lane/16) + r, j = lane % 16 (the 16x16 MFMA accumulator layout).
@@ -105,6 +105,9 @@ struct Args {
   const void* dout;
   void* dgx;
   float* dc;
+  void* rh;    // GRU: r * h_{t-1}  [dirs][T][B][H] (T), the candidate GEMM's operand
+  float* dhb;  // GRU backward: dh(t) of the previous step   [2][dirs][B][H]
+  float* drh;  // GRU backward: d(r*h)(t) of the previous step [2][dirs][B][H]
   int T, B, H, dirs, ldg;
 };
 
@@ -244,6 +247,192 @@ __global__ void __launch_bounds__(256) rnn_bwd_step_k(Args a, int s) {
   }
 }
 
+// ---------------------------------------------------------------- GRU
+// TF GRUCell: [r, u] = sigmoid([x, h] Wg + bg); c = tanh([x, r*h] Wc + bc);
+// h' = u*h + (1-u)*c.  Columns per direction: r | u | c (G = 3); the
+// candidate's recurrent GEMM reads r*h, so a step is two launches: the gate
+// kernel (writes r, u and r*h) and the candidate kernel (c and h').
+template <typename T>
+__global__ void __launch_bounds__(256) gru_gate_step_k(Args a, int s) {
+  __shared__ float red[4][16][RED_LD];
+  const int d = blockIdx.z, u0 = blockIdx.x * 16, b0 = blockIdx.y * BT;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int T_ = a.T, B = a.B, H = a.H, GH = 3 * H;
+  const int t = d ? T_ - 1 - s : s;
+  T* hp = (T*)a.hp;
+  v4f acc[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = v4f{0.f, 0.f, 0.f, 0.f};
+  if (s > 0) {
+    const int g = w & 1, p = w >> 1;
+    int kb, ke;
+    kpart(H, 2, p, kb, ke);
+    const T* A = (const T*)a.w + ((long)d * GH + g * H + u0) * H;
+    const T* Bm = hp + (((long)d * T_ + t) * B + b0) * H;
+    dot_rows<T, NB>(A, H, Bm, H, B - b0, kb, ke, acc);
+  }
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][4 * (lane >> 4) + r][nb * 16 + (lane & 15)] = acc[nb][r];
+  __syncthreads();
+  const T* __restrict__ gx = (const T*)a.gx;
+#pragma unroll
+  for (int pass = 0; pass < BT * 16 / 256; ++pass) {
+    const int e = tid + pass * 256;
+    const int ul = e & 15, bl = e >> 4;
+    const int b = b0 + bl, u = u0 + ul;
+    if (b >= B) continue;
+    const long grow = ((long)t * B + b) * a.ldg + (long)d * GH;
+    const long srow = ((long)d * T_ + t) * B + b;
+    const float rg = sigm((float)gx[grow + u] + red[0][ul][bl] + red[2][ul][bl]);
+    const float ug = sigm((float)gx[grow + H + u] + red[1][ul][bl] + red[3][ul][bl]);
+    const float hprev = s > 0 ? (float)hp[srow * H + u] : 0.f;
+    a.act[srow * GH + u] = rg;
+    a.act[srow * GH + H + u] = ug;
+    ((T*)a.rh)[srow * H + u] = (T)(rg * hprev);
+    if (s == 0) hp[srow * H + u] = (T)0.f;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) gru_cand_step_k(Args a, int s) {
+  __shared__ float red[4][16][RED_LD];
+  const int d = blockIdx.z, u0 = blockIdx.x * 16, b0 = blockIdx.y * BT;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int T_ = a.T, B = a.B, H = a.H, GH = 3 * H;
+  const int t = d ? T_ - 1 - s : s, tnext = d ? t - 1 : t + 1;
+  T* hp = (T*)a.hp;
+  v4f acc[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = v4f{0.f, 0.f, 0.f, 0.f};
+  if (s > 0) {
+    int kb, ke;
+    kpart(H, 4, w, kb, ke);
+    const T* A = (const T*)a.w + ((long)d * GH + 2 * H + u0) * H;
+    const T* Bm = (const T*)a.rh + (((long)d * T_ + t) * B + b0) * H;
+    dot_rows<T, NB>(A, H, Bm, H, B - b0, kb, ke, acc);
+  }
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][4 * (lane >> 4) + r][nb * 16 + (lane & 15)] = acc[nb][r];
+  __syncthreads();
+  const T* __restrict__ gx = (const T*)a.gx;
+#pragma unroll
+  for (int pass = 0; pass < BT * 16 / 256; ++pass) {
+    const int e = tid + pass * 256;
+    const int ul = e & 15, bl = e >> 4;
+    const int b = b0 + bl, u = u0 + ul;
+    if (b >= B) continue;
+    const long grow = ((long)t * B + b) * a.ldg + (long)d * GH;
+    const long srow = ((long)d * T_ + t) * B + b;
+    const float c = tanhf((float)gx[grow + 2 * H + u] + ((red[0][ul][bl] + red[1][ul][bl]) +
+                                                        (red[2][ul][bl] + red[3][ul][bl])));
+    const float ug = a.act[srow * GH + H + u];
+    const float hprev = s > 0 ? (float)hp[srow * H + u] : 0.f;
+    const float h = ug * hprev + (1.f - ug) * c;
+    a.act[srow * GH + 2 * H + u] = c;
+    const T hv = (T)h;
+    ((T*)a.out)[((long)t * B + b) * a.dirs * H + (long)d * H + u] = hv;
+    if (s + 1 < T_) hp[(((long)d * T_ + tnext) * B + b) * H + u] = hv;
+  }
+}
+
+// Backward step, part A: dh(t) = dout(t) + u(tn) dh(tn) + r(tn) d(rh)(tn)
+// + [dr_pre, du_pre](tn) . Wg^T; then dc_pre(t), du_pre(t).
+template <typename T>
+__global__ void __launch_bounds__(256) gru_bwd_a_k(Args a, int s) {
+  __shared__ float red[4][16][RED_LD];
+  const int d = blockIdx.z, u0 = blockIdx.x * 16, b0 = blockIdx.y * BT;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int T_ = a.T, B = a.B, H = a.H, GH = 3 * H;
+  const int t = d ? s : T_ - 1 - s, tnext = d ? t - 1 : t + 1;
+  const bool has_prev = d ? t < T_ - 1 : t > 0;
+  v4f acc[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = v4f{0.f, 0.f, 0.f, 0.f};
+  if (s > 0) {
+    int kb, ke;
+    kpart(2 * H, 4, w, kb, ke);
+    const T* A = (const T*)a.w + ((long)d * H + u0) * GH;
+    const T* Bm = (const T*)a.dgx + ((long)tnext * B + b0) * a.ldg + (long)d * GH;
+    dot_rows<T, NB>(A, GH, Bm, a.ldg, B - b0, kb, ke, acc);
+  }
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][4 * (lane >> 4) + r][nb * 16 + (lane & 15)] = acc[nb][r];
+  __syncthreads();
+  const T* __restrict__ dout = (const T*)a.dout;
+  T* __restrict__ dgx = (T*)a.dgx;
+  const long dn = (long)a.dirs * B * H;
+#pragma unroll
+  for (int pass = 0; pass < BT * 16 / 256; ++pass) {
+    const int e = tid + pass * 256;
+    const int ul = e & 15, bl = e >> 4;
+    const int b = b0 + bl, u = u0 + ul;
+    if (b >= B) continue;
+    const long srow = ((long)d * T_ + t) * B + b;
+    const long dci = ((long)d * B + b) * H + u;
+    float dh = (float)dout[((long)t * B + b) * a.dirs * H + (long)d * H + u] +
+               ((red[0][ul][bl] + red[1][ul][bl]) + (red[2][ul][bl] + red[3][ul][bl]));
+    if (s > 0) {
+      const float* an = a.act + (((long)d * T_ + tnext) * B + b) * GH;
+      const long q = ((s + 1) & 1) * dn + dci;
+      dh += an[H + u] * a.dhb[q] + an[u] * a.drh[q];
+    }
+    a.dhb[(s & 1) * dn + dci] = dh;
+    const float* ap = a.act + srow * GH;
+    const float ug = ap[H + u], c = ap[2 * H + u];
+    const float hprev = has_prev ? (float)((const T*)a.hp)[srow * H + u] : 0.f;
+    const long grow = ((long)t * B + b) * a.ldg + (long)d * GH;
+    dgx[grow + 2 * H + u] = (T)(dh * (1.f - ug) * (1.f - c * c));
+    dgx[grow + H + u] = (T)(dh * (hprev - c) * ug * (1.f - ug));
+  }
+}
+
+// Backward step, part B: d(rh)(t) = dc_pre(t) . Wc^T -> dr_pre(t).
+template <typename T>
+__global__ void __launch_bounds__(256) gru_bwd_b_k(Args a, int s) {
+  __shared__ float red[4][16][RED_LD];
+  const int d = blockIdx.z, u0 = blockIdx.x * 16, b0 = blockIdx.y * BT;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int T_ = a.T, B = a.B, H = a.H, GH = 3 * H;
+  const int t = d ? s : T_ - 1 - s;
+  const bool has_prev = d ? t < T_ - 1 : t > 0;
+  v4f acc[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = v4f{0.f, 0.f, 0.f, 0.f};
+  {
+    int kb, ke;
+    kpart(H, 4, w, kb, ke);
+    const T* A = (const T*)a.w + ((long)d * H + u0) * GH + 2 * H;
+    const T* Bm = (const T*)a.dgx + ((long)t * B + b0) * a.ldg + (long)d * GH + 2 * H;
+    dot_rows<T, NB>(A, GH, Bm, a.ldg, B - b0, kb, ke, acc);
+  }
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][4 * (lane >> 4) + r][nb * 16 + (lane & 15)] = acc[nb][r];
+  __syncthreads();
+  T* __restrict__ dgx = (T*)a.dgx;
+  const long dn = (long)a.dirs * B * H;
+#pragma unroll
+  for (int pass = 0; pass < BT * 16 / 256; ++pass) {
+    const int e = tid + pass * 256;
+    const int ul = e & 15, bl = e >> 4;
+    const int b = b0 + bl, u = u0 + ul;
+    if (b >= B) continue;
+    const long srow = ((long)d * T_ + t) * B + b;
+    const float drh = (red[0][ul][bl] + red[1][ul][bl]) + (red[2][ul][bl] + red[3][ul][bl]);
+    a.drh[(s & 1) * dn + ((long)d * B + b) * H + u] = drh;
+    const float rg = a.act[srow * GH + u];
+    const float hprev = has_prev ? (float)((const T*)a.hp)[srow * H + u] : 0.f;
+    dgx[((long)t * B + b) * a.ldg + (long)d * GH + u] = (T)(drh * hprev * rg * (1.f - rg));
+  }
+}
+
 // out[n][c][r] = (T) in[n][r][c]   (batched transpose with cast, 32x32 tiles)
 template <typename T>
 __global__ void __launch_bounds__(256) transpose_cast_k(const float* __restrict__ in,
@@ -283,8 +472,14 @@ template <typename T>
 static hipError_t fwd(int kind, const Args& a, hipStream_t st) {
   const dim3 grid(a.H / 16, (a.B + BT - 1) / BT, a.dirs);
   for (int s = 0; s < a.T; ++s) {
-    if (kind == LSTM) hipLaunchKernelGGL((rnn_fwd_step_k<T, 4>), grid, dim3(256), 0, st, a, s);
-    else hipLaunchKernelGGL((rnn_fwd_step_k<T, 1>), grid, dim3(256), 0, st, a, s);
+    if (kind == LSTM) {
+      hipLaunchKernelGGL((rnn_fwd_step_k<T, 4>), grid, dim3(256), 0, st, a, s);
+    } else if (kind == GRU) {
+      hipLaunchKernelGGL((gru_gate_step_k<T>), grid, dim3(256), 0, st, a, s);
+      hipLaunchKernelGGL((gru_cand_step_k<T>), grid, dim3(256), 0, st, a, s);
+    } else {
+      hipLaunchKernelGGL((rnn_fwd_step_k<T, 1>), grid, dim3(256), 0, st, a, s);
+    }
   }
   return hipGetLastError();
 }
@@ -293,8 +488,14 @@ template <typename T>
 static hipError_t bwd(int kind, const Args& a, hipStream_t st) {
   const dim3 grid(a.H / 16, (a.B + BT - 1) / BT, a.dirs);
   for (int s = 0; s < a.T; ++s) {
-    if (kind == LSTM) hipLaunchKernelGGL((rnn_bwd_step_k<T, 4>), grid, dim3(256), 0, st, a, s);
-    else hipLaunchKernelGGL((rnn_bwd_step_k<T, 1>), grid, dim3(256), 0, st, a, s);
+    if (kind == LSTM) {
+      hipLaunchKernelGGL((rnn_bwd_step_k<T, 4>), grid, dim3(256), 0, st, a, s);
+    } else if (kind == GRU) {
+      hipLaunchKernelGGL((gru_bwd_a_k<T>), grid, dim3(256), 0, st, a, s);
+      hipLaunchKernelGGL((gru_bwd_b_k<T>), grid, dim3(256), 0, st, a, s);
+    } else {
+      hipLaunchKernelGGL((rnn_bwd_step_k<T, 1>), grid, dim3(256), 0, st, a, s);
+    }
   }
   return hipGetLastError();
 }
@@ -304,34 +505,41 @@ static hipError_t bwd(int kind, const Args& a, hipStream_t st) {
 
 using namespace kfb;
 
+static int rnn_gates(int kind) { return kind == rnn::LSTM ? 4 : kind == rnn::GRU ? 3 : 1; }
+
 static bool rnn_shape_ok(int kind, int T, int B, int H, int dirs) {
-  return (kind == rnn::LSTM || kind == rnn::TANH) && T > 0 && B > 0 && H > 0 && H % 16 == 0 &&
+  return (kind == rnn::LSTM || kind == rnn::TANH || kind == rnn::GRU) && T > 0 && B > 0 && H > 0 && H % 16 == 0 &&
          (dirs == 1 || dirs == 2);
 }
 
 // Forward recurrence over all T steps (see the layout block at the top).
+// rh: GRU only ([dirs][T][B][H] in dtype, kept for the backward).
 KFB_API hipError_t kfb_rnn_fwd(int dtype, int kind, const void* gx, const void* whT, void* out,
-                               void* hp, float* act, float* cell, int T, int B, int H, int dirs,
-                               hipStream_t stream) {
-  if (!rnn_shape_ok(kind, T, B, H, dirs) || (kind == rnn::LSTM && !cell))
+                               void* hp, float* act, float* cell, void* rh, int T, int B, int H,
+                               int dirs, hipStream_t stream) {
+  if (!rnn_shape_ok(kind, T, B, H, dirs) || (kind == rnn::LSTM && !cell) ||
+      (kind == rnn::GRU && !rh))
     return hipErrorInvalidValue;
-  const int G = kind == rnn::LSTM ? 4 : 1;
-  rnn::Args a{gx, whT, out, hp, act, cell, nullptr, nullptr, nullptr, T, B, H, dirs,
-              dirs * G * H};
+  const int G = rnn_gates(kind);
+  rnn::Args a{gx, whT, out, hp, act, cell, nullptr, nullptr, nullptr, rh, nullptr, nullptr,
+              T, B, H, dirs, dirs * G * H};
   KFB_DISPATCH_DTYPE(dtype, T_, return rnn::fwd<T_>(kind, a, stream));
   return hipSuccess;
 }
 
-// Backward recurrence: dgx [T][B][dirs*G*H] (T) receives d(gx); dc is a
-// [2][dirs][B][H] fp32 workspace.
+// Backward recurrence: dgx [T][B][dirs*G*H] (T) receives d(gx); dc (LSTM),
+// dhb and drh (GRU) are [2][dirs][B][H] fp32 workspaces; hp is the forward's
+// h-entering-each-step tensor (GRU).
 KFB_API hipError_t kfb_rnn_bwd(int dtype, int kind, const void* dout, const void* wh,
-                               const float* act, const float* cell, void* dgx, float* dc, int T,
-                               int B, int H, int dirs, hipStream_t stream) {
-  if (!rnn_shape_ok(kind, T, B, H, dirs) || (kind == rnn::LSTM && (!cell || !dc)))
+                               const float* act, const float* cell, const void* hp, void* dgx,
+                               float* dc, float* dhb, float* drh, int T, int B, int H, int dirs,
+                               hipStream_t stream) {
+  if (!rnn_shape_ok(kind, T, B, H, dirs) || (kind == rnn::LSTM && (!cell || !dc)) ||
+      (kind == rnn::GRU && (!hp || !dhb || !drh)))
     return hipErrorInvalidValue;
-  const int G = kind == rnn::LSTM ? 4 : 1;
-  rnn::Args a{nullptr, wh, nullptr, nullptr, (float*)act, (float*)cell, dout, dgx, dc, T, B, H,
-              dirs, dirs * G * H};
+  const int G = rnn_gates(kind);
+  rnn::Args a{nullptr, wh, nullptr, (void*)hp, (float*)act, (float*)cell, dout, dgx, dc,
+              nullptr, dhb, drh, T, B, H, dirs, dirs * G * H};
   KFB_DISPATCH_DTYPE(dtype, T_, return rnn::bwd<T_>(kind, a, stream));
   return hipSuccess;
 }

@@ -108,7 +108,7 @@ class _ConvBN(nn.Module):
 
 class _RNNLayer(nn.Module):
     """One (bi)directional recurrent layer (TF BasicLSTMCell with forget bias
-    1.0, or the basic tanh cell) on ops.rnn: the [x, h] . W kernel of the
+    1.0, GRUCell, or the basic tanh cell) on ops.rnn: the [x, h] . W kernel of the
     reference split into an input part wx [din, dirs*G*H] (one GEMM over all
     steps) and a recurrent part wh [dirs, H, G*H]; glorot-uniform over the
     reference's [din+H, G*H] fan, zero bias."""
@@ -121,7 +121,10 @@ class _RNNLayer(nn.Module):
         wx = (torch.rand((din, dirs * G * hidden), generator=gen) * 2 - 1) * lim
         wh = (torch.rand((dirs, hidden, G * hidden), generator=gen) * 2 - 1) * lim
         self.wx = nn.Parameter(wx.to(device))
-        self.bx = nn.Parameter(torch.zeros(dirs * G * hidden, device=device))
+        bx = torch.zeros(dirs, G, hidden)
+        if kind == rnn_ops.GRU:
+            bx[:, :2] = 1.0  # TF GRUCell's gate bias initializer
+        self.bx = nn.Parameter(bx.reshape(-1).to(device))
         self.wh = nn.Parameter(wh.to(device))
 
     def forward(self, x):  # [T, B, din] -> [T, B, dirs*H]

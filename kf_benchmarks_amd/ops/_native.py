@@ -69,8 +69,8 @@ _SIGS = {
     "kfb_concat": [I, P, P, P, I, L, I, I, I, P],
     "kfb_ssd_loss_fwd": [I, P, P, P, P, I, I, I, I, P, P, P],
     "kfb_ssd_loss_bwd": [I, P, P, P, P, P, P, I, I, I, P, P],
-    "kfb_rnn_fwd": [I, I, P, P, P, P, P, P, I, I, I, I, P],
-    "kfb_rnn_bwd": [I, I, P, P, P, P, P, P, I, I, I, I, P],
+    "kfb_rnn_fwd": [I, I, P, P, P, P, P, P, P, I, I, I, I, P],
+    "kfb_rnn_bwd": [I, I, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "kfb_transpose_cast": [I, P, P, I, I, I, P],
     "kfb_permute01": [I, P, P, I, I, I, P],
     "kfb_ctc_loss": [I, P, L, L, P, P, P, I, I, I, I, P, P, I, P, P, P],

@@ -25,9 +25,9 @@ import torch
 from . import _native as N
 from . import nn as F_ops
 
-LSTM, TANH = 0, 1
-_KIND = {"lstm": LSTM, "rnn": TANH}
-GATES = {LSTM: 4, TANH: 1}
+LSTM, TANH, GRU = 0, 1, 2
+_KIND = {"lstm": LSTM, "rnn": TANH, "gru": GRU}
+GATES = {LSTM: 4, TANH: 1, GRU: 3}
 
 
 # ------------------------------------------------------------------ permute
@@ -67,7 +67,15 @@ def recurrence_reference(gx, wh, kind, dirs, H):
         seq = [None] * T
         order = range(T - 1, -1, -1) if d else range(T)
         for t in order:
-            pre = gx[t, :, d * G * H:(d + 1) * G * H] + h @ wh[d].float()
+            gxt = gx[t, :, d * G * H:(d + 1) * G * H]
+            if kind == GRU:  # TF GRUCell: the candidate sees r * h
+                whd = wh[d].float()
+                r, u = torch.sigmoid(gxt[:, :2 * H] + h @ whd[:, :2 * H]).split(H, dim=1)
+                c = torch.tanh(gxt[:, 2 * H:] + (r * h) @ whd[:, 2 * H:])
+                h = u * h + (1 - u) * c
+                seq[t] = h
+                continue
+            pre = gxt + h @ wh[d].float()
             if kind == LSTM:
                 i, j, f, o = pre.split(H, dim=1)
                 c = c * torch.sigmoid(f + 1.0) + torch.sigmoid(i) * torch.tanh(j)
@@ -94,15 +102,17 @@ class _Recurrence(torch.autograd.Function):
         act = torch.empty((dirs, T, B, G * H), dtype=torch.float32, device=dev)
         cell = (torch.empty((dirs, T, B, H), dtype=torch.float32, device=dev)
                 if kind == LSTM else None)
+        rh = torch.empty((dirs, T, B, H), dtype=dt, device=dev) if kind == GRU else None
         N.call("kfb_rnn_fwd", N.dt(gx), kind, gx.data_ptr(), whT.data_ptr(), out.data_ptr(),
-               hp.data_ptr(), act.data_ptr(), N.ptr(cell), T, B, H, dirs, N.stream(dev))
-        ctx.save_for_backward(hp, act, cell)
+               hp.data_ptr(), act.data_ptr(), N.ptr(cell), N.ptr(rh), T, B, H, dirs,
+               N.stream(dev))
+        ctx.save_for_backward(hp, act, cell, rh)
         ctx.wh, ctx.kind, ctx.dirs, ctx.H = wh, kind, dirs, H
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        hp, act, cell = ctx.saved_tensors
+        hp, act, cell, rh = ctx.saved_tensors
         wh, kind, dirs, H = ctx.wh, ctx.kind, ctx.dirs, ctx.H
         G = GATES[kind]
         T, B = hp.shape[1], hp.shape[2]
@@ -115,20 +125,28 @@ class _Recurrence(torch.autograd.Function):
             N.call("kfb_cast_f32", wh.data_ptr(), wl.data_ptr(), N.dt(wl), wh.numel(),
                    N.stream(dev))
         dgx = torch.empty((T, B, dirs * G * H), dtype=dt, device=dev)
-        dc = torch.empty((2, dirs, B, H), dtype=torch.float32, device=dev)
+        ws = torch.empty((3, 2, dirs, B, H), dtype=torch.float32, device=dev)
         N.call("kfb_rnn_bwd", N.dt(dout), kind, dout.data_ptr(), wl.data_ptr(), act.data_ptr(),
-               N.ptr(cell), dgx.data_ptr(), dc.data_ptr(), T, B, H, dirs, N.stream(dev))
-        # dWh[d] = sum_{t,b} hp[d,t,b,:]^T dG[t,b,d,:]   (one GEMM per direction)
+               N.ptr(cell), hp.data_ptr(), dgx.data_ptr(), ws[0].data_ptr(), ws[1].data_ptr(),
+               ws[2].data_ptr(), T, B, H, dirs, N.stream(dev))
+        # dWh[d] = sum_{t,b} hp[d,t,b,:]^T dG[t,b,d,:]   (one GEMM per direction;
+        # GRU: the candidate block's operand is r*h instead of h)
         sink = F_ops._grad_sink(wh)
         dw = None
         target = sink.view(dirs, H, G * H) if sink is not None else torch.empty(
             (dirs, H, G * H), dtype=torch.float32, device=dev)
         ldg = dirs * G * H
+        acc = sink is not None
         for d in range(dirs):
-            p = hp[d]
             q = dgx.view(T * B, ldg)[:, d * G * H:]
-            F_ops._gemm(F_ops._GEMM_WGRAD, p, H, q, ldg, H, G * H, T * B, target[d], G * H,
-                        accumulate=sink is not None)
+            if kind == GRU:
+                F_ops._gemm(F_ops._GEMM_WGRAD, hp[d], H, q, ldg, H, 2 * H, T * B, target[d],
+                            G * H, accumulate=acc)
+                F_ops._gemm(F_ops._GEMM_WGRAD, rh[d], H, F_ops._at(q, 2 * H), ldg, H, H, T * B,
+                            F_ops._at(target[d], 2 * H), G * H, accumulate=acc)
+            else:
+                F_ops._gemm(F_ops._GEMM_WGRAD, hp[d], H, q, ldg, H, G * H, T * B, target[d],
+                            G * H, accumulate=acc)
         if sink is not None:
             F_ops._grad_ready(wh)
         else:

@@ -63,6 +63,27 @@ def test_tanh_rnn_reference():
         torch.testing.assert_close(out[t], h)
 
 
+def test_gru_reference_matches_tf_gru_cell_math():
+    """TF GRUCell: r, u = sigmoid([x, h] Wg + bg); c = tanh([x, r h] Wc + bc);
+    h' = u h + (1 - u) c, written out with the concatenated kernels."""
+    torch.manual_seed(2)
+    T, B, din, H = 4, 3, 5, 6
+    x = torch.randn(T, B, din)
+    kg = torch.randn(din + H, 2 * H) * 0.3
+    kc = torch.randn(din + H, H) * 0.3
+    bg, bc = torch.ones(2 * H), torch.zeros(H)
+    wx = torch.cat([kg[:din], kc[:din]], 1)
+    wh = torch.cat([kg[din:], kc[din:]], 1)[None]
+    gx = x.reshape(T * B, din) @ wx + torch.cat([bg, bc])
+    out = R.recurrence_reference(gx.view(T, B, -1), wh, R.GRU, 1, H)
+    h = torch.zeros(B, H)
+    for t in range(T):
+        r, u = torch.sigmoid(torch.cat([x[t], h], 1) @ kg + bg).split(H, 1)
+        c = torch.tanh(torch.cat([x[t], r * h], 1) @ kc + bc)
+        h = u * h + (1 - u) * c
+        torch.testing.assert_close(out[t], h, rtol=1e-5, atol=1e-5)
+
+
 def test_permute01_cpu():
     x = torch.arange(24.).view(2, 3, 4)
     y = R.permute01(x)
@@ -71,12 +92,13 @@ def test_permute01_cpu():
 
 # ------------------------------------------------------------------ GPU
 def _relerr(a, b):
-    return float((a.float().cpu() - b.float().cpu()).norm() / (b.float().norm() + 1e-12))
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-12))
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("kind", [R.LSTM, R.TANH])
+@pytest.mark.parametrize("kind", [R.LSTM, R.TANH, R.GRU])
 @pytest.mark.parametrize("dirs,B,H,T", [(2, 20, 32, 7), (1, 33, 48, 5), (2, 64, 160, 9)])
 def test_recurrence_gpu(cuda, dt, kind, dirs, B, H, T):
     torch.manual_seed(0)
@@ -158,7 +180,8 @@ def test_permute01_gpu(cuda, dt):
 
 
 @pytest.mark.gpu
-def test_deepspeech2_small_gpu_matches_cpu(cuda):
+@pytest.mark.parametrize("rnn_type", ["lstm", "gru"])
+def test_deepspeech2_small_gpu_matches_cpu(cuda, rnn_type):
     """Tiny DeepSpeech2 forward + backward on the GPU kernels (conv, BN,
     LSTM, affine, CTC) against the same model on CPU, fp32."""
     from kf_benchmarks_amd import datasets, params as P
@@ -169,6 +192,7 @@ def test_deepspeech2_small_gpu_matches_cpu(cuda):
     for dev in ("cpu", cuda):
         m = model_config.get_model_config("deepspeech2", d, P.make_params(model="deepspeech2"))
         m.max_time_steps, m.max_label_length, m.rnn_hidden_size = 120, 20, 32
+        m.rnn_type = rnn_type
         m.set_batch_size(4)
         torch.manual_seed(0)
         net = make_network(m, d.num_classes, str(dev), torch.float32)
