@@ -732,6 +732,9 @@ struct WgArgs {
 };
 
 constexpr int WG_BK = 32;  // reduction rows per step (64 measured no faster)
+#ifndef KFB_WG_XCD
+#define KFB_WG_XCD 1
+#endif
 
 // 256-byte rows (128 elements); 32-byte unit u (0..7) of row r stored at
 // u ^ f(r), f(r) = (r & 3) | ((r >> 3) & 1) << 2.
@@ -767,8 +770,13 @@ __global__ void __launch_bounds__(256, 2) wgrad_k(WgArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int ctiles = (a.Ncol + BMC - 1) / BMC, ktiles = (a.Ktot + BNK - 1) / BNK;
   const int tiles = ctiles * ktiles;
-  const int split = blockIdx.x / tiles;
-  const int tile = blockIdx.x - split * tiles;
+  // XCD-aware order: the tiles of one reduction split (which read the same
+  // dy rows and overlapping x rows) get consecutive remapped ids, i.e. one
+  // XCD and its L2; the hardware's round-robin order spread them over 8 L2s
+  // (4-11% L2 hit rate on the 56x56 3x3 wgrad).
+  const int bid = KFB_WG_XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int split = bid / tiles;
+  const int tile = bid - split * tiles;
   const int c0 = (tile / ktiles) * BMC, k0 = (tile % ktiles) * BNK;
   const int mbeg = split * a.mper;
   const int mend = min(a.M, mbeg + a.mper);
