@@ -14,6 +14,8 @@
 // so a launch has >= 1024 workgroups on 256 CUs for the ResNet shapes.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace kfb {
 
 constexpr int BN_THREADS = 512;
@@ -204,7 +206,7 @@ __device__ __forceinline__ void coef_load(const float* __restrict__ p, int c, fl
   for (int k = 0; k < V; ++k) o[k] = p[c + k];
 }
 
-template <typename T, int V, bool RES, bool RELU>
+template <typename T, int V, bool RES, bool RELU, int U = 0>
 __global__ void __launch_bounds__(256)
 bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y, long nvec, int C,
            const float* __restrict__ scale, const float* __restrict__ shift) {
@@ -222,6 +224,31 @@ bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y
       v[k] = o;
     }
   };
+  if constexpr (U > 0) {
+    // flat: block b owns vectors [b*256*U, (b+1)*256*U); 256 % cv == 0
+    const unsigned base = blockIdx.x * 256u * U + threadIdx.x;
+    const int c = (int)(threadIdx.x % cv) * V;
+    float sc[V], sf[V], v[U][V], rr[U][V];
+    coef_load<V>(scale, c, sc);
+    coef_load<V>(shift, c, sf);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned i = base + u * 256u;
+      if (i < n) {
+        load_vec<T, V>(x + (long)i * V, v[u]);
+        if (RES) load_vec<T, V>(res + (long)i * V, rr[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned i = base + u * 256u;
+      if (i < n) {
+        apply(v[u], rr[u], sc, sf);
+        store_vec<T, V>(y + (long)i * V, v[u]);
+      }
+    }
+    return;
+  }
   if (stride % cv == 0) {
     const int c = (int)(i0 % cv) * V;
     float sc[V], sf[V];
@@ -267,7 +294,7 @@ bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y
 // is itself a BN output with no ReLU (ResNet v1 projection shortcut,
 // tcb/models/resnet_model.py:60-75), applied from both raw inputs so the
 // shortcut BN output is never materialized.
-template <typename T, int V, bool RELU>
+template <typename T, int V, bool RELU, int U = 0>
 __global__ void __launch_bounds__(256)
 bn_apply2_k(const T* __restrict__ x, const T* __restrict__ xr, T* __restrict__ y, long nvec, int C,
             const float* __restrict__ scale, const float* __restrict__ shift,
@@ -284,6 +311,32 @@ bn_apply2_k(const T* __restrict__ x, const T* __restrict__ xr, T* __restrict__ y
       v[k] = o;
     }
   };
+  if constexpr (U > 0) {  // flat (see bn_apply_k)
+    const unsigned base = blockIdx.x * 256u * U + threadIdx.x;
+    const int c = (int)(threadIdx.x % cv) * V;
+    float a[V], b[V], ar[V], br[V], v[U][V], r[U][V];
+    coef_load<V>(scale, c, a);
+    coef_load<V>(shift, c, b);
+    coef_load<V>(scale_r, c, ar);
+    coef_load<V>(shift_r, c, br);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned i = base + u * 256u;
+      if (i < n) {
+        load_vec<T, V>(x + (long)i * V, v[u]);
+        load_vec<T, V>(xr + (long)i * V, r[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned i = base + u * 256u;
+      if (i < n) {
+        apply(v[u], r[u], a, b, ar, br);
+        store_vec<T, V>(y + (long)i * V, v[u]);
+      }
+    }
+    return;
+  }
   if (stride % cv == 0) {
     const int c = (int)(i0 % cv) * V;
     float a[V], b[V], ar[V], br[V];
@@ -395,7 +448,7 @@ bn_finalize_grad_k(const float* __restrict__ pdy, const float* __restrict__ pdyx
   coefC[c] = (float)(-A * s1 / n - (double)mean[c] * B);
 }
 
-template <typename T, int V, bool MASK, bool DRES>
+template <typename T, int V, bool MASK, bool DRES, int U = 0>
 __global__ void __launch_bounds__(256)
 bn_bwd_apply_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __restrict__ x,
                T* __restrict__ dx, T* __restrict__ dres, long nvec, int C,
@@ -405,6 +458,39 @@ bn_bwd_apply_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __res
   const unsigned cv = (unsigned)(C / V);
   const unsigned n = (unsigned)nvec, stride = gridDim.x * blockDim.x;
   const unsigned i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if constexpr (U > 0) {  // flat (see bn_apply_k)
+    const unsigned base = blockIdx.x * 256u * U + threadIdx.x;
+    const int c = (int)(threadIdx.x % cv) * V;
+    float a[V], b[V], cc[V], g[U][V], xv[U][V], yv[U][V];
+    coef_load<V>(A, c, a);
+    coef_load<V>(B, c, b);
+    coef_load<V>(Cc, c, cc);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned i = base + u * 256u;
+      if (i < n) {
+        load_vec<T, V>(dy + (long)i * V, g[u]);
+        load_vec<T, V>(x + (long)i * V, xv[u]);
+        if (MASK) load_vec<T, V>(y + (long)i * V, yv[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned i = base + u * 256u;
+      if (i < n) {
+        if (MASK) {
+#pragma unroll
+          for (int k = 0; k < V; ++k) g[u][k] = yv[u][k] > 0.f ? g[u][k] : 0.f;
+        }
+        if (DRES) store_vec<T, V>(dres + (long)i * V, g[u]);
+        float o[V];
+#pragma unroll
+        for (int k = 0; k < V; ++k) o[k] = g[u][k] * a[k] + xv[u][k] * b[k] + cc[k];
+        store_vec<T, V>(dx + (long)i * V, o);
+      }
+    }
+    return;
+  }
   // g <- mask(dy); dres <- g; dx <- g*A + x*B + Cc
   auto step2 = [&](unsigned ia, unsigned ib, bool two, const float (&a)[V], const float (&b)[V],
                    const float (&cc)[V]) {
@@ -462,7 +548,7 @@ bn_bwd_apply_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __res
 
 // Backward apply of y = relu(bn(x) + bn_r(xr)) with a pre-masked dy: both
 // input gradients from one read of dy (dx = dy*A + x*B + Cc, dxr likewise).
-template <typename T, int V>
+template <typename T, int V, int U = 0>
 __global__ void __launch_bounds__(256)
 bn_bwd_apply2_k(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ xr,
                 T* __restrict__ dx, T* __restrict__ dxr, long nvec, int C,
@@ -481,6 +567,36 @@ bn_bwd_apply2_k(const T* __restrict__ dy, const T* __restrict__ x, const T* __re
     coef_load<V>(Br, c, k.br);
     coef_load<V>(Cr, c, k.cr);
   };
+  if constexpr (U > 0) {  // flat (see bn_apply_k)
+    const unsigned base = blockIdx.x * 256u * U + threadIdx.x;
+    Co k;
+    coefs((int)(threadIdx.x % cv) * V, k);
+    float g[U][V], xv[U][V], rv[U][V];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned i = base + u * 256u;
+      if (i < n) {
+        load_vec<T, V>(dy + (long)i * V, g[u]);
+        load_vec<T, V>(x + (long)i * V, xv[u]);
+        load_vec<T, V>(xr + (long)i * V, rv[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned i = base + u * 256u;
+      if (i < n) {
+        float o[V], q[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          o[j] = g[u][j] * k.a[j] + xv[u][j] * k.b[j] + k.c[j];
+          q[j] = g[u][j] * k.ar[j] + rv[u][j] * k.br[j] + k.cr[j];
+        }
+        store_vec<T, V>(dx + (long)i * V, o);
+        store_vec<T, V>(dxr + (long)i * V, q);
+      }
+    }
+    return;
+  }
   auto one = [&](unsigned i, const Co& k) {
     float g[V], xv[V], rv[V], o[V], orr[V];
     load_vec<T, V>(dy + (long)i * V, g);
@@ -802,6 +918,26 @@ bn_pool3s2_k(const T* __restrict__ dz, const T* __restrict__ z, const uint8_t* _
   }
 }
 
+// Flat apply passes (KFB_BN_FLAT=U, default 4): one block per 256*U
+// vectors, all of a thread's U loads issued before any compute, no grid-stride
+// loop; needs a power-of-two channel-vector count dividing 256 (else the
+// grid-stride kernels run).  U = 0 selects the grid-stride kernels.
+static int bn_flat_u() {
+  static const int u = [] {
+    const char* e = getenv("KFB_BN_FLAT");
+    return e ? atoi(e) : 4;
+  }();
+  return u;
+}
+
+static bool flat_ok(long nvec, int C, int V) {
+  const int cv = C / V;
+  return bn_flat_u() > 0 && cv > 0 && (cv & (cv - 1)) == 0 && 256 % cv == 0 &&
+         nvec < (1L << 31) - 256L * 8;
+}
+
+static int flat_grid(long nvec) { return (int)((nvec + 256L * 4 - 1) / (256L * 4)); }
+
 static int stream_grid(long nvec) {
   long b = (nvec + 255) / 256;
   if (b > 256L * 16) b = 256L * 16;  // grid-stride beyond 16 blocks per CU
@@ -825,8 +961,25 @@ template <typename T, int V, bool M, bool R>
 static void launch_bwd_apply(int gb, hipStream_t stream, const void* dy, const void* y,
                              const void* x, void* dx, void* dres, long nvec, int C,
                              const float* A, const float* B, const float* Cc) {
-  hipLaunchKernelGGL((bn_bwd_apply_k<T, V, M, R>), dim3(gb), dim3(256), 0, stream, (const T*)dy,
-                     (const T*)y, (const T*)x, (T*)dx, (T*)dres, nvec, C, A, B, Cc);
+  if (flat_ok(nvec, C, V))
+    hipLaunchKernelGGL((bn_bwd_apply_k<T, V, M, R, 4>), dim3(flat_grid(nvec)), dim3(256), 0,
+                       stream, (const T*)dy, (const T*)y, (const T*)x, (T*)dx, (T*)dres, nvec, C,
+                       A, B, Cc);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_k<T, V, M, R>), dim3(gb), dim3(256), 0, stream,
+                       (const T*)dy, (const T*)y, (const T*)x, (T*)dx, (T*)dres, nvec, C, A, B,
+                       Cc);
+}
+
+template <typename T, int V, bool RES, bool RELU>
+static void launch_apply(hipStream_t stream, const void* x, const void* res, void* y, long nvec,
+                         int C, const float* scale, const float* shift) {
+  if (flat_ok(nvec, C, V))
+    hipLaunchKernelGGL((bn_apply_k<T, V, RES, RELU, 4>), dim3(flat_grid(nvec)), dim3(256), 0,
+                       stream, (const T*)x, (const T*)res, (T*)y, nvec, C, scale, shift);
+  else
+    hipLaunchKernelGGL((bn_apply_k<T, V, RES, RELU>), dim3(stream_grid(nvec)), dim3(256), 0,
+                       stream, (const T*)x, (const T*)res, (T*)y, nvec, C, scale, shift);
 }
 
 }  // namespace kfb
@@ -862,21 +1015,12 @@ KFB_API hipError_t kfb_bn_fwd_train(int dtype, const void* x, const void* res, v
                          psq, nslab, C, rows, gamma, beta, decay, eps, run_mean, run_var,
                          save_mean, save_invstd, scale, shift);
       const long nvec = rows * C / VV;
-      const int gb = stream_grid(nvec);
       if (res) {
-        if (relu)
-          hipLaunchKernelGGL((bn_apply_k<T, VV, true, true>), dim3(gb), dim3(256), 0, stream,
-                             (const T*)x, (const T*)res, (T*)y, nvec, C, scale, shift);
-        else
-          hipLaunchKernelGGL((bn_apply_k<T, VV, true, false>), dim3(gb), dim3(256), 0, stream,
-                             (const T*)x, (const T*)res, (T*)y, nvec, C, scale, shift);
+        if (relu) launch_apply<T, VV, true, true>(stream, x, res, y, nvec, C, scale, shift);
+        else launch_apply<T, VV, true, false>(stream, x, res, y, nvec, C, scale, shift);
       } else {
-        if (relu)
-          hipLaunchKernelGGL((bn_apply_k<T, VV, false, true>), dim3(gb), dim3(256), 0, stream,
-                             (const T*)x, (const T*)nullptr, (T*)y, nvec, C, scale, shift);
-        else
-          hipLaunchKernelGGL((bn_apply_k<T, VV, false, false>), dim3(gb), dim3(256), 0, stream,
-                             (const T*)x, (const T*)nullptr, (T*)y, nvec, C, scale, shift);
+        if (relu) launch_apply<T, VV, false, true>(stream, x, nullptr, y, nvec, C, scale, shift);
+        else launch_apply<T, VV, false, false>(stream, x, nullptr, y, nvec, C, scale, shift);
       }
     });
   });
@@ -904,15 +1048,27 @@ KFB_API hipError_t kfb_bn_fwd_train_dual(
   KFB_DISPATCH_DTYPE(dtype, T, {
     KFB_DISPATCH_VEC(V, VV, {
       const long nvec = rows * C / VV;
-      const int gb = stream_grid(nvec);
-      if (relu)
-        hipLaunchKernelGGL((bn_apply2_k<T, VV, true>), dim3(gb), dim3(256), 0, stream,
-                           (const T*)x, (const T*)xr, (T*)y, nvec, C, scale, shift, scale_r,
-                           shift_r);
-      else
-        hipLaunchKernelGGL((bn_apply2_k<T, VV, false>), dim3(gb), dim3(256), 0, stream,
-                           (const T*)x, (const T*)xr, (T*)y, nvec, C, scale, shift, scale_r,
-                           shift_r);
+      const bool flat = flat_ok(nvec, C, VV);
+      const int gb = flat ? flat_grid(nvec) : stream_grid(nvec);
+      if (relu) {
+        if (flat)
+          hipLaunchKernelGGL((bn_apply2_k<T, VV, true, 4>), dim3(gb), dim3(256), 0, stream,
+                             (const T*)x, (const T*)xr, (T*)y, nvec, C, scale, shift, scale_r,
+                             shift_r);
+        else
+          hipLaunchKernelGGL((bn_apply2_k<T, VV, true>), dim3(gb), dim3(256), 0, stream,
+                             (const T*)x, (const T*)xr, (T*)y, nvec, C, scale, shift, scale_r,
+                             shift_r);
+      } else {
+        if (flat)
+          hipLaunchKernelGGL((bn_apply2_k<T, VV, false, 4>), dim3(gb), dim3(256), 0, stream,
+                             (const T*)x, (const T*)xr, (T*)y, nvec, C, scale, shift, scale_r,
+                             shift_r);
+        else
+          hipLaunchKernelGGL((bn_apply2_k<T, VV, false>), dim3(gb), dim3(256), 0, stream,
+                             (const T*)x, (const T*)xr, (T*)y, nvec, C, scale, shift, scale_r,
+                             shift_r);
+      }
     });
   });
   return hipGetLastError();
@@ -929,21 +1085,12 @@ KFB_API hipError_t kfb_bn_fwd_infer(int dtype, const void* x, const void* res, v
   KFB_DISPATCH_DTYPE(dtype, T, {
     KFB_DISPATCH_VEC(V, VV, {
       const long nvec = rows * C / VV;
-      const int gb = stream_grid(nvec);
       if (res) {
-        if (relu)
-          hipLaunchKernelGGL((bn_apply_k<T, VV, true, true>), dim3(gb), dim3(256), 0, stream,
-                             (const T*)x, (const T*)res, (T*)y, nvec, C, scale, shift);
-        else
-          hipLaunchKernelGGL((bn_apply_k<T, VV, true, false>), dim3(gb), dim3(256), 0, stream,
-                             (const T*)x, (const T*)res, (T*)y, nvec, C, scale, shift);
+        if (relu) launch_apply<T, VV, true, true>(stream, x, res, y, nvec, C, scale, shift);
+        else launch_apply<T, VV, true, false>(stream, x, res, y, nvec, C, scale, shift);
       } else {
-        if (relu)
-          hipLaunchKernelGGL((bn_apply_k<T, VV, false, true>), dim3(gb), dim3(256), 0, stream,
-                             (const T*)x, (const T*)nullptr, (T*)y, nvec, C, scale, shift);
-        else
-          hipLaunchKernelGGL((bn_apply_k<T, VV, false, false>), dim3(gb), dim3(256), 0, stream,
-                             (const T*)x, (const T*)nullptr, (T*)y, nvec, C, scale, shift);
+        if (relu) launch_apply<T, VV, false, true>(stream, x, nullptr, y, nvec, C, scale, shift);
+        else launch_apply<T, VV, false, false>(stream, x, nullptr, y, nvec, C, scale, shift);
       }
     });
   });
@@ -1024,9 +1171,14 @@ KFB_API hipError_t kfb_bn_bwd_dual(
                          pdy_r, pdyx_r, nslab_r, C, rows, gamma_r, save_mean_r, save_invstd_r,
                          dgamma_r, dbeta_r, coefA_r, coefB_r, coefC_r, accumulate_r);
       const long nvec = rows * C / VV;
-      hipLaunchKernelGGL((bn_bwd_apply2_k<T, VV>), dim3(stream_grid(nvec)), dim3(256), 0, stream,
-                         (const T*)dy, (const T*)x, (const T*)xr, (T*)dx, (T*)dxr, nvec, C, coefA,
-                         coefB, coefC, coefA_r, coefB_r, coefC_r);
+      if (flat_ok(nvec, C, VV))
+        hipLaunchKernelGGL((bn_bwd_apply2_k<T, VV, 4>), dim3(flat_grid(nvec)), dim3(256), 0,
+                           stream, (const T*)dy, (const T*)x, (const T*)xr, (T*)dx, (T*)dxr, nvec,
+                           C, coefA, coefB, coefC, coefA_r, coefB_r, coefC_r);
+      else
+        hipLaunchKernelGGL((bn_bwd_apply2_k<T, VV>), dim3(stream_grid(nvec)), dim3(256), 0,
+                           stream, (const T*)dy, (const T*)x, (const T*)xr, (T*)dx, (T*)dxr, nvec,
+                           C, coefA, coefB, coefC, coefA_r, coefB_r, coefC_r);
     });
   });
   return hipGetLastError();
