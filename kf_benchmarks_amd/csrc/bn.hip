@@ -85,15 +85,16 @@ __device__ __forceinline__ void block_row_reduce(float (&a)[V], float (&b)[V], f
 template <typename T, int V>
 __global__ void __launch_bounds__(BN_THREADS)
 bn_partial_stats_k(const T* __restrict__ x, long rows, int C, int cw, int tpr, int rpi,
-                   long slab_rows, float* __restrict__ psum, float* __restrict__ psq) {
+                   long slab_rows, float* __restrict__ psum, float* __restrict__ psq,
+                   const float* __restrict__ kshift) {
   extern __shared__ float lds[];
   const int tid = threadIdx.x;
   const int t = tid % tpr, r = tid / tpr;
   const int c0 = blockIdx.y * cw + t * V;
   const bool cok = (c0 < C) && (r < rpi);
-  float s[V], q[V];
+  float s[V], q[V], k[V];
 #pragma unroll
-  for (int i = 0; i < V; ++i) { s[i] = 0.f; q[i] = 0.f; }
+  for (int i = 0; i < V; ++i) { s[i] = 0.f; q[i] = 0.f; k[i] = (kshift && cok) ? kshift[c0 + i] : 0.f; }
   const long rbeg = (long)blockIdx.x * slab_rows;
   long rend = rbeg + slab_rows;
   if (rend > rows) rend = rows;
@@ -102,7 +103,11 @@ bn_partial_stats_k(const T* __restrict__ x, long rows, int C, int cw, int tpr, i
       float v[V];
       load_vec<T, V>(x + row * C + c0, v);
 #pragma unroll
-      for (int i = 0; i < V; ++i) { s[i] += v[i]; q[i] += v[i] * v[i]; }
+      for (int i = 0; i < V; ++i) {
+        const float e = v[i] - k[i];
+        s[i] += e;
+        q[i] += e * e;
+      }
     }
   }
   block_row_reduce<V>(s, q, lds, t, r, tpr, rpi);
@@ -158,15 +163,24 @@ bn_finalize_stats_k(const float* __restrict__ psum, const float* __restrict__ ps
                     const float* __restrict__ beta, float decay, float eps,
                     float* __restrict__ run_mean, float* __restrict__ run_var,
                     float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                    float* __restrict__ scale, float* __restrict__ shift) {
+                    float* __restrict__ scale, float* __restrict__ shift,
+                    float* __restrict__ kshift) {
   const int c = blockIdx.x * 64 + threadIdx.x;
   double s, q;
   fold_slabs(psum, psq, nslab, C, c, s, q);
   if (threadIdx.y != 0 || c >= C) return;
+  // Shifted statistics: the partials are sums of (x - K) and (x - K)^2 with
+  // K = kshift[c] (the previous step's batch mean of this BN, 0 at first),
+  // so var = E[(x-K)^2] - E[x-K]^2 cancels only |mean - K|^2, not mean^2
+  // (the plain E[x^2] - E[x]^2 loses every digit of a channel whose mean is
+  // large next to its spread).  This step's mean becomes the next step's K.
   const double n = (double)rows;
-  const double mean = s / n;
-  double var = q / n - mean * mean;
+  const double k = kshift ? (double)kshift[c] : 0.0;
+  const double dm = s / n;
+  const double mean = k + dm;
+  double var = q / n - dm * dm;
   if (var < 0.0) var = 0.0;
+  if (kshift) kshift[c] = (float)mean;
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   const float g = gamma ? gamma[c] : 1.f;
   const float b = beta ? beta[c] : 0.f;
@@ -1000,7 +1014,7 @@ KFB_API hipError_t kfb_bn_fwd_train(int dtype, const void* x, const void* res, v
                                     float eps, float* run_mean, float* run_var, float* save_mean,
                                     float* save_invstd, float* scale, float* shift, float* psum,
                                     float* psq, int nslab, int relu, int have_partials,
-                                    hipStream_t stream) {
+                                    float* kshift, hipStream_t stream) {
   const int V = vec_width(C);
   KFB_DISPATCH_DTYPE(dtype, T, {
     KFB_DISPATCH_VEC(V, VV, {
@@ -1010,10 +1024,11 @@ KFB_API hipError_t kfb_bn_fwd_train(int dtype, const void* x, const void* res, v
       const size_t lds = 2 * (size_t)g.rpi * g.tpr * VV * sizeof(float);
       if (!have_partials)  // else the producing conv's epilogue already summed y, y^2
         hipLaunchKernelGGL((bn_partial_stats_k<T, VV>), grid, dim3(BN_THREADS), lds, stream,
-                           (const T*)x, rows, C, g.cw, g.tpr, g.rpi, slab_rows, psum, psq);
+                           (const T*)x, rows, C, g.cw, g.tpr, g.rpi, slab_rows, psum, psq,
+                           kshift);
       hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, psum,
                          psq, nslab, C, rows, gamma, beta, decay, eps, run_mean, run_var,
-                         save_mean, save_invstd, scale, shift);
+                         save_mean, save_invstd, scale, shift, kshift);
       const long nvec = rows * C / VV;
       if (res) {
         if (relu) launch_apply<T, VV, true, true>(stream, x, res, y, nvec, C, scale, shift);
@@ -1037,14 +1052,14 @@ KFB_API hipError_t kfb_bn_fwd_train_dual(
     int nslab, const float* gamma_r, const float* beta_r, float decay_r, float eps_r,
     float* run_mean_r, float* run_var_r, float* save_mean_r, float* save_invstd_r,
     float* scale_r, float* shift_r, const float* psum_r, const float* psq_r, int nslab_r,
-    int relu, hipStream_t stream) {
+    int relu, float* kshift, float* kshift_r, hipStream_t stream) {
   const int V = vec_width(C);
   hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, psum_r,
                      psq_r, nslab_r, C, rows, gamma_r, beta_r, decay_r, eps_r, run_mean_r,
-                     run_var_r, save_mean_r, save_invstd_r, scale_r, shift_r);
+                     run_var_r, save_mean_r, save_invstd_r, scale_r, shift_r, kshift_r);
   hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, psum,
                      psq, nslab, C, rows, gamma, beta, decay, eps, run_mean, run_var, save_mean,
-                     save_invstd, scale, shift);
+                     save_invstd, scale, shift, kshift);
   KFB_DISPATCH_DTYPE(dtype, T, {
     KFB_DISPATCH_VEC(V, VV, {
       const long nvec = rows * C / VV;
@@ -1193,14 +1208,14 @@ KFB_API hipError_t kfb_bn_relu_maxpool_fwd(int dtype, const void* x, void* z, ui
                                            const float* beta, float decay, float eps,
                                            float* run_mean, float* run_var, float* save_mean,
                                            float* save_invstd, float* scale, float* shift,
-                                           float* psum, float* psq, int nslab,
+                                           float* psum, float* psq, int nslab, float* kshift,
                                            hipStream_t stream) {
   if (C % 8 || kh * kw > 255 || (long)N * H * W * C >= (1L << 31)) return hipErrorInvalidValue;
   const BPGeo g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
   const long rows = (long)N * H * W;
   hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, psum, psq,
                      nslab, C, rows, gamma, beta, decay, eps, run_mean, run_var, save_mean,
-                     save_invstd, scale, shift);
+                     save_invstd, scale, shift, kshift);
   const long total = (long)N * OH * OW * (C / 8);
   KFB_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL((bn_relu_maxpool_fwd_k<T, 8>), dim3(stream_grid(total)), dim3(256), 0,

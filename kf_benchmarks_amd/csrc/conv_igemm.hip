@@ -93,6 +93,9 @@ struct IgArgs {
   // byte size of the output layout (= that of addend / mask / xbn), or 0 if
   // >= 2 GiB (the epilogue then uses plain loads instead of buffer loads)
   int ybytes;
+  // forward statistics only: per-channel shift K (nullable); the partials
+  // are sums of (y - K) and (y - K)^2 (see bn_finalize_stats_k)
+  const float* kshift;
 };
 
 constexpr int IG_BK = 64;
@@ -135,6 +138,16 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
   T* __restrict__ y = (T*)a.y;
   T* cs = smem;  // reuse the operand buffers (the final __syncthreads above retired them)
   constexpr int CPR = BN / 8;  // 16-byte chunks per staged row
+  // statistics shift of this thread's 8 channels (forward statistics only:
+  // the host passes kshift only without addend / xbn, so the dgrad-style
+  // branch - the epilogue's register peak - never holds it); issued before
+  // the staging pass so its latency hides behind it
+  float kv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int n = n0 + (tid % CPR) * 8 + k;
+    kv[k] = (a.kshift && n < a.Ncol) ? a.kshift[n] : 0.f;
+  }
 #pragma unroll
   for (int j = 0; j < TM; ++j) {
     const int ml = wm * (BM / WGM) + j * 16 + (lane & 15);
@@ -208,7 +221,7 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
           const Vec<T, 8> tv = __builtin_bit_cast(Vec<T, 8>, raw);
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            const float v = (float)tv.v[k];
+            const float v = (float)tv.v[k] - kv[k];
             s1[k] += v;
             s2[k] += v * v;
           }
@@ -295,8 +308,8 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
       } else if (a.stats) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          s1[k] += v[k];
-          s2[k] += v[k] * v[k];
+          s1[k] += v[k] - kv[k];
+          s2[k] += (v[k] - kv[k]) * (v[k] - kv[k]);
         }
       }
       Vec<T, 8> ov;
@@ -1136,14 +1149,16 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
                                   int pt, int pl, int Ncol, int YH, int YW, int ys, int ldy,
                                   int trans, float* stats, const void* mask, const void* xbn,
                                   const float* mean, const void* addend, const float* mcoef,
-                                  const float* bias, int relu, int algo, hipStream_t stream) {
+                                  const float* bias, int relu, int algo, const float* kshift,
+                                  hipStream_t stream) {
   if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
   const long xbytes = (long)N * H * W * C * 2, wbytes = (long)Ncol * KH * KW * C * 2;
   const long ybytes = (long)N * YH * YW * ldy * 2;
   IgArgs a{x, w, y, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
            N * OH * OW, YH, YW, ys, ldy, stats, mask, xbn, mean, addend, mcoef, bias, relu,
            (int)(xbytes < (1L << 31) ? xbytes : 0), (int)(wbytes < (1L << 31) ? wbytes : 0),
-           (int)(ybytes < (1L << 31) ? ybytes : 0)};
+           (int)(ybytes < (1L << 31) ? ybytes : 0),
+           (stats && !xbn && !addend) ? kshift : nullptr};
   const bool t = trans != 0;
   const bool fast = !t && C % IG_BK == 0 && KH * KW <= 64 && xbytes < (1L << 31) &&
                     wbytes < (1L << 31) && !igemm_fast_disabled();

@@ -174,7 +174,11 @@ class ConvNetBuilder:
         if use_batch_norm and self.phase_train and not self.meta and \
                 conv_ops.fills_bn_stats(x, num_out_channels, self.impl):
             from ..ops import conv_hip
-            stats = conv_hip.stats_buffer(num_out_channels, x.device)
+            # partials centered on the BN's previous batch mean (the BN this
+            # conv feeds is created under the same scope right below)
+            stats = conv_hip.stats_buffer(num_out_channels, x.device,
+                                          shift=self._peek_bn_layer(name, num_out_channels)
+                                          .stat_shift)
         layer.stride = (d_height, d_width)
         relu = activation == "relu"
         # conv + bias (+ ReLU) without BN: applied in the conv's epilogue
@@ -382,6 +386,16 @@ class ConvNetBuilder:
         x = self.top_layer if input_layer is None else input_layer
         return self._batch_norm(x, decay=decay, scale=scale, epsilon=epsilon, relu=relu,
                                 residual=residual)
+
+    def _peek_bn_layer(self, name, C):
+        """The BN layer the next _bn_layer call under scope ``name`` returns
+        (created now if new; the batchnorm counter is not advanced)."""
+        cfg = self.batch_norm_config
+        with self.scope(name):
+            scope = self._scoped("batchnorm%d" % self.counts["batchnorm"])
+        return self._layer(scope, lambda: BatchNormLayer(
+            scope, C, cfg.get("scale", False), cfg.get("decay", 0.999), cfg.get("epsilon", 0.001),
+            self.net.param_device))
 
     def _bn_layer(self, C, scale, decay, epsilon):
         name = "batchnorm%d" % self.counts["batchnorm"]

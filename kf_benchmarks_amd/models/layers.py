@@ -129,6 +129,10 @@ class BatchNormLayer(Layer):
         self.beta = nn.Parameter(torch.zeros(channels, device=device))
         self.register_buffer("moving_mean", torch.zeros(channels, device=device))
         self.register_buffer("moving_variance", torch.ones(channels, device=device))
+        # shift of the training-mode statistics partials (the previous step's
+        # batch mean; csrc/bn.hip bn_finalize_stats_k) - not a TF variable
+        self.register_buffer("stat_shift", torch.zeros(channels, device=device),
+                             persistent=False)
 
     def tf_variables(self):
         out = {"beta": self.beta.detach(), "moving_mean": self.moving_mean,

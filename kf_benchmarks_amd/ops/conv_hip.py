@@ -21,7 +21,7 @@ import torch
 from . import _native as N
 
 _SIG = ([N.I, N.P, N.P, N.P] + [N.I] * 17 + [N.I, N.P, N.P, N.P, N.P, N.P, N.P]
-        + [N.P, N.I] + [N.I, N.P])  # ... mcoef, bias, relu, algo, stream
+        + [N.P, N.I] + [N.I, N.P, N.P])  # ... mcoef, bias, relu, algo, kshift, stream
 N.register_optional("kfb_conv_igemm", _SIG)
 N.register_optional("kfb_conv_igemm_fast", [N.I] * 4, N.c_int)
 
@@ -59,6 +59,8 @@ def _pad8(n):
 
 
 STATS_SPREAD = 32  # must match IG_SPREAD in csrc/conv_igemm.hip (checked at load)
+# KFB_BN_SHIFT=0: uncentered statistics partials (A/B switch)
+_STATS_SHIFT = os.environ.get("KFB_BN_SHIFT", "1") != "0"
 
 
 class _StatsArena:
@@ -105,8 +107,11 @@ STATS_ARENA = _StatsArena()
 _SPREAD_CHECKED = False
 
 
-def stats_buffer(channels, device):
-    """Zeroed [2][STATS_SPREAD][C] fp32 buffer for fused BN partial sums."""
+def stats_buffer(channels, device, shift=None):
+    """Zeroed [2][STATS_SPREAD][C] fp32 buffer for fused BN partial sums.
+    ``shift`` (fp32 [C], the consuming BN's stat_shift): the conv epilogue
+    sums y - shift and (y - shift)^2, and the BN finalize undoes it; the
+    buffer carries it (``_kfb_shift``) so producer and consumer agree."""
     global _SPREAD_CHECKED
     if not _SPREAD_CHECKED:
         lib_spread = N.query("kfb_conv_stats_spread")
@@ -114,14 +119,22 @@ def stats_buffer(channels, device):
             raise N.NativeError("stats spread mismatch: library %d, Python %d"
                                 % (lib_spread, STATS_SPREAD))
         _SPREAD_CHECKED = True
-    return STATS_ARENA.take(2 * STATS_SPREAD * channels, device)[:2 * STATS_SPREAD * channels]
+    buf = STATS_ARENA.take(2 * STATS_SPREAD * channels, device)[:2 * STATS_SPREAD * channels]
+    if shift is not None and _STATS_SHIFT:
+        buf._kfb_shift = shift
+    return buf
+
+
+def stats_shift(stats):
+    """The statistics shift a stats buffer was filled with (None: none)."""
+    return getattr(stats, "_kfb_shift", None) if stats is not None else None
 
 
 def _igemm_call(algo, x, wmat, y, geo, stats=None, mask=None, xbn=None, mean=None, addend=None,
                 mcoef=None, bias=None, relu=False):
     N.call("kfb_conv_igemm", N.dt(x), x.data_ptr(), wmat.data_ptr(), y.data_ptr(), *geo,
            N.ptr(stats), N.ptr(mask), N.ptr(xbn), N.ptr(mean), N.ptr(addend), N.ptr(mcoef),
-           N.ptr(bias), int(relu), algo, N.stream(x.device))
+           N.ptr(bias), int(relu), algo, N.ptr(stats_shift(stats)), N.stream(x.device))
 
 
 def _time_candidates(cands, run, rounds=2, reps=3):

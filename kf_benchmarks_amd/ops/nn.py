@@ -31,6 +31,11 @@ def _on_gpu(t: torch.Tensor) -> bool:
     return t.is_cuda
 
 
+def _conv_hip():
+    from . import conv_hip
+    return conv_hip
+
+
 # ----------------------------------------------------------------- padding math
 def same_pads(in_size: int, k: int, s: int) -> Tuple[int, int]:
     """TF 'SAME' padding (begin, end) for one spatial dim."""
@@ -202,7 +207,7 @@ class _BatchNormTrain(torch.autograd.Function):
                N.ptr(gamma), N.ptr(beta), float(decay), float(eps), N.ptr(rm), N.ptr(rv),
                st[0].data_ptr(), st[1].data_ptr(), coef[:C].data_ptr(),
                coef[C:].data_ptr(), psum.data_ptr(), psq.data_ptr(), nslab, int(relu),
-               int(stats is not None), N.stream(dev))
+               int(stats is not None), N.ptr(_conv_hip().stats_shift(stats)), N.stream(dev))
         ctx.save_for_backward(x, y if relu else None, gamma, st)
         ctx.relu = relu
         ctx.has_res = residual is not None
@@ -338,7 +343,9 @@ class _BatchNormTrainDual(torch.autograd.Function):
                nslab, N.ptr(gamma_r), N.ptr(beta_r), float(decay_r), float(eps_r), N.ptr(rm_r),
                N.ptr(rv_r), ws[1, 0].data_ptr(), ws[1, 1].data_ptr(), ws[1, 2].data_ptr(),
                ws[1, 3].data_ptr(), stats_r[:nslab_r * C].data_ptr(),
-               stats_r[nslab_r * C:].data_ptr(), nslab_r, int(relu), N.stream(dev))
+               stats_r[nslab_r * C:].data_ptr(), nslab_r, int(relu),
+               N.ptr(_conv_hip().stats_shift(stats)), N.ptr(_conv_hip().stats_shift(stats_r)),
+               N.stream(dev))
         st, st_r = ws[0, :2], ws[1, :2]
         ctx.save_for_backward(x, y if relu else None, gamma, st, xr, gamma_r, st_r)
         ctx.relu = relu
@@ -591,7 +598,7 @@ class _AvgPool(torch.autograd.Function):
 
 
 N.register_optional("kfb_bn_relu_maxpool_fwd", [N.I, N.P, N.P, N.P] + [N.I] * 12 +
-                    [N.P, N.P, N.F, N.F] + [N.P] * 8 + [N.I, N.P])
+                    [N.P, N.P, N.F, N.F] + [N.P] * 8 + [N.I, N.P, N.P])
 N.register_optional("kfb_bn_pool_num_slabs", [N.I] * 8, N.c_int)
 N.register_optional("kfb_bn_relu_maxpool_bwd", [N.I, N.P, N.P, N.P, N.P, N.P] + [N.I] * 12 +
                     [N.P] * 7 + [N.I] + [N.P] * 3 + [N.I, N.P])
@@ -616,7 +623,7 @@ class _BNReluMaxPool(torch.autograd.Function):
                *geo, N.ptr(gamma), N.ptr(beta), float(decay), float(eps), N.ptr(rm), N.ptr(rv),
                st[0].data_ptr(), st[1].data_ptr(), st[2].data_ptr(), st[3].data_ptr(),
                stats[:nslab * C].data_ptr(), stats[nslab * C:].data_ptr(), nslab,
-               N.stream(dev))
+               N.ptr(_conv_hip().stats_shift(stats)), N.stream(dev))
         ctx.save_for_backward(x, z, idx, gamma, st)
         ctx.geo = geo
         ctx.gamma, ctx.beta = gamma, beta

@@ -269,3 +269,35 @@ def test_conv_bias_relu_epilogue(cuda, shape, relu):
     torch.testing.assert_close(wa.grad.cpu(), wb.grad, rtol=3e-2,
                                atol=2e-2 * wb.grad.abs().max().item())
     torch.testing.assert_close(ba.grad.cpu(), bb.grad, rtol=2e-2, atol=2e-2 * scale * 50)
+
+
+@pytest.mark.parametrize("shifted", [True, False])
+def test_bn_stats_large_mean_shifted(cuda, shifted):
+    """Conv-epilogue BN statistics of a channel whose mean is ~500x its
+    spread (fp16 identity 1x1 conv over 500 + N(0, 1)): with the partials
+    centered on the previous batch mean (stats_buffer(shift=...), as the
+    model builder wires it) the batch variance is exact to fp32 rounding,
+    and the BN writes this step's mean back as the next step's shift."""
+    from kf_benchmarks_amd.ops import conv_hip
+    g = torch.Generator().manual_seed(11)
+    C = 64
+    x = (500.0 + torch.randn(16, 16, 16, C, generator=g)).to(torch.float16)
+    w = torch.eye(C).view(C, 1, 1, C).to(torch.float16)
+    shift = torch.full((C,), 499.5, device=cuda) if shifted else None
+    st = conv_hip.stats_buffer(C, cuda, shift=shift).zero_()
+    y = conv_hip.conv_fwd(x.to(cuda), w.to(cuda), (1, 1), (0, 0, 0, 0), st)
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    out = F.batch_norm(y, None, torch.zeros(C, device=cuda), rm, rv, 0.9, 1e-5, True,
+                       stats=st).double().cpu()
+    yd = y.double().cpu().view(-1, C)
+    mean, var = yd.mean(0), yd.var(0, unbiased=False)
+    ref = ((yd - mean) / (var + 1e-5).sqrt()).view(out.shape)
+    if shifted:
+        torch.testing.assert_close(out, ref, rtol=0, atol=2e-2)
+        torch.testing.assert_close(shift.double().cpu(), mean, rtol=0, atol=1e-3)
+        # running variance (unbiased, decay 0.9) from the exact batch variance
+        n = yd.shape[0]
+        torch.testing.assert_close(rv.double().cpu(), 0.9 + 0.1 * var * n / (n - 1),
+                                   rtol=1e-3, atol=0)
+    else:  # uncentered fp32 partials: finite, but only the shifted path is pinned
+        assert torch.isfinite(out).all()
