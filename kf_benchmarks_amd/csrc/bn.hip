@@ -932,22 +932,27 @@ bn_pool3s2_k(const T* __restrict__ dz, const T* __restrict__ z, const uint8_t* _
   }
 }
 
-// Flat apply passes (KFB_BN_FLAT=U, default 4): one block per 256*U
-// vectors, all of a thread's U loads issued before any compute, no grid-stride
-// loop; needs a power-of-two channel-vector count dividing 256 (else the
-// grid-stride kernels run).  U = 0 selects the grid-stride kernels.
-static int bn_flat_u() {
-  static const int u = [] {
+// Flat apply passes: one block per 1024 vectors, all of a thread's 4 loads
+// issued before any compute, no grid-stride loop; needs a power-of-two
+// channel-vector count dividing 256.  Used for tensors of >= 256 MB (ResNet-50
+// bs256 stage 1: 4.3 -> 5.6 TB/s in isolation, +1% on the step); below that
+// the grid-stride passes run (isolated rates within +-5%, but the flat grids
+// cost ResNet-152 bs128 ~6% beside the weight-gradient stream).
+// KFB_BN_FLAT=0: never flat; KFB_BN_FLAT=2: flat at every size.
+static int bn_flat_mode() {
+  static const int m = [] {
     const char* e = getenv("KFB_BN_FLAT");
-    return e ? atoi(e) : 4;
+    return e ? atoi(e) : 1;
   }();
-  return u;
+  return m;
 }
 
 static bool flat_ok(long nvec, int C, int V) {
   const int cv = C / V;
-  return bn_flat_u() > 0 && cv > 0 && (cv & (cv - 1)) == 0 && 256 % cv == 0 &&
-         nvec < (1L << 31) - 256L * 8;
+  const int mode = bn_flat_mode();
+  const long bytes = nvec * 16;
+  return mode > 0 && (mode == 2 || bytes >= (256L << 20)) && cv > 0 && (cv & (cv - 1)) == 0 &&
+         256 % cv == 0 && nvec < (1L << 31) - 256L * 8;
 }
 
 static int flat_grid(long nvec) { return (int)((nvec + 256L * 4 - 1) / (256L * 4)); }

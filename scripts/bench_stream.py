@@ -27,7 +27,8 @@ def timeit(fn, iters=20):
 
 def main():
     dev = torch.device("cuda", 0)
-    shapes = [(256, 56, 56, 256), (256, 28, 28, 512), (256, 14, 14, 1024), (256, 56, 56, 64)]
+    shapes = [tuple(int(v) for v in s.split("x")) for s in (sys.argv[1].split(",") if len(sys.argv) > 1 else
+              ["256x56x56x256", "256x28x28x512", "256x14x14x1024", "256x56x56x64"])]
     for shp in shapes:
         x = torch.randn(shp, device=dev, dtype=torch.bfloat16)
         r = torch.randn(shp, device=dev, dtype=torch.bfloat16)
