@@ -152,3 +152,45 @@ KFB_API hipError_t kfb_concat(int dtype, void* out, void* const* ptrs, const int
   });
   return hipGetLastError();
 }
+
+// ----------------------------------------------------- anchor-major heads
+// SSD300 prediction heads (tcb/models/ssd_model.py): each head's NHWC
+// output [nb][A = H*W][Bd = anchors per pixel][R = 4 or classes] goes to rows
+// row0 + j*A + i (anchor-major), columns col0.. of the [nb][rows][ld] logits
+// tensor - one launch per head instead of a permute copy plus two concats.
+// dir = 1 is the backward: the head's gradient gathered back from dlogits.
+namespace kfb {
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+heads_k(const T* __restrict__ src, T* __restrict__ dst, int nb, int A, int Bd, int R,
+        long row0, int col0, long ob, int ld, int dir) {
+  const long n = (long)nb * A * Bd * R;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int r = (int)(e % R);
+    long q = e / R;
+    const int j = (int)(q % Bd);
+    q /= Bd;
+    const int i = (int)(q % A);
+    const int b = (int)(q / A);
+    const long o = b * ob + (row0 + (long)j * A + i) * ld + col0 + r;  // logits element
+    if (dir == 0) dst[o] = src[e];
+    else dst[e] = src[o];
+  }
+}
+
+}  // namespace kfb
+
+KFB_API hipError_t kfb_ssd_heads(int dtype, const void* src, void* dst, int nb, int A, int Bd,
+                                 int R, long row0, int col0, long ob, int ld, int dir,
+                                 hipStream_t stream) {
+  const long n = (long)nb * A * Bd * R;
+  long blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  KFB_DISPATCH_DTYPE(dtype, T,
+                     hipLaunchKernelGGL(kfb::heads_k<T>, dim3((unsigned)blocks), dim3(256), 0,
+                                        stream, (const T*)src, (T*)dst, nb, A, Bd, R, row0, col0,
+                                        ob, ld, dir));
+  return hipGetLastError();
+}

@@ -84,7 +84,6 @@ class SSD300Model(model_lib.CNNModel):
             ssd_layer(mid, 1, 1, "VALID")
             acts.append(ssd_layer(out, 3, stride, mode))
         locs, confs = [], []
-        B = acts[0].shape[0]
         for nd, ac, oc in zip(self.num_dboxes, acts, self.out_chan):
             l = cnn.conv(nd * 4, 3, 3, 1, 1, input_layer=ac, num_channels_in=oc,
                          activation=None, use_batch_norm=False,
@@ -92,12 +91,11 @@ class SSD300Model(model_lib.CNNModel):
             c = cnn.conv(nd * self.label_num, 3, 3, 1, 1, input_layer=ac, num_channels_in=oc,
                          activation=None, use_batch_norm=False,
                          kernel_initializer=_xavier(oc, 3, nd * self.label_num))
-            H, W = l.shape[1], l.shape[2]
-            # NHWC [B,H,W,nd*k] -> [B, nd*H*W, k] in (anchor, row, col) order
-            locs.append(l.reshape(B, H, W, nd, 4).permute(0, 3, 1, 2, 4).reshape(B, -1, 4))
-            confs.append(c.reshape(B, H, W, nd, self.label_num).permute(0, 3, 1, 2, 4)
-                         .reshape(B, -1, self.label_num))
-        logits = torch.cat([torch.cat(locs, 1), torch.cat(confs, 1)], dim=2)
+            locs.append(l)
+            confs.append(c)
+        # NHWC [B,H,W,nd*k] heads -> [B, sum nd*H*W, 4 + classes] in (anchor, row, col)
+        # order (one kernel per head on the GPU)
+        logits = F_ops.ssd_heads(locs, confs, list(self.num_dboxes), self.label_num)
         cnn.top_layer = logits
         cnn.top_size = 4 + self.label_num
         return logits

@@ -1004,6 +1004,61 @@ class _SSDLoss(torch.autograd.Function):
         return dl, None, None, None, None
 
 
+class _SSDHeads(torch.autograd.Function):
+    """Anchor-major SSD logits [B, sum(nd*H*W), 4 + classes] from the NHWC
+    loc / conf head outputs (kfb_ssd_heads: one launch per head, its
+    backward the same walk gathering the head gradients)."""
+
+    @staticmethod
+    def forward(ctx, nds, ncls, *heads):
+        k = len(heads) // 2
+        locs, confs = heads[:k], heads[k:]
+        B = locs[0].shape[0]
+        rows = sum(nd * l.shape[1] * l.shape[2] for nd, l in zip(nds, locs))
+        ld = 4 + ncls
+        out = torch.empty((B, rows, ld), dtype=locs[0].dtype, device=locs[0].device)
+        st = N.stream(out.device)
+        row0 = 0
+        geo = []
+        for nd, l, c in zip(nds, locs, confs):
+            A = l.shape[1] * l.shape[2]
+            for t, col0, R in ((l, 0, 4), (c, 4, ncls)):
+                t = t.contiguous()
+                N.call("kfb_ssd_heads", N.dt(t), t.data_ptr(), out.data_ptr(), B, A, nd, R,
+                       row0, col0, rows * ld, ld, 0, st)
+            geo.append((tuple(l.shape), tuple(c.shape), A, nd, row0))
+            row0 += nd * A
+        ctx.geo, ctx.ncls, ctx.ld, ctx.rows = geo, ncls, ld, rows
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        dout = dout.contiguous()
+        B = dout.shape[0]
+        st = N.stream(dout.device)
+        dl, dc = [], []
+        for lshape, cshape, A, nd, row0 in ctx.geo:
+            for shape, col0, R, lst in ((lshape, 0, 4, dl), (cshape, 4, ctx.ncls, dc)):
+                g = torch.empty(shape, dtype=dout.dtype, device=dout.device)
+                N.call("kfb_ssd_heads", N.dt(g), dout.data_ptr(), g.data_ptr(), B, A, nd, R,
+                       row0, col0, ctx.rows * ctx.ld, ctx.ld, 1, st)
+                lst.append(g)
+        return (None, None) + tuple(dl) + tuple(dc)
+
+
+def ssd_heads(locs, confs, nds, ncls):
+    """[B, sum(nd*H*W), 4 + ncls] logits (anchor-major rows) from NHWC heads
+    l [B, H, W, nd*4], c [B, H, W, nd*ncls]."""
+    if not _on_gpu(locs[0]):
+        B = locs[0].shape[0]
+        ls = [l.reshape(B, l.shape[1], l.shape[2], nd, 4).permute(0, 3, 1, 2, 4).reshape(B, -1, 4)
+              for nd, l in zip(nds, locs)]
+        cs = [c.reshape(B, c.shape[1], c.shape[2], nd, ncls).permute(0, 3, 1, 2, 4)
+              .reshape(B, -1, ncls) for nd, c in zip(nds, confs)]
+        return torch.cat([torch.cat(ls, 1), torch.cat(cs, 1)], dim=2)
+    return _SSDHeads.apply(tuple(nds), ncls, *locs, *confs)
+
+
 def ssd_loss(logits, gt_loc, gt_label, num_matched, negs_per_pos=3):
     """SSD300 training loss (fp32 scalar); fused HIP kernels on the GPU
     (csrc/ssd_loss.hip), :func:`ssd_loss_reference` on the CPU."""

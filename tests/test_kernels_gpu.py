@@ -399,3 +399,23 @@ def test_ssd_loss(cuda, dt, case):
     (ref * 1.7).backward()
     t = dict(rtol=2e-2, atol=1e-6) if dt == torch.bfloat16 else dict(rtol=1e-4, atol=1e-8)
     torch.testing.assert_close(a.grad.float().cpu(), b.grad, **t)
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_ssd_heads(cuda, dt):
+    """Anchor-major SSD logits from NHWC heads (kfb_ssd_heads) vs the
+    permute + concat reference, forward and backward."""
+    torch.manual_seed(5)
+    B, ncls, nds, hw = 3, 5, [4, 6, 4], [(5, 5), (3, 3), (1, 1)]
+    locs = [torch.randn(B, h, w, nd * 4) for nd, (h, w) in zip(nds, hw)]
+    confs = [torch.randn(B, h, w, nd * ncls) for nd, (h, w) in zip(nds, hw)]
+    la = [t.to(cuda, dt).requires_grad_(True) for t in locs + confs]
+    lb = [t.to(dt).float().requires_grad_(True) for t in locs + confs]
+    ya = F.ssd_heads(la[:3], la[3:], nds, ncls)
+    yb = F.ssd_heads(lb[:3], lb[3:], nds, ncls)
+    assert torch.equal(ya.float().cpu(), yb.to(dt).float())
+    g = torch.randn(yb.shape).to(dt)
+    ya.backward(g.to(cuda))
+    yb.backward(g.float())
+    for a, b in zip(la, lb):
+        assert torch.equal(a.grad.float().cpu(), b.grad.to(dt).float())
