@@ -9,7 +9,8 @@
 // * Channel concat / split on NHWC activations (tf.concat(axis=3) in the
 //   inception / DenseNet / NASNet cells, tcb/convnet_builder.py:347-383):
 //   one launch over the output rows for all k inputs, the backward the same
-//   walk in the other direction.
+//   walk in the other direction.  A null input is a block of zero channels
+//   (channel padding of the CIFAR ResNet option-A shortcut).
 #include "common.h"
 
 namespace kfb {
@@ -75,8 +76,15 @@ concat_k(T* __restrict__ out, CatArgs a, long rows, int ctot) {
     int j = 0;
     while (j + 1 < a.k && a.offs[j + 1] <= c) ++j;
     const int cj = a.offs[j + 1] - a.offs[j];
-    T* p = (T*)a.ptrs[j] + r * cj + (c - a.offs[j]);
     T* o = out + r * ctot + c;
+    if (a.ptrs[j] == nullptr) {  // zero part (channel padding): written as 0, split skips it
+      if constexpr (!SPLIT) {
+        if constexpr (V == 1) *o = (T)0.f;
+        else *reinterpret_cast<Vec<T, V>*>(o) = Vec<T, V>{};
+      }
+      continue;
+    }
+    T* p = (T*)a.ptrs[j] + r * cj + (c - a.offs[j]);
     if constexpr (V == 1) {
       if (SPLIT) *p = *o;
       else *o = *p;

@@ -102,8 +102,8 @@ def residual_block(cnn, depth, stride, version, projection_shortcut=False):
         shortcut = cnn.apool(1, 1, stride, stride, input_layer=input_layer,
                              num_channels_in=in_size)
         pad = (depth - in_size) // 2
-        import torch.nn.functional as tF
-        shortcut = tF.pad(shortcut, (pad, pad)).contiguous()
+        from ..ops import nn as F_ops
+        shortcut = F_ops.channel_pad(shortcut, pad, pad)
     else:
         shortcut = input_layer
     if pre_activation:

@@ -1143,14 +1143,45 @@ def _concat_call(out, parts, offs, rows, split):
     esz = out.element_size()
     epv = 16 // esz
     vec = all(w % epv == 0 for w in (offs[j + 1] - offs[j] for j in range(k))) and \
-        all(t.data_ptr() % 16 == 0 for t in list(parts) + [out])
-    ptrs = (ctypes.c_void_p * k)(*[t.data_ptr() for t in parts])
+        all(t.data_ptr() % 16 == 0 for t in list(parts) + [out] if t is not None)
+    ptrs = (ctypes.c_void_p * k)(*[t.data_ptr() if t is not None else None for t in parts])
     offa = (ctypes.c_int * (k + 1))(*offs)
     N.call("kfb_concat", N.dt(out), out.data_ptr(), ptrs, offa, k, rows, offs[-1], int(vec),
            int(split), N.stream(out.device))
 
 
 _CAT_MAX = 16
+
+
+class _ChannelPad(torch.autograd.Function):
+    """Zero channels before / after the last dim (one concat launch with
+    null parts; the backward is the split of the middle block)."""
+
+    @staticmethod
+    def forward(ctx, x, before, after):
+        x = x.contiguous()
+        C = x.shape[-1]
+        offs = [0, before, before + C, before + C + after]
+        rows = x.numel() // C
+        out = torch.empty(x.shape[:-1] + (offs[-1],), dtype=x.dtype, device=x.device)
+        _concat_call(out, [None, x, None], offs, rows, split=False)
+        ctx.meta = (C, offs, rows)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        C, offs, rows = ctx.meta
+        dy = dy.contiguous()
+        dx = torch.empty(dy.shape[:-1] + (C,), dtype=dy.dtype, device=dy.device)
+        _concat_call(dy, [None, dx, None], offs, rows, split=True)
+        return dx, None, None
+
+
+def channel_pad(x, before: int, after: int):
+    """[..., C] -> [..., before + C + after] with zero channels around x."""
+    if not _on_gpu(x):
+        return F.pad(x, (before, after)).contiguous()
+    return _ChannelPad.apply(x, before, after)
 
 
 def concat_channels(xs: Sequence[torch.Tensor]):

@@ -419,3 +419,14 @@ def test_ssd_heads(cuda, dt):
     yb.backward(g.float())
     for a, b in zip(la, lb):
         assert torch.equal(a.grad.float().cpu(), b.grad.to(dt).float())
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_channel_pad(cuda, dt):
+    x = torch.randn(3, 4, 5, 16)
+    xa = x.to(cuda, dt).requires_grad_(True)
+    y = F.channel_pad(xa, 8, 8)
+    assert torch.equal(y.float().cpu(), torch.nn.functional.pad(x.to(dt).float(), (8, 8)))
+    g = torch.randn(y.shape).to(dt)
+    y.backward(g.to(cuda))
+    assert torch.equal(xa.grad.float().cpu(), g[..., 8:24].float())
