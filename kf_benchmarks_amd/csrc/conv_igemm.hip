@@ -744,7 +744,10 @@ struct WgArgs {
   float* slab;
 };
 
-constexpr int WG_BK = 32;  // reduction rows per step (64 measured no faster)
+#ifndef KFB_WG_BK
+#define KFB_WG_BK 32
+#endif
+constexpr int WG_BK = KFB_WG_BK;  // reduction rows per step (64 measured no faster)
 #ifndef KFB_WG_XCD
 #define KFB_WG_XCD 1
 #endif
