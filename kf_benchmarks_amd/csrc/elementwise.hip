@@ -293,6 +293,16 @@ KFB_API hipError_t kfb_act_bwd_bias(int dtype, const void* dy, const void* y, vo
   return hipGetLastError();
 }
 
+// out[c] (+)= sum_k p[k][c]: the bias gradient from the [nslab][C] column
+// partials a consumer conv's dgrad epilogue accumulated (fused ReLU/bias
+// backward of a conv without BN).
+KFB_API hipError_t kfb_slab_colsum(const float* p, int nslab, int C, float* out, int accumulate,
+                                   hipStream_t stream) {
+  hipLaunchKernelGGL(colsum_finalize_k, dim3(ceil_div(C, 16)), dim3(256), 0, stream, p, nslab, C,
+                     out, accumulate);
+  return hipGetLastError();
+}
+
 KFB_API hipError_t kfb_dropout(int dtype, const void* x, void* y, long n, float keep, uint32_t seed,
                                hipStream_t stream) {
   KFB_DISPATCH_DTYPE(dtype, T, {

@@ -77,6 +77,7 @@ _SIGS = {
     "kfb_ctc_grad_scale": [I, P, P, P, L, L, I, I, I, P],
     "kfb_ctc_max_states": [],
     "kfb_ssd_heads": [I, P, P, I, I, I, I, L, I, L, I, I, P],
+    "kfb_slab_colsum": [P, I, I, P, I, P],
 }
 _RESTYPES = {"kfb_bn_num_slabs": c_int, "kfb_colsum_num_slabs": c_int,
              "kfb_gemm_splits": c_int, "kfb_ctc_max_states": c_int}

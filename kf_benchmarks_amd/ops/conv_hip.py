@@ -35,6 +35,13 @@ IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N6
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
+# KFB_ACT_FUSE=1: the ReLU / bias backward of a conv without BN runs in the
+# consuming conv's dgrad epilogue instead of as its own pass (kfb_act_bwd_bias).
+# Off by default: on VGG-16 it removes 1.05 ms/step of act_bwd_bias but the
+# extra read of y slows the dgrad convs by 0.8 ms, and the separate pass
+# overlaps the weight-gradient side stream, so the step got 0.5 ms slower
+# (profiles/r4_act_fuse_ab.txt)
+_ACT_FUSE = os.environ.get("KFB_ACT_FUSE", "0") == "1"
 N.register_optional("kfb_conv_stats_spread", [], N.c_int)
 N.register_optional("kfb_conv_wgrad", [N.I, N.P, N.P, N.P] + [N.I] * 12 + [N.I, N.I, N.P, N.L, N.P])
 N.register_optional("kfb_conv_wgrad_splits", [N.I] * 8, N.c_int)
@@ -452,6 +459,7 @@ class _Conv2d(torch.autograd.Function):
         # bias + ReLU in the forward epilogue; their backward (ReLU mask and
         # bias column sums) runs as one pass at the top of this backward
         ctx.bact = bias is not None or relu
+        ctx.out_link = None
         ctx.relu, ctx.bias = bool(relu), bias
         bd = bias.detach() if bias is not None else None
         if use_s2d(x, wl.shape, stride, ctx.needs_input_grad[0], pads):
@@ -461,6 +469,7 @@ class _Conv2d(torch.autograd.Function):
             ctx.save_for_backward(x2, w2, y if relu else None)
             ctx.s2d = tuple(wl.shape)
             ctx.w = w
+            _Conv2d._act_link(ctx, y, cout % 8 == 0)
             return y
         cin_p, cout_p = _pad8(cin), _pad8(cout)
         xp, wp = x, wl
@@ -482,13 +491,37 @@ class _Conv2d(torch.autograd.Function):
         ctx.w = w
         ctx.wt = wt if (cin_p == cin and cout_p == cout) else None
         ctx.link = getattr(x, "_kfb_bn_link", None)
+        _Conv2d._act_link(ctx, y, cout_p == cout)
         return y
+
+    @staticmethod
+    def _act_link(ctx, y, aligned):
+        if not (ctx.bact and aligned and _ACT_FUSE and _fuse_enabled()):
+            return
+        # bias (+ReLU) without BN: a conv consuming y applies the ReLU
+        # mask and sums the bias gradient in its dgrad epilogue.  This is
+        # the BNLink protocol with y standing in for x_bn (x_bn None: the
+        # consumer passes its saved input, so the link holds no reference
+        # to y), mean 0 and the mask recomputed as y * 1 + 0 > 0 (ReLU)
+        # or y * 0 + 1 > 0 (bias only); the partials' first half is then
+        # the bias gradient
+        from .nn import BNLink
+        mean, coef = _act_link_consts(y.shape[-1], ctx.relu, y.device)
+        ctx.out_link = BNLink(None, mean, True, coef)
+        y._kfb_bn_link = ctx.out_link
 
     @staticmethod
     def backward(ctx, dy):
         db = None
         if ctx.bact:
-            dy, db = _bias_act_backward(dy, ctx.saved_tensors[2], ctx.relu, ctx.bias)
+            ol = ctx.out_link
+            if ol is not None and ol.partials is not None:
+                # the consumer's dgrad epilogue already applied the ReLU mask
+                # and summed the bias-gradient partials
+                db = _bias_from_partials(ol.partials, ctx.bias, dy.shape[-1], dy.device)
+                ol.partials = None
+            else:
+                dy, db = _bias_act_backward(dy, ctx.saved_tensors[2], ctx.relu, ctx.bias)
         if ctx.s2d is not None:
             return _Conv2d._backward_s2d(ctx, dy) + (db, None)
         xp, wp = ctx.saved_tensors[:2]
@@ -524,7 +557,8 @@ class _Conv2d(torch.autograd.Function):
                             # ReLU mask: recomputed from x_bn when the BN has no
                             # residual add (link.mcoef), else read from its output
                             rec = link.relu and link.mcoef is not None
-                            fuse = (parts, xp if link.relu and not rec else None, link.x_bn,
+                            xbn = link.x_bn if link.x_bn is not None else xp  # act link
+                            fuse = (parts, xp if link.relu and not rec else None, xbn,
                                     link.mean, link.mcoef if rec else None)
                         dx = conv_dgrad(dy, wp, xp.shape, stride, pads, fuse, addend=pend,
                                         wt=ctx.wt, addend_inplace=owned)
@@ -591,6 +625,36 @@ class _Conv2d(torch.autograd.Function):
             else:
                 dw = dw.contiguous()
         return None, dw, None, None, None, None, None
+
+
+_act_consts = {}
+
+
+def _act_link_consts(C, relu, dev):
+    """(mean = 0, [scale | shift]) of an act link (see _Conv2d.forward)."""
+    key = (C, relu, dev)
+    if key not in _act_consts:
+        coef = torch.zeros(2 * C, dtype=torch.float32, device=dev)
+        coef[C if not relu else 0:C * (2 if not relu else 1)] = 1.0
+        _act_consts[key] = (torch.zeros(C, dtype=torch.float32, device=dev), coef)
+    return _act_consts[key]
+
+
+def _bias_from_partials(parts, bias, C, dev):
+    """Bias gradient = column sums of the [STATS_SPREAD][C] slab partials
+    (first half of a stats buffer), into the flat-gradient view if any."""
+    if bias is None:
+        return None
+    sink = getattr(bias, "_kfb_grad_sink", None)
+    out = sink if sink is not None else torch.empty((C,), dtype=torch.float32, device=dev)
+    N.call("kfb_slab_colsum", parts.data_ptr(), STATS_SPREAD, C, out.data_ptr(),
+           int(sink is not None), N.stream(dev))
+    if sink is not None:
+        cb = getattr(bias, "_kfb_ready_cb", None)
+        if cb is not None:
+            cb(bias)
+        return None
+    return out
 
 
 def _bias_act_backward(dy, y, relu, bias):

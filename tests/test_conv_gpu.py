@@ -301,3 +301,53 @@ def test_bn_stats_large_mean_shifted(cuda, shifted):
                                    rtol=1e-3, atol=0)
     else:  # uncentered fp32 partials: finite, but only the shifted path is pinned
         assert torch.isfinite(out).all()
+
+
+@pytest.mark.parametrize("relu", [True, False])
+@pytest.mark.parametrize("consumers", [1, 2])
+def test_act_link_fused_backward(cuda, relu, consumers, monkeypatch):
+    """conv+bias(+ReLU) -> conv(s) without BN (VGG/AlexNet): the consumers'
+    dgrad epilogue applies the producer's ReLU mask and sums its bias
+    gradient (act link, _Conv2d.forward), so the producer runs no separate
+    act/bias backward pass; vs the fp32 CPU reference."""
+    from kf_benchmarks_amd.ops import conv_hip
+    monkeypatch.setattr(conv_hip, "_ACT_FUSE", True)  # opt-in (KFB_ACT_FUSE=1)
+    calls = []
+    real = conv_hip._bias_act_backward
+    monkeypatch.setattr(conv_hip, "_bias_act_backward",
+                        lambda *a: calls.append(1) or real(*a))
+    torch.manual_seed(5)
+    dt = torch.bfloat16
+    n, H, W, c0, c1, c2 = 4, 12, 12, 32, 64, 48
+    x = torch.randn(n, H, W, c0).to(dt).float()
+    w1 = (torch.randn(c1, 3, 3, c0) / (9 * c0) ** 0.5).to(dt).float()
+    b1 = torch.randn(c1) * 0.3
+    w2s = [(torch.randn(c2, 3, 3, c1) / (9 * c1) ** 0.5).to(dt).float() for _ in range(consumers)]
+    pads = F.resolve_pads("SAME", H, W, 3, 3, 1, 1)
+    xa = x.to(cuda, dt).requires_grad_(True)
+    w1a, b1a = w1.to(cuda).requires_grad_(True), b1.to(cuda).requires_grad_(True)
+    w2a = [w.to(cuda).requires_grad_(True) for w in w2s]
+    y1 = conv_ops.conv2d(xa, w1a, w1a.detach().to(dt), (1, 1), pads, "hip", bias=b1a, relu=relu)
+    link = y1._kfb_bn_link  # the builder counts the consumers (ConvNetBuilder._use)
+    link.convs += consumers
+    outs = [conv_ops.conv2d(y1, w, w.detach().to(dt), (1, 1), pads, "hip") for w in w2a]
+    dys = [torch.randn(o.shape).to(dt).float() for o in outs]
+    sum((o.float() * d.to(cuda)).sum() for o, d in zip(outs, dys)).backward()
+    assert not calls, "producer ran its own act/bias backward pass"
+    # reference, with the kernel's own (bf16-rounded) output deciding the mask
+    xb, w1b, b1b = (t.clone().requires_grad_(True) for t in (x, w1, b1))
+    w2b = [w.clone().requires_grad_(True) for w in w2s]
+    ylin = conv_ops.conv2d_reference(xb, w1b, (1, 1), pads) + b1b
+    mask = (y1.detach().float().cpu() > 0).float() if relu else torch.ones_like(ylin)
+    y1b = ylin * mask
+    sum((conv_ops.conv2d_reference(y1b, w, (1, 1), pads) * d).sum()
+        for w, d in zip(w2b, dys)).backward()
+    gs = max(t.grad.abs().max().item() for t in (xb,))
+    torch.testing.assert_close(xa.grad.float().cpu(), xb.grad, rtol=3e-2, atol=3e-2 * gs)
+    torch.testing.assert_close(w1a.grad.cpu(), w1b.grad, rtol=3e-2,
+                               atol=2e-2 * w1b.grad.abs().max().item())
+    torch.testing.assert_close(b1a.grad.cpu(), b1b.grad, rtol=2e-2,
+                               atol=2e-2 * b1b.grad.abs().max().item())
+    for wa, wb in zip(w2a, w2b):
+        torch.testing.assert_close(wa.grad.cpu(), wb.grad, rtol=3e-2,
+                                   atol=2e-2 * wb.grad.abs().max().item())
