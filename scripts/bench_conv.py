@@ -63,6 +63,9 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--hip_only", action="store_true", help="skip MIOpen (profiling runs)")
     ap.add_argument("--shapes", default=None, help="comma list of RESNET50 indices")
+    ap.add_argument("--sol", action="store_true",
+                    help="instead of MIOpen: %% of speed of light = max(bytes / 6 TB/s, "
+                         "flops / 2.5 PF/s), and hipBLASLt (torch.matmul) on the 1x1 s1 GEMMs")
     a = ap.parse_args()
     only = {int(i) for i in a.shapes.split(",")} if a.shapes else None
     dev = torch.device("cuda", 0)
@@ -105,10 +108,27 @@ def main():
                 dyc, xpad, wc, None, [s, s], [padarg, padarg], [1, 1], False, [0, 0], 1,
                 [False, True, False]),
         }
+        if a.sol:
+            x2, w2, dy2 = x.view(-1, cin), w.view(cout, -1), dy.view(-1, cout)
+            gemm = k == 1 and s == 1
+            mi = {"fwd": lambda: x2 @ w2.t(), "dgrad": lambda: dy2 @ w2,
+                  "wgrad": lambda: dy2.t() @ x2}
+            xb, yb = x.numel() * 2, dy.numel() * 2
+            bytes_ = {"fwd": xb + yb, "dgrad": xb + yb, "wgrad": xb + yb + w.numel() * 4}
         for i, pas in enumerate(("fwd", "dgrad", "wgrad")):
             if pas == "dgrad" and cin == 3:
                 continue
             th = timeit(hip[pas], a.iters)
+            if a.sol:
+                sol = max(bytes_[pas] / 6e12, flops / 2.5e15) * 1e6
+                tm = timeit(mi[pas], a.iters) if gemm else float("nan")
+                name = "%dx%d %d->%d k%d s%d" % (H, H, cin, cout, k, s)
+                print("%-28s %8s | %9.1f %7.1f | sol %7.1f us (%s) %5.1f%% | blaslt %9.1f" % (
+                    name, pas, th, flops / th / 1e6, sol,
+                    "mem" if bytes_[pas] / 6e12 > flops / 2.5e15 else "mfma", 100 * sol / th, tm))
+                tot["hip"][i] += th * cnt
+                tot["miopen"][i] += sol * cnt
+                continue
             tm = timeit(mi[pas], a.iters) if not a.hip_only else float("nan")
             tot["hip"][i] += th * cnt
             tot["miopen"][i] += tm * cnt
@@ -118,10 +138,11 @@ def main():
             rows.append({"shape": name, "pass": pas, "hip_us": th, "miopen_us": tm,
                          "count": cnt, "tflops_hip": flops / th / 1e6,
                          "tflops_miopen": flops / tm / 1e6})
-    for key in ("hip", "miopen"):
+    for key in (("hip", "sol") if a.sol else ("hip", "miopen")):
+        lab, key = key, "miopen" if key == "sol" else key
         f, d, wg = tot[key]
         print("%-8s ResNet-50 conv time per step: fwd %.2f ms  dgrad %.2f ms  wgrad %.2f ms  "
-              "total %.2f ms" % (key, f / 1e3, d / 1e3, wg / 1e3, (f + d + wg) / 1e3))
+              "total %.2f ms" % (lab, f / 1e3, d / 1e3, wg / 1e3, (f + d + wg) / 1e3))
     if a.json:
         with open(a.json, "w") as fh:
             json.dump({"rows": rows, "totals_us": tot}, fh, indent=1)
