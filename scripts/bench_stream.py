@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""HBM streaming rate of the elementwise passes on a ResNet-50 activation
+"""HBM streaming rate (write-only fill, read-only sum, copy) and of the elementwise passes on a ResNet-50 activation
 ([256, 56, 56, 256] bf16 = 411 MB): our BN apply (residual + ReLU, via the
 inference entry point that shares bn_apply_k) and add kernels next to
 PyTorch's own copy / add as the achievable-rate yardstick."""
@@ -44,6 +44,8 @@ def main():
         nb = x.numel() * 2
         st = N.stream(dev)
         cases = {
+            "torch fill (0R1W)": (lambda: y.fill_(1.0), 1),
+            "torch sum (1R)": (lambda: x.view(-1, 4096).sum(dim=0), 1),
             "torch copy (1R1W)": (lambda: y.copy_(x), 2),
             "torch add (2R1W)": (lambda: torch.add(x, r, out=y), 3),
             "kfb_add (2R1W)": (lambda: N.call("kfb_add", N.dt(x), x.data_ptr(), r.data_ptr(),
