@@ -202,3 +202,27 @@ def test_openmpi_environment_gives_one_rank_per_process(tmp_path):
     for r, (o, e) in enumerate(outs):
         assert procs[r].returncode == 0, e
         assert ("W %d 2 %d 2" % (r, r)) in o
+
+
+@pytest.mark.parametrize("model,batch", [("trivial", 4), ("resnet50", 2)])
+def test_bench_under_torchrun(model, batch):
+    """The driver's multi-GPU invocation, verbatim apart from --device cpu:
+    torch.distributed.run starts the ranks, bench.py joins them (no self
+    launch) and rank 0 prints one JSON line for the whole job."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = _env()
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--device", "cpu", "--model", model, "--batch_size", str(batch), "--dtype", "fp32"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _bench_json(r.stdout)
+    assert out["n_gpus"] == 2 and out["ranks"] == 2 and out["steps"] == 2
+    assert out["config"]["global_batch"] == 2 * batch
+    assert out["value"] > 0 and out["higher_is_better"] is True
