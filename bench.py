@@ -39,6 +39,10 @@ def main(argv=None):
     ap.add_argument("--bucket_size_mb", type=float, default=25.0)
     ap.add_argument("--wire_dtype", default="fp32")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--fp32_products", default=None, choices=["exact", "bf16x3"],
+                    help="--dtype fp32 conv products: exact fp32 MFMA, or three bf16 MFMAs on "
+                         "the operands' bf16 splits (ops/conv_f32.py); default KFB_F32_PRODUCTS "
+                         "or exact")
     ap.add_argument("--variable_update", default="kungfu",
                     help="kungfu (headline) | replicated | horovod | parameter_server | ...")
     ap.add_argument("--kungfu_option", default="sync_sgd",
@@ -71,6 +75,9 @@ def main(argv=None):
     from kf_benchmarks_amd.benchmark import BenchmarkCNN
 
     cuda = a.device == "gpu"
+    from kf_benchmarks_amd.ops import conv_f32
+    if a.fp32_products:
+        conv_f32.set_products(a.fp32_products)
     if cuda and torch.cuda.device_count() < a.gpus:
         print("bench.py: --gpus=%d but only %d GPU(s) visible" % (a.gpus, torch.cuda.device_count()),
               file=sys.stderr)
@@ -157,6 +164,7 @@ def main(argv=None):
                                            else a.variable_update),
                        "optimizer": a.optimizer,
                        "kernel_impl": a.kernel_impl, "loss_first": warm_loss,
+                       "fp32_products": conv_f32.products() if a.dtype == "fp32" else None,
                        "loss_last": final_loss},
         }
         print(json.dumps(out))

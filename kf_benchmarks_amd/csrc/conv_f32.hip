@@ -204,7 +204,7 @@ __device__ __forceinline__ void tile_of(int M, int Ncol, int& m0, int& n0, int& 
   n0 = (t / mt) * TILE;
 }
 
-template <bool VEC>
+template <bool VEC, bool X3>
 __global__ void __launch_bounds__(256, 2) fwd_k(Args a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * 2 * gm::img_elems<float>()];
   const Geo& g = a.g;
@@ -216,11 +216,12 @@ __global__ void __launch_bounds__(256, 2) fwd_k(Args a) {
   lp.init(a.a, FwdX{g, M}, m0, K, threadIdx.x);
   lq.init(a.b, FwdW{g.Cout, K}, n0, K, threadIdx.x);
   v4f acc[TILE / 32][TILE / 32];
-  gm::mainloop<float>(lp, lq, 0, (K + Tr<float>::BK - 1) / Tr<float>::BK, smem, acc);
+  gm::mainloop<float, decltype(lp), decltype(lq), X3>(lp, lq, 0, (K + Tr<float>::BK - 1) / Tr<float>::BK,
+                                                       smem, acc);
   store_tile(acc, a.out, g.Cout, M, g.Cout, m0, n0, false);
 }
 
-template <bool VEC>
+template <bool VEC, bool X3>
 __global__ void __launch_bounds__(256, 2) dgrad_k(Args a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * 2 * gm::img_elems<float>()];
   const Geo& g = a.g;
@@ -232,11 +233,12 @@ __global__ void __launch_bounds__(256, 2) dgrad_k(Args a) {
   lp.init(a.a, DgradDy{g, M}, m0, K, threadIdx.x);
   lq.init(a.b, DgradW{g}, n0, K, threadIdx.x);
   v4f acc[TILE / 32][TILE / 32];
-  gm::mainloop<float>(lp, lq, 0, (K + Tr<float>::BK - 1) / Tr<float>::BK, smem, acc);
+  gm::mainloop<float, decltype(lp), decltype(lq), X3>(lp, lq, 0, (K + Tr<float>::BK - 1) / Tr<float>::BK,
+                                                       smem, acc);
   store_tile(acc, a.out, g.C, M, g.C, m0, n0, false);
 }
 
-template <bool VEC>
+template <bool VEC, bool X3>
 __global__ void __launch_bounds__(256, 2) wgrad_k(Args a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * 2 * gm::img_elems<float>()];
   const Geo& g = a.g;
@@ -250,8 +252,22 @@ __global__ void __launch_bounds__(256, 2) wgrad_k(Args a) {
   lq.init(a.b, WgradX{g, K}, n0, kend, threadIdx.x);
   v4f acc[TILE / 32][TILE / 32];
   const int nk = kend > kbeg ? (kend - kbeg + Tr<float>::BK - 1) / Tr<float>::BK : 0;
-  gm::mainloop<float>(lp, lq, kbeg, nk, smem, acc);
+  gm::mainloop<float, decltype(lp), decltype(lq), X3>(lp, lq, kbeg, nk, smem, acc);
   store_tile(acc, a.out, K, g.Cout, K, m0, n0, true);
+}
+
+template <bool X3>
+static void launch(int mode, bool vec, dim3 grid, const Args& a, hipStream_t s) {
+  if (mode == 0) {
+    if (vec) hipLaunchKernelGGL((fwd_k<true, X3>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((fwd_k<false, X3>), grid, dim3(256), 0, s, a);
+  } else if (mode == 1) {
+    if (vec) hipLaunchKernelGGL((dgrad_k<true, X3>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((dgrad_k<false, X3>), grid, dim3(256), 0, s, a);
+  } else {
+    if (vec) hipLaunchKernelGGL((wgrad_k<true, X3>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_k<false, X3>), grid, dim3(256), 0, s, a);
+  }
 }
 
 }  // namespace cf
@@ -262,23 +278,25 @@ using namespace kfb;
 // mode 0: y = conv(x, w)            a = x  [N,H,W,C],    b = w [Cout,KH,KW,C], out = y  [N,OH,OW,Cout]
 // mode 1: dx = conv^T(dy, w)        a = dy [N,OH,OW,Cout], b = w,              out = dx [N,H,W,C]
 // mode 2: dw += wgrad(dy, x)        a = dy,               b = x,              out = dw [Cout,KH,KW,C]
+// mode | 8: products as three bf16 MFMAs of the operands' bf16 splits (gm::mainloop X3)
 KFB_API hipError_t kfb_conv_f32(int mode, const float* a, const float* b, float* out, int N, int H,
                                 int W, int C, int OH, int OW, int KH, int KW, int sh, int sw,
                                 int pt, int pl, int Cout, hipStream_t stream) {
+  const bool x3 = (mode & 8) != 0;
+  mode &= 7;
   cf::Geo g{N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Cout};
   cf::Args args{a, b, out, g, 0};
   const bool vec = C % 4 == 0 && Cout % 4 == 0;
   auto tiles = [](long M, long Ncol) {
     return ((M + cf::TILE - 1) / cf::TILE) * ((Ncol + cf::TILE - 1) / cf::TILE);
   };
+  dim3 grid;
   if (mode == 0) {
     const long nwg = tiles((long)N * OH * OW, Cout);
-    if (vec) hipLaunchKernelGGL(cf::fwd_k<true>, dim3(nwg), dim3(256), 0, stream, args);
-    else hipLaunchKernelGGL(cf::fwd_k<false>, dim3(nwg), dim3(256), 0, stream, args);
+    grid = dim3(nwg);
   } else if (mode == 1) {
     const long nwg = tiles((long)N * H * W, C);
-    if (vec) hipLaunchKernelGGL(cf::dgrad_k<true>, dim3(nwg), dim3(256), 0, stream, args);
-    else hipLaunchKernelGGL(cf::dgrad_k<false>, dim3(nwg), dim3(256), 0, stream, args);
+    grid = dim3(nwg);
   } else if (mode == 2) {
     const long R = (long)N * OH * OW, K = (long)KH * KW * C;
     const long t = tiles(Cout, K);
@@ -289,10 +307,11 @@ KFB_API hipError_t kfb_conv_f32(int mode, const float* a, const float* b, float*
     if (split < 1) split = 1;
     args.kper = (int)(((nk + split - 1) / split) * bk);
     split = (R + args.kper - 1) / args.kper;
-    if (vec) hipLaunchKernelGGL(cf::wgrad_k<true>, dim3(t * split), dim3(256), 0, stream, args);
-    else hipLaunchKernelGGL(cf::wgrad_k<false>, dim3(t * split), dim3(256), 0, stream, args);
+    grid = dim3(t * split);
   } else {
     return hipErrorInvalidValue;
   }
+  if (x3) cf::launch<true>(mode, vec, grid, args, stream);
+  else cf::launch<false>(mode, vec, grid, args, stream);
   return hipGetLastError();
 }

@@ -186,11 +186,33 @@ constexpr int img_elems() {  // one operand image (KS fp32 rows are padded)
 }
 
 
+// fp32 operands as bf16 pairs: x = hi + lo, hi = bf16(x), lo = bf16(x - hi)
+// (both round-to-nearest-even).  8 fp32 values -> the hi and lo fragments of
+// one 16x16x32 bf16 MFMA.
+__device__ __forceinline__ void split_bf16x2(v4f x0, v4f x1, v8s& hi, v8s& lo) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float f = e < 4 ? x0[e] : x1[e - 4];
+    const __bf16 h = (__bf16)f;
+    hi[e] = __builtin_bit_cast(short, h);
+    lo[e] = __builtin_bit_cast(short, (__bf16)(f - (float)h));
+  }
+}
+
 // The double-buffered main loop over nk K steps from kbeg: P (M-side) and
 // Q (N-side) loaders fill the two operand images of a stage one K step
 // ahead in registers; 2 x 2 waves each own a 64 x 64 block of the 128 x 128
 // tile (acc[i][j] = columns wn*64 + 16i .., rows wm*64 + 16j ..).
-template <typename T, class LP, class LQ>
+//
+// X3 (fp32 only): instead of v_mfma_f32_16x16x4_f32, each pair of 16-k
+// substeps runs as three v_mfma_f32_16x16x32_bf16 on the bf16 split of both
+// operands, a*b ~ ah*bh + ah*bl + al*bh (the dropped al*bl and the rounding of
+// lo leave a relative error ~2^-16 per product; fp32 accumulation).  Lane
+// group g supplies k = 4g..4g+3 of substep 0 and of substep 1 as its 8
+// consecutive MFMA k: the same permutation on both operands, so the sum
+// over k is unchanged.  One bf16 MFMA = 16 cycles vs 32 per 4-k fp32 MFMA:
+// 32 k cost 3 x 16 instead of 8 x 32 cycles.
+template <typename T, class LP, class LQ, bool X3 = false>
 __device__ __forceinline__ void mainloop(LP& lp, LQ& lq, int kbeg, int nk, T* smem,
                                          v4f (&acc)[TILE / 32][TILE / 32]) {
   constexpr int TM = TILE / 32, TN = TILE / 32;
@@ -219,6 +241,30 @@ __device__ __forceinline__ void mainloop(LP& lp, LQ& lq, int kbeg, int nk, T* sm
     }
     const T* pimg = smem + cur * 2 * IMG;
     const T* qimg = pimg + IMG;
+    if constexpr (X3) {
+      static_assert(sizeof(T) == 4, "X3 splits fp32 operands");
+      v8s ah[TN], al[TN], bh[TM], bl[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int r = wn * (TILE / 2) + i * 16;
+        split_bf16x2(frag<T, LQ::KS>(qimg, r, 0, lane), frag<T, LQ::KS>(qimg, r, 1, lane), ah[i],
+                     al[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int r = wm * (TILE / 2) + j * 16;
+        split_bf16x2(frag<T, LP::KS>(pimg, r, 0, lane), frag<T, LP::KS>(pimg, r, 1, lane), bh[j],
+                     bl[j]);
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+          v4f c = Mfma<bf16>::run(al[i], bh[j], acc[i][j]);
+          c = Mfma<bf16>::run(ah[i], bl[j], c);
+          acc[i][j] = Mfma<bf16>::run(ah[i], bh[j], c);
+        }
+    } else {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       Frag af[TN], bf[TM];
@@ -232,6 +278,7 @@ __device__ __forceinline__ void mainloop(LP& lp, LQ& lq, int kbeg, int nk, T* sm
       for (int i = 0; i < TN; ++i)
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = Mfma<T>::run(af[i], bf[j], acc[i][j]);
+    }
     }
     if (kt + 1 < nk) {
       T* nimg = smem + (cur ^ 1) * 2 * IMG;
