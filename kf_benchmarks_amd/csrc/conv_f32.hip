@@ -28,8 +28,25 @@ using gm::TILE;
 using gm::Tr;
 using gm::v4f;
 
+// n / d for 0 <= n < 2^31 as a multiply-high and a shift (round-up
+// multiplier method): the gather maps divide every chunk's row and k index on
+// every K step, and a true 32-bit division costs tens of VALU instructions -
+// more than the MFMAs of a K step once the products run as bf16x3.
+struct FastDiv {
+  unsigned d, mul, shift;
+  FastDiv() = default;
+  __host__ explicit FastDiv(int dv) : d((unsigned)dv), mul(0), shift(0) {
+    while ((1u << shift) < d) ++shift;
+    mul = (unsigned)(((1ull << 32) * ((1ull << shift) - d)) / d + 1);
+  }
+  __device__ __forceinline__ int div(int n) const {
+    return (int)((__umulhi((unsigned)n, mul) + (unsigned)n) >> shift);
+  }
+};
+
 struct Geo {
   int N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Cout;
+  FastDiv ohw, ow, hw, w, c, kw, cout, s_h, s_w;
 };
 
 // Element offset of operand (row, k), or -1 if it is a zero (padding or
@@ -39,10 +56,10 @@ struct FwdX {  // row m = (n, oh, ow), k = (kh, kw, ci) -> x[n][h][w][ci]
   int rows;
   __device__ __forceinline__ long operator()(int m, int k, int kend) const {
     if (m >= rows || k >= kend) return -1;
-    const int ohw = g.OH * g.OW, img = m / ohw, rem = m - img * ohw;
-    const int oh = rem / g.OW, ow = rem - oh * g.OW;
-    const int tap = k / g.C, ci = k - tap * g.C;
-    const int kh = tap / g.KW, kw = tap - kh * g.KW;
+    const int ohw = g.OH * g.OW, img = g.ohw.div(m), rem = m - img * ohw;
+    const int oh = g.ow.div(rem), ow = rem - oh * g.OW;
+    const int tap = g.c.div(k), ci = k - tap * g.C;
+    const int kh = g.kw.div(tap), kw = tap - kh * g.KW;
     const int h = oh * g.sh - g.pt + kh, w = ow * g.sw - g.pl + kw;
     if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return -1;
     return ((long)(img * g.H + h) * g.W + w) * g.C + ci;
@@ -61,13 +78,13 @@ struct DgradDy {  // row m = (n, h, w), k = (kh, kw, co) -> dy[n][oh][ow][co]
   int rows;
   __device__ __forceinline__ long operator()(int m, int k, int kend) const {
     if (m >= rows || k >= kend) return -1;
-    const int hw = g.H * g.W, img = m / hw, rem = m - img * hw;
-    const int h = rem / g.W, w = rem - h * g.W;
-    const int tap = k / g.Cout, co = k - tap * g.Cout;
-    const int kh = tap / g.KW, kw = tap - kh * g.KW;
+    const int hw = g.H * g.W, img = g.hw.div(m), rem = m - img * hw;
+    const int h = g.w.div(rem), w = rem - h * g.W;
+    const int tap = g.cout.div(k), co = k - tap * g.Cout;
+    const int kh = g.kw.div(tap), kw = tap - kh * g.KW;
     const int hn = h + g.pt - kh, wn = w + g.pl - kw;
     if (hn < 0 || wn < 0) return -1;
-    const int oh = hn / g.sh, ow = wn / g.sw;
+    const int oh = g.s_h.div(hn), ow = g.s_w.div(wn);
     if (oh * g.sh != hn || ow * g.sw != wn || oh >= g.OH || ow >= g.OW) return -1;
     return ((long)(img * g.OH + oh) * g.OW + ow) * g.Cout + co;
   }
@@ -77,7 +94,7 @@ struct DgradW {  // row ci, k = (kh, kw, co) -> w[co][kh][kw][ci]
   Geo g;
   __device__ __forceinline__ long operator()(int ci, int k, int kend) const {
     if (ci >= g.C || k >= kend) return -1;
-    const int tap = k / g.Cout, co = k - tap * g.Cout;
+    const int tap = g.cout.div(k), co = k - tap * g.Cout;
     return ((long)co * g.KH * g.KW + tap) * g.C + ci;
   }
 };
@@ -94,10 +111,10 @@ struct WgradX {  // row n = (kh, kw, ci), k = m = (img, oh, ow) -> x[img][h][w][
   int K;
   __device__ __forceinline__ long operator()(int n, int m, int kend) const {
     if (n >= K || m >= kend) return -1;
-    const int ohw = g.OH * g.OW, img = m / ohw, rem = m - img * ohw;
-    const int oh = rem / g.OW, ow = rem - oh * g.OW;
-    const int tap = n / g.C, ci = n - tap * g.C;
-    const int kh = tap / g.KW, kw = tap - kh * g.KW;
+    const int ohw = g.OH * g.OW, img = g.ohw.div(m), rem = m - img * ohw;
+    const int oh = g.ow.div(rem), ow = rem - oh * g.OW;
+    const int tap = g.c.div(n), ci = n - tap * g.C;
+    const int kh = g.kw.div(tap), kw = tap - kh * g.KW;
     const int h = oh * g.sh - g.pt + kh, w = ow * g.sw - g.pl + kw;
     if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return -1;
     return ((long)(img * g.H + h) * g.W + w) * g.C + ci;
@@ -284,7 +301,12 @@ KFB_API hipError_t kfb_conv_f32(int mode, const float* a, const float* b, float*
                                 int pt, int pl, int Cout, hipStream_t stream) {
   const bool x3 = (mode & 8) != 0;
   mode &= 7;
-  cf::Geo g{N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Cout};
+  cf::Geo g{N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Cout,
+            cf::FastDiv(OH * OW), cf::FastDiv(OW), cf::FastDiv(H * W), cf::FastDiv(W),
+            cf::FastDiv(C), cf::FastDiv(KW), cf::FastDiv(Cout), cf::FastDiv(sh), cf::FastDiv(sw)};
+  if ((long)N * H * W >= (1L << 31) || (long)N * OH * OW >= (1L << 31) ||
+      (long)KH * KW * (C > Cout ? C : Cout) >= (1L << 31))
+    return hipErrorInvalidValue;  // FastDiv range
   cf::Args args{a, b, out, g, 0};
   const bool vec = C % 4 == 0 && Cout % 4 == 0;
   auto tiles = [](long M, long Ncol) {
