@@ -16,6 +16,22 @@ namespace kfb {
 
 enum DType : int { F32 = 0, BF16 = 1, F16 = 2 };
 
+// n / d for 0 <= n < 2^31 as a multiply-high and a shift (round-up
+// multiplier method): the gather maps divide every chunk's row and k index on
+// every K step (conv_f32.hip, the generic igemm_k loader), and a true 32-bit
+// division costs tens of VALU instructions.
+struct FastDiv {
+  unsigned d, mul, shift;
+  FastDiv() = default;
+  __host__ explicit FastDiv(int dv) : d((unsigned)dv), mul(0), shift(0) {
+    while ((1u << shift) < d) ++shift;
+    mul = (unsigned)(((1ull << 32) * ((1ull << shift) - d)) / d + 1);
+  }
+  __device__ __forceinline__ int div(int n) const {
+    return (int)((__umulhi((unsigned)n, mul) + (unsigned)n) >> shift);
+  }
+};
+
 typedef __bf16 bf16;
 typedef _Float16 f16;
 

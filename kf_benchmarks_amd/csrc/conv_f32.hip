@@ -28,22 +28,6 @@ using gm::TILE;
 using gm::Tr;
 using gm::v4f;
 
-// n / d for 0 <= n < 2^31 as a multiply-high and a shift (round-up
-// multiplier method): the gather maps divide every chunk's row and k index on
-// every K step, and a true 32-bit division costs tens of VALU instructions -
-// more than the MFMAs of a K step once the products run as bf16x3.
-struct FastDiv {
-  unsigned d, mul, shift;
-  FastDiv() = default;
-  __host__ explicit FastDiv(int dv) : d((unsigned)dv), mul(0), shift(0) {
-    while ((1u << shift) < d) ++shift;
-    mul = (unsigned)(((1ull << 32) * ((1ull << shift) - d)) / d + 1);
-  }
-  __device__ __forceinline__ int div(int n) const {
-    return (int)((__umulhi((unsigned)n, mul) + (unsigned)n) >> shift);
-  }
-};
-
 struct Geo {
   int N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Cout;
   FastDiv ohw, ow, hw, w, c, kw, cout, s_h, s_w;
@@ -302,8 +286,8 @@ KFB_API hipError_t kfb_conv_f32(int mode, const float* a, const float* b, float*
   const bool x3 = (mode & 8) != 0;
   mode &= 7;
   cf::Geo g{N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Cout,
-            cf::FastDiv(OH * OW), cf::FastDiv(OW), cf::FastDiv(H * W), cf::FastDiv(W),
-            cf::FastDiv(C), cf::FastDiv(KW), cf::FastDiv(Cout), cf::FastDiv(sh), cf::FastDiv(sw)};
+            FastDiv(OH * OW), FastDiv(OW), FastDiv(H * W), FastDiv(W),
+            FastDiv(C), FastDiv(KW), FastDiv(Cout), FastDiv(sh), FastDiv(sw)};
   if ((long)N * H * W >= (1L << 31) || (long)N * OH * OW >= (1L << 31) ||
       (long)KH * KW * (C > Cout ? C : Cout) >= (1L << 31))
     return hipErrorInvalidValue;  // FastDiv range

@@ -96,6 +96,9 @@ struct IgArgs {
   // forward statistics only: per-channel shift K (nullable); the partials
   // are sums of (y - K) and (y - K)^2 (see bn_finalize_stats_k)
   const float* kshift;
+  // generic (non-FAST) loader: k -> (tap, channel) -> (kh, kw) and the
+  // transposed gather's stride divisions as multiply-high divisions
+  FastDiv fd_c, fd_kw, fd_sh, fd_sw;
 };
 
 constexpr int IG_BK = 64;
@@ -451,8 +454,8 @@ __global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : (NBUF == 1 ? 4 : 2)
     } else {
       const int k = kt * IG_BK + kc * 8;
       const bool kok = k < a.Ktot;
-      const int tap = k / a.C, cc = k - tap * a.C;
-      const int kh = tap / a.KW, kw = tap - kh * a.KW;
+      const int tap = a.fd_c.div(k), cc = k - tap * a.C;
+      const int kh = a.fd_kw.div(tap), kw = tap - kh * a.KW;
 #pragma unroll
       for (int i = 0; i < XC; ++i) {
         bool ok = kok && xok[i];
@@ -460,7 +463,7 @@ __global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : (NBUF == 1 ? 4 : 2)
         if (TRANS) {
           const int hh = xh[i] - kh, ww = xw[i] - kw;
           ok = ok && hh >= 0 && ww >= 0;
-          hi = hh / a.sh; wi = ww / a.sw;
+          hi = a.fd_sh.div(hh); wi = a.fd_sw.div(ww);  // hh, ww >= 0 when ok
           ok = ok && hi * a.sh == hh && wi * a.sw == ww && hi < a.H && wi < a.W;
         } else {
           hi = xh[i] + kh; wi = xw[i] + kw;
@@ -742,6 +745,7 @@ struct WgArgs {
   // slab[split][Ncol][Ktot] (every element of every split is written) and
   // wgrad_reduce_k folds the slabs into dw; else fp32 atomics into dw.
   float* slab;
+  FastDiv fd_ohw, fd_ow;  // WG_GENERIC: the per-step row -> (img, oh, ow)
 };
 
 #ifndef KFB_WG_BK
@@ -895,8 +899,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_k(WgArgs a) {
       const int m = mstep + xrow[i];
       bool ok = xkok[i] && m < mend;
       const int mm = ok ? m : 0;
-      const int img = mm / OHW, rem = mm - img * OHW;
-      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      const int img = a.fd_ohw.div(mm), rem = mm - img * OHW;
+      const int oh = a.fd_ow.div(rem), ow = rem - oh * a.OW;
       const int hi = oh * a.sh - a.pt + xtap_h[i], wi = ow * a.sw - a.pl + xtap_w[i];
       ok = ok && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
       xr[i] = ok ? *(const uint4*)(x + ((long)(img * a.H + hi) * a.W + wi) * a.C + xcc[i])
@@ -1161,7 +1165,8 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
            N * OH * OW, YH, YW, ys, ldy, stats, mask, xbn, mean, addend, mcoef, bias, relu,
            (int)(xbytes < (1L << 31) ? xbytes : 0), (int)(wbytes < (1L << 31) ? wbytes : 0),
            (int)(ybytes < (1L << 31) ? ybytes : 0),
-           (stats && !xbn && !addend) ? kshift : nullptr};
+           (stats && !xbn && !addend) ? kshift : nullptr,
+           FastDiv(C), FastDiv(KW), FastDiv(sh), FastDiv(sw)};
   const bool t = trans != 0;
   const bool fast = !t && C % IG_BK == 0 && KH * KW <= 64 && xbytes < (1L << 31) &&
                     wbytes < (1L << 31) && !igemm_fast_disabled();
@@ -1216,7 +1221,7 @@ KFB_API hipError_t kfb_conv_wgrad(int dtype, const void* dy, const void* x, floa
   const long dybytes = (long)N * OH * OW * Ncol * 2, xbytes = (long)N * H * W * C * 2;
   WgArgs a{dy, x, dw, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
            N * OH * OW, 0, (int)(dybytes < (1L << 31) ? dybytes : 0),
-           (int)(xbytes < (1L << 31) ? xbytes : 0), nullptr};
+           (int)(xbytes < (1L << 31) ? xbytes : 0), nullptr, FastDiv(OH * OW), FastDiv(OW)};
   const int bmc = Ncol <= 64 ? 64 : 128;
   const int tiles = ((Ncol + bmc - 1) / bmc) * ((a.Ktot + 127) / 128);
   const int split = wgrad_split(a.M, a.Ktot, Ncol, target_blocks, &a.mper);
