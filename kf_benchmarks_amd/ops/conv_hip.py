@@ -35,6 +35,9 @@ IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N6
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
+# KFB_PENDING_ADDEND=0: a non-last consumer of a BN-linked tensor deposits its
+# dgrad and the pending sum is a separate add (A/B switch)
+_PENDING_ADDEND = os.environ.get("KFB_PENDING_ADDEND", "1") != "0"
 # KFB_ACT_FUSE=1: the ReLU / bias backward of a conv without BN runs in the
 # consuming conv's dgrad epilogue instead of as its own pass (kfb_act_bwd_bias).
 # Off by default: on VGG-16 it removes 1.05 ms/step of act_bwd_bias but the
@@ -565,10 +568,20 @@ class _Conv2d(torch.autograd.Function):
                         if fuse is not None:
                             link.partials = fuse[0]
                 else:
-                    g = conv_dgrad(dy, wp, xp.shape, stride, pads, wt=ctx.wt)
                     sparse = (stride[0] if not padded and stride[0] == stride[1]
                               and is_scatter_dgrad(wp.shape, stride, pads) else None)
-                    link.deposit(g[..., :cin].contiguous() if padded else g, sparse=sparse)
+                    g = None
+                    if not padded and link.pending is not None and _PENDING_ADDEND:
+                        # accumulate onto the pending gradient in the dgrad
+                        # epilogue (one read of it) instead of a separate add
+                        link.take_pending_stream()
+                        g = conv_dgrad(dy, wp, xp.shape, stride, pads, addend=link.pending,
+                                       wt=ctx.wt, addend_inplace=link.pending_owned)
+                        if g is not None:
+                            link.accumulated(g, sparse)
+                    if g is None:
+                        g = conv_dgrad(dy, wp, xp.shape, stride, pads, wt=ctx.wt)
+                        link.deposit(g[..., :cin].contiguous() if padded else g, sparse=sparse)
             else:
                 dx = conv_dgrad(dy, wp, xp.shape, stride, pads, wt=ctx.wt)
                 if dx is not None and padded:

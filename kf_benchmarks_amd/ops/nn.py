@@ -161,6 +161,16 @@ class BNLink:
             self.pending_event = torch.cuda.Event()
             self.pending_event.record()
 
+    def accumulated(self, g, sparse=None):
+        """A contributor computed ``g`` = its gradient + ``pending`` (the
+        pending gradient as its dgrad epilogue's addend): g replaces it."""
+        if sparse != self.pending_sparse:
+            sparse = None
+        self.pending, self.pending_owned, self.pending_sparse = g, True, sparse
+        if g.is_cuda:
+            self.pending_event = torch.cuda.Event()
+            self.pending_event.record()
+
     def take_pending_stream(self):
         """Makes the current stream wait for the pending gradient (written
         on whatever stream its contributors ran on) before using it."""
