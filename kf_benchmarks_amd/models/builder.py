@@ -37,6 +37,16 @@ from .layers import AffineLayer, BatchNormLayer, ConvLayer, DepthwiseConvLayer
 _SIDE_BRANCHES = os.environ.get("KFB_SIDE_BRANCHES", "0") == "1"
 # conv(defer_bn=True) returns the BN unapplied (KFB_DEFER_BN=0: always apply)
 _DEFER_BN = os.environ.get("KFB_DEFER_BN", "1") != "0"
+# KFB_POOL_LINKS=0: a pool consuming a BN output disables that BN's fused
+# backward (the pre-pool-link behaviour; A/B switch)
+_POOL_LINKS = os.environ.get("KFB_POOL_LINKS", "1") != "0"
+# KFB_CONCAT_LINKS=1: concat outputs get an accumulation-only link (their
+# consumers' gradients sum in the last conv's dgrad epilogue).  Off by default:
+# Inception-v3 drops 112 of 124 adds per 4 steps (-0.45 ms/step GPU time) but
+# the Python link bookkeeping (events, stream waits) costs host time in these
+# host-bound models: wall time unchanged on Inception-v3, -2% on GoogLeNet
+# (profiles/r4_concat_links_ab.txt)
+_CONCAT_LINKS = os.environ.get("KFB_CONCAT_LINKS", "0") == "1"
 _BRANCH_STREAMS = {}
 
 
@@ -85,7 +95,7 @@ class ConvNetBuilder:
         return self.net.get_or_create(scope, factory)
 
     @staticmethod
-    def _use(t, conv=False, resid=False):
+    def _use(t, conv=False, resid=False, pool=False):
         """Count a consumer of a BN output (see ops.nn.BNLink): the fused BN
         backward needs every consumer to be a conv or a residual-adding BN."""
         link = getattr(t, "_kfb_bn_link", None) if t is not None else None
@@ -94,6 +104,8 @@ class ConvNetBuilder:
                 link.convs += 1
             elif resid:
                 link.resid += 1
+            elif pool:
+                link.pools += 1
             else:
                 link.other = True
 
@@ -275,7 +287,9 @@ class ConvNetBuilder:
             input_layer = self.top_layer
         else:
             self.top_size = num_channels_in
-        self._use(input_layer)
+        kind = "max" if pool_name == "mpool" else "avg"
+        self._use(input_layer, pool=_POOL_LINKS and F.pool_takes_link(
+            input_layer, k_height, k_width, d_height, d_width, mode, kind))
         self.counts[pool_name] += 1
         fn = F.max_pool if pool_name == "mpool" else F.avg_pool
         y = fn(input_layer, k_height, k_width, d_height, d_width, mode)
@@ -360,9 +374,21 @@ class ConvNetBuilder:
                     col_sizes[c].append(self.top_size)
             for l in col_layers:
                 self._use(l[-1])
-            self.top_layer = F.concat_channels([l[-1] for l in col_layers])
+            self.top_layer = self._accum_link(F.concat_channels([l[-1] for l in col_layers]))
             self.top_size = sum(s[-1] for s in col_sizes)
         return self.top_layer
+
+    @staticmethod
+    def _accum_link(y):
+        """A concat output read by several branches: an accumulation-only
+        BNLink, so its consumers' gradients sum in the last conv's dgrad
+        epilogue instead of autograd's separate adds."""
+        if _CONCAT_LINKS and y.is_cuda:
+            if conv_ops.FUSE_BN:
+                link = F.BNLink(None, None, False)
+                link.accum = True
+                y._kfb_bn_link = link
+        return y
 
     # ----------------------------------------------------------------- misc
     def spatial_mean(self, keep_dims=False):
@@ -456,7 +482,7 @@ class ConvNetBuilder:
     def concat(self, xs):
         for t in xs:
             self._use(t)
-        self.top_layer = F.concat_channels(xs)
+        self.top_layer = self._accum_link(F.concat_channels(xs))
         self.top_size = self.top_layer.shape[-1]
         return self.top_layer
 

@@ -555,7 +555,9 @@ class _Conv2d(torch.autograd.Function):
                         # projection shortcut + conv a of a ResNet v1 block).
                         sparse_ok = scatter and _SCATTER_BN_FUSE and stride[0] == stride[1] \
                             and link.pending_sparse == stride[0]
-                        if not (pend is not None and scatter) or sparse_ok:
+                        if link.accum:
+                            pass  # accumulation-only link: pend as the addend, no BN work
+                        elif not (pend is not None and scatter) or sparse_ok:
                             parts = stats_buffer(cin, dy.device)
                             # ReLU mask: recomputed from x_bn when the BN has no
                             # residual add (link.mcoef), else read from its output

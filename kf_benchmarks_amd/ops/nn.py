@@ -102,9 +102,12 @@ class BNLink:
     kernels can finish the BN's backward work in their epilogues
     (csrc/conv_igemm.hip):
 
-    * every consumer is a conv (input) or a BN that adds y as its residual;
-      the ConvNetBuilder counts them (``convs``, ``resid``) and marks any other
-      use (``other``), which disables the fusion;
+    * every consumer is a conv (input), a BN that adds y as its residual or
+      a max / average pool; the ConvNetBuilder counts them (``convs``,
+      ``resid``, ``pools``) and marks any other use (``other``), which
+      disables the fusion.  A pool contributes like a non-fused conv: it
+      deposits its input gradient, or as the last contributor returns it
+      summed with the pending one;
     * in backward, all but the last contributor *deposit* their gradient of y
       here (``pending``) and return None to autograd; the last one, if it is a
       conv, adds ``pending`` in its dgrad epilogue, applies y's ReLU mask and
@@ -113,7 +116,8 @@ class BNLink:
       returns the summed gradient instead (unfused path).
     """
 
-    __slots__ = ("x_bn", "mean", "relu", "convs", "resid", "other", "partials", "pending",
+    __slots__ = ("x_bn", "mean", "relu", "convs", "resid", "pools", "other", "accum", "partials",
+                 "pending",
                  "pending_owned", "arrived", "mcoef", "pending_sparse", "pending_event")
 
     def __init__(self, x_bn, mean, relu, mcoef=None):
@@ -122,7 +126,10 @@ class BNLink:
         # residual add: a consumer's dgrad epilogue recomputes the ReLU mask
         # from x_bn instead of reading y
         self.mcoef = mcoef
-        self.convs, self.resid, self.other = 0, 0, False
+        self.convs, self.resid, self.pools, self.other = 0, 0, 0, False
+        # accumulation-only link (a concat output, no BN behind it): the last
+        # conv adds the pending gradient in its dgrad epilogue, nothing else
+        self.accum = False
         self.partials, self.pending, self.arrived = None, None, 0
         self.pending_owned = False
         # s when every deposited gradient is zero outside the stride-s pixel
@@ -138,7 +145,7 @@ class BNLink:
 
     @property
     def total(self):
-        return self.convs + self.resid
+        return self.convs + self.resid + self.pools
 
     def arrive(self) -> bool:
         """Registers one gradient contribution; True if it is the last."""
@@ -560,9 +567,29 @@ def _pool_cpu(x, kh, kw, sh, sw, pads, kind):
     return y.permute(0, 2, 3, 1).to(x.dtype).contiguous()
 
 
+def _pool_link_grad(link, dx):
+    """A pool's input gradient under the BNLink protocol: deposited (None to
+    autograd) unless this pool is the link's last contributor, which returns
+    it summed with the pending gradient."""
+    if link is None or not link.fusable:
+        return dx
+    if not link.arrive():
+        link.deposit(dx)
+        return None
+    if link.pending is not None:
+        link.take_pending_stream()
+        if link.pending_owned:
+            dx = link.pending.add_(dx)
+        else:
+            dx = dx.add_(link.pending)
+        link.pending = None
+    return dx
+
+
 class _MaxPool(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, kh, kw, sh, sw, pads, OH, OW):
+        ctx.link = getattr(x, "_kfb_bn_link", None)
         x = x.contiguous()
         n, H, W, C = x.shape
         y = torch.empty((n, OH, OW, C), dtype=x.dtype, device=x.device)
@@ -583,12 +610,13 @@ class _MaxPool(torch.autograd.Function):
         dx = torch.empty((n, H, W, C), dtype=dy.dtype, device=dy.device)
         N.call("kfb_maxpool_bwd", N.dt(dy), dy.data_ptr(), idx.data_ptr(), dx.data_ptr(),
                *ctx.geo, N.stream(dy.device))
-        return dx, None, None, None, None, None, None, None
+        return _pool_link_grad(ctx.link, dx), None, None, None, None, None, None, None
 
 
 class _AvgPool(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, kh, kw, sh, sw, pads, OH, OW):
+        ctx.link = getattr(x, "_kfb_bn_link", None)
         x = x.contiguous()
         n, H, W, C = x.shape
         y = torch.empty((n, OH, OW, C), dtype=x.dtype, device=x.device)
@@ -604,7 +632,7 @@ class _AvgPool(torch.autograd.Function):
         dx = torch.empty((n, H, W, C), dtype=dy.dtype, device=dy.device)
         N.call("kfb_avgpool_bwd", N.dt(dy), dy.data_ptr(), dx.data_ptr(), *ctx.geo,
                N.stream(dy.device))
-        return dx, None, None, None, None, None, None, None
+        return _pool_link_grad(ctx.link, dx), None, None, None, None, None, None, None
 
 
 N.register_optional("kfb_bn_relu_maxpool_fwd", [N.I, N.P, N.P, N.P] + [N.I] * 12 +
@@ -684,6 +712,15 @@ def bn_relu_max_pool(x, gamma, beta, running_mean, running_var, decay, eps, stat
     pads, OH, OW = pool_geometry(x.shape, kh, kw, sh, sw, mode)
     return _BNReluMaxPool.apply(x, gamma, beta, running_mean, running_var, decay, eps, stats,
                                 kh, kw, sh, sw, pads, OH, OW)
+
+
+def pool_takes_link(x, kh, kw, sh, sw, mode, kind):
+    """True if max_pool / avg_pool of x runs the pool autograd Function
+    (which follows the BNLink protocol) rather than a CPU or subsample path."""
+    if not _on_gpu(x):
+        return False
+    pads = pool_geometry(x.shape, kh, kw, sh, sw, mode)[0]
+    return not (kind == "avg" and kh == 1 and kw == 1 and pads == (0, 0, 0, 0))
 
 
 def max_pool(x, kh, kw, sh, sw, mode="VALID"):
