@@ -610,8 +610,16 @@ __device__ __forceinline__ void lds_barrier() {
 // workgroup per CU): the DMAs of step t+1 are issued right after the barrier
 // that retires step t and fly during compute(t); the wait at the top of each
 // step is then vmcnt(0) (only that step's DMAs are outstanding).
+// Workgroups per CU the register budget is sized for: the 128-row 4-wave
+// tiles (48 / 64 KB rings) run 3 / 2 per CU, the rest one.
+template <int BM, int BN, int NT>
+constexpr int glds_occupancy() {
+  return NT == 256 && BM == 128 ? (BN == 64 ? 3 : 2) : 1;
+}
+
 template <typename T, int BM, int BN, int WGM, int WGN, int STAGES = GL_STAGES>
-__global__ void __launch_bounds__(WGM * WGN * 64, 1) igemm_glds_k(IgArgs a) {
+__global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * WGN * 64>()))
+    igemm_glds_k(IgArgs a) {
   constexpr int NT = WGM * WGN * 64;
   constexpr int SLAB = NT / 8;  // rows one DMA instruction of every wave covers
   static_assert(STAGES == 2 || STAGES == 3, "ring depth");
@@ -1089,6 +1097,22 @@ static void launch_glds(const IgArgs& a, bool narrow, hipStream_t s) {
                        dim3(512), 0, s, a);
 }
 
+// 128-row tiles on 4 waves through a 2-stage LDS-DMA ring: 128 x 64 (48 KB,
+// three workgroups per CU, 64 x 32 wave tiles as igemm_k's) or 128 x 128
+// (64 KB, two per CU, 64 x 64 wave tiles): no staging registers and no
+// ds_write pass (the register-staged igemm_k spends more LDS cycles on its
+// ds_write_b128 stores than on its fragment reads)
+template <typename T>
+static void launch_glds_short(const IgArgs& a, bool wide, hipStream_t s) {
+  const int mt = (a.M + 127) / 128;
+  if (wide)
+    hipLaunchKernelGGL((igemm_glds_k<T, 128, 128, 2, 2, 2>), dim3(mt * ((a.Ncol + 127) / 128)),
+                       dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((igemm_glds_k<T, 128, 64, 2, 2, 2>), dim3(mt * ((a.Ncol + 63) / 64)),
+                       dim3(256), 0, s, a);
+}
+
 template <typename T, int BM, int BN>
 static void launch_ig(const IgArgs& a, bool trans, bool fast, hipStream_t s, bool onebuf = false) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
@@ -1141,9 +1165,10 @@ using namespace kfb;
 //   IG_ALGO_TALL512 / TALL256: igemm_glds_k with 64-channel tiles and 64x64
 //   wave tiles (twice the MFMAs per fragment read of the 256x64 8-wave tile).
 //   IG_ALGO_SMALL: FAST igemm_k with 64x64 tiles, one LDS stage, 5 workgroups/CU.
+//   IG_ALGO_GSHORT64 / GSHORT128: igemm_glds_k 128x64 / 128x128 on 4 waves.
 enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_GLDS_N64 = 4,
        IG_ALGO_ONEBUF = 5, IG_ALGO_ONEBUF_N64 = 6, IG_ALGO_TALL512 = 7, IG_ALGO_TALL256 = 8,
-       IG_ALGO_SMALL = 9 };
+       IG_ALGO_SMALL = 9, IG_ALGO_GSHORT64 = 10, IG_ALGO_GSHORT128 = 11 };
 
 KFB_API int kfb_conv_igemm_fast(int C, int KH, int KW, int trans) {
   return !trans && C % IG_BK == 0 && KH * KW <= 64 && !igemm_fast_disabled();
@@ -1176,6 +1201,12 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
   if ((algo == IG_ALGO_TALL512 || algo == IG_ALGO_TALL256) && fast) {
     if (dtype == BF16) launch_glds_tall<bf16>(a, algo == IG_ALGO_TALL512, stream);
     else if (dtype == F16) launch_glds_tall<f16>(a, algo == IG_ALGO_TALL512, stream);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
+  if ((algo == IG_ALGO_GSHORT64 || algo == IG_ALGO_GSHORT128) && fast) {
+    if (dtype == BF16) launch_glds_short<bf16>(a, algo == IG_ALGO_GSHORT128, stream);
+    else if (dtype == F16) launch_glds_short<f16>(a, algo == IG_ALGO_GSHORT128, stream);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }
