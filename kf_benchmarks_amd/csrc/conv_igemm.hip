@@ -1103,14 +1103,17 @@ static void launch_glds(const IgArgs& a, bool narrow, hipStream_t s) {
 // ds_write pass (the register-staged igemm_k spends more LDS cycles on its
 // ds_write_b128 stores than on its fragment reads)
 template <typename T>
-static void launch_glds_short(const IgArgs& a, bool wide, hipStream_t s) {
+static void launch_glds_short(const IgArgs& a, bool wide, bool three, hipStream_t s) {
   const int mt = (a.M + 127) / 128;
-  if (wide)
-    hipLaunchKernelGGL((igemm_glds_k<T, 128, 128, 2, 2, 2>), dim3(mt * ((a.Ncol + 127) / 128)),
-                       dim3(256), 0, s, a);
+  const dim3 g128(mt * ((a.Ncol + 127) / 128)), g64(mt * ((a.Ncol + 63) / 64));
+  if (wide && three)
+    hipLaunchKernelGGL((igemm_glds_k<T, 128, 128, 2, 2, 3>), g128, dim3(256), 0, s, a);
+  else if (wide)
+    hipLaunchKernelGGL((igemm_glds_k<T, 128, 128, 2, 2, 2>), g128, dim3(256), 0, s, a);
+  else if (three)
+    hipLaunchKernelGGL((igemm_glds_k<T, 128, 64, 2, 2, 3>), g64, dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((igemm_glds_k<T, 128, 64, 2, 2, 2>), dim3(mt * ((a.Ncol + 63) / 64)),
-                       dim3(256), 0, s, a);
+    hipLaunchKernelGGL((igemm_glds_k<T, 128, 64, 2, 2, 2>), g64, dim3(256), 0, s, a);
 }
 
 template <typename T, int BM, int BN>
@@ -1165,10 +1168,12 @@ using namespace kfb;
 //   IG_ALGO_TALL512 / TALL256: igemm_glds_k with 64-channel tiles and 64x64
 //   wave tiles (twice the MFMAs per fragment read of the 256x64 8-wave tile).
 //   IG_ALGO_SMALL: FAST igemm_k with 64x64 tiles, one LDS stage, 5 workgroups/CU.
-//   IG_ALGO_GSHORT64 / GSHORT128: igemm_glds_k 128x64 / 128x128 on 4 waves.
+//   IG_ALGO_GSHORT64 / GSHORT128 (_3): igemm_glds_k 128x64 / 128x128 on 4 waves,
+//   2-stage (3-stage) ring.
 enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_GLDS_N64 = 4,
        IG_ALGO_ONEBUF = 5, IG_ALGO_ONEBUF_N64 = 6, IG_ALGO_TALL512 = 7, IG_ALGO_TALL256 = 8,
-       IG_ALGO_SMALL = 9, IG_ALGO_GSHORT64 = 10, IG_ALGO_GSHORT128 = 11 };
+       IG_ALGO_SMALL = 9, IG_ALGO_GSHORT64 = 10, IG_ALGO_GSHORT128 = 11,
+       IG_ALGO_GSHORT64_3 = 12, IG_ALGO_GSHORT128_3 = 13 };
 
 KFB_API int kfb_conv_igemm_fast(int C, int KH, int KW, int trans) {
   return !trans && C % IG_BK == 0 && KH * KW <= 64 && !igemm_fast_disabled();
@@ -1204,9 +1209,11 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }
-  if ((algo == IG_ALGO_GSHORT64 || algo == IG_ALGO_GSHORT128) && fast) {
-    if (dtype == BF16) launch_glds_short<bf16>(a, algo == IG_ALGO_GSHORT128, stream);
-    else if (dtype == F16) launch_glds_short<f16>(a, algo == IG_ALGO_GSHORT128, stream);
+  if (algo >= IG_ALGO_GSHORT64 && algo <= IG_ALGO_GSHORT128_3 && fast) {
+    const bool wide = algo == IG_ALGO_GSHORT128 || algo == IG_ALGO_GSHORT128_3;
+    const bool three = algo >= IG_ALGO_GSHORT64_3;
+    if (dtype == BF16) launch_glds_short<bf16>(a, wide, three, stream);
+    else if (dtype == F16) launch_glds_short<f16>(a, wide, three, stream);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }
