@@ -127,10 +127,19 @@ __device__ __forceinline__ void lds_only_barrier() {
 // Shared epilogue of the implicit-GEMM kernels: acc[i][j] holds channels
 // n..n+3 of pixel m for each (i, j) 16x16 subtile of the wave's
 // (BM/WGM) x (BN/WGN) block; NT threads; smem must hold BM*BN elements (and
-// NT*16 floats for the statistics fold).
-template <typename T, int BM, int BN, int NT, int WGM, int WGN>
+// NT*16 floats for the statistics fold).  `pre` runs once the accumulators
+// are staged in LDS (they are dead from there on): a multi-tile workgroup
+// issues the next tile's first operand loads there, so they are in flight
+// while this tile's output stores drain.
+struct NoPrefetch {
+  __device__ void operator()() const {}
+};
+
+template <typename T, int BM, int BN, int NT, int WGM, int WGN, typename Pre = NoPrefetch,
+          bool EXTRAS = true>
 __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN / 16][BM / WGM / 16],
-                                            T* smem, int m0, int n0, int wm, int wn) {
+                                            T* smem, int m0, int n0, int wm, int wn,
+                                            Pre pre = Pre()) {
   constexpr int TN = BN / WGN / 16, TM = BM / WGM / 16;
   const int tid = threadIdx.x, lane = tid & 63;
   const int OHW = a.OH * a.OW;
@@ -165,11 +174,13 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
     }
   }
   __syncthreads();
+  pre();
   const bool dense = (a.ys == 1 && a.YH == a.OH && a.YW == a.OW);
   float s1[8], s2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
-  const bool extras = a.addend || a.xbn;  // dgrad-style epilogue operands
+  // dgrad-style epilogue operands (EXTRAS = false: the kernel is never launched with them)
+  const bool extras = EXTRAS && (a.addend || a.xbn);
   // this thread's 8 output channels are fixed (column tid % CPR of every pass)
   float mu[8], msc[8], msh[8];
   const bool mrec = a.xbn && !a.mask && a.mcoef;  // recompute the ReLU mask from xbn
@@ -232,7 +243,7 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
         *(uint4*)(y + row_offset(m) + n) = raw;
       }
     }
-  } else if (a.ybytes > 0) {
+  } else if (EXTRAS && a.ybytes > 0) {
     const __amdgpu_buffer_rsrc_t rad = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.addend ? a.addend : a.y), (short)0, a.addend ? a.ybytes : 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t rmk = __builtin_amdgcn_make_buffer_rsrc(
@@ -275,7 +286,7 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
       }
       if (offb[p] >= 0) *(uint4*)((char*)y + offb[p]) = __builtin_bit_cast(uint4, ov);
     }
-  } else {
+  } else if (EXTRAS) {
     // outputs >= 2 GiB: plain loads interleaved with the stores
 #pragma unroll
     for (int p = 0; p < NPASS; ++p) {
@@ -364,6 +375,7 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
 // 64 x 64 tiles (NBUF = 1): <= 96 VGPRs and 16 KB of LDS staging for 5
 // workgroups (20 waves) per CU - more loads and stores in flight per CU, for
 // the short-K, write-heavy layers (e.g. 1x1 convs with K = 64).
+
 template <typename T, int BM, int BN, bool TRANS, bool FAST, int NBUF = 2>
 __global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : (NBUF == 1 ? 4 : 2))
     igemm_k(IgArgs a) {
@@ -567,6 +579,146 @@ __global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : (NBUF == 1 ? 4 : 2)
   }
 
   ig_epilogue<T, BM, BN, 256, 2, 2>(a, acc, smem, m0, n0, wm, wn);
+}
+
+// Multi-tile form of the FAST one-stage igemm_k: each workgroup computes TPW
+// consecutive tiles (the channel tiles of one pixel tile, in order).  The
+// first operand loads of tile t+1 are issued as soon as tile t's accumulators
+// are staged in LDS, so they fly while tile t's output stores drain: the
+// short-K write-heavy layers (one K step, then a 4x larger output) no longer
+// run their load and store phases back to back in every workgroup.  Forward
+// epilogues only (statistics / bias / ReLU): the host never launches it with
+// the dgrad-style operands (addend, mask, xbn), whose loads would spill.
+template <typename T, int BM, int BN, int TPW>
+__global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : 4) igemm_mt_k(IgArgs a) {
+  constexpr int XC = BM / 32, WC = BN / 32;  // 16-byte X / W chunks per thread per K step
+  constexpr int TM = BM / 32, TN = BN / 32;  // 16-wide pixel / channel subtiles per wave
+  static_assert(TPW > 1, "one tile per workgroup: igemm_k");
+  static_assert((BM + BN) * IG_BK >= BM * BN, "epilogue staging exceeds LDS");
+  __shared__ __attribute__((aligned(16))) T smem[(BM + BN) * IG_BK];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int mtiles = (a.M + BM - 1) / BM, ntiles = (a.Ncol + BN - 1) / BN;
+  const int ntot = mtiles * ntiles;
+  const int bid = xcd_remap(blockIdx.x, (ntot + TPW - 1) / TPW);
+  const int kc = tid & 7;  // this thread's 16-byte chunk within a 64-wide K step
+  const int OHW = a.OH * a.OW;
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.wbytes, 0x00020000);
+
+  // per-tile loader state (setup) and the step counters (X and W advance together)
+  unsigned long long tapmask[XC];
+  int xoff[XC], woff[WC];
+  int s_cc = 0, s_kh = 0, s_kw = 0, s_tap = 0, s_tapi = 0, s_k = 0;
+  auto setup = [&](int tile) {
+    const int m0 = (tile / ntiles) * BM, n0 = (tile % ntiles) * BN;
+#pragma unroll
+    for (int i = 0; i < XC; ++i) {
+      const int m = m0 + (tid >> 3) + i * 32;
+      const bool ok = m < a.M;
+      const int mm = ok ? m : 0;
+      const int img = mm / OHW, rem = mm - img * OHW;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      const int xh = oh * a.sh - a.pt, xw = ow * a.sw - a.pl;
+      unsigned long long mk = 0;
+      for (int kh = 0; kh < a.KH; ++kh)
+        for (int kw = 0; kw < a.KW; ++kw) {
+          const bool in = (unsigned)(xh + kh) < (unsigned)a.H && (unsigned)(xw + kw) < (unsigned)a.W;
+          mk |= (unsigned long long)(in && ok) << (kh * a.KW + kw);
+        }
+      tapmask[i] = mk;
+      xoff[i] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + kc * 8;
+    }
+#pragma unroll
+    for (int i = 0; i < WC; ++i) woff[i] = (n0 + (tid >> 3) + i * 32) * a.Ktot + kc * 8;
+    s_cc = s_kh = s_kw = s_tap = s_tapi = s_k = 0;
+  };
+  uint4 xr[XC], wr[WC];
+  auto load = [&]() {
+#pragma unroll
+    for (int i = 0; i < XC; ++i) {
+      const bool ok = (tapmask[i] >> s_tapi) & 1ull;
+      const int off = ok ? (xoff[i] + s_tap + s_cc) * (int)sizeof(T) : -1;
+      xr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+    }
+    s_cc += IG_BK;
+    if (s_cc == a.C) {
+      s_cc = 0;
+      ++s_tapi;
+      if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
+      s_tap = (s_kh * a.W + s_kw) * a.C;
+    }
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+      wr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            wrs, (woff[i] + s_k) * (int)sizeof(T), 0, 0));
+    s_k += IG_BK;
+  };
+  auto store = [&]() {
+    T* xs = smem;
+    T* ws = xs + BM * IG_BK;
+#pragma unroll
+    for (int i = 0; i < XC; ++i) *(uint4*)(xs + swz_off((tid >> 3) + i * 32, kc)) = xr[i];
+#pragma unroll
+    for (int i = 0; i < WC; ++i) *(uint4*)(ws + swz_off((tid >> 3) + i * 32, kc)) = wr[i];
+  };
+  const int wn = wid >> 1, wm = wid & 1;
+  const int nk = a.Ktot / IG_BK;  // FAST geometry: C % 64 == 0
+  v4f acc[TN][TM];
+  auto compute = [&]() {
+    const T* xs = smem;
+    const T* ws = xs + BM * IG_BK;
+#pragma unroll
+    for (int ks = 0; ks < IG_BK / 32; ++ks) {
+      const int chunk = ks * 4 + (lane >> 4);
+      v8s af[TN], bfr[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+        af[i] = *(const v8s*)(ws + swz_off(wn * (BN / 2) + i * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+        bfr[j] = *(const v8s*)(xs + swz_off(wm * (BM / 2) + j * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = Mfma<T>::run(af[i], bfr[j], acc[i][j]);
+    }
+  };
+
+  setup(bid * TPW);
+  load();
+#pragma unroll 1
+  for (int t = 0; t < TPW; ++t) {
+    const int tile = bid * TPW + t;
+    if (tile >= ntot) break;  // workgroup-uniform
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    store();
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) load();
+      compute();
+      if (kt + 1 < nk) {
+        __syncthreads();  // every wave done reading the stage
+        store();
+      }
+      __syncthreads();
+    }
+    const bool more = t + 1 < TPW && tile + 1 < ntot;
+    auto next = [&]() {
+      if (more) {
+        setup(tile + 1);
+        load();
+      }
+    };
+    ig_epilogue<T, BM, BN, 256, 2, 2, decltype(next), false>(
+        a, acc, smem, (tile / ntiles) * BM, (tile % ntiles) * BN, wm, wn, next);
+    if (more) __syncthreads();  // the epilogue's LDS reads precede the next tile's store
+  }
 }
 
 // ------------------------------------------------------------ LDS-DMA igemm
@@ -1116,6 +1268,17 @@ static void launch_glds_short(const IgArgs& a, bool wide, bool three, hipStream_
     hipLaunchKernelGGL((igemm_glds_k<T, 128, 64, 2, 2, 2>), g64, dim3(256), 0, s, a);
 }
 
+// Multi-tile FAST kernels (64-channel tiles: 128 x 64 or 64 x 64; the 128 x
+// 128 form spills), forward-style epilogues only.
+template <typename T, int BM>
+static void launch_mt(const IgArgs& a, int tpw, hipStream_t s) {
+  const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + 63) / 64);
+  if (tpw == 4)
+    hipLaunchKernelGGL((igemm_mt_k<T, BM, 64, 4>), dim3((nwg + 3) / 4), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((igemm_mt_k<T, BM, 64, 2>), dim3((nwg + 1) / 2), dim3(256), 0, s, a);
+}
+
 template <typename T, int BM, int BN>
 static void launch_ig(const IgArgs& a, bool trans, bool fast, hipStream_t s, bool onebuf = false) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
@@ -1170,10 +1333,16 @@ using namespace kfb;
 //   IG_ALGO_SMALL: FAST igemm_k with 64x64 tiles, one LDS stage, 5 workgroups/CU.
 //   IG_ALGO_GSHORT64 / GSHORT128 (_3): igemm_glds_k 128x64 / 128x128 on 4 waves,
 //   2-stage (3-stage) ring.
+//   IG_ALGO_MULTI2 / MULTI4: igemm_mt_k, the 128 x 64 ONEBUF kernel with 2 / 4
+//   tiles per workgroup (the next tile's loads overlap this tile's output
+//   stores); IG_ALGO_SMALL_MULTI4: 64 x 64 tiles, 4 per workgroup.  Forward-style
+//   epilogues only: with addend / mask / xbn they fall through to the
+//   one-tile kernels.
 enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_GLDS_N64 = 4,
        IG_ALGO_ONEBUF = 5, IG_ALGO_ONEBUF_N64 = 6, IG_ALGO_TALL512 = 7, IG_ALGO_TALL256 = 8,
        IG_ALGO_SMALL = 9, IG_ALGO_GSHORT64 = 10, IG_ALGO_GSHORT128 = 11,
-       IG_ALGO_GSHORT64_3 = 12, IG_ALGO_GSHORT128_3 = 13 };
+       IG_ALGO_GSHORT64_3 = 12, IG_ALGO_GSHORT128_3 = 13, IG_ALGO_MULTI2 = 14,
+       IG_ALGO_MULTI4 = 15, IG_ALGO_SMALL_MULTI4 = 16 };
 
 KFB_API int kfb_conv_igemm_fast(int C, int KH, int KW, int trans) {
   return !trans && C % IG_BK == 0 && KH * KW <= 64 && !igemm_fast_disabled();
@@ -1220,6 +1389,15 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
   if (algo == IG_ALGO_SMALL && fast) {
     if (dtype == BF16) launch_ig<bf16, 64, 64>(a, false, true, stream, true);
     else if (dtype == F16) launch_ig<f16, 64, 64>(a, false, true, stream, true);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
+  if ((algo == IG_ALGO_MULTI2 || algo == IG_ALGO_MULTI4 || algo == IG_ALGO_SMALL_MULTI4) && fast &&
+      !addend && !xbn && !mask) {
+    const int tpw = algo == IG_ALGO_MULTI2 ? 2 : 4;
+    const bool small = algo == IG_ALGO_SMALL_MULTI4;
+    if (dtype == BF16) small ? launch_mt<bf16, 64>(a, tpw, stream) : launch_mt<bf16, 128>(a, tpw, stream);
+    else if (dtype == F16) small ? launch_mt<f16, 64>(a, tpw, stream) : launch_mt<f16, 128>(a, tpw, stream);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }

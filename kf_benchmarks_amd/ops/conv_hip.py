@@ -30,16 +30,21 @@ N.register_optional("kfb_conv_igemm_fast", [N.I] * 4, N.c_int)
 IG_CLASSIC, IG_GLDS, IG_CLASSIC_N64, IG_GLDS_N64, IG_ONEBUF, IG_ONEBUF_N64 = 1, 2, 3, 4, 5, 6
 IG_TALL512, IG_TALL256, IG_SMALL, IG_GSHORT64, IG_GSHORT128 = 7, 8, 9, 10, 11
 IG_GSHORT64_3, IG_GSHORT128_3 = 12, 13
+# multi-tile workgroups (igemm_mt_k: the next tile's loads overlap this tile's
+# output stores), forward-style epilogues only
+IG_MULTI2, IG_MULTI4, IG_SMALL_MULTI4 = 14, 15, 16
 IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N64,
             "glds_n64": IG_GLDS_N64, "onebuf": IG_ONEBUF, "onebuf_n64": IG_ONEBUF_N64,
             "tall512": IG_TALL512, "tall256": IG_TALL256, "small": IG_SMALL,
             "gshort64": IG_GSHORT64, "gshort128": IG_GSHORT128, "gshort64_3": IG_GSHORT64_3,
-            "gshort128_3": IG_GSHORT128_3}
+            "gshort128_3": IG_GSHORT128_3, "multi2": IG_MULTI2, "multi4": IG_MULTI4,
+            "small_multi4": IG_SMALL_MULTI4}
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
 _NO_GSHORT = os.environ.get("KFB_IGEMM_NOGSHORT", "0") == "1"  # A/B knob: drop IG_GSHORT*
 _GSHORT3 = os.environ.get("KFB_IGEMM_GSHORT3", "1") != "0"  # A/B knob: the 3-stage forms
+_NO_MULTI = os.environ.get("KFB_IGEMM_NOMULTI", "0") == "1"  # A/B knob: drop IG_*MULTI*
 # KFB_PENDING_ADDEND=0: a non-last consumer of a BN-linked tensor deposits its
 # dgrad and the pending sum is a separate add (A/B switch)
 _PENDING_ADDEND = os.environ.get("KFB_PENDING_ADDEND", "1") != "0"
@@ -193,11 +198,15 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
         cands += (IG_GSHORT64,) + ((IG_GSHORT128,) if ncol > 64 else ())
         if _GSHORT3:
             cands += (IG_GSHORT64_3,) + ((IG_GSHORT128_3,) if ncol > 64 else ())
+    stats, mask, xbn, mean, addend, mcoef = fused
+    if fast and not _NO_MULTI and mask is None and xbn is None and addend is None \
+            and KH * KW * C <= 512:
+        # short-K layers: store-phase bound, the multi-tile overlap pays there
+        cands += (IG_MULTI2, IG_MULTI4, IG_SMALL_MULTI4)
     if ncol > 64:  # 64-wide tiles: more workgroups for small-M layers
         cands += (IG_CLASSIC_N64, IG_GLDS_N64, IG_ONEBUF_N64) if fast else (IG_CLASSIC_N64,)
     if len(cands) == 1:
         return cands[0]
-    stats, mask, xbn, mean, addend, mcoef = fused
     key = (str(x.device), x.dtype, stats is not None, mask is not None, xbn is not None,
            addend is not None, mcoef is not None, bact[0] is not None, bool(bact[1])) + tuple(geo)
     best = _ig_tuned.get(key)
