@@ -890,6 +890,139 @@ __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * 
   ig_epilogue<T, BM, BN, NT, WGM, WGN>(a, acc, smem, m0, n0, wm, wn);
 }
 
+// Multi-tile form of the 4-wave 2-stage LDS-DMA kernel (128 x 64 / 128 x 128):
+// each workgroup computes TPW consecutive tiles.  The epilogue stages its
+// output tile in ring stage 1 while the DMAs of the next tile's first K step
+// land in stage 0, so the next tile's loads are in flight while this tile's
+// stores drain (igemm_mt_k does the same for the register-staged kernel).
+template <typename T, int BM, int BN, int TPW>
+__global__ void __launch_bounds__(256, (glds_occupancy<BM, BN, 256>()))
+    igemm_glds_mt_k(IgArgs a) {
+  constexpr int WGM = 2, WGN = 2, NT = 256;
+  constexpr int SLAB = NT / 8;  // rows one DMA instruction of every wave covers
+  static_assert(BM % SLAB == 0 && BN % SLAB == 0 && SLAB % 16 == 0, "DMA slabs");
+  constexpr int TM = BM / WGM / 16, TN = BN / WGN / 16;
+  constexpr int XI = BM / SLAB, WI = BN / SLAB;  // DMA instructions per thread per K step
+  constexpr int STAGE = (BM + BN) * IG_BK;       // elements per ring stage
+  static_assert(BM * BN <= STAGE && NT * 16 * 4 <= STAGE * (int)sizeof(T),
+                "epilogue staging / statistics fold exceed one ring stage");
+  static_assert(TPW > 1, "one tile per workgroup: igemm_glds_k");
+  __shared__ __attribute__((aligned(16))) T smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mtiles = (a.M + BM - 1) / BM, ntiles = (a.Ncol + BN - 1) / BN;
+  const int ntot = mtiles * ntiles;
+  const int bid = xcd_remap(blockIdx.x, (ntot + TPW - 1) / TPW);
+  const int OHW = a.OH * a.OW;
+  const int rr = tid >> 3;                       // DMA row within each SLAB-row slab
+  const int kc = (lane & 7) ^ ((rr >> 1) & 7);   // logical chunk this lane fetches
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.wbytes, 0x00020000);
+  unsigned long long tapmask[XI];
+  int xoff[XI], woff[WI];
+  int s_cc = 0, s_kh = 0, s_kw = 0, s_tap = 0, s_tapi = 0, s_k = 0;
+  auto setup = [&](int tile) {
+    const int m0 = (tile / ntiles) * BM, n0 = (tile % ntiles) * BN;
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int m = m0 + i * SLAB + rr;
+      const bool ok = m < a.M;
+      const int mm = ok ? m : 0;
+      const int img = mm / OHW, rem = mm - img * OHW;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      const int xh = oh * a.sh - a.pt, xw = ow * a.sw - a.pl;
+      unsigned long long mk = 0;
+      for (int kh = 0; kh < a.KH; ++kh)
+        for (int kw = 0; kw < a.KW; ++kw) {
+          const bool in = (unsigned)(xh + kh) < (unsigned)a.H && (unsigned)(xw + kw) < (unsigned)a.W;
+          mk |= (unsigned long long)(in && ok) << (kh * a.KW + kw);
+        }
+      tapmask[i] = mk;
+      xoff[i] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + kc * 8;
+    }
+#pragma unroll
+    for (int j = 0; j < WI; ++j) woff[j] = (n0 + j * SLAB + rr) * a.Ktot + kc * 8;
+    s_cc = s_kh = s_kw = s_tap = s_tapi = s_k = 0;
+  };
+  auto issue = [&](int stage) {
+    T* xs = smem + stage * STAGE;
+    T* ws = xs + BM * IG_BK;
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const bool ok = (tapmask[i] >> s_tapi) & 1ull;
+      const int off = ok ? (xoff[i] + s_tap + s_cc) * (int)sizeof(T) : -1;
+      dma16(xrs, xs + (i * SLAB + wid * 8) * IG_BK, off);
+    }
+#pragma unroll
+    for (int j = 0; j < WI; ++j)
+      dma16(wrs, ws + (j * SLAB + wid * 8) * IG_BK, (woff[j] + s_k) * (int)sizeof(T));
+    s_k += IG_BK;
+    s_cc += IG_BK;
+    if (s_cc == a.C) {
+      s_cc = 0;
+      ++s_tapi;
+      if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
+      s_tap = (s_kh * a.W + s_kw) * a.C;
+    }
+  };
+  v4f acc[TN][TM];
+  const int wm = wid % WGM, wn = wid / WGM;
+  auto compute = [&](int stage) {
+    const T* xs = smem + stage * STAGE;
+    const T* ws = xs + BM * IG_BK;
+#pragma unroll
+    for (int ks = 0; ks < IG_BK / 32; ++ks) {
+      const int chunk = ks * 4 + (lane >> 4);
+      v8s af[TN], bfr[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+        af[i] = *(const v8s*)(ws + swz_off(wn * (BN / WGN) + i * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+        bfr[j] = *(const v8s*)(xs + swz_off(wm * (BM / WGM) + j * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = Mfma<T>::run(af[i], bfr[j], acc[i][j]);
+    }
+  };
+
+  const int nk = a.Ktot / IG_BK;  // FAST geometry: C % 64 == 0
+  setup(bid * TPW);
+  issue(0);
+#pragma unroll 1
+  for (int t = 0; t < TPW; ++t) {
+    const int tile = bid * TPW + t;
+    if (tile >= ntot) break;  // workgroup-uniform
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    // step 0 always sits in stage 0 (the previous epilogue staged in stage 1)
+    int st = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      wait_vmcnt<0>();  // step kt's DMAs (and the previous tile's stores)
+      lds_barrier();    // ... of every wave landed; stage st^1 fully read
+      if (kt + 1 < nk) issue(st ^ 1);
+      compute(st);
+      st ^= 1;
+    }
+    __syncthreads();  // all fragment reads done before the epilogue reuses the ring
+    const bool more = t + 1 < TPW && tile + 1 < ntot;
+    auto next = [&]() {
+      if (more) {
+        setup(tile + 1);
+        issue(0);
+      }
+    };
+    ig_epilogue<T, BM, BN, NT, WGM, WGN, decltype(next)>(
+        a, acc, smem + STAGE, (tile / ntiles) * BM, (tile % ntiles) * BN, wm, wn, next);
+  }
+}
+
 // ------------------------------------------------------------------ wgrad
 struct WgArgs {
   const void* dy;  // [M][Ncol]  (NHWC output gradient, Ncol = Cout)
@@ -1268,6 +1401,18 @@ static void launch_glds_short(const IgArgs& a, bool wide, bool three, hipStream_
     hipLaunchKernelGGL((igemm_glds_k<T, 128, 64, 2, 2, 2>), g64, dim3(256), 0, s, a);
 }
 
+// Multi-tile 4-wave LDS-DMA kernels, 2 tiles per workgroup.
+template <typename T>
+static void launch_glds_mt(const IgArgs& a, bool wide, hipStream_t s) {
+  const int mt = (a.M + 127) / 128;
+  if (wide)
+    hipLaunchKernelGGL((igemm_glds_mt_k<T, 128, 128, 2>), dim3((mt * ((a.Ncol + 127) / 128) + 1) / 2),
+                       dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((igemm_glds_mt_k<T, 128, 64, 2>), dim3((mt * ((a.Ncol + 63) / 64) + 1) / 2),
+                       dim3(256), 0, s, a);
+}
+
 // Multi-tile FAST kernels (64-channel tiles: 128 x 64 or 64 x 64; the 128 x
 // 128 form spills), forward-style epilogues only.
 template <typename T, int BM>
@@ -1335,14 +1480,18 @@ using namespace kfb;
 //   2-stage (3-stage) ring.
 //   IG_ALGO_MULTI2 / MULTI4: igemm_mt_k, the 128 x 64 ONEBUF kernel with 2 / 4
 //   tiles per workgroup (the next tile's loads overlap this tile's output
-//   stores); IG_ALGO_SMALL_MULTI4: 64 x 64 tiles, 4 per workgroup.  Forward-style
+//   stores); IG_ALGO_SMALL_MULTI4: 64 x 64 tiles, 4 per workgroup.
+//   IG_ALGO_GMULTI64 / GMULTI128: igemm_glds_mt_k, GSHORT64 / GSHORT128 with 2
+//   tiles per workgroup (next tile's DMAs land in stage 0 while the epilogue
+//   stages in stage 1).  Forward-style
 //   epilogues only: with addend / mask / xbn they fall through to the
 //   one-tile kernels.
 enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_GLDS_N64 = 4,
        IG_ALGO_ONEBUF = 5, IG_ALGO_ONEBUF_N64 = 6, IG_ALGO_TALL512 = 7, IG_ALGO_TALL256 = 8,
        IG_ALGO_SMALL = 9, IG_ALGO_GSHORT64 = 10, IG_ALGO_GSHORT128 = 11,
        IG_ALGO_GSHORT64_3 = 12, IG_ALGO_GSHORT128_3 = 13, IG_ALGO_MULTI2 = 14,
-       IG_ALGO_MULTI4 = 15, IG_ALGO_SMALL_MULTI4 = 16 };
+       IG_ALGO_MULTI4 = 15, IG_ALGO_SMALL_MULTI4 = 16, IG_ALGO_GMULTI64 = 17,
+       IG_ALGO_GMULTI128 = 18 };
 
 KFB_API int kfb_conv_igemm_fast(int C, int KH, int KW, int trans) {
   return !trans && C % IG_BK == 0 && KH * KW <= 64 && !igemm_fast_disabled();
@@ -1383,6 +1532,13 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
     const bool three = algo >= IG_ALGO_GSHORT64_3;
     if (dtype == BF16) launch_glds_short<bf16>(a, wide, three, stream);
     else if (dtype == F16) launch_glds_short<f16>(a, wide, three, stream);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
+  if ((algo == IG_ALGO_GMULTI64 || algo == IG_ALGO_GMULTI128) && fast) {
+    const bool wide = algo == IG_ALGO_GMULTI128;
+    if (dtype == BF16) launch_glds_mt<bf16>(a, wide, stream);
+    else if (dtype == F16) launch_glds_mt<f16>(a, wide, stream);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }

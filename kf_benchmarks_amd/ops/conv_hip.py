@@ -33,12 +33,15 @@ IG_GSHORT64_3, IG_GSHORT128_3 = 12, 13
 # multi-tile workgroups (igemm_mt_k: the next tile's loads overlap this tile's
 # output stores), forward-style epilogues only
 IG_MULTI2, IG_MULTI4, IG_SMALL_MULTI4 = 14, 15, 16
+# ... and the LDS-DMA 128x64 / 128x128 4-wave kernels with 2 tiles per workgroup
+IG_GMULTI64, IG_GMULTI128 = 17, 18
 IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N64,
             "glds_n64": IG_GLDS_N64, "onebuf": IG_ONEBUF, "onebuf_n64": IG_ONEBUF_N64,
             "tall512": IG_TALL512, "tall256": IG_TALL256, "small": IG_SMALL,
             "gshort64": IG_GSHORT64, "gshort128": IG_GSHORT128, "gshort64_3": IG_GSHORT64_3,
             "gshort128_3": IG_GSHORT128_3, "multi2": IG_MULTI2, "multi4": IG_MULTI4,
-            "small_multi4": IG_SMALL_MULTI4}
+            "small_multi4": IG_SMALL_MULTI4, "gmulti64": IG_GMULTI64,
+            "gmulti128": IG_GMULTI128}
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
@@ -203,6 +206,8 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
             and KH * KW * C <= 512:
         # short-K layers: store-phase bound, the multi-tile overlap pays there
         cands += (IG_MULTI2, IG_MULTI4, IG_SMALL_MULTI4)
+    if fast and not _NO_MULTI and KH * KW * C <= 1024:
+        cands += (IG_GMULTI64,) + ((IG_GMULTI128,) if ncol > 64 else ())
     if ncol > 64:  # 64-wide tiles: more workgroups for small-M layers
         cands += (IG_CLASSIC_N64, IG_GLDS_N64, IG_ONEBUF_N64) if fast else (IG_CLASSIC_N64,)
     if len(cands) == 1:
