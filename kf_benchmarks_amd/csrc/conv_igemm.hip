@@ -99,6 +99,10 @@ struct IgArgs {
   // generic (non-FAST) loader: k -> (tap, channel) -> (kh, kw) and the
   // transposed gather's stride divisions as multiply-high divisions
   FastDiv fd_c, fd_kw, fd_sh, fd_sw;
+  // stride-2 scatter (ys == 2, YH == 2*OH, YW == 2*OW): every output chunk
+  // also writes zeros to the three unsampled pixels of its 2x2 block, so the
+  // output needs no separate zero fill
+  int zfill;
 };
 
 constexpr int IG_BK = 64;
@@ -240,7 +244,14 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
             s2[k] += v * v;
           }
         }
-        *(uint4*)(y + row_offset(m) + n) = raw;
+        T* yp = y + row_offset(m) + n;
+        *(uint4*)yp = raw;
+        if (a.zfill) {
+          const uint4 z = make_uint4(0, 0, 0, 0);
+          *(uint4*)(yp + a.ldy) = z;
+          *(uint4*)(yp + (long)a.YW * a.ldy) = z;
+          *(uint4*)(yp + (long)(a.YW + 1) * a.ldy) = z;
+        }
       }
     }
   } else if (EXTRAS && a.ybytes > 0) {
@@ -284,7 +295,17 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
         }
         ov.v[k] = (T)v;
       }
-      if (offb[p] >= 0) *(uint4*)((char*)y + offb[p]) = __builtin_bit_cast(uint4, ov);
+      if (offb[p] >= 0) {
+        char* yp = (char*)y + offb[p];
+        *(uint4*)yp = __builtin_bit_cast(uint4, ov);
+        if (a.zfill) {
+          const uint4 z = make_uint4(0, 0, 0, 0);
+          const long rb = (long)a.ldy * sizeof(T);
+          *(uint4*)(yp + rb) = z;
+          *(uint4*)(yp + a.YW * rb) = z;
+          *(uint4*)(yp + (a.YW + 1) * rb) = z;
+        }
+      }
     }
   } else if (EXTRAS) {
     // outputs >= 2 GiB: plain loads interleaved with the stores
@@ -330,6 +351,12 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
 #pragma unroll
       for (int k = 0; k < 8; ++k) ov.v[k] = (T)v[k];
       *(uint4*)(y + off) = __builtin_bit_cast(uint4, ov);
+      if (a.zfill) {
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        *(uint4*)(y + off + a.ldy) = z;
+        *(uint4*)(y + off + (long)a.YW * a.ldy) = z;
+        *(uint4*)(y + off + (long)(a.YW + 1) * a.ldy) = z;
+      }
     }
   }
   if (a.stats) {
@@ -1504,9 +1531,13 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
                                   int pt, int pl, int Ncol, int YH, int YW, int ys, int ldy,
                                   int trans, float* stats, const void* mask, const void* xbn,
                                   const float* mean, const void* addend, const float* mcoef,
-                                  const float* bias, int relu, int algo, const float* kshift,
+                                  const float* bias, int flags, int algo, const float* kshift,
                                   hipStream_t stream) {
+  // flags: bit 0 = ReLU after the bias (forward epilogue), bit 1 = zero-fill
+  // the unsampled pixels of a stride-2 scatter (see IgArgs::zfill)
   if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
+  const int relu = flags & 1, zfill = (flags >> 1) & 1;
+  if (zfill && !(ys == 2 && YH == 2 * OH && YW == 2 * OW)) return hipErrorInvalidValue;
   const long xbytes = (long)N * H * W * C * 2, wbytes = (long)Ncol * KH * KW * C * 2;
   const long ybytes = (long)N * YH * YW * ldy * 2;
   IgArgs a{x, w, y, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
@@ -1514,7 +1545,7 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
            (int)(xbytes < (1L << 31) ? xbytes : 0), (int)(wbytes < (1L << 31) ? wbytes : 0),
            (int)(ybytes < (1L << 31) ? ybytes : 0),
            (stats && !xbn && !addend) ? kshift : nullptr,
-           FastDiv(C), FastDiv(KW), FastDiv(sh), FastDiv(sw)};
+           FastDiv(C), FastDiv(KW), FastDiv(sh), FastDiv(sw), zfill};
   const bool t = trans != 0;
   const bool fast = !t && C % IG_BK == 0 && KH * KW <= 64 && xbytes < (1L << 31) &&
                     wbytes < (1L << 31) && !igemm_fast_disabled();

@@ -215,6 +215,9 @@ class ConvNetBuilder:
                 with self.scope(name):
                     self.top_layer, self.top_size = y, num_out_channels
                     y = self._bn_relu_max_pool(y, stats, pool, **self.batch_norm_config)
+                # the stem's pooled output feeds conv1 and the projection
+                # shortcut: their data gradients sum in the last one's epilogue
+                y = self._accum_link(y, always=True)
                 self.top_layer, self.top_size = y, num_out_channels
                 return y
         if use_batch_norm:
@@ -379,11 +382,14 @@ class ConvNetBuilder:
         return self.top_layer
 
     @staticmethod
-    def _accum_link(y):
-        """A concat output read by several branches: an accumulation-only
-        BNLink, so its consumers' gradients sum in the last conv's dgrad
-        epilogue instead of autograd's separate adds."""
-        if _CONCAT_LINKS and y.is_cuda:
+    def _accum_link(y, always=False):
+        """A tensor read by several branches (a concat output; the fused stem
+        BN+ReLU+max-pool output): an accumulation-only BNLink, so its
+        consumers' gradients sum in the last conv's dgrad epilogue instead of
+        autograd's separate adds.  Concat outputs only with KFB_CONCAT_LINKS=1
+        (measured neutral there); ``always`` for the stem (one 103 MB add per
+        ResNet step)."""
+        if (_CONCAT_LINKS or always) and y.is_cuda:
             if conv_ops.FUSE_BN:
                 link = F.BNLink(None, None, False)
                 link.accum = True

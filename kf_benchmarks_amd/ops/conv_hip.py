@@ -48,6 +48,9 @@ _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG
 _NO_GSHORT = os.environ.get("KFB_IGEMM_NOGSHORT", "0") == "1"  # A/B knob: drop IG_GSHORT*
 _GSHORT3 = os.environ.get("KFB_IGEMM_GSHORT3", "1") != "0"  # A/B knob: the 3-stage forms
 _NO_MULTI = os.environ.get("KFB_IGEMM_NOMULTI", "0") == "1"  # A/B knob: drop IG_*MULTI*
+# KFB_SCATTER_ZFILL=0: strided-1x1 data gradients zero-fill their output with a
+# separate pass instead of zeroing the unsampled pixels in the epilogue
+_SCATTER_ZFILL = os.environ.get("KFB_SCATTER_ZFILL", "1") != "0"
 # KFB_PENDING_ADDEND=0: a non-last consumer of a BN-linked tensor deposits its
 # dgrad and the pending sum is a separate add (A/B switch)
 _PENDING_ADDEND = os.environ.get("KFB_PENDING_ADDEND", "1") != "0"
@@ -213,7 +216,7 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
     if len(cands) == 1:
         return cands[0]
     key = (str(x.device), x.dtype, stats is not None, mask is not None, xbn is not None,
-           addend is not None, mcoef is not None, bact[0] is not None, bool(bact[1])) + tuple(geo)
+           addend is not None, mcoef is not None, bact[0] is not None, int(bact[1])) + tuple(geo)
     best = _ig_tuned.get(key)
     if best is not None:
         return best
@@ -231,10 +234,13 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
 
 def _igemm(x, wmat, y, N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy,
            trans, stats=None, mask=None, xbn=None, mean=None, addend=None, mcoef=None,
-           bias=None, relu=False):
+           bias=None, relu=False, zfill=False):
+    """``zfill``: stride-2 scatter whose epilogue also zeroes the unsampled
+    pixels of each 2x2 block (the output needs no separate zero fill)."""
     geo = (N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy, int(trans))
-    algo = _igemm_algo(x, wmat, y, geo, (stats, mask, xbn, mean, addend, mcoef), (bias, relu))
-    _igemm_call(algo, x, wmat, y, geo, stats, mask, xbn, mean, addend, mcoef, bias, relu)
+    flags = int(bool(relu)) | (2 if zfill else 0)
+    algo = _igemm_algo(x, wmat, y, geo, (stats, mask, xbn, mean, addend, mcoef), (bias, flags))
+    _igemm_call(algo, x, wmat, y, geo, stats, mask, xbn, mean, addend, mcoef, bias, flags)
 
 
 def conv_fwd(x, wl, stride, pads, stats=None, bias=None, relu=False):
@@ -287,12 +293,18 @@ def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None, addend=None, wt=None,
             dx = addend if addend_inplace else addend.clone()
             fz = f5[:4] + (dx, f5[4])
         else:
-            dx = torch.zeros((n, H, W, C), dtype=dy.dtype, device=dy.device)
+            dx = None
         # GEMM over dY pixels (1x1, stride 1 in dY space), scattered by ys.
         ys = sh if sh == sw else None
         if ys is None:
             return None
-        _igemm(dy, wt, dx, n, OH, OW, cout, OH, OW, 1, 1, 1, 1, 0, 0, C, H, W, ys, C, False, *fz)
+        # stride 2 over an even grid: the epilogue zeroes the unsampled pixels
+        zfill = dx is None and _SCATTER_ZFILL and ys == 2 and H == 2 * OH and W == 2 * OW
+        if dx is None:
+            dx = (torch.empty if zfill else torch.zeros)((n, H, W, C), dtype=dy.dtype,
+                                                         device=dy.device)
+        _igemm(dy, wt, dx, n, OH, OW, cout, OH, OW, 1, 1, 1, 1, 0, 0, C, H, W, ys, C, False, *fz,
+               zfill=zfill)
         return dx
     if sh == 1 and sw == 1 and KH - 1 - pt >= 0 and KH - 1 - pb >= 0 \
             and KW - 1 - pl >= 0 and KW - 1 - pr >= 0:
