@@ -18,6 +18,8 @@
 // inverse permutation.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace kfb {
 
 // One workgroup per output row (n, oh): its KH input rows are read with
@@ -72,6 +74,64 @@ s2d_stem_k(const T* __restrict__ x, T* __restrict__ x2, int H, int W, int C, int
   }
 }
 
+// 16-bit, C == 3 (the RGB stem): LDS row kh holds input pixel w at slot
+// w + pl (3 elements per slot, zeros around the image), 2*OW2 slots, so the
+// two pixels (2j - pl, 2j + 1 - pl) of output chunk (j, kh) are the 6
+// elements at 6j: three aligned dword reads per 16-byte chunk instead of
+// eight 2-byte gathers with bounds checks.  Each LDS dword is assembled in
+// registers from the (at most two) input dwords holding its two elements, so
+// the rows go to LDS in one pass of dword stores (no zero fill, no 2-byte
+// stores).  Rows of up to S2D3_Q dwords (host-checked).
+constexpr int S2D3_Q = 512;
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+s2d_stem3_k(const T* __restrict__ x, T* __restrict__ x2, int H, int W, int OH, int OW2, int KH,
+            int pt, int pl) {
+  static_assert(sizeof(T) == 2, "16-bit elements");
+  __shared__ uint32_t raw[8 * S2D3_Q];
+  const int row = blockIdx.x;  // n * OH + oh
+  const int n = row / OH, oh = row - n * OH;
+  const int rp = 3 * OW2;      // LDS dwords per row (2 * OW2 slots of 3 elements)
+  const int n3 = 3 * W;        // input elements per row
+  const int e0 = 3 * pl;       // element shift of the padded row
+  const int tid = threadIdx.x;
+  uint32_t w0[8][2], w1[8][2];
+#pragma unroll
+  for (int kh = 0; kh < 8; ++kh) {
+    const int h = 2 * oh - pt + kh;
+    const bool okr = kh < KH && (unsigned)h < (unsigned)H;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(x + ((long)n * H + (okr ? h : 0)) * n3);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int q = tid + it * 256;
+      const int i0 = 2 * q - e0, i1 = i0 + 1;
+      const bool ok = okr && q < rp;
+      w0[kh][it] = (ok && i0 >= 0 && i0 < n3) ? src[i0 >> 1] : 0u;
+      w1[kh][it] = (ok && i1 >= 0 && i1 < n3) ? src[i1 >> 1] : 0u;
+    }
+  }
+#pragma unroll
+  for (int kh = 0; kh < 8; ++kh)
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int q = tid + it * 256;
+      const int i0 = 2 * q - e0;
+      const uint32_t lo = (w0[kh][it] >> (16 * (i0 & 1))) & 0xffffu;
+      const uint32_t hi = (w1[kh][it] >> (16 * ((i0 + 1) & 1))) & 0xffffu;
+      if (q < rp) raw[kh * rp + q] = lo | (hi << 16);
+    }
+  __syncthreads();
+  uint4* dst = reinterpret_cast<uint4*>(x2 + (long)row * OW2 * 64);
+  for (int q = tid; q < OW2 * 8; q += 256) {
+    const int j = q >> 3, kh = q & 7;
+    const uint32_t* r = raw + kh * rp + 3 * j;
+    const uint32_t d0 = r[0], d1 = r[1], d2 = r[2];
+    // [a0 a1 | a2 0 | b0 b1 | b2 0]
+    dst[q] = make_uint4(d0, d1 & 0xffffu, (d1 >> 16) | (d2 << 16), d2 >> 16);
+  }
+}
+
 }  // namespace kfb
 
 using namespace kfb;
@@ -83,6 +143,16 @@ KFB_API hipError_t kfb_s2d_stem(int dtype, const void* x, void* x2, int N, int H
   if (C > 4 || KH > 8 || (W * C * esz) % 4 || W * C * esz > 4 * S2D_ROW_DW ||
       ((uintptr_t)x & 3))
     return hipErrorInvalidValue;
+  static const bool generic = getenv("KFB_S2D_GENERIC") != nullptr;  // A/B switch
+  if (C == 3 && esz == 2 && 3 * OW2 <= S2D3_Q && !generic) {
+    if (dtype == BF16)
+      hipLaunchKernelGGL((s2d_stem3_k<bf16>), dim3(N * OH), dim3(256), 0, stream, (const bf16*)x,
+                         (bf16*)x2, H, W, OH, OW2, KH, pt, pl);
+    else
+      hipLaunchKernelGGL((s2d_stem3_k<f16>), dim3(N * OH), dim3(256), 0, stream, (const f16*)x,
+                         (f16*)x2, H, W, OH, OW2, KH, pt, pl);
+    return hipGetLastError();
+  }
   KFB_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL((s2d_stem_k<T>), dim3(N * OH), dim3(256), 0, stream, (const T*)x, (T*)x2,
                        H, W, C, OH, OW2, KH, pt, pl);
