@@ -711,7 +711,10 @@ bn_relu_maxpool_fwd_k(const T* __restrict__ x, T* __restrict__ z, uint8_t* __res
     store_vec<T, V>(z + o, best);
     Vec<uint8_t, V> iv;
 #pragma unroll
-    for (int k = 0; k < V; ++k) iv.v[k] = (uint8_t)bi[k];
+    // bit 7: the pooled value is 0 (every input <= 0 after the ReLU), so no
+    // gradient flows - the backward compares idx with a 0..8 window position
+    // and needs no read of the pooled output for the ReLU mask
+    for (int k = 0; k < V; ++k) iv.v[k] = (uint8_t)(bi[k] | (best[k] > 0.f ? 0 : 0x80));
     *reinterpret_cast<Vec<uint8_t, V>*>(idx + o) = iv;
   }
 }
@@ -738,13 +741,12 @@ __device__ __forceinline__ void pool_route_grad(const T* __restrict__ dz, const 
     for (int ow = ow_lo; ow <= ow_hi; ++ow) {
       const int pos = a * g.kw + (w - (ow * g.sw - g.pl));
       const long o = (((long)n * g.OH + oh) * g.OW + ow) * g.C + c;
-      float d[V], zv[V];
+      float d[V];
       load_vec<T, V>(dz + o, d);
-      load_vec<T, V>(z + o, zv);
       const Vec<uint8_t, V> iv = *reinterpret_cast<const Vec<uint8_t, V>*>(idx + o);
 #pragma unroll
       for (int k = 0; k < V; ++k)
-        if (iv.v[k] == pos && zv[k] > 0.f) acc[k] += d[k];
+        if (iv.v[k] == pos) acc[k] += d[k];  // bit 7 (pooled value 0) never matches
     }
   }
 }
@@ -832,19 +834,29 @@ __device__ __forceinline__ void route_block_3s2(const T* __restrict__ dz, const 
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int k = 0; k < 8; ++k) gr[a][b][k] = 0.f;
+  // all four windows' loads are issued before any routing (windows outside
+  // the pooled grid read a clamped in-range window and are masked off)
+  float d[2][2][8];
+  Vec<uint8_t, 8> ivs[2][2];
 #pragma unroll
-  for (int dy = -1; dy <= 0; ++dy) {
-    const int oh = oy + dy;
-    if ((unsigned)oh >= (unsigned)g.OH) continue;
+  for (int dy = -1; dy <= 0; ++dy)
 #pragma unroll
     for (int dx = -1; dx <= 0; ++dx) {
-      const int ow = ox + dx;
-      if ((unsigned)ow >= (unsigned)g.OW) continue;
-      const long o = (((long)n * g.OH + oh) * g.OW + ow) * g.C + c;
-      float d[8], zv[8];
-      load_vec<T, 8>(dz + o, d);
-      load_vec<T, 8>(z + o, zv);
-      const Vec<uint8_t, 8> iv = *reinterpret_cast<const Vec<uint8_t, 8>*>(idx + o);
+      const int oh = max(oy + dy, 0), ow = max(ox + dx, 0);
+      const bool in = (oy + dy) >= 0 && (ox + dx) >= 0 && oh < g.OH && ow < g.OW;
+      const long o = (((long)n * g.OH + min(oh, g.OH - 1)) * g.OW + min(ow, g.OW - 1)) * g.C + c;
+      load_vec<T, 8>(dz + o, d[dy + 1][dx + 1]);
+      ivs[dy + 1][dx + 1] = *reinterpret_cast<const Vec<uint8_t, 8>*>(idx + o);
+      if (!in) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ivs[dy + 1][dx + 1].v[k] = 0xff;
+      }
+    }
+#pragma unroll
+  for (int dy = -1; dy <= 0; ++dy) {
+#pragma unroll
+    for (int dx = -1; dx <= 0; ++dx) {
+      const Vec<uint8_t, 8> iv = ivs[dy + 1][dx + 1];
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
         const int rh = a - 2 * dy;  // row of pixel a inside window oh: 0..3
@@ -856,7 +868,7 @@ __device__ __forceinline__ void route_block_3s2(const T* __restrict__ dz, const 
           const int pos = rh * 3 + rw;
 #pragma unroll
           for (int k = 0; k < 8; ++k)
-            if (iv.v[k] == pos && zv[k] > 0.f) gr[a][b][k] += d[k];
+            if (iv.v[k] == pos) gr[a][b][k] += d[dy + 1][dx + 1][k];
         }
       }
     }
@@ -1283,6 +1295,6 @@ KFB_API hipError_t kfb_bn_relu_maxpool_bwd(int dtype, const void* dz, const void
 // Slab count kfb_bn_relu_maxpool_bwd uses (pdy/pdyx need nslab * C floats).
 KFB_API int kfb_bn_pool_num_slabs(int N, int H, int W, int C, int kh, int kw, int sh, int sw) {
   if (kh == 3 && kw == 3 && sh == 2 && sw == 2 && C % 8 == 0 && 256 % (C / 8) == 0)
-    return 1024;  // 4 blocks per CU of the latency-bound gather pass
+    return 2048;  // 8 blocks per CU of the latency-bound gather pass
   return kfb_bn_num_slabs((long)N * H * W, C);
 }
