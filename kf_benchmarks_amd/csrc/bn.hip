@@ -670,7 +670,10 @@ struct BPGeo {
   int N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl;
 };
 
-template <typename T, int V>
+// K3 = true: 3x3 windows with every tap's load issued before the max (taps
+// outside the input read a clamped in-range pixel and are masked off); the
+// generic loop leaves each load behind a bounds branch.
+template <typename T, int V, bool K3 = false>
 __global__ void __launch_bounds__(256)
 bn_relu_maxpool_fwd_k(const T* __restrict__ x, T* __restrict__ z, uint8_t* __restrict__ idx,
                       const float* __restrict__ scale, const float* __restrict__ shift, BPGeo g) {
@@ -691,7 +694,28 @@ bn_relu_maxpool_fwd_k(const T* __restrict__ x, T* __restrict__ z, uint8_t* __res
       sc[k] = scale[c + k]; sf[k] = shift[c + k]; best[k] = -INFINITY; bi[k] = 0;
     }
     const int h0 = oh * g.sh - g.pt, w0 = ow * g.sw - g.pl;
-    for (int a = 0; a < g.kh; ++a) {
+    if constexpr (K3) {
+      float v[9][V];
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+          const int h = min(max(h0 + a, 0), g.H - 1), w = min(max(w0 + b, 0), g.W - 1);
+          load_vec<T, V>(x + (((long)n * g.H + h) * g.W + w) * g.C + c, v[a * 3 + b]);
+        }
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+          const bool in = (unsigned)(h0 + a) < (unsigned)g.H && (unsigned)(w0 + b) < (unsigned)g.W;
+#pragma unroll
+          for (int k = 0; k < V; ++k) {
+            const float o = (float)from_f32<T>(fmaxf(v[a * 3 + b][k] * sc[k] + sf[k], 0.f));
+            if (in && o > best[k]) { best[k] = o; bi[k] = a * 3 + b; }
+          }
+        }
+    }
+    for (int a = 0; !K3 && a < g.kh; ++a) {
       const int h = h0 + a;
       if (h < 0 || h >= g.H) continue;
       for (int b = 0; b < g.kw; ++b) {
@@ -1235,8 +1259,12 @@ KFB_API hipError_t kfb_bn_relu_maxpool_fwd(int dtype, const void* x, void* z, ui
                      save_invstd, scale, shift, kshift);
   const long total = (long)N * OH * OW * (C / 8);
   KFB_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL((bn_relu_maxpool_fwd_k<T, 8>), dim3(stream_grid(total)), dim3(256), 0,
-                       stream, (const T*)x, (T*)z, idx, scale, shift, g);
+    if (kh == 3 && kw == 3)
+      hipLaunchKernelGGL((bn_relu_maxpool_fwd_k<T, 8, true>), dim3(stream_grid(total)), dim3(256),
+                         0, stream, (const T*)x, (T*)z, idx, scale, shift, g);
+    else
+      hipLaunchKernelGGL((bn_relu_maxpool_fwd_k<T, 8>), dim3(stream_grid(total)), dim3(256), 0,
+                         stream, (const T*)x, (T*)z, idx, scale, shift, g);
   });
   return hipGetLastError();
 }
