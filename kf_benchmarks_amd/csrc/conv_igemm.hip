@@ -1072,6 +1072,13 @@ struct WgArgs {
 #define KFB_WG_BK 32
 #endif
 constexpr int WG_BK = KFB_WG_BK;  // reduction rows per step (64 measured no faster)
+// waves per SIMD the wgrad register budget is sized for: 2 lets the 128x128
+// tiles use 134-142 VGPRs (3 workgroups per CU); 4 (<= 128 VGPRs) spills in
+// the main loop and measured 2.5x slower on the 1x1 wgrads
+// (profiles/r5_wgrad_occupancy_ab.txt)
+#ifndef KFB_WG_OCC
+#define KFB_WG_OCC 2
+#endif
 #ifndef KFB_WG_XCD
 #define KFB_WG_XCD 1
 #endif
@@ -1098,7 +1105,7 @@ __device__ __forceinline__ v4s ds_read_tr(const T* p) {
 enum { WG_GENERIC = 0, WG_GATHER = 1, WG_PLAIN = 2 };
 
 template <typename T, int BMC, int BNK, int MODE>
-__global__ void __launch_bounds__(256, 2) wgrad_k(WgArgs a) {
+__global__ void __launch_bounds__(256, KFB_WG_OCC) wgrad_k(WgArgs a) {
   // BMC = output-channel tile (rows of dW), BNK = k tile (cols of dW); both 128 or 64.
   constexpr int TN = BMC / 32, TM = BNK / 32;
   constexpr int DC = WG_BK * BMC / 8 / 256;  // dy chunks per thread
