@@ -30,6 +30,7 @@ StagingArea deferral of tcb/batch_allreduce.py:353-389.
 
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -40,8 +41,11 @@ from . import allreduce, comm
 class BucketReducer:
     def __init__(self, flat, bucket_mb: float = 25.0, wire_dtype: Optional[torch.dtype] = None,
                  overlap: bool = True, op: str = "sum", group=None, num_buckets: int = 0,
-                 relaxed: bool = False, shards: int = 1, spec=None, hierarchical=None):
+                 relaxed: bool = False, shards: int = 1, spec=None, hierarchical=None,
+                 tail_mb: Optional[float] = None):
         self.flat = flat
+        if tail_mb is None:
+            tail_mb = float(os.environ.get("KFB_BUCKET_TAIL_MB", "2"))
         self.wire_dtype = wire_dtype if wire_dtype not in (None, torch.float32) else None
         self.op = op
         self.group = group
@@ -63,19 +67,32 @@ class BucketReducer:
         self.buckets: List[List[int]] = []  # [start, end) in elements
         self.param_bucket = {}
         segs = flat.segments()
-        start, count = segs[0][2] if segs else 0, 0
-        members = []
-        for i, (name, p, off, n) in enumerate(segs):
-            members.append(p)
-            end = off + n
-            nxt = segs[i + 1][2] if i + 1 < len(segs) else flat.numel
-            if nxt - start >= limit or i + 1 == len(segs):
-                b = len(self.buckets)
-                self.buckets.append([start, nxt])
-                for q in members:
-                    self.param_bucket[id(q)] = b
-                members = []
-                start = nxt
+        # Buckets are cut from the END of the ready order: the last bucket only
+        # launches once backward is over, so its all-reduce is exposed.  Caps
+        # grow geometrically from ``tail_mb`` (the last bucket) up to the
+        # bucket size, so the exposed tail is a few MB (ResNet-50 fp32: 2, 4,
+        # 8, 16, 25, 25 MB and a 22 MB head instead of 29/26/26/17 MB).
+        tail = int(tail_mb * (1 << 20) / 4) if (tail_mb and not num_buckets) else 0
+        span = [(segs[i + 1][2] if i + 1 < len(segs) else flat.numel) - segs[i][2]
+                for i in range(len(segs))]
+        groups, cur, size, j = [], [], 0, 0
+        for i in reversed(range(len(segs))):
+            cur.append(i)
+            size += span[i]
+            cap = min(limit, tail << j) if tail > 0 else limit
+            if size >= max(cap, 1):
+                groups.append(cur)
+                cur, size, j = [], 0, j + 1
+        if cur:
+            groups.append(cur)
+        groups = [sorted(g) for g in reversed(groups)]
+        for gi, g in enumerate(groups):
+            start = segs[0][2] if gi == 0 else segs[g[0]][2]
+            end = segs[groups[gi + 1][0]][2] if gi + 1 < len(groups) else flat.numel
+            b = len(self.buckets)
+            self.buckets.append([start, end])
+            for i in g:
+                self.param_bucket[id(segs[i][1])] = b
         self.sizes = [sum(1 for v in self.param_bucket.values() if v == b)
                       for b in range(len(self.buckets))]
         self._pending = list(self.sizes)

@@ -47,3 +47,21 @@ def test_each_parameter_counts_once_per_backward():
     for p in flat.params:
         red._hook(p)
     assert launched == [0, 1, 0, 1]
+
+
+def test_geometric_tail_buckets():
+    """Buckets are cut from the end of the ready order with caps growing
+    from tail_mb: the last bucket (its all-reduce is exposed after backward)
+    stays small, every element is covered once, in order."""
+    mb = 1 << 18  # elements per MB (fp32)
+    flat = _Flat([mb // 4] * 200)  # 50 MB in 0.25 MB parameters
+    red = BucketReducer(flat, bucket_mb=16, tail_mb=1)
+    sizes = [(e - s) / mb for s, e in red.buckets]
+    assert sizes[-4:] == [8.0, 4.0, 2.0, 1.0]
+    assert all(s <= 16 for s in sizes)
+    assert red.buckets[0][0] == 0 and red.buckets[-1][1] == flat.numel
+    assert all(a[1] == b[0] for a, b in zip(red.buckets, red.buckets[1:]))
+    assert sum(red.sizes) == 200
+    # tail_mb=0: the size-capped layout, cut from the end
+    red0 = BucketReducer(flat, bucket_mb=16, tail_mb=0)
+    assert [(e - s) / mb for s, e in red0.buckets] == [2.0, 16.0, 16.0, 16.0]
