@@ -48,6 +48,9 @@ _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG
 _NO_GSHORT = os.environ.get("KFB_IGEMM_NOGSHORT", "0") == "1"  # A/B knob: drop IG_GSHORT*
 _GSHORT3 = os.environ.get("KFB_IGEMM_GSHORT3", "1") != "0"  # A/B knob: the 3-stage forms
 _NO_MULTI = os.environ.get("KFB_IGEMM_NOMULTI", "0") == "1"  # A/B knob: drop IG_*MULTI*
+# largest K (= KH*KW*Cin) offered the multi-tile candidates (register-staged;
+# the LDS-DMA form gets twice that)
+_MULTI_K = int(os.environ.get("KFB_IGEMM_MULTI_K", "2304"))
 # KFB_SCATTER_ZFILL=0: strided-1x1 data gradients zero-fill their output with a
 # separate pass instead of zeroing the unsampled pixels in the epilogue
 _SCATTER_ZFILL = os.environ.get("KFB_SCATTER_ZFILL", "1") != "0"
@@ -206,10 +209,10 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
             cands += (IG_GSHORT64_3,) + ((IG_GSHORT128_3,) if ncol > 64 else ())
     stats, mask, xbn, mean, addend, mcoef = fused
     if fast and not _NO_MULTI and mask is None and xbn is None and addend is None \
-            and KH * KW * C <= 512:
+            and KH * KW * C <= _MULTI_K:
         # short-K layers: store-phase bound, the multi-tile overlap pays there
         cands += (IG_MULTI2, IG_MULTI4, IG_SMALL_MULTI4)
-    if fast and not _NO_MULTI and KH * KW * C <= 1024:
+    if fast and not _NO_MULTI and KH * KW * C <= 2 * _MULTI_K:
         cands += (IG_GMULTI64,) + ((IG_GMULTI128,) if ncol > 64 else ())
     if ncol > 64:  # 64-wide tiles: more workgroups for small-M layers
         cands += (IG_CLASSIC_N64, IG_GLDS_N64, IG_ONEBUF_N64) if fast else (IG_CLASSIC_N64,)
