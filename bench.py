@@ -55,6 +55,10 @@ def main(argv=None):
                     help="cpu: plumbing rehearsal of the same step over gloo (tests)")
     ap.add_argument("--rccl_channels", type=int, default=0,
                     help="pin the RCCL channel count (0: RCCL's choice)")
+    ap.add_argument("--all_reduce_spec", default=None,
+                    help="tf_cnn_benchmarks --all_reduce_spec (e.g. pscpu, nccl#2, xring)")
+    ap.add_argument("--hierarchical_copy", action="store_true",
+                    help="two-level (intra-group then leaders) gradient reduction")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
@@ -78,10 +82,18 @@ def main(argv=None):
     from kf_benchmarks_amd.ops import conv_f32
     if a.fp32_products:
         conv_f32.set_products(a.fp32_products)
-    if cuda and torch.cuda.device_count() < a.gpus:
-        print("bench.py: --gpus=%d but only %d GPU(s) visible" % (a.gpus, torch.cuda.device_count()),
-              file=sys.stderr)
-        return 2
+    if cuda:
+        # ranks on this node need a GPU each: either every rank sees the
+        # whole node (device_count >= local ranks), or the launcher gave each
+        # rank its own device through a *_VISIBLE_DEVICES list
+        local_ranks = int(os.environ.get("LOCAL_WORLD_SIZE", a.gpus))
+        per_rank = any(os.environ.get(v) not in (None, "") for v in
+                       ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"))
+        have = torch.cuda.device_count()
+        if have < 1 or (have < local_ranks and not (per_rank and have == 1)):
+            print("bench.py: --gpus=%d but only %d GPU(s) visible" % (a.gpus, have),
+                  file=sys.stderr)
+            return 2
     data_name = a.data_name or {"ssd300": "coco", "deepspeech2": "librispeech"}.get(a.model)
     p = P.make_params(model=a.model, batch_size=a.batch_size, num_gpus=1, data_name=data_name,
                       variable_update=a.variable_update, kungfu_option=a.kungfu_option,
@@ -90,6 +102,7 @@ def main(argv=None):
                       rccl_channels=a.rccl_channels,
                       kernel_impl=a.kernel_impl, bucket_size_mb=a.bucket_size_mb,
                       gradient_wire_dtype=a.wire_dtype, display_every=10**9,
+                      all_reduce_spec=a.all_reduce_spec, hierarchical_copy=a.hierarchical_copy,
                       synthetic_resample=not a.reuse_synthetic)
     bench = BenchmarkCNN(p)
     bench.build()
@@ -115,6 +128,12 @@ def main(argv=None):
         print("warmup done in %.1fs, loss %.4f" % (time.time() - t0, warm_loss),
               file=sys.stderr)
 
+    reducer = getattr(bench.strategy, "reducer", None)
+    if reducer is not None and cuda:
+        reducer.pop_exposed_ms()
+        reducer.timing = True  # two timing events per step (exposed all-reduce)
+    launches0 = reducer.launch_count if reducer is not None else 0
+
     bdev = dev if cuda else None
     world.barrier(bdev)
     sync()
@@ -127,9 +146,40 @@ def main(argv=None):
     elapsed = time.perf_counter() - start
     final_loss = float(loss)
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    # replica consistency (outside the timed region): every rank's fp32
+    # master-weight checksum; synchronous strategies must agree bit for bit
+    w = bench.strategy.flat.flat
+    mine = torch.stack([w.double().sum(), w.double().square().sum()])
+    sums = [torch.zeros_like(mine) for _ in range(world.size)]
+    if world.communicates:
+        import torch.distributed as dist
+        dist.all_gather(sums, mine)
+    else:
+        sums = [mine]
+    sums = [tuple(float(v) for v in x.cpu()) for x in sums]
+    in_sync = all(x == sums[0] for x in sums)
+
+    exposed = []
+    if reducer is not None:
+        reducer.timing = False
+        exposed = reducer.pop_exposed_ms()
+    t = torch.tensor([elapsed, (sum(exposed) / len(exposed)) if exposed else 0.0],
+                     dtype=torch.float64, device=dev)
     comm.all_reduce(t, op="max")
-    elapsed = float(t.item())
+    elapsed = float(t[0].item())
+    exposed_ms = float(t[1].item())
+    comm_info = {
+        "backend": world.backend or "none",
+        "buckets": reducer.num_buckets if reducer is not None else 0,
+        "collectives_per_step": ((reducer.launch_count - launches0) / a.steps
+                                 if reducer is not None else 0),
+        "wire_dtype": a.wire_dtype,
+        "bucket_size_mb": a.bucket_size_mb,
+        "rccl_channels": os.environ.get("NCCL_MAX_NCHANNELS", "auto"),
+        "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+        # all-reduce time per step that backward did not hide (max over ranks)
+        "exposed_allreduce_ms": round(exposed_ms, 3) if (reducer is not None and cuda) else None,
+    }
     n = world.size
     images = a.batch_size * n * a.steps
     value = images / elapsed
@@ -162,13 +212,18 @@ def main(argv=None):
                        "variable_update": (a.variable_update + "/" + a.kungfu_option
                                            if a.variable_update == "kungfu"
                                            else a.variable_update),
+                       "all_reduce_spec": a.all_reduce_spec,
+                       "hierarchical_copy": a.hierarchical_copy,
                        "optimizer": a.optimizer,
                        "kernel_impl": a.kernel_impl, "loss_first": warm_loss,
                        "fp32_products": conv_f32.products() if a.dtype == "fp32" else None,
                        "loss_last": final_loss},
+            "comm": comm_info,
+            "weights_in_sync": in_sync,
         }
         print(json.dumps(out))
         sys.stdout.flush()
+    bench.strategy.close()  # collective: model stores / peers released on every rank
     world.shutdown()
     return 0
 
@@ -180,8 +235,9 @@ def _self_launch(a, argv) -> int:
     import subprocess
     import tempfile
     if a.device == "gpu":
-        import torch  # device_count() does not initialise the GPU on this image
-        n = torch.cuda.device_count()
+        # counted without any HIP call in this (launching) process
+        from kf_benchmarks_amd.parallel import comm
+        n = comm.visible_gpu_count()
         if n < a.gpus:
             print("bench.py: --gpus=%d but only %d GPU(s) visible" % (a.gpus, n), file=sys.stderr)
             return 2

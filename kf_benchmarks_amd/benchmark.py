@@ -278,10 +278,18 @@ class BenchmarkCNN:
                 self.benchmark_logger = None
                 return
             self.cluster_manager.setup_worker_env()
-        self.world = comm.init_world(self.device_type, params.all_reduce_spec,
-                                     channels=params.rccl_channels)
+        # the compute GPU and the RCCL communicator's GPU come from ONE
+        # function (comm.select_device_index), decided before the world exists
+        env_size = comm.env_world_size()
         self.tower_mode = (os.environ.get("KFB_TOWER_GROUP") == "1" and self.num_gpus > 1
-                           and self.world.size == self.num_gpus)
+                           and env_size == self.num_gpus)
+        dev_index = None
+        if self.device_type == "cuda":
+            dev_index = comm.select_device_index(self.gpu_indices, self.num_gpus, self.tower_mode,
+                                                 comm.env_local_rank(), env_size,
+                                                 torch.cuda.device_count())
+        self.world = comm.init_world(self.device_type, params.all_reduce_spec,
+                                     channels=params.rccl_channels, device_index=dev_index)
         self.task_index = self.world.rank
         self.num_replicas = self.world.size  # data shards / gradient contributors
         if self.tower_mode:
@@ -295,14 +303,6 @@ class BenchmarkCNN:
                 # device (tower-mean gradient; see Strategy.tower_factor)
                 self.model.set_batch_size(self.batch_size)
         if self.device_type == "cuda":
-            local = self.world.local_rank if self.world.size > 1 else 0
-            if self.num_gpus == 1:
-                dev_index = self.gpu_indices[0] + local
-            elif self.tower_mode:
-                dev_index = self.gpu_indices[local % len(self.gpu_indices)]
-            else:
-                dev_index = self.gpu_indices[0]
-            dev_index = dev_index % max(torch.cuda.device_count(), 1)
             torch.cuda.set_device(dev_index)
             self.device = torch.device("cuda", dev_index)
             _native.load()  # fail loudly now if the kernels are missing

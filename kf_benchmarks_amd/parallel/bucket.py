@@ -106,6 +106,12 @@ class BucketReducer:
         # has the previous step's reduction outstanding while it launches)
         self._wire = [None, None]
         self.launch_count = 0  # collectives issued (tests, all_reduce_benchmark)
+        # exposed-communication probe (bench.py): per step, an event when the
+        # backward's kernels are done (both streams) and one when the compute
+        # stream may use the reduced gradients; their distance is the
+        # all-reduce time backward did not hide
+        self.timing = False
+        self._timing_events = []
         self._handles = []
         if overlap:
             for _, p, _, _ in segs:
@@ -223,6 +229,7 @@ class BucketReducer:
         if self.relaxed:
             self._finish_relaxed()
             return
+        ev = self._backward_done_event() if self.timing else None
         while self._next < len(self.buckets):
             self._launch(self._next)
             self._next += 1
@@ -231,8 +238,37 @@ class BucketReducer:
                 work.wait()
             if buf is not None and buf is not view:
                 view.copy_(buf)
+        if ev is not None:
+            end = torch.cuda.Event(enable_timing=True)
+            end.record()
+            self._timing_events.append((ev, end))
         self._works = []
         self._active = False
+
+    def _backward_done_event(self):
+        g = self.flat.grad
+        if not g.is_cuda:
+            return None
+        from ..ops.conv_hip import wgrad_stream
+        side = wgrad_stream(g.device)
+        cur = torch.cuda.current_stream(g.device)
+        ev = torch.cuda.Event(enable_timing=True)
+        if side is not None and side != cur:
+            side.wait_stream(cur)
+            ev.record(side)
+        else:
+            ev.record(cur)
+        return ev
+
+    def pop_exposed_ms(self) -> List[float]:
+        """Exposed all-reduce milliseconds of every timed step since the last
+        call (synchronizes on the recorded events)."""
+        out = []
+        for a, b in self._timing_events:
+            b.synchronize()
+            out.append(max(a.elapsed_time(b), 0.0))
+        self._timing_events = []
+        return out
 
     def reduce_now(self):
         """Synchronous all-reduce of the whole gradient (no backward hooks)."""

@@ -30,6 +30,7 @@ class World:
         # a process group exists (always for size > 1; at size 1 only with
         # KFB_FORCE_PG=1, so the 1-GPU run exercises the real RCCL path)
         self.has_pg = (size > 1) if has_pg is None else bool(has_pg)
+        self.device_index = None  # the rank's GPU (select_device_index), cuda worlds only
 
     @property
     def distributed(self) -> bool:
@@ -117,12 +118,76 @@ def rccl_channel_env(channels: Optional[int]) -> dict:
     return {"NCCL_MIN_NCHANNELS": str(channels), "NCCL_MAX_NCHANNELS": str(channels)}
 
 
+def merge_rccl_env(channel_env: dict, spec_env: dict) -> dict:
+    """Combine the ``--rccl_channels`` pin with the ``--all_reduce_spec``
+    settings: the spec's ``#shards`` raises the channel floor, and the
+    ceiling is never left below the floor (RCCL would otherwise clamp one of
+    the two settings silently)."""
+    env = dict(channel_env)
+    for k, v in spec_env.items():
+        if k != "NCCL_MIN_NCHANNELS":
+            env[k] = v
+    lo = max(int(channel_env.get("NCCL_MIN_NCHANNELS", 0)),
+             int(spec_env.get("NCCL_MIN_NCHANNELS", 0)))
+    if lo:
+        env["NCCL_MIN_NCHANNELS"] = str(lo)
+        if "NCCL_MAX_NCHANNELS" in env:
+            env["NCCL_MAX_NCHANNELS"] = str(max(int(env["NCCL_MAX_NCHANNELS"]), lo))
+    return env
+
+
+def _count_device_list(v: str) -> int:
+    return len([d for d in v.split(",") if d.strip() != ""])
+
+
+def visible_gpu_count() -> int:
+    """GPUs this process may use, WITHOUT a HIP call in this process (a
+    launcher parent must not initialise the runtime before it starts its
+    ranks).  HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES
+    when set; otherwise a child interpreter asks the runtime."""
+    for name in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        v = os.environ.get(name)
+        if v is not None:
+            return _count_device_list(v)
+    import subprocess
+    import sys
+    try:
+        out = subprocess.run([sys.executable, "-c",
+                              "import torch; print(torch.cuda.device_count())"],
+                             capture_output=True, text=True, timeout=300)
+        return int(out.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError, OSError):
+        return 0
+
+
+def select_device_index(gpu_indices, num_gpus: int, tower_mode: bool, local_rank: int,
+                        world_size: int, device_count: int) -> int:
+    """The ONE place a rank's GPU is chosen: the compute device and the RCCL
+    communicator's device both come from here.  ``device_count`` is what
+    this process sees, so a launcher that gives every rank its own
+    HIP_VISIBLE_DEVICES (1 visible device) maps every rank to device 0,
+    and one that exposes the whole node maps local rank r to GPU r
+    (shifted by ``--gpu_indices``)."""
+    gpu_indices = list(gpu_indices) or [0]
+    local = local_rank if world_size > 1 else 0
+    if num_gpus == 1:
+        idx = gpu_indices[0] + local
+    elif tower_mode:
+        idx = gpu_indices[local % len(gpu_indices)]
+    else:
+        idx = gpu_indices[0]
+    return idx % max(int(device_count), 1)
+
+
 def init_world(device_type: str = "cuda", all_reduce_spec: Optional[str] = None,
-               timeout_s: int = 1800, channels: Optional[int] = None) -> World:
+               timeout_s: int = 1800, channels: Optional[int] = None,
+               device_index: Optional[int] = None) -> World:
     """Initializes the default process group once (idempotent).
     ``all_reduce_spec`` picks RCCL's algorithm / channel count before the
     communicator exists (parallel/allreduce.py:rccl_env_for_spec).  At world
-    size 1 no group is created unless KFB_FORCE_PG=1."""
+    size 1 no group is created unless KFB_FORCE_PG=1.  ``device_index`` is
+    the rank's compute GPU (:func:`select_device_index`); the communicator
+    is bound to the same device."""
     global _WORLD
     if _WORLD is not None:
         return _WORLD
@@ -131,6 +196,7 @@ def init_world(device_type: str = "cuda", all_reduce_spec: Optional[str] = None,
     local_rank = env_local_rank()
     if size <= 1 and not force_pg():
         _WORLD = World(0, 1, local_rank, None)
+        _WORLD.device_index = device_index
         return _WORLD
     if size <= 1:
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
@@ -138,31 +204,35 @@ def init_world(device_type: str = "cuda", all_reduce_spec: Optional[str] = None,
     # on one device) - the 2-rank GPU rehearsal on a 1-GPU box
     backend = os.environ.get("KFB_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
     if backend == "nccl":
-        env = dict(rccl_channel_env(channels))
+        spec_env = {}
         if all_reduce_spec:
             from .allreduce import rccl_env_for_spec
-            env.update(rccl_env_for_spec(all_reduce_spec))
-        for k, v in env.items():
+            spec_env = rccl_env_for_spec(all_reduce_spec)
+        for k, v in merge_rccl_env(rccl_channel_env(channels), spec_env).items():
             os.environ.setdefault(k, v)
     here = False
+    if device_index is None and device_type == "cuda":
+        device_index = select_device_index([0], 1, False, local_rank, size,
+                                           torch.cuda.device_count())
     if backend == "nccl":
-        _reserve_compute_streams(local_rank)
+        _reserve_compute_streams(device_index)
     if not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kwargs = dict(backend=backend, init_method="env://", rank=rank, world_size=size,
                       timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
-            kwargs["device_id"] = torch.device("cuda", local_rank)
+            kwargs["device_id"] = torch.device("cuda", device_index)
             opts = _pg_options(backend)
             if opts is not None:
                 kwargs["pg_options"] = opts
         dist.init_process_group(**kwargs)
         here = True
     _WORLD = World(rank, size, local_rank, dist.get_backend(), here, has_pg=True)
+    _WORLD.device_index = device_index
     return _WORLD
 
 
-def _reserve_compute_streams(local_rank: int):
+def _reserve_compute_streams(device_index: int):
     """Create the compute side streams (weight-gradient stream) BEFORE the
     RCCL communicator: HIP maps streams onto a few hardware queues
     (GPU_MAX_HW_QUEUES, 4 by default) in creation order, and a side stream
@@ -170,9 +240,9 @@ def _reserve_compute_streams(local_rank: int):
     serializing the weight gradients behind the dgrad chain (measured: the
     1-rank RCCL run lost the side-stream overlap, 22.5 vs 21.0 ms/step)."""
     try:
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(device_index)
         from ..ops import conv_hip
-        conv_hip.wgrad_stream(torch.device("cuda", local_rank))
+        conv_hip.wgrad_stream(torch.device("cuda", device_index))
     except Exception:  # noqa: BLE001 - best effort; the streams are created lazily anyway
         pass
 
