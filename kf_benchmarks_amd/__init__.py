@@ -17,14 +17,32 @@ __version__ = "0.1.0"
 # streams present, 4 queues put the weight-gradient stream behind the dgrad
 # chain (ResNet-50 bs256 with a 1-rank RCCL group: 22.3 ms/step at 4 queues,
 # 21.4 at 8, 20.8 without RCCL).  Must be set before HIP initializes, i.e.
-# before the first GPU call of the process.  KFB_HW_QUEUES overrides
-# (clamped to 1..32).
-_q = _os.environ.get("KFB_HW_QUEUES")
-if _q is None:
+# before the first GPU call of the process.  Precedence: KFB_HW_QUEUES, then
+# a GPU_MAX_HW_QUEUES other than HIP's own default of 4 (respected as is;
+# some environments export the default explicitly, and that is not a
+# choice: ask for exactly 4 with KFB_HW_QUEUES=4), then 8.  Clamped to 1..32.
+
+
+def _set_hw_queues():
+    import sys
+    import warnings
+    v = _os.environ.get("KFB_HW_QUEUES")
+    if v is None and _os.environ.get("GPU_MAX_HW_QUEUES", "4").strip() != "4":
+        return  # the user's explicit choice
     try:
-        _cur = int(_os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+        q = int(v) if v is not None else 8
     except ValueError:
-        _cur = 4
-    _q = max(_cur, 8)
-_os.environ["GPU_MAX_HW_QUEUES"] = str(min(max(int(_q), 1), 32))  # HIP allows 1..32
-del _q
+        warnings.warn("KFB_HW_QUEUES=%r is not an integer; using 8" % v)
+        q = 8
+    torch = sys.modules.get("torch")
+    if torch is not None and getattr(torch, "cuda", None) is not None:
+        try:
+            if torch.cuda.is_initialized():
+                warnings.warn("kf_benchmarks_amd imported after the GPU runtime started: "
+                              "GPU_MAX_HW_QUEUES=%d has no effect in this process" % q)
+        except Exception:  # noqa: BLE001
+            pass
+    _os.environ["GPU_MAX_HW_QUEUES"] = str(min(max(q, 1), 32))
+
+
+_set_hw_queues()

@@ -503,8 +503,9 @@ class BenchmarkCNN:
                     # so its gradient uses them, not the master being updated
                     self.flat.grad.add_(self.flat.flat, alpha=wd / grad_scale)
                     wd = 0.0
+                mix, wout = self.strategy.fused_update()
                 self.optimizer.step(self.learning_rate(step), grad_scale=grad_scale,
-                                    weight_decay=wd, clip=p.gradient_clip)
+                                    weight_decay=wd, clip=p.gradient_clip, mix=mix, wout=wout)
             except BaseException:
                 self.strategy.abort_update(step)
                 raise

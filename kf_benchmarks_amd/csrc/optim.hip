@@ -12,6 +12,14 @@
 //     Optimizer (tcb/benchmark_cnn.py:1172-1190)
 //   * the low-precision (bf16/fp16) shadow copy of the weights the kernels read.
 // A per-element decay mask (1 byte, optional) excludes variables from L2.
+//
+// Model averaging (KungFu PairAveraging / SMA, tcb/benchmark_cnn.py:1196-1201)
+// is folded into the same pass: with ``mix`` set, w <- mix_a * w + mix_b * mix
+// before the update (PairAveraging: (w + w_peer) / 2; SMA: w - alpha (w - avg)),
+// gated by a device flag ``mix_ok`` (the peer snapshot's seqlock check, see
+// seqlock_check_k); ``wout`` receives a copy of the updated weights (the
+// PairAveraging publish slot, the SMA all-reduce buffer), so neither strategy
+// runs extra elementwise passes over the model.
 #include "common.h"
 
 namespace kfb {
@@ -27,6 +35,10 @@ struct OptArgs {
   float b1, b2, eps;  // rmsprop decay in b1; adam betas
   float lr_t;         // adam bias-corrected step size
   int nesterov;
+  const float* mix;   // model to average in before the update (nullable)
+  float mix_a, mix_b; // w <- mix_a * w + mix_b * mix
+  const int* mix_ok;  // nullable; *mix_ok == 0 skips the averaging
+  float* wout;        // nullable; receives the updated weights
 };
 
 template <int KIND, typename LP>
@@ -34,10 +46,16 @@ __global__ void __launch_bounds__(256)
 opt_step_k(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ s1,
            float* __restrict__ s2, LP* __restrict__ wlp, const uint8_t* __restrict__ decay_mask,
            long n4, OptArgs a) {
+  const bool mix = a.mix && (!a.mix_ok || *a.mix_ok);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (long)gridDim.x * blockDim.x) {
     float4 wv = reinterpret_cast<float4*>(w)[i];
     float4 gv = reinterpret_cast<const float4*>(g)[i];
+    if (mix) {
+      const float4 pv = reinterpret_cast<const float4*>(a.mix)[i];
+      wv = make_float4(a.mix_a * wv.x + a.mix_b * pv.x, a.mix_a * wv.y + a.mix_b * pv.y,
+                       a.mix_a * wv.z + a.mix_b * pv.z, a.mix_a * wv.w + a.mix_b * pv.w);
+    }
     float ww[4] = {wv.x, wv.y, wv.z, wv.w};
     float gg[4] = {gv.x, gv.y, gv.z, gv.w};
     float m1[4], m2[4];
@@ -79,6 +97,7 @@ opt_step_k(float* __restrict__ w, const float* __restrict__ g, float* __restrict
       }
     }
     reinterpret_cast<float4*>(w)[i] = make_float4(ww[0], ww[1], ww[2], ww[3]);
+    if (a.wout) reinterpret_cast<float4*>(a.wout)[i] = make_float4(ww[0], ww[1], ww[2], ww[3]);
     if (KIND != SGD)
       reinterpret_cast<float4*>(s1)[i] = make_float4(m1[0], m1[1], m1[2], m1[3]);
     if (KIND == RMSPROP || KIND == ADAM)
@@ -90,6 +109,18 @@ opt_step_k(float* __restrict__ w, const float* __restrict__ g, float* __restrict
       reinterpret_cast<Vec<LP, 4>*>(wlp)[i] = o;
     }
   }
+}
+
+// Seqlock validation of a peer-model snapshot, run on the pull stream right
+// after the copy: the snapshot is good iff the peer's sequence word for the
+// slot (host memory, mapped for the device) still holds the even value read
+// before the copy - a rewrite overlapping the copy makes it odd first and
+// leaves it at a larger value.  ok[0] = 1 / 0; torn[0] counts rejections.
+__global__ void seqlock_check_k(const long long* seq, long long expect, int* ok, int* torn) {
+  const long long v = __hip_atomic_load(seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const int good = v == expect;
+  ok[0] = good;
+  if (!good) atomicAdd(torn, 1);
 }
 
 // Non-finite detector for dynamic loss scaling: flag[0] |= any(!isfinite(x)).
@@ -137,9 +168,11 @@ KFB_API hipError_t kfb_opt_step(int kind, float* w, const float* g, float* s1, f
                                 int lp_dtype, const uint8_t* decay_mask, long n, float lr,
                                 float grad_scale, float weight_decay, float clip, float mom,
                                 float b1, float b2, float eps, float lr_t, int nesterov,
-                                hipStream_t stream) {
+                                const float* mix, float mix_a, float mix_b, const int* mix_ok,
+                                float* wout, hipStream_t stream) {
   if (n % 4) return hipErrorInvalidValue;
-  OptArgs a{lr, grad_scale, weight_decay, clip, mom, b1, b2, eps, lr_t, nesterov};
+  OptArgs a{lr, grad_scale, weight_decay, clip, mom, b1, b2, eps, lr_t, nesterov,
+            mix, mix_a, mix_b, mix_ok, wout};
   const long n4 = n / 4;
   const int gb = grid_for(n4);
 #define KFB_OPT(K, LP)                                                                      \
@@ -181,3 +214,19 @@ KFB_API hipError_t kfb_cast_f32(const float* x, void* y, int dtype, long n, hipS
     return hipErrorInvalidValue;
   return hipGetLastError();
 }
+
+KFB_API hipError_t kfb_seqlock_check(const long long* seq, long long expect, int* ok, int* torn,
+                                     hipStream_t stream) {
+  hipLaunchKernelGGL(seqlock_check_k, dim3(1), dim3(1), 0, stream, seq, expect, ok, torn);
+  return hipGetLastError();
+}
+
+// Page-locks host memory (e.g. a /dev/shm mapping) for device access;
+// *dev receives its device address.
+KFB_API hipError_t kfb_host_register(void* p, size_t bytes, void** dev) {
+  hipError_t e = hipHostRegister(p, bytes, hipHostRegisterMapped);
+  if (e != hipSuccess) return e;
+  return hipHostGetDevicePointer(dev, p, 0);
+}
+
+KFB_API hipError_t kfb_host_unregister(void* p) { return hipHostUnregister(p); }

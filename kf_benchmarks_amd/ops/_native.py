@@ -40,7 +40,10 @@ _SIGS = {
                         P, P, P, P, P, P, P, I, P, P, P, I, P],
     "kfb_bn_fwd_infer": [I, P, P, P, L, I, P, P, P, P, F, P, P, I, P],
     "kfb_bn_bwd": [I, P, P, P, P, P, L, I, P, P, P, P, P, P, P, I, P, P, P, I, I, I, P],
-    "kfb_opt_step": [I, P, P, P, P, P, I, P, L, F, F, F, F, F, F, F, F, F, I, P],
+    "kfb_opt_step": [I, P, P, P, P, P, I, P, L, F, F, F, F, F, F, F, F, F, I, P, F, F, P, P, P],
+    "kfb_seqlock_check": [P, ctypes.c_longlong, P, P, P],
+    "kfb_host_register": [P, ctypes.c_size_t, P],
+    "kfb_host_unregister": [P],
     "kfb_nonfinite": [P, L, P, P],
     "kfb_half_sumsq": [P, L, P, P],
     "kfb_cast_f32": [P, P, I, L, P],

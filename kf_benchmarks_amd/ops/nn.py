@@ -1233,14 +1233,23 @@ def channel_pad(x, before: int, after: int):
 
 def concat_channels(xs: Sequence[torch.Tensor]):
     xs = list(xs)
-    if (xs[0].is_cuda and 1 < len(xs) <= _CAT_MAX
-            and all(x.dtype == xs[0].dtype and x.shape[:-1] == xs[0].shape[:-1] for x in xs)):
-        return _Concat.apply(*xs)
     if len(xs) == 1:
         return xs[0]
-    if xs[0].is_cuda:
-        raise N.NativeError("no HIP concat for %d inputs" % len(xs))
-    return torch.cat(xs, dim=-1)
+    if not xs[0].is_cuda:
+        return torch.cat(xs, dim=-1)
+    if any(x.shape[:-1] != xs[0].shape[:-1] for x in xs):
+        raise N.NativeError("concat inputs differ outside the channel dim: %s"
+                            % [tuple(x.shape) for x in xs])
+    dt = xs[0].dtype
+    for x in xs[1:]:
+        dt = torch.promote_types(dt, x.dtype)
+    xs = [x if x.dtype == dt else x.to(dt) for x in xs]
+    if len(xs) > _CAT_MAX:
+        # the kernel takes up to _CAT_MAX inputs per launch: concat groups,
+        # then the groups (one extra pass over the output's bytes)
+        xs = [concat_channels(xs[i:i + _CAT_MAX]) for i in range(0, len(xs), _CAT_MAX)]
+        return concat_channels(xs)
+    return _Concat.apply(*xs)
 
 
 # ------------------------------------------------------------------ embedding

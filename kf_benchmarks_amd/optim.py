@@ -166,9 +166,13 @@ class FusedOptimizer:
         return out
 
     def step(self, lr: float, grad_scale: float = 1.0, weight_decay: float = 0.0,
-             clip: Optional[float] = None, grad: Optional[torch.Tensor] = None):
+             clip: Optional[float] = None, grad: Optional[torch.Tensor] = None,
+             mix=None, wout: Optional[torch.Tensor] = None):
         """One update of every variable. ``grad`` overrides the flat gradient
-        buffer (e.g. an all-reduced copy)."""
+        buffer (e.g. an all-reduced copy).  ``mix = (src, a, b, ok)`` first
+        sets w <- a*w + b*src (model averaging; skipped when the device flag
+        ``ok`` (nullable) is 0); ``wout`` receives a copy of the updated
+        weights.  Both ride the same single pass over the model."""
         self.t += 1
         f = self.flat
         g = f.grad if grad is None else grad
@@ -184,15 +188,26 @@ class FusedOptimizer:
             f.stage_reads()
         w = f.update_target
         lp = None if staged else f.lp
+        msrc, ma, mb, mok = mix if mix is not None else (None, 1.0, 0.0, None)
+        for t in (msrc, wout):
+            if t is not None and (t.numel() != f.numel or t.dtype != torch.float32
+                                  or not t.is_contiguous()):
+                raise ValueError("mix / wout must be contiguous fp32 of the flat size")
         if f.device.type == "cuda":
             N.call("kfb_opt_step", _KINDS[self.kind], w.data_ptr(), g.data_ptr(),
                    N.ptr(self.s1), N.ptr(self.s2), N.ptr(lp),
                    N.dt(lp) if lp is not None else 0, None, f.numel, float(lr),
                    float(grad_scale), float(weight_decay), clipv, float(mom), float(b1),
-                   float(b2), float(eps), float(lr_t), int(self.nesterov), N.stream(f.device))
+                   float(b2), float(eps), float(lr_t), int(self.nesterov), N.ptr(msrc),
+                   float(ma), float(mb), N.ptr(mok), N.ptr(wout), N.stream(f.device))
             f.after_update()
             return
+        if msrc is not None and (mok is None or int(mok.reshape(-1)[0]) != 0):
+            with torch.no_grad():
+                w.mul_(ma).add_(msrc, alpha=mb)
         self._step_torch(g, lr, grad_scale, weight_decay, clipv, mom, b1, b2, eps, lr_t)
+        if wout is not None:
+            wout.copy_(w)
         f.after_update()
 
     @torch.no_grad()

@@ -138,7 +138,17 @@ def _side_stream(buf):
 def launch_collective(comm, buf, alg: str, bucket_index: int, world_size: int, op: str = "sum",
                       hierarchical: Optional["Hierarchical"] = None):
     """Issue one bucket piece's collective(s) asynchronously; returns the
-    list of work handles (the last one completes the piece)."""
+    list of work handles (the last one completes the piece).
+
+    Multi-stage chains (parameter-server reduce -> broadcast, and the
+    hierarchical reduce -> leader all-reduce -> broadcast) order their stages
+    with ``Work.wait()``: on RCCL that is a stream wait on the side stream
+    (the host and the compute stream run on), on gloo - the CPU test
+    backend, whose async ops are not ordered - it is a host wait inside the
+    backward hook.  The chains are verified over gloo at 2-8 ranks
+    (tests/test_variable_update.py, tests/test_scale_rehearsal.py) and over
+    a 1-rank RCCL group; their RCCL form at more than one GPU runs for the
+    first time on the round-end multi-GPU node."""
     if hierarchical is not None and world_size > 1:
         return hierarchical.launch(buf, op)
     if is_parameter_server(alg) and world_size > 1:

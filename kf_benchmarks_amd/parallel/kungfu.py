@@ -23,12 +23,26 @@ accepted.  Retries are bounded and exhausting them raises.
 * GPU ranks: the two slots live in device memory and are shared with every
   peer through HIP IPC (torch CUDA-tensor sharing over dmabuf), so a pull is
   a device-to-device copy over xGMI that the owner never sees.  Nothing
-  blocks the host inside the step: the peer pull is issued on a side stream
-  at the start of the step (overlapping forward/backward) and checked at the
-  update; the publish copy is enqueued after the update and committed
-  (sequence word made even) as soon as its event has completed - at the
-  latest at the next publish.
-* CPU ranks (tests, plumbing config): the slots live in /dev/shm.
+  blocks the host inside the step:
+  - the peer pull is issued on a side stream at the start of the step
+    (overlapping forward/backward) and validated ON THE DEVICE: a one-thread
+    kernel behind the copy re-reads the peer's sequence word (the /dev/shm
+    header, page-locked and mapped for the GPU) and sets a flag; the fused
+    optimizer averages with the snapshot only if the flag says untorn (a
+    torn snapshot - a rewrite overlapped the copy - skips that step's
+    averaging and is counted);
+  - the optimizer writes the updated model straight into the publish slot
+    (no copy pass); the slot is committed (sequence word made even) once
+    the update's event has completed, polled at the next step.  If it has
+    not completed by the next publish, that publish rewrites the same
+    (still odd, never readable) slot.
+  ``--kungfu_pair_prefetch=false`` pulls at update time instead (the peer
+  model is then as fresh as KungFu's, whose PairAveragingOptimizer requests
+  it in apply_gradients); the default prefetch at the start of the step
+  averages with a model one forward/backward older, the price of overlapping
+  the pull.
+* CPU ranks (tests, plumbing config): the slots live in /dev/shm and the
+  seqlock is checked on the host.
 """
 
 from __future__ import annotations
@@ -58,6 +72,7 @@ class _Header:
             f.write(b"\0" * 64)
         self.rank = rank
         self._maps = {}
+        self._dev = {}
 
     def _map(self, r):
         if r not in self._maps:
@@ -73,7 +88,33 @@ class _Header:
         # sees the new ``latest`` also sees the sequence word written before it
         struct.pack_into("<q", self._map(self.rank), 8 * word, v)
 
+    def device_word(self, r, word):
+        """Device address of peer ``r``'s header word (page-locked host
+        memory); None if the mapping cannot be registered."""
+        if r not in self._dev:
+            import ctypes
+            from ..ops import _native as N
+            m = self._map(r)
+            host = ctypes.addressof(ctypes.c_char.from_buffer(m))
+            dev = ctypes.c_void_p()
+            try:
+                N.call("kfb_host_register", host, 64, ctypes.byref(dev))
+                self._dev[r] = (host, dev.value)
+            except N.NativeError:
+                self._dev[r] = (None, None)
+        host, dev = self._dev[r]
+        return None if dev is None else dev + 8 * word
+
     def close(self):
+        if self._dev:
+            from ..ops import _native as N
+            for host, dev in self._dev.values():
+                if host is not None:
+                    try:
+                        N.call("kfb_host_unregister", host)
+                    except N.NativeError:
+                        pass
+            self._dev = {}
         for f, m in self._maps.values():
             m.close()
             f.close()
@@ -114,6 +155,12 @@ class ModelStore:
                 if r != self.rank:
                     self.peer_slots[r] = fn(*args)
             self.pull_stream = torch.cuda.Stream(flat.device)
+            # device-side seqlock validation (flag read by the fused
+            # optimizer) when every peer header can be mapped for the GPU
+            self.ok = torch.ones(1, dtype=torch.int32, device=flat.device)
+            self.torn = torch.zeros(1, dtype=torch.int32, device=flat.device)
+            self.device_check = all(self.hdr.device_word(r, 0) is not None
+                                    for r in range(self.size) if r != self.rank)
         else:
             self.path = "/dev/shm/kfb_model_%s_%d" % (job, self.rank)
             arr = np.memmap(self.path, dtype=np.float32, mode="w+", shape=(2, n))
@@ -132,12 +179,14 @@ class ModelStore:
                         self.peer_slots[r] = torch.from_numpy(
                             np.memmap(p, dtype=np.float32, mode="r", shape=(2, n)))
             self.pull_stream = None
+            self.device_check = False
         self.seq = [0, 0]
         self.latest = 0
         self.hdr.write(self.SEQ0, 0)
         self.hdr.write(self.SEQ1, 0)
         self.hdr.write(self.LATEST, 0)
         self._pending = None  # (slot, event) of a publish not yet committed
+        self._writing = None  # slot the current update writes into
         self._inflight = None  # (peer, slot, seq, event, out) of a prefetch
         self.publishes = 0
         self.retries = 0
@@ -164,22 +213,43 @@ class ModelStore:
         """Commit a completed publish without blocking."""
         self._commit(wait=False)
 
-    def publish(self, flat: torch.Tensor):
-        """Enqueue a snapshot of ``flat`` (on the current stream, after the
-        update that produced it); committed once the copy has completed."""
-        self._commit(wait=True)
-        slot = 1 - self.latest
-        self.seq[slot] += 1  # odd: write in progress on this slot
-        self.hdr.write(slot, self.seq[slot])
-        self.slots[slot].copy_(flat)
+    def begin_publish(self) -> torch.Tensor:
+        """The slot the coming update writes the new model into (the fused
+        optimizer's ``wout``); marked in progress (odd) for readers."""
+        if self._pending is not None and not self._commit(wait=False):
+            slot = self._pending[0]  # still odd: rewrite it, commit later
+            self._pending = None
+        else:
+            slot = 1 - self.latest
+            self.seq[slot] += 1  # odd: write in progress on this slot
+            self.hdr.write(slot, self.seq[slot])
+        self._writing = slot
+        return self.slots[slot]
+
+    def end_publish(self):
+        """The update writing the slot is enqueued (current stream);
+        committed once it has completed."""
+        slot, self._writing = self._writing, None
         ev = None
         if self.cuda:
             ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(flat.device))
+            ev.record(torch.cuda.current_stream(self.device))
         self._pending = (slot, ev)
         self.publishes += 1
         if ev is None:
             self._commit(wait=True)
+
+    def abort_publish(self):
+        """The update failed: the slot stays odd (never read) until the
+        next publish rewrites it."""
+        if self._writing is not None:
+            self._pending = (self._writing, None)
+            self._writing = None
+
+    def publish(self, flat: torch.Tensor):
+        """Copy ``flat`` into the next slot and commit it once written."""
+        self.begin_publish().copy_(flat)
+        self.end_publish()
 
     def flush(self):
         self._commit(wait=True)
@@ -203,11 +273,25 @@ class ModelStore:
             self.pull_stream.wait_stream(cur)  # ``out`` is free to overwrite
             with torch.cuda.stream(self.pull_stream):
                 out.copy_(self.peer_slots[peer][slot], non_blocking=True)
+                if self.device_check:
+                    from ..ops import _native as N
+                    N.call("kfb_seqlock_check", self.hdr.device_word(peer, slot), v,
+                           self.ok.data_ptr(), self.torn.data_ptr(),
+                           self.pull_stream.cuda_stream)
                 ev = torch.cuda.Event()
                 ev.record(self.pull_stream)
         else:
             out.copy_(self.peer_slots[peer][slot])
         self._inflight = (peer, slot, v, ev, out)
+
+    def finish_pull_async(self):
+        """Device-validated pull: the current stream waits for the copy and
+        its seqlock check; returns the device flag (1 = untorn) the fused
+        optimizer gates the averaging on.  The host never blocks."""
+        peer, slot, v, ev, out = self._inflight
+        self._inflight = None
+        torch.cuda.current_stream(out.device).wait_event(ev)
+        return self.ok
 
     def finish_pull(self) -> int:
         """Wait for the prefetch, validate it against the seqlock (retrying
@@ -233,10 +317,19 @@ class ModelStore:
         self.begin_pull(peer, out)
         return self.finish_pull()
 
+    def torn_count(self) -> int:
+        """Snapshots rejected so far (host retries + device-side rejections)."""
+        n = self.retries
+        if self.cuda:
+            n += int(self.torn.item())
+        return n
+
     def close(self):
         if self._inflight is not None and self._inflight[3] is not None:
             self._inflight[3].synchronize()
         self._inflight = None
+        if self._writing is not None:
+            self.abort_publish()
         self.flush()
         self.hdr.close()
         if not self.cuda:
@@ -252,8 +345,11 @@ class PairAveraging(Strategy):
     def __init__(self, params, world, flat, **kw):
         super().__init__(params, world, flat, **kw)
         self.rng = random.Random(params.kungfu_peer_seed * 7919 + world.rank)
+        self.prefetch = bool(getattr(params, "kungfu_pair_prefetch", True))
         self.store = None
         self._peer_buf = None
+        self._mix = None
+        self._wout = None
 
     def broadcast_initial_model(self, slots=()):
         super().broadcast_initial_model(slots)
@@ -270,19 +366,38 @@ class PairAveraging(Strategy):
         if self.store is None:
             return
         self.store.poll()
-        # prefetch a random peer's model while forward/backward run
-        self.store.begin_pull(self._pick_peer(), self._peer_buf)
+        if self.prefetch:
+            # pull a random peer's model while forward/backward run
+            self.store.begin_pull(self._pick_peer(), self._peer_buf)
 
     def before_update(self, step):
         if self.store is None:
             return
-        self.store.finish_pull()
-        w = self.flat.flat
-        w.add_(self._peer_buf).mul_(0.5)
+        if not self.prefetch:
+            self.store.begin_pull(self._pick_peer(), self._peer_buf)
+        if self.store.device_check:
+            ok = self.store.finish_pull_async()
+        else:
+            self.store.finish_pull()
+            ok = None
+        # w <- (w + w_peer) / 2 and the update in ONE pass, written straight
+        # into the publish slot
+        self._mix = (self._peer_buf, 0.5, 0.5, ok)
+        self._wout = self.store.begin_publish()
+
+    def fused_update(self):
+        mix, wout = self._mix, self._wout
+        self._mix = self._wout = None
+        return mix, wout
 
     def after_update(self, step):
         if self.store is not None:
-            self.store.publish(self.flat.flat)
+            self.store.end_publish()
+
+    def abort_update(self, step):
+        self._mix = self._wout = None
+        if self.store is not None:
+            self.store.abort_publish()
 
     def close(self):
         """Collective: every rank stops reading before any slot is freed."""
@@ -290,5 +405,6 @@ class PairAveraging(Strategy):
             self.store.flush()
             w = self.flat.flat
             self.world.barrier(w.device if w.is_cuda else None)
+            self.torn_snapshots = self.store.torn_count()
             self.store.close()
             self.store = None

@@ -95,6 +95,12 @@ class Strategy:
     def abort_update(self, step: int):
         """Called instead of after_update when the update raised."""
 
+    def fused_update(self):
+        """(mix, wout) for the optimizer's single pass (FusedOptimizer.step):
+        model averaging folded into the update, and where to copy the
+        updated weights.  Called between before_update and the step."""
+        return None, None
+
     @property
     def update_is_empty(self) -> bool:
         """True when the gradient to apply is the all-zero first step of
@@ -135,24 +141,59 @@ class KungFuSyncSGD(Strategy):
 class KungFuSMA(Strategy):
     """SynchronousAveragingOptimizer: every step all-reduce-average the model,
     move the local model toward it (w <- w - alpha (w - avg)), then apply the
-    local gradient."""
+    local gradient.
+
+    The average is of the weights the step's forward used (w_t), so its
+    all-reduce is launched as soon as w_t exists - right after the previous
+    update, whose fused kernel also writes the copy of w_t that is reduced
+    (``wout``) - and runs beside the next forward/backward.  The update waits
+    for it (a stream wait on RCCL) and folds the averaging into its single
+    pass (``mix``): no separate copy or elementwise passes over the model."""
     name = "kungfu/sma"
 
     def __init__(self, *a, alpha=0.1, **kw):
         super().__init__(*a, **kw)
         self.alpha = float(alpha)
         self._avg = None
+        self._work = None
+
+    def _launch(self):
+        self._work = comm.all_reduce(self._avg, async_op=True)
+
+    def broadcast_initial_model(self, slots=()):
+        super().broadcast_initial_model(slots)
+        if self.world.communicates:
+            self._avg = self.flat.flat.clone()
+            self._launch()
 
     def before_update(self, step):
         if not self.world.communicates:
             return
-        w = self.flat.flat
-        if self._avg is None:
-            self._avg = torch.empty_like(w)
-        self._avg.copy_(w)
-        comm.all_reduce(self._avg)
-        # w <- (1-alpha) w + alpha * avg
-        w.mul_(1.0 - self.alpha).add_(self._avg, alpha=self.alpha / self.world.size)
+        if self._avg is None:  # no initial broadcast: start from the local model
+            self._avg = self.flat.update_target.clone()
+            self._launch()
+        if self._work is not None:
+            self._work.wait()
+            self._work = None
+
+    def fused_update(self):
+        if not self.world.communicates or self._avg is None:
+            return None, None
+        # w <- (1 - alpha) w + alpha * sum / size; then the updated w goes to
+        # the buffer the next all-reduce sums
+        return (self._avg, 1.0 - self.alpha, self.alpha / self.world.size, None), self._avg
+
+    def after_update(self, step):
+        if self.world.communicates and self._avg is not None:
+            self._launch()
+
+    def abort_update(self, step):
+        self._work = None
+
+    def close(self):
+        if self._work is not None:
+            self._work.wait()
+            self._work = None
 
 
 class KungFuAdaSGD(Strategy):
@@ -180,9 +221,27 @@ class KungFuAdaSGD(Strategy):
         if step >= self.switch_step:
             super().after_backward(step)
 
+    def broadcast_initial_model(self, slots=()):
+        super().broadcast_initial_model(slots)
+        if self.switch_step > 0:
+            self.sma._avg = None  # started lazily by the first SMA update
+
     def before_update(self, step):
         if step < self.switch_step:
             self.sma.before_update(step)
+
+    def fused_update(self):
+        if self._step < self.switch_step:
+            return self.sma.fused_update()
+        return None, None
+
+    def after_update(self, step):
+        # launch the next average only if the next step still averages
+        if step + 1 < self.switch_step:
+            self.sma.after_update(step)
+
+    def close(self):
+        self.sma.close()
 
 
 MEAN_OVER_TOWERS = ("parameter_server", "distributed_replicated")

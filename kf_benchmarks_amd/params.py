@@ -211,6 +211,10 @@ D.DEFINE_integer("rccl_channels", 0,
 D.DEFINE_float("kungfu_sma_alpha", 0.1, "SMA: pull factor toward the model average.")
 D.DEFINE_integer("kungfu_ada_switch_step", 100, "ada_sgd: step at which SMA switches to S-SGD.")
 D.DEFINE_integer("kungfu_peer_seed", 0, "Seed for PairAveraging peer selection.")
+D.DEFINE_boolean("kungfu_pair_prefetch", True,
+                 "PairAveraging: pull the peer model at the start of the step, overlapping "
+                 "forward/backward (the averaged model is one step older than KungFu's); "
+                 "false pulls it at update time, as KungFu's apply_gradients does.")
 D.DEFINE_boolean("synthetic_resample", True,
                  "Re-sample the synthetic batch on device every step, inside the timed step "
                  "(as the fork's graph does; --nosynthetic_resample reuses one batch like "

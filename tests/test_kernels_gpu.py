@@ -4,6 +4,8 @@ Every test runs the op on cuda:0 through libkfb_hip.so and the same op on
 CPU in fp32 (stock PyTorch), for forward and backward.
 """
 
+import os
+
 import pytest
 import torch
 
@@ -195,6 +197,70 @@ def test_fused_optimizer(cuda, kind):
     torch.testing.assert_close(b[1], a[1], rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("ok", [None, 1, 0])
+def test_fused_optimizer_model_averaging(cuda, ok):
+    """The averaging folded into the optimizer pass (PairAveraging / SMA):
+    w <- a*w + b*src before the update, gated by a device flag, and the
+    updated weights copied to ``wout``; the HIP pass vs the CPU path (the
+    explicit formula)."""
+    from kf_benchmarks_amd import optim
+    from kf_benchmarks_amd.models.model import Network
+    from kf_benchmarks_amd.models.resnet_model import create_resnet20_cifar_model
+
+    res = {}
+    for dev in ("cpu", cuda):
+        model = create_resnet20_cifar_model(None)
+        net = Network(model, 11, dev, torch.float32, seed=5)
+        flat = optim.FlatParams(net, torch.bfloat16)
+        opt = optim.FusedOptimizer(flat, "momentum")
+        g = torch.Generator().manual_seed(3)
+        src = torch.randn(flat.numel, generator=g).to(flat.flat.device)
+        wout = torch.zeros_like(flat.flat)
+        flag = None if ok is None else torch.tensor([ok], dtype=torch.int32,
+                                                     device=flat.flat.device)
+        for i in range(2):
+            flat.grad.copy_(torch.randn(flat.numel, generator=g).to(flat.grad.device))
+            opt.step(0.01, grad_scale=0.5, weight_decay=1e-3, mix=(src, 0.75, 0.25, flag),
+                     wout=wout)
+        res[str(dev)] = (flat.flat.cpu().clone(), wout.cpu().clone())
+    a, b = res["cpu"], res[str(cuda)]
+    torch.testing.assert_close(b[0], a[0], rtol=1e-5, atol=1e-6)
+    assert torch.equal(b[1], b[0]) and torch.equal(a[1], a[0])
+
+
+def test_seqlock_check_reads_host_word(cuda):
+    """The device-side PairAveraging snapshot check reads the peer's sequence
+    word from page-locked host memory (a /dev/shm mapping) at kernel time."""
+    import ctypes
+    import mmap
+    import struct
+    from kf_benchmarks_amd.ops import _native as N
+    path = "/dev/shm/kfb_test_seq_%d" % os.getpid()
+    with open(path, "wb") as f:
+        f.write(b"\0" * 64)
+    f = open(path, "r+b")
+    m = mmap.mmap(f.fileno(), 64)
+    try:
+        host = ctypes.addressof(ctypes.c_char.from_buffer(m))
+        dev = ctypes.c_void_p()
+        N.call("kfb_host_register", host, 64, ctypes.byref(dev))
+        ok = torch.zeros(1, dtype=torch.int32, device=cuda)
+        torn = torch.zeros(1, dtype=torch.int32, device=cuda)
+        s = N.stream(cuda)
+        for word, val, expect, good in ((0, 4, 4, 1), (1, 7, 6, 0), (0, 6, 4, 0), (1, 8, 8, 1)):
+            struct.pack_into("<q", m, 8 * word, val)
+            N.call("kfb_seqlock_check", dev.value + 8 * word, expect, ok.data_ptr(),
+                   torn.data_ptr(), s)
+            torch.cuda.synchronize()
+            assert int(ok.item()) == good, (word, val, expect)
+        assert int(torn.item()) == 2
+        N.call("kfb_host_unregister", host)
+    finally:
+        m.close()
+        f.close()
+        os.remove(path)
+
+
 def _epilogue_stats(x):
     """[2][32][C] partial sums as a conv epilogue leaves them (slot 0 only)."""
     from kf_benchmarks_amd.ops import conv_hip
@@ -337,7 +403,8 @@ def test_lrn(cuda, dt, shape, r):
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("widths", [(64, 128, 32), (3, 5, 8, 1), (96, 96), (16,) * 16])
+@pytest.mark.parametrize("widths", [(64, 128, 32), (3, 5, 8, 1), (96, 96), (16,) * 16,
+                                    tuple(8 + (i % 3) * 8 for i in range(37))])
 def test_concat_channels(cuda, dt, widths):
     """Channel concat (csrc/gather.hip) and its split backward vs torch.cat."""
     torch.manual_seed(4)
