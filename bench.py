@@ -59,6 +59,14 @@ def main(argv=None):
                     help="tf_cnn_benchmarks --all_reduce_spec (e.g. pscpu, nccl#2, xring)")
     ap.add_argument("--hierarchical_copy", action="store_true",
                     help="two-level (intra-group then leaders) gradient reduction")
+    ap.add_argument("--data_dir", default=None,
+                    help="real TFRecord ImageNet-format data (train preprocessing: distorted bbox "
+                         "crop, flip, resize) instead of synthetic batches")
+    ap.add_argument("--input_threads", type=int, default=0,
+                    help="host preprocessing threads with --data_dir (0: the default)")
+    ap.add_argument("--launch_tape", type=int, default=0,
+                    help="1: record one step's native launches after warmup and replay them "
+                         "from C++ (ops/tape.py); falls back to eager where not eligible")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
@@ -103,6 +111,9 @@ def main(argv=None):
                       kernel_impl=a.kernel_impl, bucket_size_mb=a.bucket_size_mb,
                       gradient_wire_dtype=a.wire_dtype, display_every=10**9,
                       all_reduce_spec=a.all_reduce_spec, hierarchical_copy=a.hierarchical_copy,
+                      launch_tape=bool(a.launch_tape), data_dir=a.data_dir,
+                      datasets_num_private_threads=a.input_threads or None,
+                      datasets_repeat_cached_sample=bool(a.data_dir),
                       synthetic_resample=not a.reuse_synthetic)
     bench = BenchmarkCNN(p)
     bench.build()
@@ -149,14 +160,9 @@ def main(argv=None):
     # replica consistency (outside the timed region): every rank's fp32
     # master-weight checksum; synchronous strategies must agree bit for bit
     w = bench.strategy.flat.flat
-    mine = torch.stack([w.double().sum(), w.double().square().sum()])
-    sums = [torch.zeros_like(mine) for _ in range(world.size)]
-    if world.communicates:
-        import torch.distributed as dist
-        dist.all_gather(sums, mine)
-    else:
-        sums = [mine]
-    sums = [tuple(float(v) for v in x.cpu()) for x in sums]
+    mine = tuple(float(v) for v in torch.stack([w.double().sum(),
+                                                 w.double().square().sum()]).cpu())
+    sums = comm.all_gather_object(mine)
     in_sync = all(x == sums[0] for x in sums)
 
     exposed = []
@@ -169,7 +175,7 @@ def main(argv=None):
     elapsed = float(t[0].item())
     exposed_ms = float(t[1].item())
     comm_info = {
-        "backend": world.backend or "none",
+        "backend": world.device_backend,
         "buckets": reducer.num_buckets if reducer is not None else 0,
         "collectives_per_step": ((reducer.launch_count - launches0) / a.steps
                                  if reducer is not None else 0),
@@ -200,8 +206,11 @@ def main(argv=None):
             "vs_baseline": round(value / base, 3) if base else None,
             "dtype": a.dtype,
             "ranks": world.size,
-            "backend": world.backend or "none",
-            "data": ("synthetic (%dx%dx3 ImageNet-shaped images %s, random-init weights)"
+            "backend": world.device_backend,
+            "data": ("real TFRecords from %s (train preprocessing on %s host threads, "
+                     "repeat-cached records)" % (a.data_dir, a.input_threads or "default")
+                     if a.data_dir else
+                     "synthetic (%dx%dx3 ImageNet-shaped images %s, random-init weights)"
                      % (bench.model.image_size, bench.model.image_size,
                         "generated once" if a.reuse_synthetic
                         else "re-sampled on device every step")
@@ -213,6 +222,8 @@ def main(argv=None):
                                            if a.variable_update == "kungfu"
                                            else a.variable_update),
                        "all_reduce_spec": a.all_reduce_spec,
+                       "launch_tape": (getattr(bench, "_tape", None) is not None
+                                       and bench._tape.replays > 0),
                        "hierarchical_copy": a.hierarchical_copy,
                        "optimizer": a.optimizer,
                        "kernel_impl": a.kernel_impl, "loss_first": warm_loss,

@@ -419,6 +419,11 @@ class BenchmarkCNN:
                     mask[off:off + n] = 1.0
             self.l2_mask = mask
         self.input = self._make_input()
+        self._tape = None
+        self._tape_warm = 0
+        self._tape_reason = self.tape_eligible() if p.launch_tape else "off"
+        if p.launch_tape and self._tape_reason is not None:
+            log_fn("launch tape: not used (%s)" % self._tape_reason)
         self._built = True
 
     def _make_input(self):
@@ -462,8 +467,82 @@ class BenchmarkCNN:
             acc = self.model.accuracy_function(inputs, res.logits.detach())
         return loss.detach(), acc
 
+    # ------------------------------------------------------------ launch tape
+    def tape_eligible(self):
+        """Why the step cannot be taped (None: it can).  The tape replays the
+        native launches of one step; host logic that must run every step
+        (collectives issued from Python, host-side data, loss-scale checks,
+        global-step-dependent graphs) keeps a configuration eager."""
+        p = self.params
+        if self.device_type != "cuda" or p.kernel_impl != "hip":
+            return "not a HIP device run"
+        if self.world.communicates:
+            if self.world.native is None:
+                return "device collectives go through torch.distributed (not recordable)"
+            from .parallel.variable_mgr import KungFuSyncSGD, SumAllReduceStrategy
+            s = self.strategy
+            r = getattr(s, "reducer", None)
+            if not isinstance(s, (KungFuSyncSGD, SumAllReduceStrategy)) or r is None:
+                return "%s runs host-side logic every step" % s.name
+            if r.relaxed or r.hierarchical is not None:
+                return "relaxed / hierarchical reductions keep host-side state"
+        if not self.dataset.use_synthetic_gpu_inputs() or getattr(self, "fake_data", None):
+            return "host-side input pipeline"
+        if self.enable_auto_loss_scale:
+            return "dynamic loss scaling reads the gradients on the host"
+        if p.staged_vars or self.l2_mask is not None:
+            return "staged variables / masked L2 use torch ops in the update"
+        if self.model.get_model_name().startswith("nasnet"):
+            return "NASNet's drop-path schedule follows the host step"
+        return None
+
+    def _tape_values(self, step):
+        vals = {"lr": self.learning_rate(step)}
+        vals.update(self.optimizer.tape_values(vals["lr"]))
+        vals.update(self.input.tape_values())
+        vals.update(self.net.tape_dropout_values())
+        return vals
+
+    def _tape_step(self, need_loss, need_accuracy):
+        """Replays (or records) the step; None = run it eagerly."""
+        if need_accuracy:
+            return None
+        t = getattr(self, "_tape", None)
+        if t is None:
+            if self._tape_warm < 2:  # autotune / arena sizing settle first
+                self._tape_warm += 1
+                return None
+            from .ops.tape import StepTape
+            self.net.tape_begin_recording()
+            t = self._tape = StepTape(self.device)
+            loss, acc = t.record(lambda: self._eager_train_step(False, False))
+            self._tape_loss = loss
+            log_fn("launch tape: recorded %d native calls (per-step arguments: %s)"
+                   % (len(t.recorder), ", ".join(t.recorder.keys()) or "none"))
+            return loss, acc
+        p = self.params
+        step = self.global_step
+        l2 = None
+        if need_loss and p.loss_type_to_report == "total_loss" and p.weight_decay:
+            l2 = self.l2_loss_value()  # of the weights this step's forward reads
+        self.input.tape_advance()
+        vals = self._tape_values(step)
+        t.replay(vals)
+        self.global_step += 1
+        loss = self._tape_loss
+        if l2 is not None:
+            loss = loss + len(self.devices) * p.weight_decay * l2
+        return loss, None
+
     def train_step(self, need_loss=False, need_accuracy=False):
         """One full training step; returns (loss_tensor, accuracy_dict)."""
+        if self.params.launch_tape and self._tape_reason is None:
+            r = self._tape_step(need_loss, need_accuracy)
+            if r is not None:
+                return r
+        return self._eager_train_step(need_loss, need_accuracy)
+
+    def _eager_train_step(self, need_loss=False, need_accuracy=False):
         p = self.params
         inputs = tuple(self.input.next())
         self.net.global_step = self.global_step  # NASNet drop-path schedule

@@ -152,6 +152,14 @@ cast_f32_k(const float* __restrict__ x, LP* __restrict__ y, long n) {
     y[i] = (LP)x[i];
 }
 
+template <typename LP>
+__global__ void __launch_bounds__(256)
+cast_to_f32_k(const LP* __restrict__ x, float* __restrict__ y, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    y[i] = (float)x[i];
+}
+
 static int grid_for(long n) {
   long b = (n + 255) / 256;
   if (b > 256L * 8) b = 256L * 8;
@@ -230,3 +238,17 @@ KFB_API hipError_t kfb_host_register(void* p, size_t bytes, void** dev) {
 }
 
 KFB_API hipError_t kfb_host_unregister(void* p) { return hipHostUnregister(p); }
+
+// y (fp32) = x (bf16 / fp16): a low-precision gradient wire buffer back into
+// the flat fp32 gradient.
+KFB_API hipError_t kfb_cast_to_f32(const void* x, int dtype, float* y, long n, hipStream_t stream) {
+  if (dtype == BF16)
+    hipLaunchKernelGGL((cast_to_f32_k<bf16>), dim3(grid_for(n)), dim3(256), 0, stream,
+                       (const bf16*)x, y, n);
+  else if (dtype == F16)
+    hipLaunchKernelGGL((cast_to_f32_k<f16>), dim3(grid_for(n)), dim3(256), 0, stream,
+                       (const f16*)x, y, n);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}

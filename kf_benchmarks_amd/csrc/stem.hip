@@ -132,9 +132,97 @@ s2d_stem3_k(const T* __restrict__ x, T* __restrict__ x2, int H, int W, int OH, i
   }
 }
 
+// ---------------------------------------------------------------- "pairs"
+// The stride-2 stem as a plain strided conv over PIXEL PAIRS, with no
+// repacked copy of the input: pad the image to 4 channels and by
+// (pt, pl) zeros, then view it as [N, Hp, Wp/2, 8] (two adjacent 4-channel
+// pixels per 8-channel "pixel").  Output (oh, ow) of the 7x7/2 conv reads
+// padded rows 2*oh + kh (kh < 8) and pair columns ow + j (j < 4), i.e. it is
+// an 8x4-tap conv with stride (2, 1) and C = 8 over the pair view:
+//   y[oh][ow][n] = sum_{kh<8, j<4, t<2, c<4} xp[2oh+kh][2(ow+j)+t][c] *
+//                  w2[n][kh][j][t*4+c],   w2[n][kh][j][t*4+c] = w[n][kh][2j+t][c]
+// (zero where kh >= KH, 2j+t >= KW or c >= C).  K = 256 as in the s2d repack,
+// but the kernels read the 1.4x padded image (108 MB at ResNet-50 bs256)
+// instead of writing and re-reading a 4.2x repack (422 MB).
+template <typename T>
+__global__ void __launch_bounds__(256)
+stem_pad_k(const T* __restrict__ x, T* __restrict__ xp, long npix, int H, int W, int C, int Hp,
+           int Wp, int pt, int pl) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < npix; i += (long)gridDim.x * 256) {
+    const long n = i / ((long)Hp * Wp);
+    const int r = (int)(i - n * Hp * Wp);
+    const int hp = r / Wp, wp = r - hp * Wp;
+    const int h = hp - pt, w = wp - pl;
+    Vec<T, 4> o;
+    const bool in = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+    const T* src = x + ((n * H + (in ? h : 0)) * W + (in ? w : 0)) * C;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) o.v[c] = (in && c < C) ? src[c] : (T)0.f;
+    reinterpret_cast<Vec<T, 4>*>(xp)[i] = o;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+stem_weight_k(const T* __restrict__ w, T* __restrict__ w2, int cout, int KH, int KW, int C) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // [cout][8][4][8]
+  if (i >= cout * 256) return;
+  const int n = i >> 8, kh = (i >> 5) & 7, j = (i >> 3) & 3, e = i & 7;
+  const int kw = 2 * j + (e >> 2), c = e & 3;
+  w2[i] = (kh < KH && kw < KW && c < C) ? w[((n * KH + kh) * KW + kw) * C + c] : (T)0.f;
+}
+
+// dw [cout][KH][KW][C] (fp32) += the pair-view weight gradient dw2
+__global__ void __launch_bounds__(256)
+stem_weight_grad_k(const float* __restrict__ dw2, float* __restrict__ dw, int cout, int KH,
+                   int KW, int C) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= cout * KH * KW * C) return;
+  const int c = i % C, kw = (i / C) % KW, kh = (i / (C * KW)) % KH, n = i / (C * KW * KH);
+  dw[i] += dw2[(((n * 8 + kh) * 4 + (kw >> 1)) * 8) + (kw & 1) * 4 + c];
+}
+
 }  // namespace kfb
 
 using namespace kfb;
+
+// x [N,H,W,C<=4] -> xp [N,Hp,Wp,4] (zero border: rows [pt, pt+H), cols [pl, pl+W))
+KFB_API hipError_t kfb_stem_pad(int dtype, const void* x, void* xp, int N, int H, int W, int C,
+                                int Hp, int Wp, int pt, int pl, hipStream_t stream) {
+  if (C > 4 || dtype == F32) return hipErrorInvalidValue;
+  const long npix = (long)N * Hp * Wp;
+  long blocks = (npix + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (dtype == BF16)
+    hipLaunchKernelGGL((stem_pad_k<bf16>), dim3((unsigned)blocks), dim3(256), 0, stream,
+                       (const bf16*)x, (bf16*)xp, npix, H, W, C, Hp, Wp, pt, pl);
+  else
+    hipLaunchKernelGGL((stem_pad_k<f16>), dim3((unsigned)blocks), dim3(256), 0, stream,
+                       (const f16*)x, (f16*)xp, npix, H, W, C, Hp, Wp, pt, pl);
+  return hipGetLastError();
+}
+
+// w [cout][KH][KW][C] -> w2 [cout][8][4][8] (KH <= 8, KW <= 8, C <= 4)
+KFB_API hipError_t kfb_stem_weight(int dtype, const void* w, void* w2, int cout, int KH, int KW,
+                                   int C, hipStream_t stream) {
+  if (KH > 8 || KW > 8 || C > 4 || dtype == F32) return hipErrorInvalidValue;
+  const int blocks = (cout * 256 + 255) / 256;
+  if (dtype == BF16)
+    hipLaunchKernelGGL((stem_weight_k<bf16>), dim3(blocks), dim3(256), 0, stream, (const bf16*)w,
+                       (bf16*)w2, cout, KH, KW, C);
+  else
+    hipLaunchKernelGGL((stem_weight_k<f16>), dim3(blocks), dim3(256), 0, stream, (const f16*)w,
+                       (f16*)w2, cout, KH, KW, C);
+  return hipGetLastError();
+}
+
+KFB_API hipError_t kfb_stem_weight_grad(const float* dw2, float* dw, int cout, int KH, int KW,
+                                        int C, hipStream_t stream) {
+  const int n = cout * KH * KW * C;
+  hipLaunchKernelGGL(stem_weight_grad_k, dim3((n + 255) / 256), dim3(256), 0, stream, dw2, dw,
+                     cout, KH, KW, C);
+  return hipGetLastError();
+}
 
 // x [N,H,W,C] (C <= 4) -> x2 [N,OH,OW2,64]; requires KH <= 8.
 KFB_API hipError_t kfb_s2d_stem(int dtype, const void* x, void* x2, int N, int H, int W, int C,

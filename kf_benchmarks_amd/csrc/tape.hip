@@ -1,0 +1,245 @@
+// Launch tape: the native step executor.
+//
+// The reference runs a training step as ONE call into TF's C++ executor
+// (sess.run, tcb/benchmark_cnn.py:821).  Here a step is ~450 kernel launches
+// whose host-side preparation (autograd, shape logic, epilogue wiring,
+// autotune lookups) costs ~20 us each in Python - a ~10 ms/step host floor.
+// A tape removes that floor without HIP graphs (whose replay executes the
+// nodes of a two-stream step one after another on this stack: 27.9 vs 19.8
+// ms/step for ResNet-50 bs256, profiles/r6_graph_env_probe.txt):
+//
+//   record  one eager step runs normally while every native entry point it
+//           calls (kernels, memsets, cross-stream waits) is appended to the
+//           tape with its raw arguments (device pointers, shapes, streams);
+//   replay  kfb_tape_replay re-issues the recorded calls in order from C++,
+//           patching the few per-step scalars (learning rate, RNG seeds)
+//           first.  Each call is the same KFB_API function the eager path
+//           calls, so kernels, launch shapes and stream assignment (compute
+//           stream + weight-gradient side stream, joined by events) are
+//           identical and the two streams stay concurrent.
+//
+// Memory: the recording step allocates from a private pool that nothing
+// else allocates from afterwards (ops/tape.py), so every recorded address
+// stays valid and owned by the tape.
+//
+// Calls are made through libffi (the library ctypes itself uses, loaded at
+// run time): argument type codes come from the Python-side signature table.
+#include "common.h"
+
+#include <dlfcn.h>
+
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace kfb {
+namespace tape {
+
+// ---- minimal libffi ABI (libffi >= 3.3, x86-64 SysV) -----------------------
+struct ffi_type_t {
+  size_t size;
+  unsigned short alignment;
+  unsigned short type;
+  ffi_type_t** elements;
+};
+constexpr int FFI_UNIX64 = 2;
+// ffi_cif is { abi, nargs, arg_types, rtype, bytes, flags } on x86-64; the
+// buffer is over-sized so a longer layout cannot overflow it.
+struct alignas(16) Cif {
+  unsigned char raw[128];
+};
+typedef int (*prep_cif_fn)(void*, int, unsigned, ffi_type_t*, ffi_type_t**);
+typedef void (*call_fn)(void*, void (*)(void), void*, void**);
+
+struct Ffi {
+  bool ok = false;
+  prep_cif_fn prep = nullptr;
+  call_fn call = nullptr;
+  ffi_type_t *t_sint32 = nullptr, *t_uint32 = nullptr, *t_sint64 = nullptr, *t_ptr = nullptr,
+             *t_float = nullptr, *t_uint64 = nullptr;
+};
+
+static Ffi& ffi() {
+  static Ffi f;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("libffi.so.8", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("libffi.so.7", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("libffi.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return;
+    f.prep = (prep_cif_fn)dlsym(h, "ffi_prep_cif");
+    f.call = (call_fn)dlsym(h, "ffi_call");
+    f.t_sint32 = (ffi_type_t*)dlsym(h, "ffi_type_sint32");
+    f.t_uint32 = (ffi_type_t*)dlsym(h, "ffi_type_uint32");
+    f.t_sint64 = (ffi_type_t*)dlsym(h, "ffi_type_sint64");
+    f.t_uint64 = (ffi_type_t*)dlsym(h, "ffi_type_uint64");
+    f.t_ptr = (ffi_type_t*)dlsym(h, "ffi_type_pointer");
+    f.t_float = (ffi_type_t*)dlsym(h, "ffi_type_float");
+    f.ok = f.prep && f.call && f.t_sint32 && f.t_uint32 && f.t_sint64 && f.t_uint64 && f.t_ptr &&
+           f.t_float;
+  });
+  return f;
+}
+
+// One signature (type string -> prepared call interface), shared by every op
+// with that signature.  Type codes: i int32, u uint32, l int64, q uint64 /
+// size_t, p pointer, f float.
+struct Sig {
+  Cif cif;
+  std::vector<ffi_type_t*> types;
+};
+
+struct Op {
+  void (*fn)(void);
+  const Sig* sig;
+  std::vector<uint64_t> slots;  // one 64-bit slot per argument (value in the low bytes)
+  std::vector<void*> argp;      // ffi avalue: &slots[k]
+};
+
+struct Tape {
+  std::vector<Op> ops;
+  std::unordered_map<std::string, Sig*> sigs;
+  ~Tape() {
+    for (auto& kv : sigs) delete kv.second;
+  }
+};
+
+static ffi_type_t* type_of(char c) {
+  Ffi& f = ffi();
+  switch (c) {
+    case 'i': return f.t_sint32;
+    case 'u': return f.t_uint32;
+    case 'l': return f.t_sint64;
+    case 'q': return f.t_uint64;
+    case 'p': return f.t_ptr;
+    case 'f': return f.t_float;
+    default: return nullptr;
+  }
+}
+
+static const Sig* get_sig(Tape* t, const char* types) {
+  auto it = t->sigs.find(types);
+  if (it != t->sigs.end()) return it->second;
+  Sig* s = new Sig();
+  const int n = (int)strlen(types);
+  for (int k = 0; k < n; ++k) {
+    ffi_type_t* ty = type_of(types[k]);
+    if (!ty) {
+      delete s;
+      return nullptr;
+    }
+    s->types.push_back(ty);
+  }
+  memset(&s->cif, 0, sizeof(s->cif));
+  if (ffi().prep(&s->cif, FFI_UNIX64, (unsigned)n, ffi().t_sint32, s->types.data()) != 0) {
+    delete s;
+    return nullptr;
+  }
+  t->sigs.emplace(types, s);
+  return s;
+}
+
+}  // namespace tape
+}  // namespace kfb
+
+using namespace kfb::tape;
+
+KFB_API int kfb_tape_available() { return ffi().ok ? 1 : 0; }
+
+KFB_API void* kfb_tape_new() {
+  if (!ffi().ok) return nullptr;
+  return new Tape();
+}
+
+KFB_API void kfb_tape_free(void* h) { delete (Tape*)h; }
+
+KFB_API int kfb_tape_size(void* h) { return h ? (int)((Tape*)h)->ops.size() : 0; }
+
+// Appends fn(args...) with ``types`` (one code per argument) and the raw
+// 64-bit argument slots; returns the op index or -1.
+KFB_API int kfb_tape_add(void* h, void* fn, const char* types, const uint64_t* slots, int n) {
+  Tape* t = (Tape*)h;
+  if (!t || !fn || (int)strlen(types) != n) return -1;
+  const Sig* s = get_sig(t, types);
+  if (!s) return -1;
+  t->ops.emplace_back();
+  Op& op = t->ops.back();
+  op.fn = (void (*)(void))fn;
+  op.sig = s;
+  op.slots.assign(slots, slots + n);
+  return (int)t->ops.size() - 1;
+}
+
+// Overwrites argument ``arg`` of op ``op`` (a per-step scalar).
+KFB_API int kfb_tape_patch(void* h, int op, int arg, uint64_t value) {
+  Tape* t = (Tape*)h;
+  if (!t || op < 0 || op >= (int)t->ops.size() || arg < 0 ||
+      arg >= (int)t->ops[op].slots.size())
+    return -1;
+  t->ops[op].slots[arg] = value;
+  return 0;
+}
+
+// Re-issues every recorded call in order: patches first (npatch triples
+// op/arg/value), then the calls.  Returns 0, or the first non-zero return
+// code; *failed_op receives its index.
+KFB_API int kfb_tape_replay(void* h, const int* pop, const int* parg, const uint64_t* pval,
+                            int npatch, int* failed_op) {
+  Tape* t = (Tape*)h;
+  if (!t) return -1;
+  for (int k = 0; k < npatch; ++k)
+    if (kfb_tape_patch(h, pop[k], parg[k], pval[k]) != 0) return -2;
+  call_fn call = ffi().call;
+  for (size_t i = 0; i < t->ops.size(); ++i) {
+    Op& op = t->ops[i];
+    if (op.argp.size() != op.slots.size()) {
+      op.argp.resize(op.slots.size());
+      for (size_t k = 0; k < op.slots.size(); ++k) op.argp[k] = &op.slots[k];
+    }
+    int64_t rc = 0;  // ffi widens an int return to a full register
+    call((void*)&op.sig->cif, op.fn, &rc, op.argp.data());
+    if ((int)rc != 0) {
+      if (failed_op) *failed_op = (int)i;
+      return (int)rc;
+    }
+  }
+  return 0;
+}
+
+// ---- recordable stream-ordering and memory primitives ----------------------
+// (the eager path uses them too, so a recorded step orders its streams with
+// exactly the calls the tape replays)
+
+KFB_API hipError_t kfb_event_create(hipEvent_t* ev) {
+  return hipEventCreateWithFlags(ev, hipEventDisableTiming);
+}
+
+KFB_API hipError_t kfb_event_destroy(hipEvent_t ev) { return hipEventDestroy(ev); }
+
+// dst waits for everything enqueued on src so far (ev: scratch event).
+KFB_API hipError_t kfb_stream_wait(hipStream_t dst, hipStream_t src, hipEvent_t ev) {
+  hipError_t e = hipEventRecord(ev, src);
+  if (e != hipSuccess) return e;
+  return hipStreamWaitEvent(dst, ev, 0);
+}
+
+KFB_API hipError_t kfb_memset(void* p, int byte, size_t bytes, hipStream_t s) {
+  return hipMemsetAsync(p, byte, bytes, s);
+}
+
+KFB_API hipError_t kfb_memcpy_d2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s);
+}
+
+// ---- host-side self test (no GPU): records calls of a probe function with
+// every argument type and replays them with a patch
+static uint64_t g_probe_sum = 0;
+KFB_API int kfb_tape_probe(int a, float b, long c, void* d, unsigned e, int f, float g, long h,
+                           int i, int j, float k) {
+  g_probe_sum += (uint64_t)(a + (long)(b * 4) + c + (long)(uintptr_t)d + e + f + (long)(g * 4) +
+                            h + i + j + (long)(k * 4));
+  return a == -7 ? 5 : 0;  // a == -7: report an error
+}
+KFB_API uint64_t kfb_tape_probe_sum() { return g_probe_sum; }

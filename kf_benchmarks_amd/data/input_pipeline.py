@@ -40,6 +40,16 @@ class SyntheticInput:
                 "input", self.bench.dataset.num_classes, self.bench.device, self.seed + self.step))
         return self.inputs
 
+    # launch tape: a replayed step re-samples the batch with the seeds an
+    # eager step would use
+    def tape_advance(self):
+        if self.resample:
+            self.step += 1
+
+    def tape_values(self):
+        s = self.seed + self.step
+        return {"input_seed": s & 0xFFFFFFFF, "input_seed_labels": (s + 1) & 0xFFFFFFFF}
+
     def close(self):
         pass
 

@@ -409,8 +409,8 @@ class ConvNetBuilder:
         if input_layer is not None:
             self.top_size = None
         self.counts["dropout"] += 1
-        seed = self.net.next_dropout_seed()
-        self.top_layer = F.dropout(x, keep_prob, self.phase_train and not self.meta, seed)
+        seed, key = self.net.next_dropout_seed(with_key=True)
+        self.top_layer = F.dropout(x, keep_prob, self.phase_train and not self.meta, seed, key)
         return self.top_layer
 
     def batch_norm(self, input_layer=None, decay=0.999, scale=False, epsilon=0.001, relu=False,

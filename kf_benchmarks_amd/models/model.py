@@ -211,9 +211,27 @@ class Network(nn.Module):
         self.scopes.append(scope)
         return layer
 
-    def next_dropout_seed(self) -> int:
+    def next_dropout_seed(self, with_key=False):
         self._dropout_seed = (self._dropout_seed * 1103515245 + 12345) & 0x7FFFFFFF
-        return self._dropout_seed
+        if not with_key:
+            return self._dropout_seed
+        # launch tape: the k-th dropout of the recorded step is the per-step
+        # argument "dropout<k>" (tape_dropout_values re-derives them)
+        k = getattr(self, "_dropout_calls", 0)
+        self._dropout_calls = k + 1
+        return self._dropout_seed, "dropout%d" % k
+
+    def tape_begin_recording(self):
+        self._dropout_calls = 0
+
+    def tape_dropout_values(self):
+        """The dropout seeds of the next replayed step: the generator
+        advanced exactly as an eager step advances it."""
+        out = {}
+        for k in range(getattr(self, "_dropout_calls", 0)):
+            self._dropout_seed = (self._dropout_seed * 1103515245 + 12345) & 0x7FFFFFFF
+            out["dropout%d" % k] = self._dropout_seed & 0xFFFFFFFF
+        return out
 
     def materialize(self):
         shape = self.model.get_input_shapes("train")[0]

@@ -42,11 +42,24 @@ _SIGS = {
     "kfb_bn_bwd": [I, P, P, P, P, P, L, I, P, P, P, P, P, P, P, I, P, P, P, I, I, I, P],
     "kfb_opt_step": [I, P, P, P, P, P, I, P, L, F, F, F, F, F, F, F, F, F, I, P, F, F, P, P, P],
     "kfb_seqlock_check": [P, ctypes.c_longlong, P, P, P],
+    "kfb_event_create": [P],
+    "kfb_event_destroy": [P],
+    "kfb_stream_wait": [P, P, P],
+    "kfb_memset": [P, I, ctypes.c_size_t, P],
+    "kfb_memcpy_d2d": [P, P, ctypes.c_size_t, P],
+    "kfb_tape_available": [],
+    "kfb_tape_new": [],
+    "kfb_tape_free": [P],
+    "kfb_tape_size": [P],
+    "kfb_tape_add": [P, P, ctypes.c_char_p, P, I],
+    "kfb_tape_patch": [P, I, I, ctypes.c_uint64],
+    "kfb_tape_replay": [P, P, P, P, I, P],
     "kfb_host_register": [P, ctypes.c_size_t, P],
     "kfb_host_unregister": [P],
     "kfb_nonfinite": [P, L, P, P],
     "kfb_half_sumsq": [P, L, P, P],
     "kfb_cast_f32": [P, P, I, L, P],
+    "kfb_cast_to_f32": [P, I, P, L, P],
     "kfb_xent_fwd": [I, P, P, L, I, P, P, P],
     "kfb_xent_bwd": [I, P, P, P, P, F, L, I, P, P],
     "kfb_in_top_k": [I, P, P, L, I, P, P, P],
@@ -83,7 +96,8 @@ _SIGS = {
     "kfb_slab_colsum": [P, I, I, P, I, P],
 }
 _RESTYPES = {"kfb_bn_num_slabs": c_int, "kfb_colsum_num_slabs": c_int,
-             "kfb_gemm_splits": c_int, "kfb_ctc_max_states": c_int}
+             "kfb_gemm_splits": c_int, "kfb_ctc_max_states": c_int, "kfb_tape_new": c_void_p,
+             "kfb_tape_free": None}
 # Optional symbols (added by later kernel files); bound if present.
 _OPTIONAL = {}
 
@@ -139,12 +153,37 @@ def register_optional(name, argtypes, restype=c_int):
 
 _FN = {}
 
+# The launch tape being recorded (ops/tape.py), or None.  While set, every
+# call() is appended to it (and still executed).
+_TAPE = None
+
+
+class Dyn:
+    """A per-step argument of a recorded call (learning rate, RNG seed): the
+    tape patches it with the value for ``key`` at every replay."""
+    __slots__ = ("key", "value")
+
+    def __init__(self, key, value):
+        self.key, self.value = key, value
+
+
+def dyn(key, value):
+    """``value``, marked as the per-step scalar ``key`` while a tape is being
+    recorded (a plain value otherwise)."""
+    return Dyn(key, value) if _TAPE is not None else value
+
+
+def recording() -> bool:
+    return _TAPE is not None
+
 
 def call(name, *args):
     """Calls a kernel entry point and raises on a non-zero hipError_t."""
     fn = _FN.get(name)
     if fn is None:
         fn = _FN[name] = getattr(load(), name)
+    if _TAPE is not None:
+        args = _TAPE.add(name, fn, args)
     err = fn(*args)
     if err != 0:
         raise NativeError("%s failed with hipError %d" % (name, err))
@@ -186,3 +225,34 @@ def stream(device=None) -> int:
 
 def loaded_path():
     return lib_path() if _LIB is not None else None
+
+
+# ------------------------------------------------- stream ordering / memory
+_EVENTS = {}
+
+
+def _pair_event(dst, src):
+    key = (dst, src)
+    ev = _EVENTS.get(key)
+    if ev is None:
+        h = ctypes.c_void_p()
+        err = load().kfb_event_create(ctypes.byref(h))
+        if err != 0:
+            raise NativeError("kfb_event_create failed with hipError %d" % err)
+        ev = _EVENTS[key] = h.value
+    return ev
+
+
+def stream_wait(dst_stream: int, src_stream: int):
+    """``dst`` waits for the work enqueued on ``src`` so far (raw hipStream_t
+    handles) - the recordable form of torch's Stream.wait_stream."""
+    if dst_stream == src_stream:
+        return
+    call("kfb_stream_wait", dst_stream, src_stream, _pair_event(dst_stream, src_stream))
+
+
+def zero_(t: torch.Tensor):
+    """Recordable zero fill of a contiguous device tensor."""
+    if t.numel():
+        call("kfb_memset", t.data_ptr(), 0, t.numel() * t.element_size(), stream(t.device))
+    return t

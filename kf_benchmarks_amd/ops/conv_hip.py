@@ -112,8 +112,11 @@ class _StatsArena:
         if buf is None or buf.numel() < need:
             self.buf[key] = buf = torch.zeros((max(need, 1 << 16),), dtype=torch.float32,
                                               device=device)
+        elif buf.is_cuda:
+            # only the part handed out last step can be dirty (native memset:
+            # part of a recorded launch tape)
+            N.zero_(buf[:min(self.off.get(key, buf.numel()), buf.numel())])
         else:
-            # only the part handed out last step can be dirty
             buf[:min(self.off.get(key, buf.numel()), buf.numel())].zero_()
         self.off[key] = 0
 
@@ -428,7 +431,7 @@ def join_wgrad_stream(device=None):
     cur = torch.cuda.current_stream(device)
     st = _SIDE_STREAMS.get(cur.device.index)
     if st is not None and st != cur:
-        cur.wait_stream(st)
+        N.stream_wait(cur.cuda_stream, st.cuda_stream)
 
 
 N.register_optional("kfb_s2d_stem", [N.I, N.P, N.P] + [N.I] * 9 + [N.P])
@@ -451,6 +454,35 @@ def use_s2d(x, wl_shape, stride, needs_dx, pads) -> bool:
     row_bytes = x.shape[2] * cin * x.element_size()
     return (x.shape[0] * OH * OW2 * 64 < (1 << 31) and row_bytes % 4 == 0
             and row_bytes <= 4096 and x.data_ptr() % 4 == 0)
+
+
+# "pairs": the stem as an 8x4-tap stride-(2,1) conv over a padded pixel-pair
+# view of the image (csrc/stem.hip); "s2d": a 64-channel space-to-depth repack
+_STEM_MODE = os.environ.get("KFB_STEM_MODE", "pairs")
+N.register_optional("kfb_stem_pad", [N.I, N.P, N.P] + [N.I] * 8 + [N.P])
+N.register_optional("kfb_stem_weight", [N.I, N.P, N.P] + [N.I] * 4 + [N.P])
+N.register_optional("kfb_stem_weight_grad", [N.P, N.P] + [N.I] * 4 + [N.P])
+
+
+def stem_pairs_input(x, wl_shape, pads):
+    """x [N,H,W,C<=4] -> the padded pair view [N, Hp, Wp/2, 8] (csrc/stem.hip)."""
+    n, H, W, cin = x.shape
+    OH, OW, _, _ = s2d_geometry(x.shape, wl_shape, pads)
+    Hp = 2 * (OH - 1) + 8  # 8 tap rows at stride 2
+    Wp = 2 * (OW + 3)      # 4 pair taps at stride 1
+    xp = torch.empty((n, Hp, Wp // 2, 8), dtype=x.dtype, device=x.device)
+    N.call("kfb_stem_pad", N.dt(x), x.data_ptr(), xp.data_ptr(), n, H, W, cin, Hp, Wp,
+           pads[0], pads[2], N.stream(x.device))
+    return xp
+
+
+def stem_pairs_weight(wl):
+    """[Cout,KH,KW,C] -> [Cout,8,4,8] (w2[n][kh][j][t*4+c] = w[n][kh][2j+t][c])."""
+    cout, KH, KW, cin = wl.shape
+    w2 = torch.empty((cout, 8, 4, 8), dtype=wl.dtype, device=wl.device)
+    N.call("kfb_stem_weight", N.dt(wl), wl.data_ptr(), w2.data_ptr(), cout, KH, KW, cin,
+           N.stream(wl.device))
+    return w2
 
 
 def s2d_geometry(x_shape, wl_shape, pads):
@@ -506,6 +538,17 @@ class _Conv2d(torch.autograd.Function):
         ctx.out_link = None
         ctx.relu, ctx.bias = bool(relu), bias
         bd = bias.detach() if bias is not None else None
+        if use_s2d(x, wl.shape, stride, ctx.needs_input_grad[0], pads) and \
+                _STEM_MODE == "pairs" and wl.shape[2] <= 8 and x.dtype != torch.float32 \
+                and hasattr(N.load(), "kfb_stem_pad"):
+            xv = stem_pairs_input(x, wl.shape, pads)
+            w2 = stem_pairs_weight(wl.contiguous())
+            y = conv_fwd(xv, w2, (2, 1), (0, 0, 0, 0), stats, bd, relu)
+            ctx.save_for_backward(xv, w2, y if relu else None)
+            ctx.s2d = ("pairs",) + tuple(wl.shape)
+            ctx.w = w
+            _Conv2d._act_link(ctx, y, cout % 8 == 0)
+            return y
         if use_s2d(x, wl.shape, stride, ctx.needs_input_grad[0], pads):
             x2 = s2d_input(x, wl.shape, pads)
             w2 = s2d_weight(wl).contiguous()
@@ -642,7 +685,7 @@ class _Conv2d(torch.autograd.Function):
                 # (backward of the small-grid stage-4/5 layers under-fills
                 # the chip).  Its inputs are kept alive for the side stream;
                 # gradient consumers join it (join_wgrad_stream).
-                side.wait_stream(torch.cuda.current_stream(dy.device))
+                N.stream_wait(side.cuda_stream, N.stream(dy.device))
                 _queue_join(dy.device)
                 with torch.cuda.stream(side):
                     conv_wgrad(dy, xp, wp.shape, stride, pads, out=sink)
@@ -664,7 +707,32 @@ class _Conv2d(torch.autograd.Function):
 
 
     @staticmethod
+    def _backward_pairs(ctx, dy):
+        xv, w2 = ctx.saved_tensors[:2]
+        _, cout, KH, KW, cin = ctx.s2d
+        if not ctx.needs_input_grad[1]:
+            return None, None, None, None, None, None, None
+        w = ctx.w
+        sink = getattr(w, "_kfb_grad_sink", None)
+        direct = sink is not None and _fuse_enabled()
+        dw = sink if direct else torch.zeros((cout, KH, KW, cin), dtype=torch.float32,
+                                             device=dy.device)
+        scratch = torch.empty((cout, 8, 4, 8), dtype=torch.float32, device=dy.device)
+        N.zero_(scratch)
+        conv_wgrad(dy.contiguous(), xv, w2.shape, (2, 1), (0, 0, 0, 0), out=scratch)
+        N.call("kfb_stem_weight_grad", scratch.data_ptr(), dw.data_ptr(), cout, KH, KW, cin,
+               N.stream(dy.device))
+        if direct:
+            cb = getattr(w, "_kfb_ready_cb", None)
+            if cb is not None:
+                cb(w)
+            dw = None
+        return None, dw, None, None, None, None, None
+
+    @staticmethod
     def _backward_s2d(ctx, dy):
+        if ctx.s2d[0] == "pairs":
+            return _Conv2d._backward_pairs(ctx, dy)
         x2, w2 = ctx.saved_tensors[:2]
         dw = None
         if ctx.needs_input_grad[1]:

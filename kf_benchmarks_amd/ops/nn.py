@@ -161,12 +161,20 @@ class BNLink:
             self.pending_sparse = sparse
         else:
             self.take_pending_stream()
-            self.pending, self.pending_owned = self.pending + g, True
+            if g.is_cuda and g.is_contiguous() and self.pending.is_contiguous() \
+                    and g.dtype == self.pending.dtype and g.shape == self.pending.shape:
+                y = torch.empty_like(g)
+                N.call("kfb_add", N.dt(g), self.pending.data_ptr(), g.data_ptr(), y.data_ptr(),
+                       g.numel(), 0, N.stream(g.device))
+                self.pending = y
+            else:
+                self.pending = self.pending + g
+            self.pending_owned = True
             if sparse != self.pending_sparse:
                 self.pending_sparse = None
         if g.is_cuda:
-            self.pending_event = torch.cuda.Event()
-            self.pending_event.record()
+            # the stream that produced it (a recordable wait replaces an event)
+            self.pending_event = N.stream(g.device)
 
     def accumulated(self, g, sparse=None):
         """A contributor computed ``g`` = its gradient + ``pending`` (the
@@ -175,16 +183,16 @@ class BNLink:
             sparse = None
         self.pending, self.pending_owned, self.pending_sparse = g, True, sparse
         if g.is_cuda:
-            self.pending_event = torch.cuda.Event()
-            self.pending_event.record()
+            self.pending_event = N.stream(g.device)
 
     def take_pending_stream(self):
         """Makes the current stream wait for the pending gradient (written
         on whatever stream its contributors ran on) before using it."""
         if self.pending is not None and self.pending_event is not None:
-            cur = torch.cuda.current_stream(self.pending.device)
-            cur.wait_event(self.pending_event)
-            self.pending.record_stream(cur)
+            cur = N.stream(self.pending.device)
+            if cur != self.pending_event:
+                N.stream_wait(cur, self.pending_event)
+                self.pending.record_stream(torch.cuda.current_stream(self.pending.device))
             self.pending_event = None
 
 
@@ -893,29 +901,32 @@ def linear(x, w, b, w_lp=None, relu=False):
 # --------------------------------------------------------------------- dropout
 class _Dropout(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, keep, seed):
+    def forward(ctx, x, keep, seed, key):
         x = x.contiguous()
         y = torch.empty_like(x)
         N.call("kfb_dropout", N.dt(x), x.data_ptr(), y.data_ptr(), x.numel(), float(keep),
-               int(seed) & 0xFFFFFFFF, N.stream(x.device))
-        ctx.keep, ctx.seed = keep, seed
+               N.dyn(key, int(seed) & 0xFFFFFFFF) if key else int(seed) & 0xFFFFFFFF,
+               N.stream(x.device))
+        ctx.keep, ctx.seed, ctx.key = keep, seed, key
         return y
 
     @staticmethod
     def backward(ctx, dy):
         dy = dy.contiguous()
         dx = torch.empty_like(dy)
+        seed = int(ctx.seed) & 0xFFFFFFFF
         N.call("kfb_dropout", N.dt(dy), dy.data_ptr(), dx.data_ptr(), dy.numel(),
-               float(ctx.keep), int(ctx.seed) & 0xFFFFFFFF, N.stream(dy.device))
-        return dx, None, None
+               float(ctx.keep), N.dyn(ctx.key, seed) if ctx.key else seed, N.stream(dy.device))
+        return dx, None, None, None
 
 
-def dropout(x, keep_prob: float, training: bool, seed: int):
+def dropout(x, keep_prob: float, training: bool, seed: int, key=None):
+    """``key``: name of the seed as a per-step launch-tape argument."""
     if not training or keep_prob >= 1.0:
         return x
     if not _on_gpu(x):
         return F.dropout(x, p=1.0 - keep_prob, training=True)
-    return _Dropout.apply(x, keep_prob, seed)
+    return _Dropout.apply(x, keep_prob, seed, key)
 
 
 # ------------------------------------------------------------------------- LRN
@@ -1140,7 +1151,7 @@ def synthetic_images(shape, dtype, device, seed: int, mean=127.0, std=60.0):
         return x.to(dtype)
     x = torch.empty(shape, dtype=dtype, device=device)
     N.call("kfb_synthetic_images", N.dt(x), x.data_ptr(), x.numel(), float(mean), float(std),
-           seed & 0xFFFFFFFF, N.stream(x.device))
+           N.dyn("input_seed", seed & 0xFFFFFFFF), N.stream(x.device))
     return x
 
 
@@ -1151,8 +1162,8 @@ def synthetic_labels(n, nclass, device, seed: int):
         g = torch.Generator().manual_seed(seed + 1)
         return torch.randint(0, maxval, (n,), generator=g, dtype=torch.int32)
     y = torch.empty((n,), dtype=torch.int32, device=device)
-    N.call("kfb_synthetic_labels", y.data_ptr(), n, maxval, (seed + 1) & 0xFFFFFFFF,
-           N.stream(device))
+    N.call("kfb_synthetic_labels", y.data_ptr(), n, maxval,
+           N.dyn("input_seed_labels", (seed + 1) & 0xFFFFFFFF), N.stream(device))
     return y
 
 

@@ -1,0 +1,236 @@
+"""Recording and replaying a training step as a launch tape (csrc/tape.hip).
+
+The reference executes a step as one call into TF's C++ executor
+(tcb/benchmark_cnn.py:821, ``sess.run(fetches)``); eager PyTorch spends
+~20 us of Python per kernel launch instead.  A :class:`StepTape` records
+one eager step - every native call it makes, with its raw arguments - and
+replays it from C++ afterwards, so a step costs one Python call.
+
+What makes a recorded step replayable:
+
+* every GPU operation of the step goes through :func:`_native.call`
+  (kernels, zero fills :func:`_native.zero_`, cross-stream waits
+  :func:`_native.stream_wait`); a torch kernel inside the step would be
+  silently skipped at replay, so :meth:`StepTape.record` checks with the
+  profiler-free counter below that no torch op ran on the device;
+* the step allocates from a private memory pool that nothing else allocates
+  from afterwards, so every recorded address stays owned by the tape;
+  tensors handed to another stream (``record_stream``) are held until the
+  step ends, so no address is reused within the step across streams;
+* per-step scalars are passed as :func:`_native.dyn` values (learning rate,
+  RNG seeds) and patched at every replay.
+
+Used by ``BenchmarkCNN.train_step`` under ``--launch_tape`` (single-process
+runs and runs whose gradient collectives are native calls).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import struct
+from typing import Callable, Dict, List, Optional, Tuple
+
+import torch
+
+from . import _native as N
+
+_CODE = {ctypes.c_int: "i", ctypes.c_uint32: "u", ctypes.c_long: "l", ctypes.c_longlong: "l",
+         ctypes.c_size_t: "q", ctypes.c_uint64: "q", ctypes.c_void_p: "p", ctypes.c_char_p: "p",
+         ctypes.c_float: "f"}
+_MASK = (1 << 64) - 1
+
+
+class TapeError(RuntimeError):
+    pass
+
+
+def _pack(v, code):
+    if isinstance(v, ctypes._SimpleCData):
+        v = v.value
+    if code == "f":
+        return struct.unpack("<I", struct.pack("<f", float(v)))[0]
+    if code == "p":
+        if v is None:
+            return 0
+        if isinstance(v, int):
+            return v & _MASK
+        raise TapeError("pointer argument %r cannot be recorded" % (v,))
+    return int(v) & _MASK
+
+
+class Recorder:
+    """One native launch tape: ``add`` appends calls, ``replay`` re-issues them."""
+
+    def __init__(self):
+        lib = N.load()
+        if not lib.kfb_tape_available():
+            raise TapeError("launch tape unavailable (libffi not loadable)")
+        self.h = lib.kfb_tape_new()
+        self.dyn: List[Tuple[int, int, str, str]] = []  # (op, arg, key, code)
+        self._codes = {}
+        self.names: List[str] = []
+
+    def _types(self, name, fn):
+        t = self._codes.get(name)
+        if t is None:
+            try:
+                t = "".join(_CODE[a] for a in fn.argtypes)
+            except KeyError as e:
+                raise TapeError("%s: argument type %s cannot be recorded" % (name, e))
+            self._codes[name] = t
+        return t
+
+    def add(self, name, fn, args):
+        types = self._types(name, fn)
+        if len(args) != len(types):
+            raise TapeError("%s: %d args for %d types" % (name, len(args), len(types)))
+        slots = (ctypes.c_uint64 * max(len(args), 1))()
+        out = list(args)
+        op = len(self.names)
+        dyn = []
+        for k, (a, c) in enumerate(zip(args, types)):
+            if isinstance(a, N.Dyn):
+                dyn.append((op, k, a.key, c))
+                a = out[k] = a.value
+            slots[k] = _pack(a, c)
+        fp = ctypes.cast(fn, ctypes.c_void_p).value
+        got = N.load().kfb_tape_add(self.h, fp, types.encode(), slots, len(args))
+        if got != op:
+            raise TapeError("kfb_tape_add(%s) failed" % name)
+        self.names.append(name)
+        self.dyn.extend(dyn)
+        return out
+
+    def keys(self):
+        return sorted({k for _, _, k, _ in self.dyn})
+
+    def replay(self, values: Dict[str, float]):
+        n = len(self.dyn)
+        if n:
+            po = (ctypes.c_int * n)()
+            pa = (ctypes.c_int * n)()
+            pv = (ctypes.c_uint64 * n)()
+            for i, (op, arg, key, code) in enumerate(self.dyn):
+                if key not in values:
+                    raise TapeError("no value for per-step argument %r" % key)
+                po[i], pa[i], pv[i] = op, arg, _pack(values[key], code)
+        else:
+            po = pa = pv = None
+        bad = ctypes.c_int(-1)
+        rc = N.load().kfb_tape_replay(self.h, po, pa, pv, n, ctypes.byref(bad))
+        if rc != 0:
+            name = self.names[bad.value] if 0 <= bad.value < len(self.names) else "?"
+            raise TapeError("tape replay failed at op %d (%s): error %d" % (bad.value, name, rc))
+
+    def __len__(self):
+        return len(self.names)
+
+    def close(self):
+        if self.h:
+            N.load().kfb_tape_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
+class _TorchKernelProbe:
+    """Counts torch device work launched while recording (a torch op inside
+    the step would be missing from the tape): wraps the dispatcher with a
+    TorchDispatchMode that flags every op producing or mutating a CUDA
+    tensor, except allocation/view ops, which launch nothing."""
+
+    _HOST_ONLY = {"empty", "empty_strided", "empty_like", "view", "_unsafe_view", "reshape",
+                  "as_strided", "slice", "select", "detach", "alias", "t", "transpose",
+                  "permute", "expand", "unsqueeze", "squeeze", "split", "split_with_sizes",
+                  "narrow", "_reshape_alias", "lift_fresh", "unbind", "chunk",
+                  "tensor_split", "view_as", "_to_copy_noop", "set_", "resize_",
+                  "new_empty", "new_empty_strided", "clone_noop", "is_same_size", "sym_size",
+                  "sym_stride", "sym_numel", "sym_storage_offset"}
+
+    def __init__(self):
+        from torch.utils._python_dispatch import TorchDispatchMode
+        probe = self
+
+        class Mode(TorchDispatchMode):
+            def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+                name = func.__name__.split(".")[0]
+                out = func(*args, **(kwargs or {}))
+                if name not in probe._HOST_ONLY:
+                    flat = [out] if isinstance(out, torch.Tensor) else (
+                        list(out) if isinstance(out, (tuple, list)) else [])
+                    flat += [a for a in args if isinstance(a, torch.Tensor)]
+                    if any(isinstance(t, torch.Tensor) and t.is_cuda for t in flat):
+                        probe.ops.append(name)
+                return out
+
+        self.mode = Mode()
+        self.ops: List[str] = []
+
+
+class StepTape:
+    """A recorded training step for one device (see module docstring)."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.recorder: Optional[Recorder] = None
+        self.pool = None
+        self.outputs = None
+        self.replays = 0
+
+    @property
+    def ready(self) -> bool:
+        return self.recorder is not None
+
+    def record(self, step: Callable[[], object], check_torch_ops: bool = True):
+        """Runs ``step()`` once eagerly while recording it; returns its result
+        (tensors in it stay valid and are rewritten by every replay)."""
+        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        torch.cuda.synchronize(self.device)
+        rec = Recorder()
+        self.pool = torch.cuda.MemPool()
+        keep = []
+        orig_rs = torch.Tensor.record_stream
+
+        def record_stream(t, s):
+            keep.append(t)  # no cross-stream reuse inside the recorded step
+            return orig_rs(t, s)
+
+        probe = _TorchKernelProbe() if check_torch_ops else None
+        torch._C._cuda_beginAllocateToPool(dev, self.pool.id)
+        torch.Tensor.record_stream = record_stream
+        N._TAPE = rec
+        try:
+            if probe is not None:
+                with probe.mode:
+                    out = step()
+            else:
+                out = step()
+        finally:
+            N._TAPE = None
+            torch.Tensor.record_stream = orig_rs
+            torch._C._cuda_endAllocateToPool(dev, self.pool.id)
+        torch.cuda.synchronize(self.device)
+        del keep
+        if probe is not None and probe.ops:
+            rec.close()
+            raise TapeError("torch device ops inside the recorded step (not replayable): %s"
+                            % sorted(set(probe.ops)))
+        self.recorder = rec
+        self.outputs = out
+        return out
+
+    def replay(self, values: Dict[str, float]):
+        self.recorder.replay(values)
+        self.replays += 1
+        return self.outputs
+
+    def close(self):
+        if self.recorder is not None:
+            self.recorder.close()
+            self.recorder = None
+        self.outputs = None
+        self.pool = None

@@ -125,7 +125,10 @@ class FlatParams:
             fn()
 
     def zero_grad(self):
-        self.grad.zero_()
+        if self.grad.is_cuda:
+            N.zero_(self.grad)  # a native call: part of a recorded launch tape
+        else:
+            self.grad.zero_()
 
     def segments(self):
         """[(name, param, offset, numel)] in flat order."""
@@ -196,9 +199,10 @@ class FusedOptimizer:
         if f.device.type == "cuda":
             N.call("kfb_opt_step", _KINDS[self.kind], w.data_ptr(), g.data_ptr(),
                    N.ptr(self.s1), N.ptr(self.s2), N.ptr(lp),
-                   N.dt(lp) if lp is not None else 0, None, f.numel, float(lr),
+                   N.dt(lp) if lp is not None else 0, None, f.numel, N.dyn("lr", float(lr)),
                    float(grad_scale), float(weight_decay), clipv, float(mom), float(b1),
-                   float(b2), float(eps), float(lr_t), int(self.nesterov), N.ptr(msrc),
+                   float(b2), float(eps), N.dyn("lr_t", float(lr_t)), int(self.nesterov),
+                   N.ptr(msrc),
                    float(ma), float(mb), N.ptr(mok), N.ptr(wout), N.stream(f.device))
             f.after_update()
             return
@@ -209,6 +213,16 @@ class FusedOptimizer:
         if wout is not None:
             wout.copy_(w)
         f.after_update()
+
+    def tape_values(self, lr: float):
+        """Per-step arguments of a replayed step's update (launch tape): the
+        step counter advances as step() advances it."""
+        self.t += 1
+        lr_t = 0.0
+        if self.kind == "adam":
+            b1, b2, _ = self.adam
+            lr_t = lr * math.sqrt(1 - b2 ** self.t) / (1 - b1 ** self.t)
+        return {"lr_t": lr_t}
 
     @torch.no_grad()
     def _step_torch(self, g, lr, grad_scale, wd, clip, mom, b1, b2, eps, lr_t):

@@ -178,12 +178,16 @@ class Hierarchical:
         gsize = max(1, min(gsize, world_size))
         self.rank, self.size, self.gsize = rank, world_size, gsize
         groups = [list(range(i, min(i + gsize, world_size))) for i in range(0, world_size, gsize)]
-        self.groups = [dist.new_group(g) for g in groups]  # collective: every rank, every group
+        # device tensors need RCCL subgroups even when the default group is
+        # the host-side gloo group of a native-communicator world
+        from . import comm as _comm
+        be = "nccl" if _comm.get_world().device_backend in ("rccl", "nccl") else None
+        self.groups = [dist.new_group(g, backend=be) for g in groups]  # collective: all ranks
         self.my = rank // gsize
         self.members = groups[self.my]
         self.leader = self.members[0]
         leaders = [g[0] for g in groups]
-        self.leaders = dist.new_group(leaders)
+        self.leaders = dist.new_group(leaders, backend=be)
         self.is_leader = rank == self.leader
 
     def launch(self, buf, op: str = "sum"):

@@ -38,6 +38,16 @@ import torch
 from . import allreduce, comm
 
 
+def _unwire(view, buf):
+    """The reduced low-precision wire slice back into the fp32 gradient."""
+    if view.is_cuda:
+        from ..ops import _native as N
+        N.call("kfb_cast_to_f32", buf.data_ptr(), N.dt(buf), view.data_ptr(), view.numel(),
+               N.stream(view.device))
+    else:
+        view.copy_(buf)
+
+
 class BucketReducer:
     def __init__(self, flat, bucket_mb: float = 25.0, wire_dtype: Optional[torch.dtype] = None,
                  overlap: bool = True, op: str = "sum", group=None, num_buckets: int = 0,
@@ -165,7 +175,8 @@ class BucketReducer:
             side = wgrad_stream(g.device)
             cur = torch.cuda.current_stream(g.device)
             if side is not None and side != cur:
-                side.wait_stream(cur)
+                from ..ops import _native as N
+                N.stream_wait(side.cuda_stream, cur.cuda_stream)  # recordable
                 ctx = torch.cuda.stream(side)
         if ctx is None:
             self._launch_on_current(b, g)
@@ -181,7 +192,12 @@ class BucketReducer:
             if self._wire[k] is None or self._wire[k].device != g.device:
                 self._wire[k] = torch.empty(g.numel(), dtype=self.wire_dtype, device=g.device)
             buf = self._wire[k][s:e]
-            buf.copy_(view)
+            if buf.is_cuda:  # native cast: recordable in a launch tape
+                from ..ops import _native as N
+                N.call("kfb_cast_f32", view.data_ptr(), buf.data_ptr(), N.dt(buf), view.numel(),
+                       N.stream(view.device))
+            else:
+                buf.copy_(view)
         else:
             buf = view
         if self.spec:
@@ -218,7 +234,7 @@ class BucketReducer:
                 for work in works:
                     work.wait()
                 if buf is not None and buf is not view:
-                    view.copy_(buf)
+                    _unwire(view, buf)
             g.copy_(self._stash[(self._relaxed_step - 1) % 2])
         self._relaxed_step += 1
         self._active = False
@@ -237,7 +253,7 @@ class BucketReducer:
             for work in works:
                 work.wait()
             if buf is not None and buf is not view:
-                view.copy_(buf)
+                _unwire(view, buf)
         if ev is not None:
             end = torch.cuda.Event(enable_timing=True)
             end.record()

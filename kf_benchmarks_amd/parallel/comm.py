@@ -31,6 +31,10 @@ class World:
         # KFB_FORCE_PG=1, so the 1-GPU run exercises the real RCCL path)
         self.has_pg = (size > 1) if has_pg is None else bool(has_pg)
         self.device_index = None  # the rank's GPU (select_device_index), cuda worlds only
+        # device collectives: the native RCCL communicator (parallel/rccl.py),
+        # else a torch NCCL group (device_group), else the default group
+        self.native = None
+        self.device_group = None
 
     @property
     def distributed(self) -> bool:
@@ -51,6 +55,9 @@ class World:
         all-reduce on the device, then a host wait."""
         if not self.has_pg:
             return
+        if self.native is not None and device is not None:
+            self.native.barrier()
+            return
         if self.backend == "nccl" and device is not None:
             t = torch.zeros(1, device=device)
             dist.all_reduce(t)
@@ -58,7 +65,20 @@ class World:
         else:
             dist.barrier()
 
+    @property
+    def device_backend(self) -> str:
+        """What device collectives run on: rccl (native communicator), nccl
+        (torch's ProcessGroupNCCL = RCCL), gloo (CPU tests) or none."""
+        if self.native is not None:
+            return "rccl"
+        if self.device_group is not None:
+            return "nccl"
+        return self.backend or "none"
+
     def shutdown(self):
+        if self.native is not None:
+            self.native.close()
+            self.native = None
         if self.initialized_here and dist.is_initialized():
             dist.destroy_process_group()
 
@@ -202,8 +222,11 @@ def init_world(device_type: str = "cuda", all_reduce_spec: Optional[str] = None,
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
     # KFB_DIST_BACKEND=gloo: ranks that share one GPU (RCCL refuses two ranks
     # on one device) - the 2-rank GPU rehearsal on a 1-GPU box
-    backend = os.environ.get("KFB_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
-    if backend == "nccl":
+    forced = os.environ.get("KFB_DIST_BACKEND")
+    backend = forced or ("nccl" if device_type == "cuda" else "gloo")
+    from . import rccl as _rccl
+    native = backend == "nccl" and not forced and _rccl.enabled() and _rccl.available()
+    if native or backend == "nccl":
         spec_env = {}
         if all_reduce_spec:
             from .allreduce import rccl_env_for_spec
@@ -216,6 +239,10 @@ def init_world(device_type: str = "cuda", all_reduce_spec: Optional[str] = None,
                                            torch.cuda.device_count())
     if backend == "nccl":
         _reserve_compute_streams(device_index)
+    if native:
+        # host-side traffic (object gathers, CPU barriers, the TCP store) on
+        # gloo; device collectives on the native communicator created below
+        backend = "gloo"
     if not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kwargs = dict(backend=backend, init_method="env://", rank=rank, world_size=size,
@@ -227,8 +254,18 @@ def init_world(device_type: str = "cuda", all_reduce_spec: Optional[str] = None,
                 kwargs["pg_options"] = opts
         dist.init_process_group(**kwargs)
         here = True
-    _WORLD = World(rank, size, local_rank, dist.get_backend(), here, has_pg=True)
-    _WORLD.device_index = device_index
+    world = World(rank, size, local_rank, dist.get_backend(), here, has_pg=True)
+    world.device_index = device_index
+    if native:
+        try:
+            store = dist.distributed_c10d._get_default_store()
+            world.native = _rccl.NativeComm(rank, size, device_index, store)
+        except Exception as e:  # noqa: BLE001 - fall back to torch's RCCL group
+            import warnings
+            warnings.warn("native RCCL communicator unavailable (%s); using torch's "
+                          "ProcessGroupNCCL for device collectives" % e)
+            world.device_group = dist.new_group(list(range(size)), backend="nccl")
+    _WORLD = world
     return _WORLD
 
 
@@ -264,24 +301,47 @@ def reset_world():
     _WORLD = None
 
 
+_ROP = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+
+
+def _finish(work, async_op):
+    if async_op:
+        return work
+    work.wait()
+    return None
+
+
 def all_reduce(t: torch.Tensor, op: str = "sum", async_op: bool = False):
-    if not get_world().has_pg:
+    """Device tensors: the native communicator (the returned work's wait()
+    orders the caller's stream after it; no host wait); host tensors: the
+    default (gloo) group."""
+    w = get_world()
+    if not w.has_pg:
         return None
-    rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
-    return dist.all_reduce(t, op=rop, async_op=async_op)
+    if t.is_cuda and w.native is not None:
+        return _finish(w.native.all_reduce(t, op), async_op)
+    group = w.device_group if t.is_cuda else None
+    return dist.all_reduce(t, op=_ROP[op], async_op=async_op, group=group)
 
 
 def reduce(t: torch.Tensor, dst: int = 0, op: str = "sum", async_op: bool = False):
-    if not get_world().has_pg:
+    w = get_world()
+    if not w.has_pg:
         return None
-    rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
-    return dist.reduce(t, dst=dst, op=rop, async_op=async_op)
+    if t.is_cuda and w.native is not None:
+        return _finish(w.native.reduce(t, dst, op), async_op)
+    group = w.device_group if t.is_cuda else None
+    return dist.reduce(t, dst=dst, op=_ROP[op], async_op=async_op, group=group)
 
 
 def broadcast(t: torch.Tensor, src: int = 0, async_op: bool = False):
-    if not get_world().has_pg:
+    w = get_world()
+    if not w.has_pg:
         return None
-    return dist.broadcast(t, src=src, async_op=async_op)
+    if t.is_cuda and w.native is not None:
+        return _finish(w.native.broadcast(t, src), async_op)
+    group = w.device_group if t.is_cuda else None
+    return dist.broadcast(t, src=src, async_op=async_op, group=group)
 
 
 def all_gather_object(obj):

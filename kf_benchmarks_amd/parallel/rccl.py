@@ -1,0 +1,184 @@
+"""Python face of the native RCCL communicator (csrc/comm.hip).
+
+One communicator per process (one process per GPU).  Rank 0 creates the
+RCCL unique id and publishes it in the job's TCP store (the rendezvous of
+``torch.distributed``'s env:// init, which here only carries host-side
+traffic over gloo); every rank then calls ``ncclCommInitRank`` on its GPU.
+
+Collectives run on a dedicated high-priority stream: the stream first
+waits for the caller's current stream (the gradients are ready there), the
+collective is enqueued, and :meth:`Work.wait` makes the then-current stream
+wait for the comm stream.  All three steps are native calls
+(``kfb_stream_wait``, ``kfb_rccl_*``), so a recorded launch tape replays
+them with the rest of the step.  Replaces the reference's NCCL / Horovod /
+KungFu device collectives (tcb/allreduce.py:297-299, tcb/benchmark_cnn.py:
+3122-3130, 2094-2100); SURVEY section 7.1.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+from ..ops import _native as N
+
+_OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3}
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int32: 3,
+       torch.float64: 4}
+
+N.register_optional("kfb_rccl_available", [], N.c_int)
+N.register_optional("kfb_rccl_error_string", [N.c_int], ctypes.c_char_p)
+N.register_optional("kfb_rccl_unique_id", [N.P], N.c_int)
+N.register_optional("kfb_rccl_init", [N.I, N.P, N.I, N.I, N.P], N.c_int)
+N.register_optional("kfb_rccl_destroy", [N.P, N.I], N.c_int)
+N.register_optional("kfb_rccl_async_error", [N.P], N.c_int)
+N.register_optional("kfb_rccl_all_reduce", [N.P, N.P, N.P, ctypes.c_size_t, N.I, N.I, N.P],
+                    N.c_int)
+N.register_optional("kfb_rccl_reduce", [N.P, N.P, N.P, ctypes.c_size_t, N.I, N.I, N.I, N.P],
+                    N.c_int)
+N.register_optional("kfb_rccl_broadcast", [N.P, N.P, N.P, ctypes.c_size_t, N.I, N.I, N.P],
+                    N.c_int)
+N.register_optional("kfb_rccl_all_gather", [N.P, N.P, N.P, ctypes.c_size_t, N.I, N.P], N.c_int)
+N.register_optional("kfb_rccl_send", [N.P, N.P, ctypes.c_size_t, N.I, N.I, N.P], N.c_int)
+N.register_optional("kfb_rccl_recv", [N.P, N.P, ctypes.c_size_t, N.I, N.I, N.P], N.c_int)
+N.register_optional("kfb_rccl_group_start", [], N.c_int)
+N.register_optional("kfb_rccl_group_end", [], N.c_int)
+
+
+class RcclError(RuntimeError):
+    pass
+
+
+def available() -> bool:
+    try:
+        return bool(N.load().kfb_rccl_available())
+    except (OSError, AttributeError, N.NativeError):
+        return False
+
+
+def enabled() -> bool:
+    """KFB_NATIVE_COMM=0 selects torch's ProcessGroupNCCL instead."""
+    return os.environ.get("KFB_NATIVE_COMM", "1") != "0"
+
+
+class Work:
+    """Completion handle of the collectives enqueued so far on a comm stream."""
+
+    __slots__ = ("comm", "device")
+
+    def __init__(self, comm, device):
+        self.comm, self.device = comm, device
+
+    def wait(self):
+        """The caller's current stream waits for the collective (no host wait)."""
+        N.stream_wait(N.stream(self.device), self.comm.stream_h)
+
+    def synchronize(self):
+        self.comm.stream.synchronize()
+
+
+class NativeComm:
+    """This rank's RCCL communicator (see module docstring)."""
+
+    def __init__(self, rank: int, size: int, device_index: int, store, tag: str = "world"):
+        lib = N.load()
+        if not lib.kfb_rccl_available():
+            raise RcclError("RCCL could not be loaded")
+        self.rank, self.size = rank, size
+        self.device = torch.device("cuda", device_index)
+        key = "kfb_rccl_id/%s" % tag
+        uid = ctypes.create_string_buffer(128)
+        if rank == 0:
+            self._check(lib.kfb_rccl_unique_id(uid), "ncclGetUniqueId")
+            store.set(key, bytes(uid.raw))
+        else:
+            raw = store.get(key)
+            ctypes.memmove(uid, raw, 128)
+        # a high-priority stream: the collectives are scheduled ahead of the
+        # compute kernels queued beside them
+        self.stream = torch.cuda.Stream(self.device, priority=-1)
+        self.stream_h = self.stream.cuda_stream
+        h = ctypes.c_void_p()
+        self._check(lib.kfb_rccl_init(size, uid, rank, device_index, ctypes.byref(h)),
+                    "ncclCommInitRank")
+        self.h = h.value
+        self.collectives = 0
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = N.load().kfb_rccl_error_string(rc)
+            raise RcclError("%s failed: %s (%d)" % (what, msg.decode() if msg else "?", rc))
+
+    def _enter(self, t: torch.Tensor):
+        if not t.is_cuda or not t.is_contiguous():
+            raise RcclError("native collectives take contiguous device tensors")
+        if t.dtype not in _DT:
+            raise RcclError("dtype %s not supported by the native communicator" % t.dtype)
+        N.stream_wait(self.stream_h, N.stream(t.device))  # inputs are ready
+        t.record_stream(self.stream)
+        self.collectives += 1
+
+    def all_reduce(self, t, op="sum"):
+        self._enter(t)
+        N.call("kfb_rccl_all_reduce", self.h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype],
+               _OPS[op], self.stream_h)
+        return Work(self, t.device)
+
+    def reduce(self, t, dst=0, op="sum"):
+        self._enter(t)
+        N.call("kfb_rccl_reduce", self.h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype],
+               _OPS[op], int(dst), self.stream_h)
+        return Work(self, t.device)
+
+    def broadcast(self, t, src=0):
+        self._enter(t)
+        N.call("kfb_rccl_broadcast", self.h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype],
+               int(src), self.stream_h)
+        return Work(self, t.device)
+
+    def all_gather(self, out, t):
+        """out [size * t.numel()] receives every rank's t, rank-major."""
+        self._enter(t)
+        out.record_stream(self.stream)
+        N.call("kfb_rccl_all_gather", self.h, t.data_ptr(), out.data_ptr(), t.numel(),
+               _DT[t.dtype], self.stream_h)
+        return Work(self, t.device)
+
+    def send(self, t, peer):
+        self._enter(t)
+        N.call("kfb_rccl_send", self.h, t.data_ptr(), t.numel(), _DT[t.dtype], int(peer),
+               self.stream_h)
+        return Work(self, t.device)
+
+    def recv(self, t, peer):
+        self._enter(t)
+        N.call("kfb_rccl_recv", self.h, t.data_ptr(), t.numel(), _DT[t.dtype], int(peer),
+               self.stream_h)
+        return Work(self, t.device)
+
+    def group_start(self):
+        N.call("kfb_rccl_group_start")
+
+    def group_end(self):
+        N.call("kfb_rccl_group_end")
+
+    def barrier(self):
+        t = torch.zeros(1, device=self.device)
+        self.all_reduce(t).wait()
+        torch.cuda.synchronize(self.device)
+
+    def check(self):
+        rc = N.load().kfb_rccl_async_error(self.h)
+        if rc != 0:
+            self._check(rc, "RCCL asynchronous error")
+
+    def close(self, abort=False):
+        if getattr(self, "h", None):
+            try:
+                self.stream.synchronize()
+            except RuntimeError:
+                abort = True
+            N.load().kfb_rccl_destroy(self.h, int(abort))
+            self.h = None

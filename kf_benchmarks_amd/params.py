@@ -211,6 +211,11 @@ D.DEFINE_integer("rccl_channels", 0,
 D.DEFINE_float("kungfu_sma_alpha", 0.1, "SMA: pull factor toward the model average.")
 D.DEFINE_integer("kungfu_ada_switch_step", 100, "ada_sgd: step at which SMA switches to S-SGD.")
 D.DEFINE_integer("kungfu_peer_seed", 0, "Seed for PairAveraging peer selection.")
+D.DEFINE_boolean("launch_tape", False,
+                 "Record one training step's native launches after warmup and replay them "
+                 "from C++ every step (ops/tape.py): one Python call per step instead of one "
+                 "per kernel. Single-process synthetic-data runs; other configurations "
+                 "run eagerly.")
 D.DEFINE_boolean("kungfu_pair_prefetch", True,
                  "PairAveraging: pull the peer model at the start of the step, overlapping "
                  "forward/backward (the averaged model is one step older than KungFu's); "

@@ -72,7 +72,8 @@ def main():
            "gsegs": gsegs, "trace": trace,
            "segs": {name: flat[off:off + n].double().sum().item()
                     for name, _, off, n in bench.flat.segments()},
-           "size": comm.get_world().size, "backend": comm.get_world().backend,
+           "size": comm.get_world().size, "backend": comm.get_world().device_backend,
+           "taped": getattr(getattr(bench, "_tape", None), "replays", 0),
            "bucket_launches": (bench.strategy.reducer.launch_count
                                if bench.strategy.reducer is not None else 0),
            "num_buckets": (bench.strategy.reducer.num_buckets

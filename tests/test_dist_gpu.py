@@ -102,17 +102,19 @@ _RCCL = dict(KFB_FORCE_PG="1", KFB_DIST_BACKEND=None, WORLD_SIZE=None, RANK=None
 _NOCOMM = dict(KFB_DIST_BACKEND=None, WORLD_SIZE=None, RANK=None, LOCAL_RANK=None)
 
 
-def test_one_rank_rccl_is_identity(cuda, tmp_path):
-    """FC-only model through a real 1-rank RCCL group: every bucket launches
-    every step, a synchronous all-reduce of the gradient returns it bit for
-    bit, and training tracks the run without any process group."""
+@pytest.mark.parametrize("native", ["1", "0"], ids=["native_comm", "torch_pg"])
+def test_one_rank_rccl_is_identity(cuda, tmp_path, native):
+    """FC-only model through a real 1-rank RCCL communicator - ours
+    (csrc/comm.hip) or torch's ProcessGroupNCCL: every bucket launches every
+    step, a synchronous all-reduce of the gradient returns it bit for bit,
+    and training tracks the run without any process group."""
     kw = dict(model="trivial", batch_size=16, num_gpus=1, use_bf16=True, optimizer="momentum",
               data_format="NHWC", variable_update="kungfu", kungfu_option="sync_sgd",
               bucket_size_mb=8.0)
-    env = dict(_RCCL, KFB_TEST_REDUCE_IDENTITY="1")
+    env = dict(_RCCL, KFB_TEST_REDUCE_IDENTITY="1", KFB_NATIVE_COMM=native)
     (a,) = _run(kw, 3, tmp_path, n=1, env_extra=env, tag="rccl")
     (b,) = _run(kw, 3, tmp_path, n=1, env_extra=_NOCOMM, tag="nocomm")
-    assert a["backend"] == "nccl" and a["size"] == 1
+    assert a["backend"] == ("rccl" if native == "1" else "nccl") and a["size"] == 1
     # 3 steps + the identity check's synchronous reduction
     assert a["bucket_launches"] == 4 * a["num_buckets"] > 0
     assert b["bucket_launches"] == 0
@@ -122,18 +124,27 @@ def test_one_rank_rccl_is_identity(cuda, tmp_path):
         assert abs(la - lb) <= 1e-4 * max(1.0, abs(lb)), (a["losses"], b["losses"])
 
 
-def test_one_rank_rccl_resnet50_overlap(cuda, tmp_path):
+@pytest.mark.parametrize("native,tape", [("1", False), ("0", False), ("1", True)],
+                         ids=["native_comm", "torch_pg", "native_comm_taped"])
+def test_one_rank_rccl_resnet50_overlap(cuda, tmp_path, native, tape):
     """ResNet-50 bs 8 through RCCL with backward-overlapped buckets and the
     side-stream weight gradients: every bucket launches every step, and the
     weights track the no-comm run (the BN statistics' fp32 atomics make
-    either run non-bitwise at these shapes, so the bound is a tolerance)."""
+    either run non-bitwise at these shapes, so the bound is a tolerance).
+    Taped: the bucket all-reduces are replayed from the launch tape with
+    the kernels (2 eager steps, 1 recorded, the rest replayed)."""
     kw = dict(model="resnet50", batch_size=8, num_gpus=1, use_bf16=True, optimizer="momentum",
               data_format="NHWC", variable_update="kungfu", kungfu_option="sync_sgd",
-              bucket_size_mb=4.0)
-    (a,) = _run(kw, 3, tmp_path, n=1, env_extra=_RCCL, tag="rccl")
-    (b,) = _run(kw, 3, tmp_path, n=1, env_extra=_NOCOMM, tag="nocomm")
-    assert a["backend"] == "nccl"
-    assert a["num_buckets"] >= 4 and a["bucket_launches"] == 3 * a["num_buckets"]
+              bucket_size_mb=4.0, launch_tape=tape)
+    steps = 5 if tape else 3
+    (a,) = _run(kw, steps, tmp_path, n=1, env_extra=dict(_RCCL, KFB_NATIVE_COMM=native),
+                tag="rccl")
+    (b,) = _run(dict(kw, launch_tape=False), steps, tmp_path, n=1, env_extra=_NOCOMM,
+                tag="nocomm")
+    assert a["backend"] == ("rccl" if native == "1" else "nccl")
+    assert a["taped"] == (2 if tape else 0)
+    launches = 3 * a["num_buckets"] if not tape else 3 * a["num_buckets"]  # eager+recorded
+    assert a["num_buckets"] >= 4 and a["bucket_launches"] == launches
     assert a["w0"] == b["w0"]
     import math
     for k in a["segs"]:

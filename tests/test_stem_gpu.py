@@ -22,9 +22,13 @@ STEM_SHAPES = [
 ]
 
 
+@pytest.mark.parametrize("mode", ["pairs", "s2d"])
 @pytest.mark.parametrize("shape", STEM_SHAPES, ids=[str(s) for s in STEM_SHAPES])
-def test_s2d_stem_conv(cuda, shape):
+def test_s2d_stem_conv(cuda, shape, mode, monkeypatch):
+    """Both stem forms: the pixel-pair strided conv (default) and the
+    space-to-depth repack."""
     from kf_benchmarks_amd.ops import conv_hip
+    monkeypatch.setattr(conv_hip, "_STEM_MODE", mode)
     n, H, W, cin, cout, kh, kw, mode = shape
     g = torch.Generator().manual_seed(3)
     dt = torch.bfloat16

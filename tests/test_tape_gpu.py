@@ -1,0 +1,51 @@
+"""Launch tape on the GPU: a recorded-and-replayed training step must train
+exactly like the eager step it was recorded from (same kernels, same
+per-step seeds and learning rates), including the weight-gradient side
+stream, dropout seeds and Adam's step-dependent rate."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(model, optimizer, tape, steps=6, bs=8, **kw):
+    from kf_benchmarks_amd import params as P
+    from kf_benchmarks_amd.benchmark import BenchmarkCNN
+    p = P.make_params(model=model, batch_size=bs, num_gpus=1, use_bf16=True,
+                      optimizer=optimizer, data_format="NHWC", variable_update="kungfu",
+                      launch_tape=tape, init_learning_rate=0.05, display_every=10 ** 9, **kw)
+    b = BenchmarkCNN(p)
+    b.build()
+    losses = []
+    for _ in range(steps):
+        loss, _ = b.train_step(need_loss=True)
+        losses.append(float(loss))
+    torch.cuda.synchronize()
+    w = b.flat.flat.detach().float().cpu().clone()
+    replays = b._tape.replays if getattr(b, "_tape", None) is not None else 0
+    return losses, w, replays
+
+
+@pytest.mark.parametrize("model,optimizer", [("resnet50", "momentum"), ("alexnet", "adam"),
+                                             ("googlenet", "sgd")])
+def test_tape_matches_eager(cuda, model, optimizer):
+    le, we, _ = _run(model, optimizer, False)
+    lt, wt, replays = _run(model, optimizer, True)
+    assert replays == 3  # 2 warm eager steps, 1 recorded, 3 replayed
+    # BN statistics use float atomics: equal up to summation order
+    for a, b in zip(le, lt):
+        assert abs(a - b) <= 2e-2 * max(1.0, abs(a)), (le, lt)
+    torch.testing.assert_close(wt, we, rtol=5e-2, atol=5e-3)
+    # the replayed steps changed the weights (they ran at all)
+    assert lt[-1] != lt[2]
+
+
+def test_tape_refuses_torch_ops_in_step(cuda):
+    """A step that launches a torch kernel cannot be taped: recording raises
+    instead of producing a tape that silently skips it."""
+    from kf_benchmarks_amd.ops.tape import StepTape, TapeError
+    x = torch.ones(1024, device=cuda)
+    t = StepTape(cuda)
+    with pytest.raises(TapeError, match="torch device ops"):
+        t.record(lambda: x.mul_(2))
