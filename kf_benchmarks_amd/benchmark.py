@@ -457,8 +457,21 @@ class BenchmarkCNN:
     def forward_backward(self, inputs, need_accuracy=False):
         res = self.net.forward_inputs(inputs, phase_train=True)
         loss = self.model.loss_function(inputs, res)
-        scaled = loss * self.loss_scale if self.loss_scale else loss
-        scaled.backward()
+        if loss.is_cuda:
+            # the backward is seeded with the (static) loss scale: d(s*L) = s*dL,
+            # from a persistent tensor (no fill or multiply kernel in the step)
+            seed = getattr(self, "_loss_seed", None)
+            val = float(self.loss_scale or 1.0)
+            if seed is None or seed.device != loss.device or seed.dtype != loss.dtype \
+                    or seed.shape != loss.shape or self._loss_seed_val != val:
+                # (re)made only when the loss scale changes (dynamic loss scaling)
+                seed = self._loss_seed = torch.full(loss.shape, val, dtype=loss.dtype,
+                                                    device=loss.device)
+                self._loss_seed_val = val
+            loss.backward(seed)
+        else:
+            scaled = loss * self.loss_scale if self.loss_scale else loss
+            scaled.backward()
         if self.device_type == "cuda":
             from .ops.conv_hip import join_wgrad_stream
             join_wgrad_stream(self.device)
@@ -512,11 +525,27 @@ class BenchmarkCNN:
             if self._tape_warm < 2:  # autotune / arena sizing settle first
                 self._tape_warm += 1
                 return None
-            from .ops.tape import StepTape
+            from .ops.tape import StepTape, TapeError
+            p = self.params
+            l2 = None
+            if need_loss and p.loss_type_to_report == "total_loss" and p.weight_decay:
+                l2 = self.l2_loss_value()  # of the weights this step's forward reads
             self.net.tape_begin_recording()
-            t = self._tape = StepTape(self.device)
-            loss, acc = t.record(lambda: self._eager_train_step(False, False))
-            self._tape_loss = loss
+            t = StepTape(self.device)
+            try:
+                loss, acc = t.record(lambda: self._eager_train_step(False, False))
+                if l2 is not None:
+                    loss = loss + len(self.devices) * p.weight_decay * l2
+            except TapeError as e:
+                # the step itself ran to completion eagerly; stay eager from now on
+                self._tape_reason = "recording failed: %s" % e
+                log_fn("launch tape: not used (%s)" % self._tape_reason)
+                t.close()
+                if os.environ.get("KFB_TAPE_STRICT") == "1" or e.outputs is None:
+                    raise
+                return e.outputs
+            self._tape = t
+            self._tape_loss = t.outputs[0]
             log_fn("launch tape: recorded %d native calls (per-step arguments: %s)"
                    % (len(t.recorder), ", ".join(t.recorder.keys()) or "none"))
             return loss, acc

@@ -103,9 +103,21 @@ struct IgArgs {
   // also writes zeros to the three unsampled pixels of its 2x2 block, so the
   // output needs no separate zero fill
   int zfill;
+  // 8-channel geometry (C == 8, KW | 8, KH*KW % 8 == 0; e.g. the stem's
+  // pixel-pair conv, csrc/stem.hip): a 64-deep K step spans 8 taps, one
+  // 16-byte chunk each, so each lane's chunk kc is its own tap
+  // (kh, kw) = (8s + kc) / KW, (8s + kc) % KW of step s; the step advances
+  // the rows by 8 / KW (c8_step elements)
+  int c8, c8_step;
 };
 
 constexpr int IG_BK = 64;
+
+// offset (elements) of chunk kc's tap within step 0 (8-channel geometry) or
+// of the 16-byte channel chunk kc (C % 64 == 0)
+__device__ __forceinline__ int fast_lane_off(const IgArgs& a, int kc) {
+  return a.c8 ? ((kc / a.KW) * a.W + kc % a.KW) * a.C : kc * 8;
+}
 constexpr int IG_SPREAD = 32;
 
 __device__ __forceinline__ int swz_off(int row, int chunk) {
@@ -469,7 +481,7 @@ __global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : (NBUF == 1 ? 4 : 2)
           mk |= (unsigned long long)(in && xok[i]) << (kh * a.KW + kw);
         }
       tapmask[i] = mk;
-      xoff[i] = xbase[i] + (xh[i] * a.W + xw[i]) * a.C + kc * 8;
+      xoff[i] = xbase[i] + (xh[i] * a.W + xw[i]) * a.C + fast_lane_off(a, kc);
     }
 #pragma unroll
     for (int i = 0; i < WC; ++i) woff[i] = (n0 + (tid >> 3) + i * 32) * a.Ktot + kc * 8;
@@ -479,16 +491,21 @@ __global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : (NBUF == 1 ? 4 : 2)
     if constexpr (FAST) {
 #pragma unroll
       for (int i = 0; i < XC; ++i) {
-        const bool ok = (tapmask[i] >> s_tapi) & 1ull;
+        const bool ok = (tapmask[i] >> (a.c8 ? s_tapi * 8 + kc : s_tapi)) & 1ull;
         const int off = ok ? (xoff[i] + s_tap + s_cc) * (int)sizeof(T) : -1;
         xr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
       }
-      s_cc += IG_BK;
-      if (s_cc == a.C) {
-        s_cc = 0;
+      if (a.c8) {
         ++s_tapi;
-        if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
-        s_tap = (s_kh * a.W + s_kw) * a.C;
+        s_tap += a.c8_step;
+      } else {
+        s_cc += IG_BK;
+        if (s_cc == a.C) {
+          s_cc = 0;
+          ++s_tapi;
+          if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
+          s_tap = (s_kh * a.W + s_kw) * a.C;
+        }
       }
     } else {
       const int k = kt * IG_BK + kc * 8;
@@ -656,7 +673,7 @@ __global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : 4) igemm_mt_k(IgArg
           mk |= (unsigned long long)(in && ok) << (kh * a.KW + kw);
         }
       tapmask[i] = mk;
-      xoff[i] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + kc * 8;
+      xoff[i] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + fast_lane_off(a, kc);
     }
 #pragma unroll
     for (int i = 0; i < WC; ++i) woff[i] = (n0 + (tid >> 3) + i * 32) * a.Ktot + kc * 8;
@@ -666,16 +683,21 @@ __global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : 4) igemm_mt_k(IgArg
   auto load = [&]() {
 #pragma unroll
     for (int i = 0; i < XC; ++i) {
-      const bool ok = (tapmask[i] >> s_tapi) & 1ull;
+      const bool ok = (tapmask[i] >> (a.c8 ? s_tapi * 8 + kc : s_tapi)) & 1ull;
       const int off = ok ? (xoff[i] + s_tap + s_cc) * (int)sizeof(T) : -1;
       xr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     }
-    s_cc += IG_BK;
-    if (s_cc == a.C) {
-      s_cc = 0;
+    if (a.c8) {
       ++s_tapi;
-      if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
-      s_tap = (s_kh * a.W + s_kw) * a.C;
+      s_tap += a.c8_step;
+    } else {
+      s_cc += IG_BK;
+      if (s_cc == a.C) {
+        s_cc = 0;
+        ++s_tapi;
+        if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
+        s_tap = (s_kh * a.W + s_kw) * a.C;
+      }
     }
 #pragma unroll
     for (int i = 0; i < WC; ++i)
@@ -839,7 +861,7 @@ __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * 
         mk |= (unsigned long long)(in && ok) << (kh * a.KW + kw);
       }
     tapmask[i] = mk;
-    xoff[i] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + kc * 8;
+    xoff[i] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + fast_lane_off(a, kc);
   }
 #pragma unroll
   for (int j = 0; j < WI; ++j) woff[j] = (n0 + j * SLAB + rr) * a.Ktot + kc * 8;
@@ -850,7 +872,7 @@ __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * 
     T* ws = xs + BM * IG_BK;
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
-      const bool ok = (tapmask[i] >> s_tapi) & 1ull;
+      const bool ok = (tapmask[i] >> (a.c8 ? s_tapi * 8 + kc : s_tapi)) & 1ull;
       const int off = ok ? (xoff[i] + s_tap + s_cc) * (int)sizeof(T) : -1;
       dma16(xrs, xs + (i * SLAB + wid * 8) * IG_BK, off);
     }
@@ -858,12 +880,17 @@ __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * 
     for (int j = 0; j < WI; ++j)
       dma16(wrs, ws + (j * SLAB + wid * 8) * IG_BK, (woff[j] + s_k) * (int)sizeof(T));
     s_k += IG_BK;
-    s_cc += IG_BK;
-    if (s_cc == a.C) {
-      s_cc = 0;
+    if (a.c8) {
       ++s_tapi;
-      if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
-      s_tap = (s_kh * a.W + s_kw) * a.C;
+      s_tap += a.c8_step;
+    } else {
+      s_cc += IG_BK;
+      if (s_cc == a.C) {
+        s_cc = 0;
+        ++s_tapi;
+        if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
+        s_tap = (s_kh * a.W + s_kw) * a.C;
+      }
     }
   };
 
@@ -968,7 +995,7 @@ __global__ void __launch_bounds__(256, (glds_occupancy<BM, BN, 256>()))
           mk |= (unsigned long long)(in && ok) << (kh * a.KW + kw);
         }
       tapmask[i] = mk;
-      xoff[i] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + kc * 8;
+      xoff[i] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + fast_lane_off(a, kc);
     }
 #pragma unroll
     for (int j = 0; j < WI; ++j) woff[j] = (n0 + j * SLAB + rr) * a.Ktot + kc * 8;
@@ -979,7 +1006,7 @@ __global__ void __launch_bounds__(256, (glds_occupancy<BM, BN, 256>()))
     T* ws = xs + BM * IG_BK;
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
-      const bool ok = (tapmask[i] >> s_tapi) & 1ull;
+      const bool ok = (tapmask[i] >> (a.c8 ? s_tapi * 8 + kc : s_tapi)) & 1ull;
       const int off = ok ? (xoff[i] + s_tap + s_cc) * (int)sizeof(T) : -1;
       dma16(xrs, xs + (i * SLAB + wid * 8) * IG_BK, off);
     }
@@ -987,12 +1014,17 @@ __global__ void __launch_bounds__(256, (glds_occupancy<BM, BN, 256>()))
     for (int j = 0; j < WI; ++j)
       dma16(wrs, ws + (j * SLAB + wid * 8) * IG_BK, (woff[j] + s_k) * (int)sizeof(T));
     s_k += IG_BK;
-    s_cc += IG_BK;
-    if (s_cc == a.C) {
-      s_cc = 0;
+    if (a.c8) {
       ++s_tapi;
-      if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
-      s_tap = (s_kh * a.W + s_kw) * a.C;
+      s_tap += a.c8_step;
+    } else {
+      s_cc += IG_BK;
+      if (s_cc == a.C) {
+        s_cc = 0;
+        ++s_tapi;
+        if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
+        s_tap = (s_kh * a.W + s_kw) * a.C;
+      }
     }
   };
   v4f acc[TN][TM];
@@ -1527,8 +1559,13 @@ enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_G
        IG_ALGO_MULTI4 = 15, IG_ALGO_SMALL_MULTI4 = 16, IG_ALGO_GMULTI64 = 17,
        IG_ALGO_GMULTI128 = 18 };
 
+static bool c8_geometry(int C, int KH, int KW) {
+  return C == 8 && (KW == 1 || KW == 2 || KW == 4 || KW == 8) && (KH * KW) % 8 == 0;
+}
+
 KFB_API int kfb_conv_igemm_fast(int C, int KH, int KW, int trans) {
-  return !trans && C % IG_BK == 0 && KH * KW <= 64 && !igemm_fast_disabled();
+  return !trans && (C % IG_BK == 0 || c8_geometry(C, KH, KW)) && KH * KW <= 64 &&
+         !igemm_fast_disabled();
 }
 
 // Forward conv or dgrad (trans=1) or scattered 1x1 GEMM (ys>1).
@@ -1552,9 +1589,14 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
            (int)(xbytes < (1L << 31) ? xbytes : 0), (int)(wbytes < (1L << 31) ? wbytes : 0),
            (int)(ybytes < (1L << 31) ? ybytes : 0),
            (stats && !xbn && !addend) ? kshift : nullptr,
-           FastDiv(C), FastDiv(KW), FastDiv(sh), FastDiv(sw), zfill};
+           FastDiv(C), FastDiv(KW), FastDiv(sh), FastDiv(sw), zfill, 0, 0};
   const bool t = trans != 0;
-  const bool fast = !t && C % IG_BK == 0 && KH * KW <= 64 && xbytes < (1L << 31) &&
+  const bool c8 = !t && C % IG_BK != 0 && c8_geometry(C, KH, KW);
+  if (c8) {
+    a.c8 = 1;
+    a.c8_step = (8 / KW) * W * C;
+  }
+  const bool fast = !t && (C % IG_BK == 0 || c8) && KH * KW <= 64 && xbytes < (1L << 31) &&
                     wbytes < (1L << 31) && !igemm_fast_disabled();
   const bool narrow = algo == IG_ALGO_CLASSIC_N64 || algo == IG_ALGO_GLDS_N64 ||
                       algo == IG_ALGO_ONEBUF_N64;

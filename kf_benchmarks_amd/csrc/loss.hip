@@ -97,9 +97,27 @@ in_top_k_k(const T* __restrict__ logits, const int* __restrict__ labels, int K,
   }
 }
 
+// out[0] = mean(x[0..n)) in one workgroup (fixed summation order: the loss
+// a step reports is bitwise reproducible).
+__global__ void __launch_bounds__(256) mean_f32_k(const float* __restrict__ x, long n,
+                                                  float* __restrict__ out) {
+  __shared__ float part[4];
+  float s = 0.f;
+  for (long i = threadIdx.x; i < n; i += 256) s += x[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = ((part[0] + part[1]) + (part[2] + part[3])) / (float)n;
+}
+
 }  // namespace kfb
 
 using namespace kfb;
+
+KFB_API hipError_t kfb_mean_f32(const float* x, long n, float* out, hipStream_t stream) {
+  hipLaunchKernelGGL(mean_f32_k, dim3(1), dim3(256), 0, stream, x, n, out);
+  return hipGetLastError();
+}
 
 KFB_API hipError_t kfb_xent_fwd(int dtype, const void* logits, const int* labels, long N, int K,
                                 float* loss, float* lse, hipStream_t stream) {

@@ -61,6 +61,7 @@ _SIGS = {
     "kfb_cast_f32": [P, P, I, L, P],
     "kfb_cast_to_f32": [P, I, P, L, P],
     "kfb_xent_fwd": [I, P, P, L, I, P, P, P],
+    "kfb_mean_f32": [P, L, P, P],
     "kfb_xent_bwd": [I, P, P, P, P, F, L, I, P, P],
     "kfb_in_top_k": [I, P, P, L, I, P, P, P],
     "kfb_maxpool_fwd": [I, P, P, P] + [I] * 12 + [P],

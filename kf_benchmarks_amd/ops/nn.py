@@ -980,7 +980,9 @@ class _SoftmaxXent(torch.autograd.Function):
         N.call("kfb_xent_fwd", N.dt(logits), logits.data_ptr(), labels.data_ptr(), n, k,
                loss.data_ptr(), lse.data_ptr(), N.stream(logits.device))
         ctx.save_for_backward(logits, labels, lse)
-        return loss.mean()
+        mean = torch.empty((), dtype=torch.float32, device=logits.device)
+        N.call("kfb_mean_f32", loss.data_ptr(), n, mean.data_ptr(), N.stream(logits.device))
+        return mean
 
     @staticmethod
     def backward(ctx, g):

@@ -41,7 +41,9 @@ _MASK = (1 << 64) - 1
 
 
 class TapeError(RuntimeError):
-    pass
+    def __init__(self, msg, outputs=None):
+        super().__init__(msg)
+        self.outputs = outputs  # the step's results when the step itself completed
 
 
 def _pack(v, code):
@@ -149,7 +151,7 @@ class _TorchKernelProbe:
                   "narrow", "_reshape_alias", "lift_fresh", "unbind", "chunk",
                   "tensor_split", "view_as", "_to_copy_noop", "set_", "resize_",
                   "new_empty", "new_empty_strided", "clone_noop", "is_same_size", "sym_size",
-                  "sym_stride", "sym_numel", "sym_storage_offset"}
+                  "sym_stride", "sym_numel", "sym_storage_offset", "record_stream"}
 
     def __init__(self):
         from torch.utils._python_dispatch import TorchDispatchMode
@@ -164,7 +166,12 @@ class _TorchKernelProbe:
                         list(out) if isinstance(out, (tuple, list)) else [])
                     flat += [a for a in args if isinstance(a, torch.Tensor)]
                     if any(isinstance(t, torch.Tensor) and t.is_cuda for t in flat):
-                        probe.ops.append(name)
+                        import traceback
+                        where = [f for f in traceback.extract_stack()
+                                 if "kf_benchmarks_amd" in f.filename and "tape.py" not in f.filename]
+                        site = ("%s:%d" % (where[-1].filename.split("kf_benchmarks_amd/")[-1],
+                                           where[-1].lineno)) if where else "?"
+                        probe.ops.append("%s@%s" % (name, site))
                 return out
 
         self.mode = Mode()
@@ -218,7 +225,7 @@ class StepTape:
         if probe is not None and probe.ops:
             rec.close()
             raise TapeError("torch device ops inside the recorded step (not replayable): %s"
-                            % sorted(set(probe.ops)))
+                            % sorted(set(probe.ops)), outputs=out)
         self.recorder = rec
         self.outputs = out
         return out

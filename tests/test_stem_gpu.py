@@ -112,3 +112,30 @@ def test_bn_relu_maxpool_fused(cuda, shape):
     torch.testing.assert_close(xa.grad.float().cpu(), xb.grad, rtol=5e-2, atol=3e-2 * sc)
     torch.testing.assert_close(ba.grad.cpu(), bb.grad, rtol=2e-2, atol=2e-2 * bb.grad.abs().max().item())
     torch.testing.assert_close(ga.grad.cpu(), gb.grad, rtol=3e-2, atol=3e-2 * gb.grad.abs().max().item())
+
+
+C8_ALGOS = ["classic", "glds", "classic_n64", "glds_n64", "onebuf", "onebuf_n64", "tall256",
+            "small", "gshort64", "gshort128", "gshort64_3", "multi2", "multi4", "gmulti64"]
+C8_SHAPES = [  # (N, H, W, Cout, KH, KW, stride): 8-channel FAST geometry (C == 8, KW | 8)
+    (2, 30, 20, 64, 8, 4, (2, 1)),     # the stem's pixel-pair conv
+    (3, 17, 13, 32, 4, 2, (1, 1)),
+    (1, 21, 19, 128, 1, 8, (2, 2)),
+]
+
+
+@pytest.mark.parametrize("algo", C8_ALGOS)
+@pytest.mark.parametrize("shape", C8_SHAPES, ids=[str(s) for s in C8_SHAPES])
+def test_c8_fast_conv_every_kernel(cuda, shape, algo, monkeypatch):
+    """The FAST implicit-GEMM kernels in 8-channel geometry (each lane's
+    16-byte chunk is its own tap) vs an fp32 reference, every kernel."""
+    from kf_benchmarks_amd.ops import conv_hip
+    monkeypatch.setattr(conv_hip, "_IG_FORCE", conv_hip.IG_ALGOS[algo])
+    n, H, W, cout, kh, kw, stride = shape
+    g = torch.Generator().manual_seed(11)
+    dt = torch.bfloat16
+    x = torch.randn(n, H, W, 8, generator=g).to(dt).float()
+    w = (torch.randn(cout, kh, kw, 8, generator=g) / (kh * kw * 8) ** 0.5).to(dt).float()
+    y = conv_hip.conv_fwd(x.to(cuda, dt), w.to(cuda, dt), stride, (0, 0, 0, 0))
+    ref = conv_ops.conv2d_reference(x, w, stride, (0, 0, 0, 0))
+    assert y.shape == ref.shape
+    torch.testing.assert_close(y.float().cpu(), ref, rtol=2e-2, atol=2e-2)

@@ -9,12 +9,17 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _strict(monkeypatch):
+    monkeypatch.setenv("KFB_TAPE_STRICT", "1")  # a failed recording raises
+
+
 def _run(model, optimizer, tape, steps=6, bs=8, **kw):
     from kf_benchmarks_amd import params as P
     from kf_benchmarks_amd.benchmark import BenchmarkCNN
     p = P.make_params(model=model, batch_size=bs, num_gpus=1, use_bf16=True,
                       optimizer=optimizer, data_format="NHWC", variable_update="kungfu",
-                      launch_tape=tape, init_learning_rate=0.05, display_every=10 ** 9, **kw)
+                      launch_tape=tape, init_learning_rate=0.002, display_every=10 ** 9, **kw)
     b = BenchmarkCNN(p)
     b.build()
     losses = []
@@ -31,12 +36,17 @@ def _run(model, optimizer, tape, steps=6, bs=8, **kw):
                                              ("googlenet", "sgd")])
 def test_tape_matches_eager(cuda, model, optimizer):
     le, we, _ = _run(model, optimizer, False)
+    le2, we2, _ = _run(model, optimizer, False)
     lt, wt, replays = _run(model, optimizer, True)
     assert replays == 3  # 2 warm eager steps, 1 recorded, 3 replayed
-    # BN statistics use float atomics: equal up to summation order
-    for a, b in zip(le, lt):
-        assert abs(a - b) <= 2e-2 * max(1.0, abs(a)), (le, lt)
-    torch.testing.assert_close(wt, we, rtol=5e-2, atol=5e-3)
+    # BN statistics use float atomics, so two eager runs already differ in
+    # the last bits; the taped run must stay as close to eager as eager is
+    # to itself (plus a small floor)
+    # (run 1 also autotunes; runs 2 and 3 reuse its kernel choices)
+    for a, a2, b in zip(le, le2, lt):
+        assert abs(a2 - b) <= max(4 * abs(a - a2), 1e-2 * max(1.0, abs(a2))), (le, le2, lt)
+    ref = (we - we2).abs().max().item()
+    assert (wt - we2).abs().max().item() <= max(4 * ref, 1e-3), ref
     # the replayed steps changed the weights (they ran at all)
     assert lt[-1] != lt[2]
 
