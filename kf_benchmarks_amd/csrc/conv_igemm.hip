@@ -480,7 +480,7 @@ __global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : (NBUF == 1 ? 4 : 2)
                           (unsigned)(xw[i] + kw) < (unsigned)a.W;
           mk |= (unsigned long long)(in && xok[i]) << (kh * a.KW + kw);
         }
-      tapmask[i] = mk;
+      tapmask[i] = a.c8 ? mk >> kc : mk;  // 8-channel: bit 8s = this lane's tap of step s
       xoff[i] = xbase[i] + (xh[i] * a.W + xw[i]) * a.C + fast_lane_off(a, kc);
     }
 #pragma unroll
@@ -491,12 +491,12 @@ __global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : (NBUF == 1 ? 4 : 2)
     if constexpr (FAST) {
 #pragma unroll
       for (int i = 0; i < XC; ++i) {
-        const bool ok = (tapmask[i] >> (a.c8 ? s_tapi * 8 + kc : s_tapi)) & 1ull;
+        const bool ok = (tapmask[i] >> s_tapi) & 1ull;
         const int off = ok ? (xoff[i] + s_tap + s_cc) * (int)sizeof(T) : -1;
         xr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
       }
       if (a.c8) {
-        ++s_tapi;
+        s_tapi += 8;  // the 8 taps of the next step (lane kc's at bit kc)
         s_tap += a.c8_step;
       } else {
         s_cc += IG_BK;
@@ -673,7 +673,7 @@ __global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : 4) igemm_mt_k(IgArg
           mk |= (unsigned long long)(in && ok) << (kh * a.KW + kw);
         }
       tapmask[i] = mk;
-      xoff[i] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + fast_lane_off(a, kc);
+      xoff[i] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + kc * 8;
     }
 #pragma unroll
     for (int i = 0; i < WC; ++i) woff[i] = (n0 + (tid >> 3) + i * 32) * a.Ktot + kc * 8;
@@ -683,21 +683,16 @@ __global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : 4) igemm_mt_k(IgArg
   auto load = [&]() {
 #pragma unroll
     for (int i = 0; i < XC; ++i) {
-      const bool ok = (tapmask[i] >> (a.c8 ? s_tapi * 8 + kc : s_tapi)) & 1ull;
+      const bool ok = (tapmask[i] >> s_tapi) & 1ull;
       const int off = ok ? (xoff[i] + s_tap + s_cc) * (int)sizeof(T) : -1;
       xr[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     }
-    if (a.c8) {
+    s_cc += IG_BK;
+    if (s_cc == a.C) {
+      s_cc = 0;
       ++s_tapi;
-      s_tap += a.c8_step;
-    } else {
-      s_cc += IG_BK;
-      if (s_cc == a.C) {
-        s_cc = 0;
-        ++s_tapi;
-        if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
-        s_tap = (s_kh * a.W + s_kw) * a.C;
-      }
+      if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
+      s_tap = (s_kh * a.W + s_kw) * a.C;
     }
 #pragma unroll
     for (int i = 0; i < WC; ++i)
@@ -818,7 +813,8 @@ constexpr int glds_occupancy() {
   return NT == 256 && BM == 128 ? (BN == 64 ? 3 : 2) : 1;
 }
 
-template <typename T, int BM, int BN, int WGM, int WGN, int STAGES = GL_STAGES>
+template <typename T, int BM, int BN, int WGM, int WGN, int STAGES = GL_STAGES,
+          bool EXTRAS = true>
 __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * WGN * 64>()))
     igemm_glds_k(IgArgs a) {
   constexpr int NT = WGM * WGN * 64;
@@ -860,7 +856,7 @@ __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * 
         const bool in = (unsigned)(xh + kh) < (unsigned)a.H && (unsigned)(xw + kw) < (unsigned)a.W;
         mk |= (unsigned long long)(in && ok) << (kh * a.KW + kw);
       }
-    tapmask[i] = mk;
+    tapmask[i] = a.c8 ? mk >> kc : mk;  // 8-channel: bit 8s = this lane's tap of step s
     xoff[i] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + fast_lane_off(a, kc);
   }
 #pragma unroll
@@ -872,7 +868,7 @@ __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * 
     T* ws = xs + BM * IG_BK;
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
-      const bool ok = (tapmask[i] >> (a.c8 ? s_tapi * 8 + kc : s_tapi)) & 1ull;
+      const bool ok = (tapmask[i] >> s_tapi) & 1ull;
       const int off = ok ? (xoff[i] + s_tap + s_cc) * (int)sizeof(T) : -1;
       dma16(xrs, xs + (i * SLAB + wid * 8) * IG_BK, off);
     }
@@ -881,7 +877,7 @@ __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * 
       dma16(wrs, ws + (j * SLAB + wid * 8) * IG_BK, (woff[j] + s_k) * (int)sizeof(T));
     s_k += IG_BK;
     if (a.c8) {
-      ++s_tapi;
+      s_tapi += 8;  // the 8 taps of the next step (lane kc's at bit kc)
       s_tap += a.c8_step;
     } else {
       s_cc += IG_BK;
@@ -941,7 +937,7 @@ __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * 
     }
   }
   __syncthreads();  // all fragment reads done before the epilogue reuses the ring
-  ig_epilogue<T, BM, BN, NT, WGM, WGN>(a, acc, smem, m0, n0, wm, wn);
+  ig_epilogue<T, BM, BN, NT, WGM, WGN, NoPrefetch, EXTRAS>(a, acc, smem, m0, n0, wm, wn);
 }
 
 // Multi-tile form of the 4-wave 2-stage LDS-DMA kernel (128 x 64 / 128 x 128):
@@ -995,7 +991,7 @@ __global__ void __launch_bounds__(256, (glds_occupancy<BM, BN, 256>()))
           mk |= (unsigned long long)(in && ok) << (kh * a.KW + kw);
         }
       tapmask[i] = mk;
-      xoff[i] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + fast_lane_off(a, kc);
+      xoff[i] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + kc * 8;
     }
 #pragma unroll
     for (int j = 0; j < WI; ++j) woff[j] = (n0 + j * SLAB + rr) * a.Ktot + kc * 8;
@@ -1006,7 +1002,7 @@ __global__ void __launch_bounds__(256, (glds_occupancy<BM, BN, 256>()))
     T* ws = xs + BM * IG_BK;
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
-      const bool ok = (tapmask[i] >> (a.c8 ? s_tapi * 8 + kc : s_tapi)) & 1ull;
+      const bool ok = (tapmask[i] >> s_tapi) & 1ull;
       const int off = ok ? (xoff[i] + s_tap + s_cc) * (int)sizeof(T) : -1;
       dma16(xrs, xs + (i * SLAB + wid * 8) * IG_BK, off);
     }
@@ -1014,17 +1010,12 @@ __global__ void __launch_bounds__(256, (glds_occupancy<BM, BN, 256>()))
     for (int j = 0; j < WI; ++j)
       dma16(wrs, ws + (j * SLAB + wid * 8) * IG_BK, (woff[j] + s_k) * (int)sizeof(T));
     s_k += IG_BK;
-    if (a.c8) {
+    s_cc += IG_BK;
+    if (s_cc == a.C) {
+      s_cc = 0;
       ++s_tapi;
-      s_tap += a.c8_step;
-    } else {
-      s_cc += IG_BK;
-      if (s_cc == a.C) {
-        s_cc = 0;
-        ++s_tapi;
-        if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
-        s_tap = (s_kh * a.W + s_kw) * a.C;
-      }
+      if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
+      s_tap = (s_kh * a.W + s_kw) * a.C;
     }
   };
   v4f acc[TN][TM];
@@ -1467,6 +1458,22 @@ static void launch_glds_short(const IgArgs& a, bool wide, bool three, hipStream_
     hipLaunchKernelGGL((igemm_glds_k<T, 128, 64, 2, 2, 2>), g64, dim3(256), 0, s, a);
 }
 
+// Big-tile LDS-DMA kernels, one 8-wave workgroup per CU with 128 x 64 wave
+// tiles (twice the MFMAs per fragment read of the 64 x 64 wave tiles, and
+// half the L2 bytes per MFMA of the 256 x 128 workgroup tile): 256 x 256 for
+// >= 256 output channels (2 x 64 KB ring), 512 x 128 for 128-channel layers
+// (2 x 80 KB ring, the whole 160 KB LDS).
+template <typename T>
+static void launch_glds_big(const IgArgs& a, bool wide, hipStream_t s) {
+  // forward-style epilogues only (the dgrad operands' loads would spill)
+  if (wide)
+    hipLaunchKernelGGL((igemm_glds_k<T, 256, 256, 2, 4, 2, false>),
+                       dim3(((a.M + 255) / 256) * ((a.Ncol + 255) / 256)), dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((igemm_glds_k<T, 512, 128, 4, 2, 2, false>),
+                       dim3(((a.M + 511) / 512) * ((a.Ncol + 127) / 128)), dim3(512), 0, s, a);
+}
+
 // Multi-tile 4-wave LDS-DMA kernels, 2 tiles per workgroup.
 template <typename T>
 static void launch_glds_mt(const IgArgs& a, bool wide, hipStream_t s) {
@@ -1557,7 +1564,7 @@ enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_G
        IG_ALGO_SMALL = 9, IG_ALGO_GSHORT64 = 10, IG_ALGO_GSHORT128 = 11,
        IG_ALGO_GSHORT64_3 = 12, IG_ALGO_GSHORT128_3 = 13, IG_ALGO_MULTI2 = 14,
        IG_ALGO_MULTI4 = 15, IG_ALGO_SMALL_MULTI4 = 16, IG_ALGO_GMULTI64 = 17,
-       IG_ALGO_GMULTI128 = 18 };
+       IG_ALGO_GMULTI128 = 18, IG_ALGO_GBIG256 = 19, IG_ALGO_GBIG512 = 20 };
 
 static bool c8_geometry(int C, int KH, int KW) {
   return C == 8 && (KW == 1 || KW == 2 || KW == 4 || KW == 8) && (KH * KW) % 8 == 0;
@@ -1615,7 +1622,13 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }
-  if ((algo == IG_ALGO_GMULTI64 || algo == IG_ALGO_GMULTI128) && fast) {
+  if ((algo == IG_ALGO_GBIG256 || algo == IG_ALGO_GBIG512) && fast && !addend && !xbn && !mask) {
+    if (dtype == BF16) launch_glds_big<bf16>(a, algo == IG_ALGO_GBIG256, stream);
+    else if (dtype == F16) launch_glds_big<f16>(a, algo == IG_ALGO_GBIG256, stream);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
+  if ((algo == IG_ALGO_GMULTI64 || algo == IG_ALGO_GMULTI128) && fast && !c8) {
     const bool wide = algo == IG_ALGO_GMULTI128;
     if (dtype == BF16) launch_glds_mt<bf16>(a, wide, stream);
     else if (dtype == F16) launch_glds_mt<f16>(a, wide, stream);
@@ -1629,7 +1642,7 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
     return hipGetLastError();
   }
   if ((algo == IG_ALGO_MULTI2 || algo == IG_ALGO_MULTI4 || algo == IG_ALGO_SMALL_MULTI4) && fast &&
-      !addend && !xbn && !mask) {
+      !addend && !xbn && !mask && !c8) {
     const int tpw = algo == IG_ALGO_MULTI2 ? 2 : 4;
     const bool small = algo == IG_ALGO_SMALL_MULTI4;
     if (dtype == BF16) small ? launch_mt<bf16, 64>(a, tpw, stream) : launch_mt<bf16, 128>(a, tpw, stream);

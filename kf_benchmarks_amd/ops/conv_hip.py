@@ -35,19 +35,22 @@ IG_GSHORT64_3, IG_GSHORT128_3 = 12, 13
 IG_MULTI2, IG_MULTI4, IG_SMALL_MULTI4 = 14, 15, 16
 # ... and the LDS-DMA 128x64 / 128x128 4-wave kernels with 2 tiles per workgroup
 IG_GMULTI64, IG_GMULTI128 = 17, 18
+# 8-wave LDS-DMA kernels with 128 x 64 wave tiles: 256 x 256 / 512 x 128 tiles
+IG_GBIG256, IG_GBIG512 = 19, 20
 IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N64,
             "glds_n64": IG_GLDS_N64, "onebuf": IG_ONEBUF, "onebuf_n64": IG_ONEBUF_N64,
             "tall512": IG_TALL512, "tall256": IG_TALL256, "small": IG_SMALL,
             "gshort64": IG_GSHORT64, "gshort128": IG_GSHORT128, "gshort64_3": IG_GSHORT64_3,
             "gshort128_3": IG_GSHORT128_3, "multi2": IG_MULTI2, "multi4": IG_MULTI4,
             "small_multi4": IG_SMALL_MULTI4, "gmulti64": IG_GMULTI64,
-            "gmulti128": IG_GMULTI128}
+            "gmulti128": IG_GMULTI128, "gbig256": IG_GBIG256, "gbig512": IG_GBIG512}
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
 _NO_GSHORT = os.environ.get("KFB_IGEMM_NOGSHORT", "0") == "1"  # A/B knob: drop IG_GSHORT*
 _GSHORT3 = os.environ.get("KFB_IGEMM_GSHORT3", "1") != "0"  # A/B knob: the 3-stage forms
 _NO_MULTI = os.environ.get("KFB_IGEMM_NOMULTI", "0") == "1"  # A/B knob: drop IG_*MULTI*
+_NO_BIG = os.environ.get("KFB_IGEMM_NOBIG", "0") == "1"  # A/B knob: drop IG_GBIG*
 # largest K (= KH*KW*Cin) offered the multi-tile candidates (register-staged;
 # the LDS-DMA form gets twice that)
 _MULTI_K = int(os.environ.get("KFB_IGEMM_MULTI_K", "2304"))
@@ -219,11 +222,18 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
         if _GSHORT3:
             cands += (IG_GSHORT64_3,) + ((IG_GSHORT128_3,) if ncol > 64 else ())
     if fast and not _NO_MULTI and mask is None and xbn is None and addend is None \
-            and KH * KW * C <= _MULTI_K:
+            and KH * KW * C <= _MULTI_K and C % 64 == 0:
         # short-K layers: store-phase bound, the multi-tile overlap pays there
         cands += (IG_MULTI2, IG_MULTI4, IG_SMALL_MULTI4)
-    if fast and not _NO_MULTI and KH * KW * C <= 2 * _MULTI_K:
+    if fast and not _NO_MULTI and KH * KW * C <= 2 * _MULTI_K and C % 64 == 0:
         cands += (IG_GMULTI64,) + ((IG_GMULTI128,) if ncol > 64 else ())
+    if fast and not _NO_BIG and mask is None and xbn is None and addend is None:
+        # big tiles only where they still give every CU a workgroup or more
+        M = geo[0] * geo[4] * geo[5]
+        if ncol >= 256 and ((M + 255) // 256) * ((ncol + 255) // 256) >= 256:
+            cands += (IG_GBIG256,)
+        if 64 < ncol <= 256 and ((M + 511) // 512) * ((ncol + 127) // 128) >= 256:
+            cands += (IG_GBIG512,)
     if ncol > 64:  # 64-wide tiles: more workgroups for small-M layers
         cands += (IG_CLASSIC_N64, IG_GLDS_N64, IG_ONEBUF_N64) if fast else (IG_CLASSIC_N64,)
     if len(cands) == 1:

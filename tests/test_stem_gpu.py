@@ -114,8 +114,10 @@ def test_bn_relu_maxpool_fused(cuda, shape):
     torch.testing.assert_close(ga.grad.cpu(), gb.grad, rtol=3e-2, atol=3e-2 * gb.grad.abs().max().item())
 
 
+# (the multi-tile kernels take the 64-channel geometry only; forced for an
+# 8-channel conv they fall back to the one-tile kernel)
 C8_ALGOS = ["classic", "glds", "classic_n64", "glds_n64", "onebuf", "onebuf_n64", "tall256",
-            "small", "gshort64", "gshort128", "gshort64_3", "multi2", "multi4", "gmulti64"]
+            "small", "gshort64", "gshort128", "gshort64_3", "gbig512", "multi2", "gmulti64"]
 C8_SHAPES = [  # (N, H, W, Cout, KH, KW, stride): 8-channel FAST geometry (C == 8, KW | 8)
     (2, 30, 20, 64, 8, 4, (2, 1)),     # the stem's pixel-pair conv
     (3, 17, 13, 32, 4, 2, (1, 1)),
