@@ -273,49 +273,66 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
         (void*)(a.mask ? a.mask : a.y), (short)0, (a.mask && a.xbn) ? a.ybytes : 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t rxb = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.xbn ? a.xbn : a.y), (short)0, a.xbn ? a.ybytes : 0, 0x00020000);
-    int offb[NPASS];
-    uint4 ad[NPASS], mk[NPASS], xb[NPASS];
+    // Passes go in groups of G: the extra-operand loads of group g+1 are
+    // issued before group g is processed and stored, so they fly meanwhile
+    // and a store never precedes the loads it would make wait (loads and
+    // stores share the in-order vmcnt).  Small tiles (NPASS <= 4) form one
+    // group: every load before any store.  Big tiles keep 2 groups of 3 x G
+    // 16-byte operands in registers instead of 3 x NPASS.
+    constexpr int G = NPASS > 4 ? 4 : NPASS;
+    constexpr int NG = NPASS / G;
+    static_assert(NPASS % G == 0, "pass groups");
+    int offb[2][G];
+    uint4 ad[2][G], mk[2][G], xb[2][G];
+    auto load_group = [&](int g, int b) {
 #pragma unroll
-    for (int p = 0; p < NPASS; ++p) {
-      const int t = tid + p * NT;
-      const int m = m0 + t / CPR, n = n0 + (t % CPR) * 8;
-      offb[p] = (m < a.M && n < a.Ncol) ? (int)((row_offset(m) + n) * (long)sizeof(T)) : -1;
-      ad[p] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rad, offb[p], 0, 0));
-      mk[p] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rmk, offb[p], 0, 0));
-      xb[p] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rxb, offb[p], 0, 0));
-    }
-#pragma unroll
-    for (int p = 0; p < NPASS; ++p) {
-      const uint4 raw = lds_chunk(tid + p * NT);
-      const Vec<T, 8> tv = __builtin_bit_cast(Vec<T, 8>, raw);
-      const Vec<T, 8> av = __builtin_bit_cast(Vec<T, 8>, ad[p]);
-      const Vec<T, 8> mv = __builtin_bit_cast(Vec<T, 8>, mk[p]);
-      const Vec<T, 8> xv = __builtin_bit_cast(Vec<T, 8>, xb[p]);
-      Vec<T, 8> ov;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float v = (float)tv.v[k] + (float)av.v[k];  // zero addend when absent
-        if (a.xbn) {
-          if (a.mask) v = (float)mv.v[k] > 0.f ? v : 0.f;
-          // same expression as the BN apply (bn_apply_k), so the same sign
-          else if (mrec) v = (float)xv.v[k] * msc[k] + msh[k] > 0.f ? v : 0.f;
-          s1[k] += v;
-          s2[k] += v * ((float)xv.v[k] - mu[k]);
-        } else if (a.stats) {
-          s1[k] += v;
-          s2[k] += v * v;
-        }
-        ov.v[k] = (T)v;
+      for (int q = 0; q < G; ++q) {
+        const int t = tid + (g * G + q) * NT;
+        const int m = m0 + t / CPR, n = n0 + (t % CPR) * 8;
+        offb[b][q] = (m < a.M && n < a.Ncol) ? (int)((row_offset(m) + n) * (long)sizeof(T)) : -1;
+        ad[b][q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rad, offb[b][q], 0, 0));
+        mk[b][q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rmk, offb[b][q], 0, 0));
+        xb[b][q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rxb, offb[b][q], 0, 0));
       }
-      if (offb[p] >= 0) {
-        char* yp = (char*)y + offb[p];
-        *(uint4*)yp = __builtin_bit_cast(uint4, ov);
-        if (a.zfill) {
-          const uint4 z = make_uint4(0, 0, 0, 0);
-          const long rb = (long)a.ldy * sizeof(T);
-          *(uint4*)(yp + rb) = z;
-          *(uint4*)(yp + a.YW * rb) = z;
-          *(uint4*)(yp + (a.YW + 1) * rb) = z;
+    };
+    load_group(0, 0);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int b = g & 1;
+      if (g + 1 < NG) load_group(g + 1, b ^ 1);
+#pragma unroll
+      for (int q = 0; q < G; ++q) {
+        const uint4 raw = lds_chunk(tid + (g * G + q) * NT);
+        const Vec<T, 8> tv = __builtin_bit_cast(Vec<T, 8>, raw);
+        const Vec<T, 8> av = __builtin_bit_cast(Vec<T, 8>, ad[b][q]);
+        const Vec<T, 8> mv = __builtin_bit_cast(Vec<T, 8>, mk[b][q]);
+        const Vec<T, 8> xv = __builtin_bit_cast(Vec<T, 8>, xb[b][q]);
+        Vec<T, 8> ov;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float v = (float)tv.v[k] + (float)av.v[k];  // zero addend when absent
+          if (a.xbn) {
+            if (a.mask) v = (float)mv.v[k] > 0.f ? v : 0.f;
+            // same expression as the BN apply (bn_apply_k), so the same sign
+            else if (mrec) v = (float)xv.v[k] * msc[k] + msh[k] > 0.f ? v : 0.f;
+            s1[k] += v;
+            s2[k] += v * ((float)xv.v[k] - mu[k]);
+          } else if (a.stats) {
+            s1[k] += v;
+            s2[k] += v * v;
+          }
+          ov.v[k] = (T)v;
+        }
+        if (offb[b][q] >= 0) {
+          char* yp = (char*)y + offb[b][q];
+          *(uint4*)yp = __builtin_bit_cast(uint4, ov);
+          if (a.zfill) {
+            const uint4 z = make_uint4(0, 0, 0, 0);
+            const long rb = (long)a.ldy * sizeof(T);
+            *(uint4*)(yp + rb) = z;
+            *(uint4*)(yp + a.YW * rb) = z;
+            *(uint4*)(yp + (a.YW + 1) * rb) = z;
+          }
         }
       }
     }
@@ -1465,12 +1482,11 @@ static void launch_glds_short(const IgArgs& a, bool wide, bool three, hipStream_
 // (2 x 80 KB ring, the whole 160 KB LDS).
 template <typename T>
 static void launch_glds_big(const IgArgs& a, bool wide, hipStream_t s) {
-  // forward-style epilogues only (the dgrad operands' loads would spill)
   if (wide)
-    hipLaunchKernelGGL((igemm_glds_k<T, 256, 256, 2, 4, 2, false>),
+    hipLaunchKernelGGL((igemm_glds_k<T, 256, 256, 2, 4, 2>),
                        dim3(((a.M + 255) / 256) * ((a.Ncol + 255) / 256)), dim3(512), 0, s, a);
   else
-    hipLaunchKernelGGL((igemm_glds_k<T, 512, 128, 4, 2, 2, false>),
+    hipLaunchKernelGGL((igemm_glds_k<T, 512, 128, 4, 2, 2>),
                        dim3(((a.M + 511) / 512) * ((a.Ncol + 127) / 128)), dim3(512), 0, s, a);
 }
 
@@ -1622,7 +1638,7 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }
-  if ((algo == IG_ALGO_GBIG256 || algo == IG_ALGO_GBIG512) && fast && !addend && !xbn && !mask) {
+  if ((algo == IG_ALGO_GBIG256 || algo == IG_ALGO_GBIG512) && fast) {
     if (dtype == BF16) launch_glds_big<bf16>(a, algo == IG_ALGO_GBIG256, stream);
     else if (dtype == F16) launch_glds_big<f16>(a, algo == IG_ALGO_GBIG256, stream);
     else return hipErrorInvalidValue;

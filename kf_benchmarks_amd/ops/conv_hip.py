@@ -227,7 +227,7 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
         cands += (IG_MULTI2, IG_MULTI4, IG_SMALL_MULTI4)
     if fast and not _NO_MULTI and KH * KW * C <= 2 * _MULTI_K and C % 64 == 0:
         cands += (IG_GMULTI64,) + ((IG_GMULTI128,) if ncol > 64 else ())
-    if fast and not _NO_BIG and mask is None and xbn is None and addend is None:
+    if fast and not _NO_BIG:
         # big tiles only where they still give every CU a workgroup or more
         M = geo[0] * geo[4] * geo[5]
         if ncol >= 256 and ((M + 255) // 256) * ((ncol + 255) // 256) >= 256:
