@@ -1580,7 +1580,8 @@ enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_G
        IG_ALGO_SMALL = 9, IG_ALGO_GSHORT64 = 10, IG_ALGO_GSHORT128 = 11,
        IG_ALGO_GSHORT64_3 = 12, IG_ALGO_GSHORT128_3 = 13, IG_ALGO_MULTI2 = 14,
        IG_ALGO_MULTI4 = 15, IG_ALGO_SMALL_MULTI4 = 16, IG_ALGO_GMULTI64 = 17,
-       IG_ALGO_GMULTI128 = 18, IG_ALGO_GBIG256 = 19, IG_ALGO_GBIG512 = 20 };
+       IG_ALGO_GMULTI128 = 18, IG_ALGO_GBIG256 = 19, IG_ALGO_GBIG512 = 20,
+       IG_ALGO_GENERIC = 21 };
 
 static bool c8_geometry(int C, int KH, int KW) {
   return C == 8 && (KW == 1 || KW == 2 || KW == 4 || KW == 8) && (KH * KW) % 8 == 0;
@@ -1614,13 +1615,15 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
            (stats && !xbn && !addend) ? kshift : nullptr,
            FastDiv(C), FastDiv(KW), FastDiv(sh), FastDiv(sw), zfill, 0, 0};
   const bool t = trans != 0;
-  const bool c8 = !t && C % IG_BK != 0 && c8_geometry(C, KH, KW);
+  // IG_ALGO_GENERIC: the per-chunk division loader (autotune candidate for
+  // the 8-channel geometry, where it can beat the FAST tap stepping)
+  const bool c8 = !t && C % IG_BK != 0 && c8_geometry(C, KH, KW) && algo != IG_ALGO_GENERIC;
   if (c8) {
     a.c8 = 1;
     a.c8_step = (8 / KW) * W * C;
   }
   const bool fast = !t && (C % IG_BK == 0 || c8) && KH * KW <= 64 && xbytes < (1L << 31) &&
-                    wbytes < (1L << 31) && !igemm_fast_disabled();
+                    wbytes < (1L << 31) && !igemm_fast_disabled() && algo != IG_ALGO_GENERIC;
   const bool narrow = algo == IG_ALGO_CLASSIC_N64 || algo == IG_ALGO_GLDS_N64 ||
                       algo == IG_ALGO_ONEBUF_N64;
   const bool onebuf = algo == IG_ALGO_ONEBUF || algo == IG_ALGO_ONEBUF_N64;

@@ -348,3 +348,50 @@ KFB_API hipError_t kfb_add(int dtype, const void* a, const void* b, void* y, lon
   });
   return hipGetLastError();
 }
+
+// ---- layout padding for few-channel / odd-width convs (recordable in a
+// launch tape, unlike torch's pad): dst [Rp][K][Cp] = src [R][K][C] with zeros
+// in the padding (activations: R = 1, K = pixels; weights: R = Cout,
+// K = KH*KW).
+template <typename T>
+__global__ void __launch_bounds__(256)
+pad_rkc_k(const T* __restrict__ src, T* __restrict__ dst, long total, int R, int K, int C,
+          int Cp) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % Cp);
+    const long rk = i / Cp;
+    const int r = (int)(rk / K);
+    dst[i] = (r < R && c < C) ? src[rk * C + c] : (T)0.f;
+  }
+}
+
+// dst [R][K][C] (fp32) += src [Rp][K][Cp] over r < R, c < C: a padded conv's
+// weight gradient accumulated into the parameter's gradient view
+__global__ void __launch_bounds__(256)
+unpad_accum_f32_k(const float* __restrict__ src, float* __restrict__ dst, long total, int K,
+                  int C, int Cp) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const long rk = i / C;
+    dst[i] += src[rk * Cp + c];
+  }
+}
+
+KFB_API hipError_t kfb_pad_rkc(int dtype, const void* src, void* dst, int R, long K, int C, int Rp,
+                               int Cp, hipStream_t stream) {
+  if (C > Cp || R > Rp) return hipErrorInvalidValue;
+  const long total = (long)Rp * K * Cp;
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((pad_rkc_k<T>), dim3(egrid(total)), dim3(256), 0, stream, (const T*)src,
+                       (T*)dst, total, R, (int)K, C, Cp);
+  });
+  return hipGetLastError();
+}
+
+KFB_API hipError_t kfb_unpad_accum_f32(const float* src, float* dst, int R, long K, int C, int Cp,
+                                       hipStream_t stream) {
+  const long total = (long)R * K * C;
+  hipLaunchKernelGGL(unpad_accum_f32_k, dim3(egrid(total)), dim3(256), 0, stream, src, dst, total,
+                     (int)K, C, Cp);
+  return hipGetLastError();
+}

@@ -37,13 +37,15 @@ IG_MULTI2, IG_MULTI4, IG_SMALL_MULTI4 = 14, 15, 16
 IG_GMULTI64, IG_GMULTI128 = 17, 18
 # 8-wave LDS-DMA kernels with 128 x 64 wave tiles: 256 x 256 / 512 x 128 tiles
 IG_GBIG256, IG_GBIG512 = 19, 20
+IG_GENERIC = 21  # the generic (per-chunk division) loader, forced
 IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N64,
             "glds_n64": IG_GLDS_N64, "onebuf": IG_ONEBUF, "onebuf_n64": IG_ONEBUF_N64,
             "tall512": IG_TALL512, "tall256": IG_TALL256, "small": IG_SMALL,
             "gshort64": IG_GSHORT64, "gshort128": IG_GSHORT128, "gshort64_3": IG_GSHORT64_3,
             "gshort128_3": IG_GSHORT128_3, "multi2": IG_MULTI2, "multi4": IG_MULTI4,
             "small_multi4": IG_SMALL_MULTI4, "gmulti64": IG_GMULTI64,
-            "gmulti128": IG_GMULTI128, "gbig256": IG_GBIG256, "gbig512": IG_GBIG512}
+            "gmulti128": IG_GMULTI128, "gbig256": IG_GBIG256, "gbig512": IG_GBIG512,
+            "generic": IG_GENERIC}
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
@@ -234,6 +236,9 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
             cands += (IG_GBIG256,)
         if 64 < ncol <= 256 and ((M + 511) // 512) * ((ncol + 127) // 128) >= 256:
             cands += (IG_GBIG512,)
+    if fast and C % 64 != 0:
+        # 8-channel geometry: the generic loader competes with the FAST ones
+        cands += (IG_GENERIC,)
     if ncol > 64:  # 64-wide tiles: more workgroups for small-M layers
         cands += (IG_CLASSIC_N64, IG_GLDS_N64, IG_ONEBUF_N64) if fast else (IG_CLASSIC_N64,)
     if len(cands) == 1:
@@ -383,19 +388,43 @@ def conv_wgrad(dy, x, w_shape, stride, pads, out=None):
     _, OH, OW, _ = dy.shape
     sh, sw = stride
     pt, pb, pl, pr = pads
-    dw = out if out is not None else torch.zeros((cout, KH, KW, C), dtype=torch.float32,
-                                                 device=x.device)
+    if out is not None:
+        dw = out
+    elif x.is_cuda:
+        dw = N.zero_(torch.empty((cout, KH, KW, C), dtype=torch.float32, device=x.device))
+    else:
+        dw = torch.zeros((cout, KH, KW, C), dtype=torch.float32, device=x.device)
     geo = (n, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, cout)
     target = _tune_wgrad(dy, x, dw, geo) if _AUTOTUNE else _WGRAD_TARGET_BLOCKS
     _wgrad_launch(dy, x, dw, geo, target)
     return dw
 
 
+N.register_optional("kfb_pad_rkc", [N.I, N.P, N.P, N.I, N.L, N.I, N.I, N.I, N.P])
+N.register_optional("kfb_unpad_accum_f32", [N.P, N.P, N.I, N.L, N.I, N.I, N.P])
+
+
+def _pad_rkc(t, R, K, C, Rp, Cp):
+    """[R][K][C] -> zero-padded [Rp][K][Cp] (native: recordable in a launch tape)."""
+    out = torch.empty((Rp * K * Cp,), dtype=t.dtype, device=t.device)
+    N.call("kfb_pad_rkc", N.dt(t), t.contiguous().data_ptr(), out.data_ptr(), R, K, C, Rp, Cp,
+           N.stream(t.device))
+    return out
+
+
 def _padded_input(x, cin_p):
     """Channel-padded copy of a few-channel network input (RGB 3 -> 8),
     made every step (no cross-step caching, also for the constant synthetic
     batch: the timed step does all of its work)."""
-    return torch.nn.functional.pad(x, (0, cin_p - x.shape[-1]))
+    if not x.is_cuda:
+        return torch.nn.functional.pad(x, (0, cin_p - x.shape[-1]))
+    n, H, W, C = x.shape
+    return _pad_rkc(x, 1, n * H * W, C, 1, cin_p).view(n, H, W, cin_p)
+
+
+def _padded_weight(wl, cout_p, cin_p):
+    cout, KH, KW, cin = wl.shape
+    return _pad_rkc(wl, cout, KH * KW, cin, cout_p, cin_p).view(cout_p, KH, KW, cin_p)
 
 
 # Weight gradients on a side stream (KFB_WGRAD_STREAM=0: on the compute stream)
@@ -572,9 +601,9 @@ class _Conv2d(torch.autograd.Function):
         xp, wp = x, wl
         if cin_p != cin:
             xp = _padded_input(x, cin_p)
-            wp = torch.nn.functional.pad(wp, (0, cin_p - cin))
+        if cin_p != cin or cout_p != cout:
+            wp = _padded_weight(wl.contiguous(), cout_p, cin_p)
         if cout_p != cout:
-            wp = torch.nn.functional.pad(wp, (0, 0, 0, 0, 0, 0, 0, cout_p - cout))
             stats = None
             if bd is not None:
                 bd = torch.nn.functional.pad(bd, (0, cout_p - cout))
@@ -626,7 +655,8 @@ class _Conv2d(torch.autograd.Function):
         dy = dy.contiguous()
         cout_p = wp.shape[0]
         if cout_p != cout:
-            dy = torch.nn.functional.pad(dy, (0, cout_p - cout))
+            rows = dy.numel() // cout
+            dy = _pad_rkc(dy, 1, rows, cout, 1, cout_p).view(tuple(dy.shape[:-1]) + (cout_p,))
         dx = None
         if ctx.x_needs_grad:
             link = ctx.link
@@ -704,6 +734,20 @@ class _Conv2d(torch.autograd.Function):
                     cb = getattr(w, "_kfb_ready_cb", None)
                     if cb is not None:
                         cb(w)
+                return dx, None, None, None, None, None, None, db, None
+            padded_w = cout_p != cout or wp.shape[-1] != cin
+            if padded_w and sink is not None and _fuse_enabled():
+                # padded weight gradient, accumulated natively into the
+                # parameter's gradient view (no slicing copy, no autograd add)
+                full = torch.empty(tuple(wp.shape), dtype=torch.float32, device=dy.device)
+                N.zero_(full)
+                conv_wgrad(dy, xp, wp.shape, stride, pads, out=full)
+                KH, KW = wp.shape[1], wp.shape[2]
+                N.call("kfb_unpad_accum_f32", full.data_ptr(), sink.data_ptr(), cout, KH * KW,
+                       cin, wp.shape[-1], N.stream(dy.device))
+                cb = getattr(w, "_kfb_ready_cb", None)
+                if cb is not None:
+                    cb(w)
                 return dx, None, None, None, None, None, None, db, None
             dw = conv_wgrad(dy, xp, wp.shape, stride, pads, out=sink if direct else None)
             if direct:
