@@ -149,8 +149,11 @@ def main(argv=None):
     world.barrier(bdev)
     sync()
     start = time.perf_counter()
+    host = 0.0
     for _ in range(a.steps):
+        h0 = time.perf_counter()
         loss, _ = bench.train_step()
+        host += time.perf_counter() - h0
     sync()
     world.barrier(bdev)
     sync()
@@ -230,6 +233,9 @@ def main(argv=None):
                        "fp32_products": conv_f32.products() if a.dtype == "fp32" else None,
                        "loss_last": final_loss},
             "comm": comm_info,
+            # host time spent issuing a step (rank 0; the step is host-bound
+            # when this approaches ms_per_step)
+            "host_ms_per_step": round(1000.0 * host / a.steps, 3),
             "weights_in_sync": in_sync,
         }
         print(json.dumps(out))

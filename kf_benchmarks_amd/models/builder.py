@@ -356,12 +356,16 @@ class ConvNetBuilder:
         self.counts[name] += 1
         with self.scope(name):
             col_layers, col_sizes = [], []
+            # every column reads x: their input gradients sum natively
+            heads = [c for c, col in enumerate(cols) if col and col[0][0] != "share"]
+            xs = dict(zip(heads, F.fanout(x, len(heads)))) if not self.meta else {}
             for c, col in enumerate(cols):
                 col_layers.append([])
                 col_sizes.append([])
                 for li, layer in enumerate(col):
                     ltype, args = layer[0], layer[1:]
-                    kwargs = {"input_layer": x, "num_channels_in": cin} if li == 0 else {}
+                    kwargs = ({"input_layer": xs.get(c, x), "num_channels_in": cin}
+                              if li == 0 else {})
                     if ltype == "conv":
                         self.conv(*args, **kwargs)
                     elif ltype == "mpool":

@@ -544,6 +544,39 @@ class _Add(torch.autograd.Function):
         return dy, dy, None
 
 
+class _FanOut(torch.autograd.Function):
+    """One tensor read by k branches: k aliases whose gradients are summed by
+    native adds in the backward (autograd would sum them with torch kernels,
+    which a launch tape cannot record)."""
+
+    @staticmethod
+    def forward(ctx, x, k):
+        ctx.k = k
+        return tuple(x.view_as(x) for _ in range(k))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        gs = [g for g in grads if g is not None]
+        if not gs:
+            return None, None
+        acc = gs[0].contiguous()
+        for g in gs[1:]:
+            g = g.contiguous()
+            y = torch.empty_like(acc)
+            N.call("kfb_add", N.dt(acc), acc.data_ptr(), g.data_ptr(), y.data_ptr(), acc.numel(),
+                   0, N.stream(acc.device))
+            acc = y
+        return acc, None
+
+
+def fanout(x, k: int):
+    """``k`` aliases of ``x`` for ``k`` consumers (GPU: native gradient sum)."""
+    if k <= 1 or not _on_gpu(x) or getattr(x, "_kfb_bn_link", None) is not None \
+            or not x.requires_grad:
+        return [x] * k
+    return list(_FanOut.apply(x, k))
+
+
 def add(a, b, relu: bool = False):
     if not _on_gpu(a):
         y = a + b

@@ -46,7 +46,7 @@ class TapeError(RuntimeError):
         self.outputs = outputs  # the step's results when the step itself completed
 
 
-def _pack(v, code):
+def _pack(v, code, keep=None):
     if isinstance(v, ctypes._SimpleCData):
         v = v.value
     if code == "f":
@@ -56,6 +56,12 @@ def _pack(v, code):
             return 0
         if isinstance(v, int):
             return v & _MASK
+        if isinstance(v, ctypes.Array) and keep is not None:
+            # a host argument table (e.g. the concat kernel's pointer list):
+            # the tape keeps its own copy alive and passes that every replay
+            copy = (v._type_ * len(v))(*v)
+            keep.append(copy)
+            return ctypes.addressof(copy)
         raise TapeError("pointer argument %r cannot be recorded" % (v,))
     return int(v) & _MASK
 
@@ -71,6 +77,7 @@ class Recorder:
         self.dyn: List[Tuple[int, int, str, str]] = []  # (op, arg, key, code)
         self._codes = {}
         self.names: List[str] = []
+        self._keep = []  # host argument tables the recorded calls point into
 
     def _types(self, name, fn):
         t = self._codes.get(name)
@@ -94,7 +101,7 @@ class Recorder:
             if isinstance(a, N.Dyn):
                 dyn.append((op, k, a.key, c))
                 a = out[k] = a.value
-            slots[k] = _pack(a, c)
+            slots[k] = _pack(a, c, self._keep)
         fp = ctypes.cast(fn, ctypes.c_void_p).value
         got = N.load().kfb_tape_add(self.h, fp, types.encode(), slots, len(args))
         if got != op:

@@ -137,8 +137,12 @@ def test_one_rank_rccl_resnet50_overlap(cuda, tmp_path, native, tape):
               data_format="NHWC", variable_update="kungfu", kungfu_option="sync_sgd",
               bucket_size_mb=4.0, launch_tape=tape)
     steps = 5 if tape else 3
-    (a,) = _run(kw, steps, tmp_path, n=1, env_extra=dict(_RCCL, KFB_NATIVE_COMM=native),
-                tag="rccl")
+    # (taped: no per-step gradient probe - its torch reads inside the step
+    # would make the recording fall back to eager)
+    env = dict(_RCCL, KFB_NATIVE_COMM=native, KFB_TAPE_STRICT="1" if tape else None)
+    if tape:
+        env["KFB_TEST_GRAD_SEGS"] = None
+    (a,) = _run(kw, steps, tmp_path, n=1, env_extra=env, tag="rccl")
     (b,) = _run(dict(kw, launch_tape=False), steps, tmp_path, n=1, env_extra=_NOCOMM,
                 tag="nocomm")
     assert a["backend"] == ("rccl" if native == "1" else "nccl")
