@@ -102,7 +102,8 @@ def main(argv=None):
             print("bench.py: --gpus=%d but only %d GPU(s) visible" % (a.gpus, have),
                   file=sys.stderr)
             return 2
-    data_name = a.data_name or {"ssd300": "coco", "deepspeech2": "librispeech"}.get(a.model)
+    data_name = a.data_name or {"ssd300": "coco", "deepspeech2": "librispeech"}.get(a.model) \
+        or ("imagenet" if a.data_dir else None)
     p = P.make_params(model=a.model, batch_size=a.batch_size, num_gpus=1, data_name=data_name,
                       variable_update=a.variable_update, kungfu_option=a.kungfu_option,
                       optimizer=a.optimizer, use_bf16=a.dtype == "bf16",
@@ -193,11 +194,12 @@ def main(argv=None):
     images = a.batch_size * n * a.steps
     value = images / elapsed
     if world.is_chief:
-        headline = a.model == "resnet50"
+        headline = a.model == "resnet50" and not a.data_dir
         base = BASELINE_IMG_PER_SEC.get(n) if headline else None
         out = {
             "metric": ("images/sec (whole node) ResNet-50 synthetic at 1/2/4/8 MI355X"
-                       if headline else "images/sec (whole node) %s synthetic" % a.model),
+                       if headline else "images/sec (whole node) %s %s"
+                       % (a.model, "real data" if a.data_dir else "synthetic")),
             "value": round(value, 2),
             "unit": "images/sec",
             "n_gpus": n,

@@ -32,6 +32,7 @@ for spec in "$@"; do
   if [ "$kind" = prof ] && [ $rc -eq 0 ]; then
     f=$(find "$OUT/prof$n" -name "*kernel_trace.csv" | head -n 1)
     [ -n "$f" ] && python3 scripts/kernel_stats.py "$f" --last-steps 4 --top 40 > "$OUT/kernel_summary$n.txt" && head -n 25 "$OUT/kernel_summary$n.txt"
+    [ -n "$f" ] && (cd scripts && python3 step_overlap.py "$f" > "$OUT/overlap$n.txt" 2>&1; head -n 8 "$OUT/overlap$n.txt")
     rm -f "$OUT"/prof$n/*kernel_stats.csv "$OUT"/prof$n/*domain_stats.csv
   fi
   case $rc in 124|134|137|139) echo "FATAL in step $n, stopping"; exit $rc;; esac
