@@ -489,6 +489,8 @@ class BenchmarkCNN:
         p = self.params
         if self.device_type != "cuda" or p.kernel_impl != "hip":
             return "not a HIP device run"
+        if self.tower_mode:
+            return "tower processes average the reported loss on the host"
         if self.world.communicates:
             if self.world.native is None:
                 return "device collectives go through torch.distributed (not recordable)"

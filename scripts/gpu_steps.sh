@@ -21,7 +21,7 @@ for spec in "$@"; do
     pytest) timeout -k 10 900 python -u -m pytest $args -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > "$log" 2>&1 ;;
     bench) env $(echo "$args" | tr ' ' '\n' | grep '=' | grep -v '^--') timeout -k 10 600 python bench.py $(echo "$args" | tr ' ' '\n' | grep -v '^[A-Z_]*=' ) > "$log" 2>&1 ;;
     smoke) timeout -k 10 400 python -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1 ;;
-    py) timeout -k 10 600 python $args > "$log" 2>&1 ;;
+    py) env $(echo "$args" | tr ' ' '\n' | grep '^[A-Z_][A-Z0-9_]*=' ) timeout -k 10 600 python $(echo "$args" | tr ' ' '\n' | grep -v '^[A-Z_][A-Z0-9_]*=' ) > "$log" 2>&1 ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
          -d "$OUT/prof$n" -o run -- python3 "$ROOT/bench.py" $args) > "$log" 2>&1 ;;
