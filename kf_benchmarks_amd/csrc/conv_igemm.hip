@@ -30,6 +30,9 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <utility>
 
 namespace kfb {
 
@@ -1090,6 +1093,256 @@ __global__ void __launch_bounds__(256, (glds_occupancy<BM, BN, 256>()))
   }
 }
 
+// ------------------------------------------------------------ stream-K igemm
+// Persistent form of the 4-wave 128 x 128 LDS-DMA tile whose workgroups
+// share the tail of the tile space along K.  A launch of T tiles on P
+// resident workgroups (2 per CU) otherwise ends in a partial round: 784
+// tiles (the 14x14 3x3 convs at batch 256) on 512 slots are 1.53 rounds run
+// as 2, i.e. 23 % of the chip idles.  Here tiles [0, Tdp) run data-parallel
+// (Tdp a multiple of P, tile w + r*P on workgroup w), and the K steps of the
+// other Tsk = T - Tdp tiles (P + T % P of them, or all T when T < P) are cut
+// into P equal contiguous ranges, one per workgroup, so every workgroup ends
+// at the same time.  A tile whose K steps span several workgroups is summed
+// by its last-arriving contributor: each contributor stores its fp32 partial
+// tile (workspace slot 0 = the tile its range starts in, 1 = the tile it
+// ends in; every other tile of a range is whole) with write-through stores,
+// waits for them and takes a relaxed agent-scope ticket; the one that draws
+// the last ticket acquires (agent scope), sums every contributor's partial in contributor
+// order (so the result does not depend on who arrived last), resets the
+// ticket for the next launch and runs the ordinary epilogue.  No workgroup
+// ever waits for another, so nothing can deadlock whatever else occupies
+// the chip (the weight-gradient side stream).  The split sums K in a
+// different order than the one-tile kernels: the autotune's candidates no
+// longer agree bitwise, only to fp32 rounding.
+struct SkArgs {
+  float* ws;  // [P][2][128 * 128] partial tiles
+  int* cnt;   // [Tsk] tickets, zero between launches
+  int T, nk, Tdp;
+  long L;  // Tsk * nk: K steps of the stream-K region
+};
+
+// workgroup whose range holds step i of the stream-K region (P ranges of L)
+__device__ __forceinline__ int sk_owner(long i, long L, int P) {
+  return (int)(((i + 1) * P - 1) / L);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256, 2) igemm_sk_k(IgArgs a, SkArgs sk) {
+  constexpr int BM = 128, BN = 128, WGM = 2, WGN = 2, NT = 256;
+  constexpr int SLAB = NT / 8;
+  constexpr int TM = BM / WGM / 16, TN = BN / WGN / 16;
+  constexpr int XI = BM / SLAB, WI = BN / SLAB;
+  constexpr int STAGE = (BM + BN) * IG_BK;
+  static_assert(BM * BN <= STAGE && NT * 16 * 4 <= STAGE * (int)sizeof(T), "epilogue staging");
+  __shared__ __attribute__((aligned(16))) T smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int P = gridDim.x;
+  const int w = xcd_remap(blockIdx.x, P);  // consecutive ranges share an XCD's L2
+  const int ntiles = (a.Ncol + BN - 1) / BN;
+  const int OHW = a.OH * a.OW;
+  const int rr = tid >> 3;
+  const int kc = (lane & 7) ^ ((rr >> 1) & 7);
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.wbytes, 0x00020000);
+  unsigned long long tapmask[XI];
+  int xoff[XI], woff[WI];
+  int s_cc = 0, s_kh = 0, s_kw = 0, s_tap = 0, s_tapi = 0, s_k = 0;
+  // operand offsets of `tile` and the K state of step k0
+  auto setup = [&](int tile, int k0) {
+    const int m0 = (tile / ntiles) * BM, n0 = (tile % ntiles) * BN;
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int m = m0 + i * SLAB + rr;
+      const bool ok = m < a.M;
+      const int mm = ok ? m : 0;
+      const int img = mm / OHW, rem = mm - img * OHW;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      const int xh = oh * a.sh - a.pt, xw = ow * a.sw - a.pl;
+      unsigned long long mk = 0;
+      for (int kh = 0; kh < a.KH; ++kh)
+        for (int kw = 0; kw < a.KW; ++kw) {
+          const bool in = (unsigned)(xh + kh) < (unsigned)a.H && (unsigned)(xw + kw) < (unsigned)a.W;
+          mk |= (unsigned long long)(in && ok) << (kh * a.KW + kw);
+        }
+      tapmask[i] = mk;
+      xoff[i] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + kc * 8;
+    }
+#pragma unroll
+    for (int j = 0; j < WI; ++j) woff[j] = (n0 + j * SLAB + rr) * a.Ktot + kc * 8;
+    s_k = k0 * IG_BK;
+    s_tapi = s_k / a.C;
+    s_cc = s_k - s_tapi * a.C;
+    s_kh = s_tapi / a.KW;
+    s_kw = s_tapi - s_kh * a.KW;
+    s_tap = (s_kh * a.W + s_kw) * a.C;
+  };
+  auto issue = [&](int stage) {
+    T* xs = smem + stage * STAGE;
+    T* ws = xs + BM * IG_BK;
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const bool ok = (tapmask[i] >> s_tapi) & 1ull;
+      const int off = ok ? (xoff[i] + s_tap + s_cc) * (int)sizeof(T) : -1;
+      dma16(xrs, xs + (i * SLAB + wid * 8) * IG_BK, off);
+    }
+#pragma unroll
+    for (int j = 0; j < WI; ++j)
+      dma16(wrs, ws + (j * SLAB + wid * 8) * IG_BK, (woff[j] + s_k) * (int)sizeof(T));
+    s_k += IG_BK;
+    s_cc += IG_BK;
+    if (s_cc == a.C) {
+      s_cc = 0;
+      ++s_tapi;
+      if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
+      s_tap = (s_kh * a.W + s_kw) * a.C;
+    }
+  };
+  v4f acc[TN][TM];
+  const int wm = wid % WGM, wn = wid / WGM;
+  auto compute = [&](int stage) {
+    const T* xs = smem + stage * STAGE;
+    const T* ws = xs + BM * IG_BK;
+#pragma unroll
+    for (int ks = 0; ks < IG_BK / 32; ++ks) {
+      const int chunk = ks * 4 + (lane >> 4);
+      v8s af[TN], bfr[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+        af[i] = *(const v8s*)(ws + swz_off(wn * (BN / WGN) + i * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+        bfr[j] = *(const v8s*)(xs + swz_off(wm * (BM / WGM) + j * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = Mfma<T>::run(af[i], bfr[j], acc[i][j]);
+    }
+  };
+
+  // Work items: the data-parallel tiles w, w + P, ... < Tdp, then the K
+  // range [i, e) of the stream-K region cut at tile boundaries.
+  int dp = w;
+  long si = (long)w * sk.L / P;
+  const long se = (long)(w + 1) * sk.L / P;
+  auto next_item = [&](int& tile, int& k0, int& k1) -> bool {
+    if (dp < sk.Tdp) {
+      tile = dp;
+      k0 = 0;
+      k1 = sk.nk;
+      dp += P;
+      return true;
+    }
+    if (si >= se) return false;
+    const int tl = (int)(si / sk.nk);
+    k0 = (int)(si - (long)tl * sk.nk);
+    k1 = (se - si) < (long)(sk.nk - k0) ? k0 + (int)(se - si) : sk.nk;
+    tile = sk.Tdp + tl;
+    si += k1 - k0;
+    return true;
+  };
+
+  int tile, k0, k1;
+  bool have = next_item(tile, k0, k1);
+  if (have) {
+    setup(tile, k0);
+    issue(0);
+  }
+  volatile int* flag = (volatile int*)smem;  // stage 0, read before any later DMA lands there
+  const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)sk.ws, (short)0, (int)((long)P * 2 * BM * BN * sizeof(float)), 0x00020000);
+#pragma unroll 1
+  while (have) {
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    int st = 0;  // every item's first step sits in stage 0
+    for (int kt = k0; kt < k1; ++kt) {
+      wait_vmcnt<0>();
+      lds_barrier();
+      if (kt + 1 < k1) issue(st ^ 1);
+      compute(st);
+      st ^= 1;
+    }
+    __syncthreads();  // fragment reads done: the ring is free
+    int ntile = 0, nk0 = 0, nk1 = 0;
+    const bool more = next_item(ntile, nk0, nk1);
+    auto next = [&]() {
+      if (more) {
+        setup(ntile, nk0);
+        issue(0);
+      }
+    };
+    const int m0 = (tile / ntiles) * BM, n0 = (tile % ntiles) * BN;
+    bool finish = k0 == 0 && k1 == sk.nk;
+    if (!finish) {
+      // partial tile: publish it, and sum the tile if this is the last piece
+      const int tl = tile - sk.Tdp;
+      const long t0 = (long)tl * sk.nk;
+      const int c0 = sk_owner(t0, sk.L, P), c1 = sk_owner(t0 + sk.nk - 1, sk.L, P);
+      auto slot_of = [&](int c) -> float* {
+        const int first_tile = (int)(((long)c * sk.L / P) / sk.nk);
+        return sk.ws + ((long)c * 2 + (first_tile == tl ? 0 : 1)) * (BM * BN);
+      };
+      // write-through (sc1) stores: visible past this XCD's L2 once waited
+      // for, so no release fence (an agent release writes back every dirty
+      // line of the L2, this launch's output tiles included)
+      const int pbase = (int)((slot_of(w) - sk.ws) * sizeof(float));
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[i][j]), wsr,
+                                                 pbase + ((i * TM + j) * NT + tid) * 16, 0, 16);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const int prev =
+            __hip_atomic_fetch_add(sk.cnt + tl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == c1 - c0;
+        if (last) {
+          __hip_atomic_store(sk.cnt + tl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *flag = last;
+      }
+      __syncthreads();
+      finish = __builtin_amdgcn_readfirstlane(*flag) != 0;
+      lds_barrier();  // every wave has read the flag before stage 0 is reused
+      if (finish) {
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+        for (int c = c0; c <= c1; ++c) {
+          const int cbase = (int)((slot_of(c) - sk.ws) * sizeof(float));
+#pragma unroll
+          for (int i = 0; i < TN; ++i)
+#pragma unroll
+            for (int j = 0; j < TM; ++j)
+              acc[i][j] += __builtin_bit_cast(
+                  v4f, __builtin_amdgcn_raw_buffer_load_b128(
+                           wsr, cbase + ((i * TM + j) * NT + tid) * 16, 0, 16));
+        }
+      }
+    }
+    if (finish)
+      ig_epilogue<T, BM, BN, NT, WGM, WGN, decltype(next)>(a, acc, smem + STAGE, m0, n0, wm, wn,
+                                                           next);
+    else
+      next();
+    tile = ntile;
+    k0 = nk0;
+    k1 = nk1;
+    have = more;
+  }
+}
+
 // ------------------------------------------------------------------ wgrad
 struct WgArgs {
   const void* dy;  // [M][Ncol]  (NHWC output gradient, Ncol = Cout)
@@ -1513,6 +1766,64 @@ static void launch_mt(const IgArgs& a, int tpw, hipStream_t s) {
     hipLaunchKernelGGL((igemm_mt_k<T, BM, 64, 2>), dim3((nwg + 1) / 2), dim3(256), 0, s, a);
 }
 
+// Stream-K launch: P = CUs x resident workgroups, per-(device, stream)
+// workspace (partial tiles + tickets) allocated on first use and kept (a
+// recorded launch tape replays the same pointers; kernels of one stream run
+// in order, so one workspace per stream is never shared by two launches in
+// flight).
+struct SkWorkspace {
+  float* ws = nullptr;
+  int* cnt = nullptr;
+  int P = 0;
+};
+
+template <typename T>
+static hipError_t launch_sk(const IgArgs& a, hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, SkWorkspace> cache;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  SkWorkspace wsp;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    SkWorkspace& c = cache[{dev, s}];
+    if (!c.ws) {
+      int cus = 0, per = 0;
+      e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (e != hipSuccess) return e;
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, igemm_sk_k<T>, 256, 0);
+      if (e != hipSuccess) return e;
+      if (per < 1) per = 1;
+      const int P = cus * per;
+      e = hipMalloc((void**)&c.ws, (size_t)P * 2 * 128 * 128 * sizeof(float));
+      if (e != hipSuccess) return e;
+      e = hipMalloc((void**)&c.cnt, (size_t)2 * P * sizeof(int));
+      if (e != hipSuccess) return e;
+      e = hipMemsetAsync(c.cnt, 0, (size_t)2 * P * sizeof(int), s);
+      if (e != hipSuccess) return e;
+      c.P = P;
+    }
+    wsp = c;
+  }
+  const int P = wsp.P;
+  const int tiles = ((a.M + 127) / 128) * ((a.Ncol + 127) / 128);
+  SkArgs sk;
+  sk.ws = wsp.ws;
+  sk.cnt = wsp.cnt;
+  sk.T = tiles;
+  sk.nk = a.Ktot / IG_BK;
+  // stream-K region: the last partial round plus one full round (or all of
+  // a launch smaller than one round); none when the rounds come out even
+  const int Tsk = tiles < P ? tiles : (tiles % P == 0 ? 0 : P + tiles % P);
+  sk.Tdp = tiles - Tsk;
+  sk.L = (long)Tsk * sk.nk;
+  const int grid = (sk.Tdp > 0 || sk.L >= P) ? P : (int)sk.L;
+  if (grid < 1) return hipSuccess;
+  hipLaunchKernelGGL(igemm_sk_k<T>, dim3(grid), dim3(256), 0, s, a, sk);
+  return hipGetLastError();
+}
+
 template <typename T, int BM, int BN>
 static void launch_ig(const IgArgs& a, bool trans, bool fast, hipStream_t s, bool onebuf = false) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
@@ -1572,7 +1883,8 @@ using namespace kfb;
 //   stores); IG_ALGO_SMALL_MULTI4: 64 x 64 tiles, 4 per workgroup.
 //   IG_ALGO_GMULTI64 / GMULTI128: igemm_glds_mt_k, GSHORT64 / GSHORT128 with 2
 //   tiles per workgroup (next tile's DMAs land in stage 0 while the epilogue
-//   stages in stage 1).  Forward-style
+//   stages in stage 1).  IG_ALGO_SK128: igemm_sk_k, the GSHORT128 tile
+//   persistent with the last partial round split along K.  Forward-style
 //   epilogues only: with addend / mask / xbn they fall through to the
 //   one-tile kernels.
 enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_GLDS_N64 = 4,
@@ -1581,7 +1893,7 @@ enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_G
        IG_ALGO_GSHORT64_3 = 12, IG_ALGO_GSHORT128_3 = 13, IG_ALGO_MULTI2 = 14,
        IG_ALGO_MULTI4 = 15, IG_ALGO_SMALL_MULTI4 = 16, IG_ALGO_GMULTI64 = 17,
        IG_ALGO_GMULTI128 = 18, IG_ALGO_GBIG256 = 19, IG_ALGO_GBIG512 = 20,
-       IG_ALGO_GENERIC = 21 };
+       IG_ALGO_GENERIC = 21, IG_ALGO_SK128 = 22 };
 
 static bool c8_geometry(int C, int KH, int KW) {
   return C == 8 && (KW == 1 || KW == 2 || KW == 4 || KW == 8) && (KH * KW) % 8 == 0;
@@ -1646,6 +1958,11 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
     else if (dtype == F16) launch_glds_big<f16>(a, algo == IG_ALGO_GBIG256, stream);
     else return hipErrorInvalidValue;
     return hipGetLastError();
+  }
+  if (algo == IG_ALGO_SK128 && fast && !c8) {
+    if (dtype == BF16) return launch_sk<bf16>(a, stream);
+    if (dtype == F16) return launch_sk<f16>(a, stream);
+    return hipErrorInvalidValue;
   }
   if ((algo == IG_ALGO_GMULTI64 || algo == IG_ALGO_GMULTI128) && fast && !c8) {
     const bool wide = algo == IG_ALGO_GMULTI128;

@@ -15,6 +15,7 @@ Channel counts that are not multiples of 8 (the RGB stem, DenseNet growth
 from __future__ import annotations
 
 import os
+import sys
 
 import torch
 
@@ -38,6 +39,8 @@ IG_GMULTI64, IG_GMULTI128 = 17, 18
 # 8-wave LDS-DMA kernels with 128 x 64 wave tiles: 256 x 256 / 512 x 128 tiles
 IG_GBIG256, IG_GBIG512 = 19, 20
 IG_GENERIC = 21  # the generic (per-chunk division) loader, forced
+# persistent 128 x 128 LDS-DMA tile, last partial round split along K (stream-K)
+IG_SK128 = 22
 IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N64,
             "glds_n64": IG_GLDS_N64, "onebuf": IG_ONEBUF, "onebuf_n64": IG_ONEBUF_N64,
             "tall512": IG_TALL512, "tall256": IG_TALL256, "small": IG_SMALL,
@@ -45,7 +48,7 @@ IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N6
             "gshort128_3": IG_GSHORT128_3, "multi2": IG_MULTI2, "multi4": IG_MULTI4,
             "small_multi4": IG_SMALL_MULTI4, "gmulti64": IG_GMULTI64,
             "gmulti128": IG_GMULTI128, "gbig256": IG_GBIG256, "gbig512": IG_GBIG512,
-            "generic": IG_GENERIC}
+            "generic": IG_GENERIC, "sk128": IG_SK128}
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
@@ -53,6 +56,7 @@ _NO_GSHORT = os.environ.get("KFB_IGEMM_NOGSHORT", "0") == "1"  # A/B knob: drop 
 _GSHORT3 = os.environ.get("KFB_IGEMM_GSHORT3", "1") != "0"  # A/B knob: the 3-stage forms
 _NO_MULTI = os.environ.get("KFB_IGEMM_NOMULTI", "0") == "1"  # A/B knob: drop IG_*MULTI*
 _NO_BIG = os.environ.get("KFB_IGEMM_NOBIG", "0") == "1"  # A/B knob: drop IG_GBIG*
+_NO_SK = os.environ.get("KFB_IGEMM_NOSK", "0") == "1"  # A/B knob: drop IG_SK128
 # largest K (= KH*KW*Cin) offered the multi-tile candidates (register-staged;
 # the LDS-DMA form gets twice that)
 _MULTI_K = int(os.environ.get("KFB_IGEMM_MULTI_K", "2304"))
@@ -174,7 +178,11 @@ def _igemm_call(algo, x, wmat, y, geo, stats=None, mask=None, xbn=None, mean=Non
            N.ptr(bias), int(relu), algo, N.ptr(stats_shift(stats)), N.stream(x.device))
 
 
-def _time_candidates(cands, run, rounds=2, reps=3):
+_TUNE_LOG = os.environ.get("KFB_AUTOTUNE_LOG", "0") == "1"  # print every timed choice
+_ALGO_NAMES = {}
+
+
+def _time_candidates(cands, run, rounds=2, reps=3, label=None):
     """The fastest candidate: each is warmed once, then timed ``reps``
     back-to-back calls per round over ``rounds`` interleaved rounds (min
     per candidate).  The device is synchronized first so no other stream's
@@ -194,14 +202,23 @@ def _time_candidates(cands, run, rounds=2, reps=3):
             ev1.record()
             ev1.synchronize()
             best_t[c] = min(best_t[c], ev0.elapsed_time(ev1))
-    return min(best_t, key=best_t.get)
+    best = min(best_t, key=best_t.get)
+    if _TUNE_LOG and label is not None:
+        if not _ALGO_NAMES:
+            _ALGO_NAMES.update({v: k for k, v in IG_ALGOS.items()})
+        ranked = sorted(best_t.items(), key=lambda kv: kv[1])
+        print("[autotune] %s: %s" % (label, "  ".join(
+            "%s %.1f" % (_ALGO_NAMES.get(c, c), 1e3 * t / reps) for c, t in ranked)),
+            file=sys.stderr, flush=True)
+    return best
 
 
 def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bact=(None, False)):
     """Per-geometry kernel choice, timed once on the real operands with the
     real fused epilogue (the role cuDNN's algorithm autotune plays for the
-    reference): all kernels run the same K order, so the choice does not
-    change the numerics.  ``fused`` = (stats, mask, xbn, mean, addend, mcoef); the
+    reference): all kernels but IG_SK128 run the same K order (stream-K adds
+    fp32 partial sums of K ranges), so the choice changes the numerics by
+    fp32 rounding at most.  ``fused`` = (stats, mask, xbn, mean, addend, mcoef); the
     timing runs write a scratch output and scratch statistics."""
     if _IG_FORCE is not None:
         return _IG_FORCE
@@ -236,6 +253,9 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
             cands += (IG_GBIG256,)
         if 64 < ncol <= 256 and ((M + 511) // 512) * ((ncol + 127) // 128) >= 256:
             cands += (IG_GBIG512,)
+    if fast and not _NO_SK and C % 64 == 0 and ncol > 64:
+        # stream-K: pays where the 128 x 128 tiles leave a partial last round
+        cands += (IG_SK128,)
     if fast and C % 64 != 0:
         # 8-channel geometry: the generic loader competes with the FAST ones
         cands += (IG_GENERIC,)
@@ -251,7 +271,8 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
         addend = addend.clone()  # in-place accumulation target: time on a copy
     sstats = torch.zeros_like(stats) if stats is not None else None
     args = (x, wmat, scratch, geo, sstats, mask, xbn, mean, addend, mcoef) + tuple(bact)
-    best = _time_candidates(cands, lambda algo: _igemm_call(algo, *args))
+    best = _time_candidates(cands, lambda algo: _igemm_call(algo, *args),
+                            label="igemm %s%s" % (geo, " +bn" if xbn is not None else ""))
     _ig_tuned[key] = best
     return best
 

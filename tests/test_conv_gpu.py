@@ -32,7 +32,8 @@ SHAPES = [
 @pytest.fixture(params=["classic", "glds", "classic_n64", "glds_n64", "onebuf", "onebuf_n64",
                         "tall512", "tall256", "small", "gshort64", "gshort128",
                         "gshort64_3", "gshort128_3", "multi2", "multi4", "small_multi4",
-                        "gmulti64", "gmulti128", "gbig256", "gbig512", "generic"])
+                        "gmulti64", "gmulti128", "gbig256", "gbig512", "generic",
+                        "sk128"])
 def ig_algo(request, monkeypatch):
     """Runs a test once per igemm kernel (register-staged / LDS-DMA ring /
     single LDS stage, 128- or 64-channel-wide tiles)."""
@@ -90,6 +91,51 @@ def test_dgrad_weight_relayout_matches(cuda):
             assert torch.equal(wt, ref.contiguous()), layer.tf_scope
             n += 1
         assert n > 10
+
+
+# (N, H, W, Cin, Cout, KH, KW): tile counts around the stream-K boundaries
+# (P = 512 slots): fewer tiles than slots, several data-parallel rounds plus a
+# split tail, and a 1-tile launch whose 18 K steps span many workgroups
+SK_SHAPES = [
+    (16, 100, 100, 128, 128, 3, 3),   # 1250 tiles: 512 data-parallel + 738 split
+    (8, 14, 14, 256, 256, 3, 3),      # 25 x 2 tiles, K = 2304
+    (1, 7, 7, 512, 256, 3, 3),        # one 128-row tile x 2, 72 K steps
+    (4, 28, 28, 1024, 256, 1, 1),     # 1x1, 25 x 2 tiles
+]
+
+
+@pytest.mark.parametrize("shape", SK_SHAPES, ids=[str(s) for s in SK_SHAPES])
+def test_stream_k_matches_one_tile_kernel(cuda, shape):
+    """Stream-K (IG_SK128) against the one-tile LDS-DMA kernel of the same
+    tile on the same operands: equal to fp32-rounding of the split sums, and
+    bitwise repeatable (the last contributor sums the partials in fixed
+    order; the tickets reset themselves between launches)."""
+    from kf_benchmarks_amd.ops import conv_hip
+    n, H, W, cin, cout, kh, kw = shape
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(n, H, W, cin, generator=g).to(cuda, torch.bfloat16)
+    w = (torch.randn(cout, kh, kw, cin, generator=g) / (kh * kw * cin) ** 0.5).to(
+        cuda, torch.bfloat16)
+    wmat = w.reshape(cout, -1).contiguous()
+    pt, pl = (kh - 1) // 2, (kw - 1) // 2
+    geo = (n, H, W, cin, H, W, kh, kw, 1, 1, pt, pl, cout, H, W, 1, cout, 0)
+    outs = {}
+    for algo in ("gshort128", "sk128", "sk128", "sk128"):
+        y = torch.empty(n, H, W, cout, device=cuda, dtype=torch.bfloat16)
+        stats = torch.zeros(2 * conv_hip.STATS_SPREAD * cout, device=cuda)
+        conv_hip._igemm_call(conv_hip.IG_ALGOS[algo], x, wmat, y, geo, stats)
+        outs.setdefault(algo, []).append((y, stats))
+    torch.cuda.synchronize()
+    ref, sref = outs["gshort128"][0]
+    y0, s0 = outs["sk128"][0]
+    torch.testing.assert_close(y0.float(), ref.float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(s0.view(2, -1, cout).sum(1), sref.view(2, -1, cout).sum(1),
+                               rtol=1e-3, atol=1e-1)
+    for y1, _ in outs["sk128"][1:]:
+        assert torch.equal(y1, y0)
+    want = conv_ops.conv2d_reference(x.float().cpu(), w.float().cpu(), (1, 1),
+                                     F.resolve_pads("SAME", H, W, kh, kw, 1, 1))
+    torch.testing.assert_close(y0.float().cpu(), want, rtol=2e-2, atol=2e-2)
 
 
 FUSED_SHAPES = [
