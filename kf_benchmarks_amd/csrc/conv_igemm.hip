@@ -29,6 +29,7 @@
 // 8 distinct 32-byte bank windows.
 #include "common.h"
 
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -1118,7 +1119,8 @@ struct SkArgs {
   float* ws;  // [P][2][128 * 128] partial tiles
   int* cnt;   // [Tsk] tickets, zero between launches
   int T, nk, Tdp;
-  long L;  // Tsk * nk: K steps of the stream-K region
+  long L;     // Tsk * nk: K steps of the stream-K region
+  int probe;  // KFB_SK_PROBE=1 (timing probe only, wrong results): no fix-up
 };
 
 // workgroup whose range holds step i of the stream-K region (P ranges of L)
@@ -1278,7 +1280,7 @@ __global__ void __launch_bounds__(256, 2) igemm_sk_k(IgArgs a, SkArgs sk) {
       }
     };
     const int m0 = (tile / ntiles) * BM, n0 = (tile % ntiles) * BN;
-    bool finish = k0 == 0 && k1 == sk.nk;
+    bool finish = (k0 == 0 && k1 == sk.nk) || sk.probe;
     if (!finish) {
       // partial tile: publish it, and sum the tile if this is the last piece
       const int tl = tile - sk.Tdp;
@@ -1818,8 +1820,13 @@ static hipError_t launch_sk(const IgArgs& a, hipStream_t s) {
   const int Tsk = tiles < P ? tiles : (tiles % P == 0 ? 0 : P + tiles % P);
   sk.Tdp = tiles - Tsk;
   sk.L = (long)Tsk * sk.nk;
+  static const int probe = getenv("KFB_SK_PROBE") ? atoi(getenv("KFB_SK_PROBE")) : 0;
+  sk.probe = probe;
   const int grid = (sk.Tdp > 0 || sk.L >= P) ? P : (int)sk.L;
   if (grid < 1) return hipSuccess;
+  if (probe >= 2)
+    fprintf(stderr, "[sk] P %d tiles %d nk %d Tdp %d L %ld grid %d\n", P, tiles, sk.nk, sk.Tdp, sk.L,
+            grid);
   hipLaunchKernelGGL(igemm_sk_k<T>, dim3(grid), dim3(256), 0, s, a, sk);
   return hipGetLastError();
 }

@@ -56,7 +56,7 @@ _NO_GSHORT = os.environ.get("KFB_IGEMM_NOGSHORT", "0") == "1"  # A/B knob: drop 
 _GSHORT3 = os.environ.get("KFB_IGEMM_GSHORT3", "1") != "0"  # A/B knob: the 3-stage forms
 _NO_MULTI = os.environ.get("KFB_IGEMM_NOMULTI", "0") == "1"  # A/B knob: drop IG_*MULTI*
 _NO_BIG = os.environ.get("KFB_IGEMM_NOBIG", "0") == "1"  # A/B knob: drop IG_GBIG*
-_NO_SK = os.environ.get("KFB_IGEMM_NOSK", "0") == "1"  # A/B knob: drop IG_SK128
+_SK = os.environ.get("KFB_IGEMM_SK", "0") == "1"  # offer IG_SK128 to the autotune
 # largest K (= KH*KW*Cin) offered the multi-tile candidates (register-staged;
 # the LDS-DMA form gets twice that)
 _MULTI_K = int(os.environ.get("KFB_IGEMM_MULTI_K", "2304"))
@@ -247,14 +247,19 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
     if fast and not _NO_MULTI and KH * KW * C <= 2 * _MULTI_K and C % 64 == 0:
         cands += (IG_GMULTI64,) + ((IG_GMULTI128,) if ncol > 64 else ())
     if fast and not _NO_BIG:
-        # big tiles only where they still give every CU a workgroup or more
+        # big tiles only where they give most CUs a workgroup: 196 256x256
+        # tiles on 256 CUs (the 14x14 3x3 convs at batch 256) still beat 784
+        # 128x128 tiles on 512 slots (71 vs 79 us, profiles/r7_stream_k.txt)
         M = geo[0] * geo[4] * geo[5]
-        if ncol >= 256 and ((M + 255) // 256) * ((ncol + 255) // 256) >= 256:
+        if ncol >= 256 and ((M + 255) // 256) * ((ncol + 255) // 256) >= 192:
             cands += (IG_GBIG256,)
         if 64 < ncol <= 256 and ((M + 511) // 512) * ((ncol + 127) // 128) >= 256:
             cands += (IG_GBIG512,)
-    if fast and not _NO_SK and C % 64 == 0 and ncol > 64:
-        # stream-K: pays where the 128 x 128 tiles leave a partial last round
+    if fast and _SK and C % 64 == 0 and ncol > 64:
+        # stream-K: measured slower than the one-tile kernels on every
+        # ResNet-50 geometry (per-item setup, pipeline refill and the fix-up
+        # tail cost more than the partial round it removes at K <= 4608,
+        # profiles/r7_stream_k.txt); candidate only with KFB_IGEMM_SK=1
         cands += (IG_SK128,)
     if fast and C % 64 != 0:
         # 8-channel geometry: the generic loader competes with the FAST ones
