@@ -1094,6 +1094,193 @@ __global__ void __launch_bounds__(256, (glds_occupancy<BM, BN, 256>()))
   }
 }
 
+// ------------------------------------------------------------ 8-phase igemm
+// 256 x 256 FAST-geometry tile on 8 waves (2 pixel halves x 4 channel
+// quarters, 128 x 64 wave tiles) with the K-tile split into four phases of
+// 16 MFMAs, one wave-tile quadrant each, and the two pixel-half wave groups
+// running one barrier apart: while the waves of one group issue their
+// quadrant's fragment reads and LDS-DMA prefetch, the other group's MFMAs
+// run on the same SIMDs (a workgroup's waves w and w + 4 share a SIMD), so
+// the fragment-read latency and issue slots hide behind the other group's
+// matrix work (MI355X guide: the 256^2 8-phase template).
+//
+// LDS: two K-tile buffers of X [256][64] + W [256][64] (128 KB, one
+// workgroup per CU), rows XOR-swizzled as in igemm_glds_k.  Each K-tile is
+// moved as four half-tiles, one per phase, for the NEXT K-tile, in the order
+// they are consumed: XA (pixel rows of quadrant half 0 of both groups), WA
+// (channel rows of quadrant half 0 of every quarter), WB, XB; consumed in
+// phases 0, 0, 1, 2.  Every barrier is preceded by vmcnt(4) (vmcnt(0) in the
+// last K-tile): a half-tile is read >= 3 phases after its issue, so with the
+// groups one barrier apart the two most recent half-tiles (4 DMAs per
+// thread) may stay in flight and everything older has landed on every wave
+// before the barrier the reader passes.  A buffer is overwritten 4 phases
+// after its last read.
+template <typename T, bool EXTRAS = true>
+__global__ void __launch_bounds__(512, 1) igemm_8p_k(IgArgs a) {
+  constexpr int BM = 256, BN = 256, NT = 512;
+  constexpr int TM = 8, TN = 4;             // 16-wide pixel / channel subtiles per wave
+  constexpr int STAGE = (BM + BN) * IG_BK;  // elements per K-tile buffer
+  __shared__ __attribute__((aligned(16))) T smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;  // pixel half, channel quarter
+  const int mtiles = (a.M + BM - 1) / BM, ntiles = (a.Ncol + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int m0 = (bid / ntiles) * BM, n0 = (bid % ntiles) * BN;
+  const int OHW = a.OH * a.OW;
+  const int kc = (lane & 7) ^ ((tid >> 4) & 7);  // logical 16-byte chunk this lane fetches
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.wbytes, 0x00020000);
+  // DMA slots s = 2 h + i (half h, instruction i): X row i*128 + h*64 + wid*8
+  // + lane/8; W 8-row group g = 8 i + wid at (g/4)*64 + h*32 + (g%4)*8
+  unsigned long long tapmask[4];
+  int xoff[4], woff[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int h = s >> 1, i = s & 1;
+    const int m = m0 + i * 128 + h * 64 + wid * 8 + (lane >> 3);
+    const bool ok = m < a.M;
+    const int mm = ok ? m : 0;
+    const int img = mm / OHW, rem = mm - img * OHW;
+    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+    const int xh = oh * a.sh - a.pt, xw = ow * a.sw - a.pl;
+    unsigned long long mk = 0;
+    for (int kh = 0; kh < a.KH; ++kh)
+      for (int kw = 0; kw < a.KW; ++kw) {
+        const bool in = (unsigned)(xh + kh) < (unsigned)a.H && (unsigned)(xw + kw) < (unsigned)a.W;
+        mk |= (unsigned long long)(in && ok) << (kh * a.KW + kw);
+      }
+    tapmask[s] = mk;
+    xoff[s] = img * a.H * a.W * a.C + (xh * a.W + xw) * a.C + kc * 8;
+    const int g = i * 8 + wid;
+    woff[s] = (n0 + (g >> 2) * 64 + h * 32 + (g & 3) * 8 + (lane >> 3)) * a.Ktot + kc * 8;
+  }
+  // K state of the K-tile being issued
+  int s_cc = 0, s_kh = 0, s_kw = 0, s_tap = 0, s_tapi = 0, s_k = 0;
+  auto advance = [&]() {
+    s_k += IG_BK;
+    s_cc += IG_BK;
+    if (s_cc == a.C) {
+      s_cc = 0;
+      ++s_tapi;
+      if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
+      s_tap = (s_kh * a.W + s_kw) * a.C;
+    }
+  };
+  auto issue_x = [&](int h, int buf) {
+    T* xs = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int s = h * 2 + i;
+      const bool ok = (tapmask[s] >> s_tapi) & 1ull;
+      const int off = ok ? (xoff[s] + s_tap + s_cc) * (int)sizeof(T) : -1;
+      dma16(xrs, xs + (i * 128 + h * 64 + wid * 8) * IG_BK, off);
+    }
+  };
+  auto issue_w = [&](int h, int buf) {
+    T* ws = smem + buf * STAGE + BM * IG_BK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int g = i * 8 + wid;
+      dma16(wrs, ws + ((g >> 2) * 64 + h * 32 + (g & 3) * 8) * IG_BK,
+            (woff[h * 2 + i] + s_k) * (int)sizeof(T));
+    }
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  v4f acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  v8s xf[4][2], wf0[2][2], wf1[2][2];
+  auto read_x = [&](const T* xs, int ph) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        xf[j][ks] = *(const v8s*)(xs + swz_off(wr * 128 + ph * 64 + j * 16 + (lane & 15),
+                                               ks * 4 + (lane >> 4)));
+  };
+  auto read_w = [&](const T* ws, int chh, v8s (&wf)[2][2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        wf[i][ks] = *(const v8s*)(ws + swz_off(wc * 64 + chh * 32 + i * 16 + (lane & 15),
+                                               ks * 4 + (lane >> 4)));
+  };
+  auto mfma = [&](int ph, int chh, const v8s (&wf)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[chh * 2 + i][ph * 4 + j] =
+              Mfma<T>::run(wf[i][ks], xf[j][ks], acc[chh * 2 + i][ph * 4 + j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = a.Ktot / IG_BK;  // FAST geometry: C % 64 == 0
+  issue_x(0, 0);
+  issue_w(0, 0);
+  issue_w(1, 0);
+  issue_x(1, 0);
+  advance();
+  wait_vmcnt<0>();
+  barrier();
+  if (wr) barrier();  // group 1 runs one barrier behind group 0
+#pragma unroll 1
+  for (int t = 0; t < nk; ++t) {
+    const int b = t & 1;
+    const bool more = t + 1 < nk;
+    const T* xs = smem + b * STAGE;
+    const T* ws = xs + BM * IG_BK;
+    auto sync = [&]() {
+      if (more) wait_vmcnt<4>(); else wait_vmcnt<0>();
+      barrier();
+    };
+    // phase 0: quadrant (pixel half 0, channel half 0)
+    read_x(xs, 0);
+    read_w(ws, 0, wf0);
+    if (more) issue_x(0, b ^ 1);
+    sync();
+    mfma(0, 0, wf0);
+    sync();
+    // phase 1: (0, 1)
+    read_w(ws, 1, wf1);
+    if (more) issue_w(0, b ^ 1);
+    sync();
+    mfma(0, 1, wf1);
+    sync();
+    // phase 2: (1, 1)
+    read_x(xs, 1);
+    if (more) issue_w(1, b ^ 1);
+    sync();
+    mfma(1, 1, wf1);
+    sync();
+    // phase 3: (1, 0)
+    if (more) {
+      issue_x(1, b ^ 1);
+      advance();
+    }
+    sync();
+    mfma(1, 0, wf0);
+    sync();
+  }
+  if (!wr) barrier();  // group 0 matches group 1's extra barrier
+  __syncthreads();     // every fragment read done before the epilogue reuses the buffers
+  ig_epilogue<T, BM, BN, NT, 2, 4, NoPrefetch, EXTRAS>(a, acc, smem, m0, n0, wr, wc);
+}
+
 // ------------------------------------------------------------ stream-K igemm
 // Persistent form of the 4-wave 128 x 128 LDS-DMA tile whose workgroups
 // share the tail of the tile space along K.  A launch of T tiles on P
@@ -1745,6 +1932,12 @@ static void launch_glds_big(const IgArgs& a, bool wide, hipStream_t s) {
                        dim3(((a.M + 511) / 512) * ((a.Ncol + 127) / 128)), dim3(512), 0, s, a);
 }
 
+template <typename T>
+static void launch_8p(const IgArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((igemm_8p_k<T>), dim3(((a.M + 255) / 256) * ((a.Ncol + 255) / 256)),
+                     dim3(512), 0, s, a);
+}
+
 // Multi-tile 4-wave LDS-DMA kernels, 2 tiles per workgroup.
 template <typename T>
 static void launch_glds_mt(const IgArgs& a, bool wide, hipStream_t s) {
@@ -1891,7 +2084,8 @@ using namespace kfb;
 //   IG_ALGO_GMULTI64 / GMULTI128: igemm_glds_mt_k, GSHORT64 / GSHORT128 with 2
 //   tiles per workgroup (next tile's DMAs land in stage 0 while the epilogue
 //   stages in stage 1).  IG_ALGO_SK128: igemm_sk_k, the GSHORT128 tile
-//   persistent with the last partial round split along K.  Forward-style
+//   persistent with the last partial round split along K.  IG_ALGO_G8P:
+//   igemm_8p_k, the 256 x 256 tile with the 8-phase staggered schedule.  Forward-style
 //   epilogues only: with addend / mask / xbn they fall through to the
 //   one-tile kernels.
 enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_GLDS_N64 = 4,
@@ -1900,7 +2094,7 @@ enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_G
        IG_ALGO_GSHORT64_3 = 12, IG_ALGO_GSHORT128_3 = 13, IG_ALGO_MULTI2 = 14,
        IG_ALGO_MULTI4 = 15, IG_ALGO_SMALL_MULTI4 = 16, IG_ALGO_GMULTI64 = 17,
        IG_ALGO_GMULTI128 = 18, IG_ALGO_GBIG256 = 19, IG_ALGO_GBIG512 = 20,
-       IG_ALGO_GENERIC = 21, IG_ALGO_SK128 = 22 };
+       IG_ALGO_GENERIC = 21, IG_ALGO_SK128 = 22, IG_ALGO_G8P = 23 };
 
 static bool c8_geometry(int C, int KH, int KW) {
   return C == 8 && (KW == 1 || KW == 2 || KW == 4 || KW == 8) && (KH * KW) % 8 == 0;
@@ -1963,6 +2157,12 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
   if ((algo == IG_ALGO_GBIG256 || algo == IG_ALGO_GBIG512) && fast) {
     if (dtype == BF16) launch_glds_big<bf16>(a, algo == IG_ALGO_GBIG256, stream);
     else if (dtype == F16) launch_glds_big<f16>(a, algo == IG_ALGO_GBIG256, stream);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
+  if (algo == IG_ALGO_G8P && fast && !c8) {
+    if (dtype == BF16) launch_8p<bf16>(a, stream);
+    else if (dtype == F16) launch_8p<f16>(a, stream);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }

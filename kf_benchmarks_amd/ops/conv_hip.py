@@ -41,6 +41,8 @@ IG_GBIG256, IG_GBIG512 = 19, 20
 IG_GENERIC = 21  # the generic (per-chunk division) loader, forced
 # persistent 128 x 128 LDS-DMA tile, last partial round split along K (stream-K)
 IG_SK128 = 22
+# 256 x 256 LDS-DMA tile, 8-phase schedule with the two wave groups staggered
+IG_G8P = 23
 IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N64,
             "glds_n64": IG_GLDS_N64, "onebuf": IG_ONEBUF, "onebuf_n64": IG_ONEBUF_N64,
             "tall512": IG_TALL512, "tall256": IG_TALL256, "small": IG_SMALL,
@@ -48,7 +50,7 @@ IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N6
             "gshort128_3": IG_GSHORT128_3, "multi2": IG_MULTI2, "multi4": IG_MULTI4,
             "small_multi4": IG_SMALL_MULTI4, "gmulti64": IG_GMULTI64,
             "gmulti128": IG_GMULTI128, "gbig256": IG_GBIG256, "gbig512": IG_GBIG512,
-            "generic": IG_GENERIC, "sk128": IG_SK128}
+            "generic": IG_GENERIC, "sk128": IG_SK128, "g8p": IG_G8P}
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
@@ -252,7 +254,7 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
         # 128x128 tiles on 512 slots (71 vs 79 us, profiles/r7_stream_k.txt)
         M = geo[0] * geo[4] * geo[5]
         if ncol >= 256 and ((M + 255) // 256) * ((ncol + 255) // 256) >= 192:
-            cands += (IG_GBIG256,)
+            cands += (IG_GBIG256,) + ((IG_G8P,) if C % 64 == 0 else ())
         if 64 < ncol <= 256 and ((M + 511) // 512) * ((ncol + 127) // 128) >= 256:
             cands += (IG_GBIG512,)
     if fast and _SK and C % 64 == 0 and ncol > 64:
