@@ -104,6 +104,18 @@ def _check_no_missing_stubs(lib):
         raise RuntimeError("undefined kernel launch stubs in %s: %s" % (lib, missing))
 
 
+# jpeglib.h for the native image pipeline (csrc/runtime/kfb_images.cpp); the
+# library itself is dlopen'ed at run time, so a build without the header just
+# leaves the pipeline unavailable (Python's PIL path runs instead)
+JPEG_INCLUDE = os.environ.get("KFB_JPEG_INCLUDE", "/opt/conda/include")
+
+
+def _jpeg_flags():
+    if os.path.exists(os.path.join(JPEG_INCLUDE, "jpeglib.h")):
+        return ["-DKFB_HAVE_JPEGLIB", "-idirafter", JPEG_INCLUDE]
+    return []
+
+
 def build_rt(force=False):
     srcs = rt_sources()
     if not srcs:
@@ -113,7 +125,8 @@ def build_rt(force=False):
     newest = max([os.path.getmtime(s) for s in srcs] + [hdr])
     if force or not os.path.exists(RT_LIB) or os.path.getmtime(RT_LIB) < newest:
         tmp = RT_LIB + ".tmp"
-        _run([CXX] + CXX_FLAGS + ["-shared", "-o", tmp] + srcs + ["-lpthread"])
+        _run([CXX] + CXX_FLAGS + _jpeg_flags() + ["-shared", "-o", tmp] + srcs
+             + ["-lpthread", "-ldl"])
         os.replace(tmp, RT_LIB)
     return RT_LIB
 

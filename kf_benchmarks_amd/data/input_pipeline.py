@@ -149,6 +149,14 @@ class PrefetchInput:
 
     def _to_device(self, ts):
         img = ts[0].to(self.device, non_blocking=True)
+        if len(ts) == 3 and img.dtype == torch.uint8:
+            # (uint8 images, labels, augmentation params): flip, colour
+            # distortions and [-1, 1] scaling on the device (csrc/augment.hip)
+            from ..ops import nn as F
+            prm = ts[2].to(self.device, non_blocking=True)
+            lab = ts[1].to(self.device, non_blocking=True)
+            return [F.augment_u8(img, prm, self.dtype),
+                    lab.to(torch.int32) if lab.dtype == torch.int64 else lab]
         if img.dtype == torch.uint8:
             # raw pixels: normalize on the device (x / 127.5 - 1)
             img = img.to(torch.float32).mul_(1.0 / 127.5).sub_(1.0)

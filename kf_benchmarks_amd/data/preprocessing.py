@@ -256,6 +256,83 @@ def train_image(image_buffer, height, width, bbox, batch_position, resize_method
     return image
 
 
+# KFB_JPEG_DRAFT=0: decode every JPEG at full size (the DCT-domain 1/2-1/8
+# scaling below changes the pixels slightly; the crop keeps >= the output size)
+_JPEG_DRAFT = os.environ.get("KFB_JPEG_DRAFT", "1") != "0"
+AUG_PARAMS = 8  # per-image parameter row of the device augmentation (csrc/augment.hip)
+
+
+def train_image_u8(image_buffer, height, width, bbox, batch_position, resize_method, distortions,
+                   rng, distort_color_in_yiq=False, draft=None):
+    """Host half of the train preprocessing when the colour distortions run on
+    the device (csrc/augment.hip): decode + bbox crop + resize to uint8
+    [height, width, 3], and the image's augmentation parameters
+    (flip, brightness, saturation, hue, contrast, order, distort, 0), drawn
+    from ``rng`` in train_image's order so both paths see the same randoms.
+    The JPEG is opened once; with ``draft`` (default KFB_JPEG_DRAFT) libjpeg
+    decodes at the largest 1/2^k scale that keeps the crop >= the output."""
+    im = Image.open(io.BytesIO(image_buffer))
+    W0, H0 = im.size
+    y, x, h, w = sample_distorted_bounding_box((H0, W0, 3), bbox, rng)
+    flip = rng.random() < 0.5
+    if _JPEG_DRAFT if draft is None else draft:
+        scale = min(w / float(width), h / float(height))
+        if scale >= 2.0:
+            im.draft("RGB", (int(math.ceil(W0 / scale)), int(math.ceil(H0 / scale))))
+            W1, H1 = im.size
+            if (W1, H1) != (W0, H0):
+                fx, fy = W1 / float(W0), H1 / float(H0)
+                x, w = int(x * fx), max(1, int(round(w * fx)))
+                y, h = int(y * fy), max(1, int(round(h * fy)))
+    im = im.convert("RGB").crop((x, y, x + w, y + h))
+    if (w, h) != (width, height):
+        im = im.resize((width, height), _pil_filter(get_image_resize_method(resize_method,
+                                                                           batch_position)))
+    image = np.asarray(im, dtype=np.uint8)
+    prm = np.zeros(AUG_PARAMS, dtype=np.float32)
+    prm[0] = 1.0 if flip else 0.0
+    if distortions:
+        prm[1] = rng.uniform(-32. / 255., 32. / 255.)
+        order = batch_position % 2
+        if order == 0:
+            if distort_color_in_yiq:
+                prm[3], prm[2] = rng.uniform(-0.2, 0.2), rng.uniform(0.5, 1.5)
+            else:
+                prm[2], prm[3] = rng.uniform(0.5, 1.5), rng.uniform(-0.2, 0.2)
+            prm[4] = rng.uniform(0.5, 1.5)
+        else:
+            prm[4] = rng.uniform(0.5, 1.5)
+            if distort_color_in_yiq:
+                prm[3], prm[2] = rng.uniform(-0.2, 0.2), rng.uniform(0.5, 1.5)
+            else:
+                prm[2], prm[3] = rng.uniform(0.5, 1.5), rng.uniform(-0.2, 0.2)
+        prm[5] = float(order)
+        prm[6] = 1.0
+    return image, prm
+
+
+def augment_reference(images_u8, params):
+    """numpy reference of csrc/augment.hip: uint8 [N,H,W,3] + [N,8] params ->
+    float32 [N,H,W,3] in [-1, 1] (the train_image + normalized_image result)."""
+    out = []
+    for img, p in zip(images_u8, params):
+        f = img.astype(np.float32) / 255.0
+        if p[0]:
+            f = f[:, ::-1]
+        if p[6]:
+            f = f + p[1]
+
+            def sat_hue(z):
+                return adjust_hue(adjust_saturation(z, p[2]), p[3])
+            if p[5] == 0:
+                f = adjust_contrast(sat_hue(f), p[4])
+            else:
+                f = sat_hue(adjust_contrast(f, p[4]))
+            f = np.clip(f, 0.0, 1.0)
+        out.append(normalized_image(f * 255.0))
+    return np.stack(out).astype(np.float32)
+
+
 def eval_image(image, height, width, batch_position, resize_method):
     """Resize so both sides cover the target x1.15, then central crop."""
     ih, iw = image.shape[0], image.shape[1]
@@ -427,8 +504,20 @@ def _batched(pre, records: Iterator[bytes], threads: int):
     thread pool; the per-image RNG depends only on (batch, position) so the
     output is deterministic regardless of thread scheduling."""
     bs = pre.batch_size
-    pool = ThreadPoolExecutor(max_workers=threads, thread_name_prefix="kfb-input")
     base = np.random.SeedSequence(pre.seed)
+    if getattr(pre, "device_augment", False) and _NATIVE_PIPE and runtime.ImagePipe.available():
+        # every per-image step in native threads (csrc/runtime/kfb_images.cpp)
+        pipe = runtime.ImagePipe(threads, pre.height, pre.width, pre.distortions,
+                                 pre.distort_color_in_yiq)
+        try:
+            while True:
+                recs = [next(records) for _ in range(bs)]
+                seeds = base.spawn(1)[0].generate_state(bs, dtype=np.uint64)
+                imgs, prms, labels, _ = pipe.run(recs, seeds)
+                yield imgs, labels, prms
+        finally:
+            pipe.close()
+    pool = ThreadPoolExecutor(max_workers=threads, thread_name_prefix="kfb-input")
     try:
         while True:
             recs = [next(records) for _ in range(bs)]
@@ -436,6 +525,13 @@ def _batched(pre, records: Iterator[bytes], threads: int):
             results = list(pool.map(
                 lambda i: pre.parse_and_preprocess(recs[i], i, np.random.default_rng(int(seeds[i]))),
                 range(bs)))
+            if getattr(pre, "device_augment", False):
+                # (uint8 images, params) per image: colour work on the device
+                imgs = np.stack([r[0][0] for r in results])
+                prms = np.stack([r[0][1] for r in results])
+                labels = np.asarray([r[1] for r in results], dtype=np.int32)
+                yield imgs, labels, prms
+                continue
             imgs = [r[0] for r in results]
             floaty = any(im.dtype != np.uint8 for im in imgs)
             out = np.stack([im.astype(np.float32) if floaty else im for im in imgs])
@@ -450,7 +546,16 @@ def _batched(pre, records: Iterator[bytes], threads: int):
 class RecordInputImagePreprocessor(BaseImagePreprocessor):
     """The default ImageNet-style pipeline (tcb/preprocessing.py:551-632)."""
 
+    # set by make_batch_iterator for GPU consumers: train batches come out as
+    # (uint8 images, labels, augmentation params) and csrc/augment.hip does
+    # the flip, colour distortions and scaling after the copy
+    device_augment = False
+
     def preprocess(self, image_buffer, bbox, batch_position, rng):
+        if self.train and self.device_augment:
+            return train_image_u8(image_buffer, self.height, self.width, bbox, batch_position,
+                                  self.resize_method, self.distortions, rng,
+                                  self.distort_color_in_yiq)
         if self.train:
             return train_image(image_buffer, self.height, self.width, bbox, batch_position,
                                self.resize_method, self.distortions, rng,
@@ -684,7 +789,17 @@ def get_preprocessor(bench, subset):
                fuse_decode_and_crop=params.fuse_decode_and_crop)
 
 
+# KFB_NATIVE_PIPE=0: with device augmentation, decode/crop/resize on Python
+# threads over PIL instead of the native pipeline
+_NATIVE_PIPE = os.environ.get("KFB_NATIVE_PIPE", "1") != "0"
+# KFB_DEVICE_AUGMENT=0: the whole train preprocessing on the host threads
+_DEVICE_AUGMENT = os.environ.get("KFB_DEVICE_AUGMENT", "1") != "0"
+
+
 def make_batch_iterator(bench, subset="train"):
     pre = get_preprocessor(bench, subset)
+    if (type(pre) is RecordInputImagePreprocessor and pre.train and _DEVICE_AUGMENT
+            and getattr(bench, "device", None) is not None and bench.device.type == "cuda"):
+        pre.device_augment = True
     shift = bench.task_index / float(max(bench.num_replicas, 1))
     return pre.minibatch(bench.dataset, subset, bench.params, shift_ratio=shift)

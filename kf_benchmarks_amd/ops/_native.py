@@ -75,6 +75,8 @@ _SIGS = {
     "kfb_act_bwd_bias": [I, P, P, P, L, I, I, P, I, P, I, P],
     "kfb_dropout": [I, P, P, L, F, c_uint32, P],
     "kfb_synthetic_images": [I, P, L, F, F, c_uint32, P],
+    "kfb_augment": [I, P, P, P, I, I, I, P, P],
+    "kfb_augment_blocks": [],
     "kfb_synthetic_labels": [P, L, I, c_uint32, P],
     "kfb_add": [I, P, P, P, L, I, P],
     "kfb_gemm": [I, I, P, I, P, I, I, I, I, P, I, P, I, I, P, L, I, P],

@@ -1190,6 +1190,28 @@ def synthetic_images(shape, dtype, device, seed: int, mean=127.0, std=60.0):
     return x
 
 
+def augment_u8(images, params, dtype):
+    """Device half of the train preprocessing (csrc/augment.hip): uint8
+    [N, H, W, 3] pixels + [N, 8] float32 parameters (flip, brightness,
+    saturation, hue, contrast, order, distort) -> [N, H, W, 3] in [-1, 1],
+    ``dtype``.  CPU tensors take the numpy reference."""
+    if images.device.type != "cuda":
+        from ..data.preprocessing import augment_reference
+        out = augment_reference(images.numpy(), params.numpy())
+        return torch.from_numpy(out).to(dtype)
+    n, h, w, c = images.shape
+    if c != 3 or params.shape != (n, 8) or images.dtype != torch.uint8:
+        raise ValueError("augment_u8 takes uint8 [N,H,W,3] and float32 [N,8]")
+    images = images.contiguous()
+    params = params.to(torch.float32).contiguous()
+    part = torch.empty((n * N.query("kfb_augment_blocks") * 3,), dtype=torch.float32,
+                       device=images.device)
+    out = torch.empty((n, h, w, 3), dtype=dtype, device=images.device)
+    N.call("kfb_augment", N.dt(out), images.data_ptr(), params.data_ptr(), part.data_ptr(), n, h,
+           w, out.data_ptr(), N.stream(images.device))
+    return out
+
+
 def synthetic_labels(n, nclass, device, seed: int):
     # Reference: uniform in [0, nclass-1) (tcb/models/model.py:232-236).
     maxval = max(nclass - 1, 1)

@@ -353,3 +353,65 @@ def adjust_saturation_hue(img, sat: float, hue: float):
     assert img.dtype == np.float32 and img.flags["C_CONTIGUOUS"] and img.shape[-1] == 3
     _load().kfbrt_adjust_sat_hue(img.ctypes.data, img.size // 3, float(sat), float(hue))
     return img
+
+
+class ImagePipe:
+    """Native batch image pipeline (csrc/runtime/kfb_images.cpp): records ->
+    uint8 [n, height, width, 3] crops, [n, 8] device-augmentation parameters
+    and int32 labels, on ``threads`` native threads (the calling thread one
+    of them), the GIL released for the whole batch."""
+
+    def __init__(self, threads: int, height: int, width: int, distortions: bool,
+                 distort_color_in_yiq: bool, draft: bool = True):
+        lib = _load()
+        if not getattr(lib, "_imgpipe_sigs", False):
+            lib.kfbrt_imgpipe_available.restype = ctypes.c_int
+            lib.kfbrt_imgpipe_create.argtypes = [ctypes.c_int] * 6
+            lib.kfbrt_imgpipe_create.restype = ctypes.c_void_p
+            lib.kfbrt_imgpipe_run.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 7
+            lib.kfbrt_imgpipe_run.restype = ctypes.c_int
+            lib.kfbrt_imgpipe_destroy.argtypes = [ctypes.c_void_p]
+            lib._imgpipe_sigs = True
+        self._lib = lib
+        self.height, self.width = height, width
+        self._h = lib.kfbrt_imgpipe_create(int(threads), int(height), int(width),
+                                           int(bool(distortions)), int(bool(distort_color_in_yiq)),
+                                           int(bool(draft)))
+
+    @staticmethod
+    def available() -> bool:
+        try:
+            lib = _load()
+            lib.kfbrt_imgpipe_available.restype = ctypes.c_int
+            return bool(lib.kfbrt_imgpipe_available())
+        except (OSError, AttributeError):
+            return False
+
+    def run(self, records, seeds, positions=None):
+        """-> (images uint8 [n,H,W,3], params float32 [n,8], labels int32 [n],
+        number of undecodable images)."""
+        import numpy as np
+        n = len(records)
+        bufs = (ctypes.c_char_p * n)(*records)
+        lens = np.asarray([len(r) for r in records], dtype=np.uint64)
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+        pos = np.ascontiguousarray(np.arange(n) if positions is None else positions, dtype=np.int32)
+        images = np.empty((n, self.height, self.width, 3), dtype=np.uint8)
+        params = np.empty((n, 8), dtype=np.float32)
+        labels = np.empty((n,), dtype=np.int32)
+        bad = self._lib.kfbrt_imgpipe_run(self._h, n, ctypes.cast(bufs, ctypes.c_void_p),
+                                          lens.ctypes.data, seeds.ctypes.data, pos.ctypes.data,
+                                          images.ctypes.data, params.ctypes.data,
+                                          labels.ctypes.data)
+        return images, params, labels, bad
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.kfbrt_imgpipe_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -239,3 +239,80 @@ def test_batch_group_size_stages_groups(tmp_path):
     assert prod is not None and prod.batch_group_size == 3
     assert prod._consumed >= 6 and prod._produced % 3 == 0
     assert prod._produced - prod._consumed <= 2 * 3 + 3
+
+
+def test_u8_host_path_plus_augment_reference_matches_host_path():
+    """The device-augmentation split (host: decode/crop/resize to uint8 +
+    parameter draws; device: flip, colour, scaling) reproduces the all-host
+    train_image + normalized_image result for the same randoms."""
+    img = np.clip(np.random.default_rng(0).normal(120, 50, (90, 120, 3)), 0, 255).astype(np.uint8)
+    buf = test_data.encode_jpeg(img)
+    bbox = np.array([[0.1, 0.1, 0.9, 0.8]], np.float32)
+    for pos in range(4):
+        for distort in (False, True):
+            a = pre.train_image(buf, 64, 48, bbox, pos, "bilinear", distort,
+                                np.random.default_rng(pos), False, True)
+            u8, prm = pre.train_image_u8(buf, 64, 48, bbox, pos, "bilinear", distort,
+                                         np.random.default_rng(pos), False, draft=False)
+            assert u8.dtype == np.uint8 and u8.shape == (64, 48, 3) and prm.shape == (8,)
+            b = pre.augment_reference(u8[None], prm[None])[0]
+            ref = pre.normalized_image(a.astype(np.float32))
+            np.testing.assert_allclose(b, ref, atol=2e-5)
+
+
+def test_native_image_pipe_on_reference_fixtures():
+    """csrc/runtime/kfb_images.cpp on the reference's fixture shards (flat
+    gray JPEGs of level label * 25.5): crops stay flat at that level, labels
+    agree with the Python parser, and the augmentation parameters are in the
+    reference's ranges and batch-position order."""
+    if not runtime.ImagePipe.available():
+        pytest.skip("libjpeg not loadable")
+    d = os.path.join(REF_DATA, "fake_tf_record_data")
+    recs = []
+    for name in sorted(os.listdir(d)):
+        recs += list(runtime.tf_record_iterator(os.path.join(d, name)))
+    recs = recs[:48]
+    pipe = runtime.ImagePipe(3, 40, 56, True, False)
+    try:
+        imgs, prm, labels, bad = pipe.run(recs, np.arange(len(recs), dtype=np.uint64) + 5)
+        imgs2, prm2, _, _ = pipe.run(recs, np.arange(len(recs), dtype=np.uint64) + 5)
+    finally:
+        pipe.close()
+    assert bad == 0 and imgs.shape == (48, 40, 56, 3) and imgs.dtype == np.uint8
+    assert np.array_equal(imgs, imgs2) and np.array_equal(prm, prm2)  # seeded, deterministic
+    for i, rec in enumerate(recs):
+        _, label, _, _ = pre.parse_example_proto(rec)
+        assert labels[i] == label
+        assert abs(float(imgs[i].mean()) - label * 25.5) < 4
+    assert set(np.unique(prm[:, 0])) <= {0.0, 1.0}
+    assert (np.abs(prm[:, 1]) <= 32 / 255 + 1e-6).all()
+    assert ((prm[:, 2] >= 0.5) & (prm[:, 2] <= 1.5)).all()
+    assert (np.abs(prm[:, 3]) <= 0.2 + 1e-6).all()
+    assert ((prm[:, 4] >= 0.5) & (prm[:, 4] <= 1.5)).all()
+    assert np.array_equal(prm[:, 5], np.arange(48) % 2) and (prm[:, 6] == 1).all()
+
+
+def test_device_augment_batches_on_host(tmp_path):
+    """With device augmentation the train batches are (uint8 images, labels,
+    params); the CPU form of the device op turns them into the [-1, 1] images."""
+    import torch
+    from kf_benchmarks_amd.ops import nn as F
+    test_data.write_black_and_white_tfrecord_data(str(tmp_path), 10, 32, 8, 2, 1)
+
+    class Bench:
+        pass
+    from kf_benchmarks_amd import datasets
+    from kf_benchmarks_amd.models import model_config
+    b = Bench()
+    b.params = P.make_params(model="trivial", data_dir=str(tmp_path), distortions=True)
+    b.dataset = datasets.create_dataset(str(tmp_path), "imagenet")
+    b.model = model_config.get_model_config("trivial", b.dataset, b.params)
+    b.model.set_batch_size(8)
+    b.task_index, b.num_workers, b.num_replicas, b.local_batch_size = 0, 1, 1, 8
+    p = pre.get_preprocessor(b, "train")
+    p.device_augment = True
+    imgs, labels, prm = next(p.minibatch(b.dataset, "train", b.params))
+    assert imgs.dtype == np.uint8 and imgs.shape == (8, 227, 227, 3)
+    assert prm.shape == (8, 8) and labels.dtype == np.int32
+    out = F.augment_u8(torch.from_numpy(imgs), torch.from_numpy(prm), torch.float32)
+    assert out.shape == (8, 227, 227, 3) and out.min() >= -1.0 and out.max() <= 1.0
