@@ -1824,6 +1824,183 @@ __global__ void __launch_bounds__(256, KFB_WG_OCC) wgrad_k(WgArgs a) {
     }
 }
 
+// LDS-DMA form of wgrad_k (128 x 128 dW tiles, 4 waves of 64 x 64): both
+// operand tiles go global -> LDS by buffer_load ... lds into a 2-stage ring
+// of 64-row steps (2 x 32 KB, two workgroups per CU), so there is no
+// register staging, no ds_write pass and half the barriers per reduction row
+// of the register-staged kernel (32-row steps).  The LDS images keep
+// wgrad_k's 256-byte rows with XOR-swizzled 32-byte units (tr_off) for the
+// transposed fragment reads; the swizzle moves to the source side: a DMA
+// wave-instruction fills 4 rows linearly, lane l writing 16-byte chunk l & 15
+// of row l >> 4, so it fetches the logical chunk that tr_off maps there.
+// Row (l >> 4) & 3 and bit 3 of the row (the wave's 4-row group parity) fix
+// that chunk, so each lane's columns (and for 3x3 gathers its filter tap and
+// channel) are constant over the whole reduction.
+template <typename T, int MODE>
+__global__ void __launch_bounds__(256, 2) wgrad_glds_k(WgArgs a) {
+  constexpr int BMC = 128, BNK = 128, TN = 4, TM = 4, BK = 64;
+  constexpr int STAGE = 2 * BK * 128;  // dy [64][128] + x [64][128] elements
+  __shared__ __attribute__((aligned(16))) T smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ctiles = (a.Ncol + BMC - 1) / BMC, ktiles = (a.Ktot + BNK - 1) / BNK;
+  const int tiles = ctiles * ktiles;
+  const int bid = KFB_WG_XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int split = bid / tiles;
+  const int tile = bid - split * tiles;
+  const int c0 = (tile / ktiles) * BMC, k0 = (tile % ktiles) * BNK;
+  const int mbeg = split * a.mper;
+  const int mend = min(a.M, mbeg + a.mper);
+  const int OHW = a.OH * a.OW;
+
+  // this lane's logical 8-element column chunk (see above)
+  const int lrow = lane >> 4;                                  // row within the 4-row group
+  const int f = lrow | (((wid >> 1) & 1) << 2);                // tr_off's f(row)
+  const int pc = lane & 15;                                    // physical 16-byte chunk
+  const int col = ((((pc >> 1) ^ f) << 4) | ((pc & 1) << 3));  // logical column
+  const int n = c0 + col, k = k0 + col;
+  const bool nok = n < a.Ncol, kok = k < a.Ktot;
+  const int tap = kok ? k / a.C : 0, cc = k - tap * a.C;
+  const int kh = tap / a.KW, kw = tap - kh * a.KW;
+  const __amdgpu_buffer_rsrc_t drs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, a.dybytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.xbytes, 0x00020000);
+  // rows of DMA instruction i (0..3) at step s: mbeg + s*64 + i*16 + wid*4 + lrow
+  int doff[4], ximg[4], xoh[4], xow[4], xo[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = mbeg + i * 16 + wid * 4 + lrow;
+    doff[i] = m * a.Ncol + n;
+    if constexpr (MODE == WG_PLAIN) {
+      xo[i] = m * a.C + cc;
+    } else {
+      ximg[i] = m / OHW;
+      const int rem = m - ximg[i] * OHW;
+      xoh[i] = rem / a.OW;
+      xow[i] = rem - xoh[i] * a.OW;
+    }
+  }
+  const int dq = BK / a.OW, dr = BK - dq * a.OW;
+  int s_m = mbeg;  // first row of the next step to issue
+  auto issue = [&](int stage) {
+    T* ds = smem + stage * STAGE;
+    T* xs = ds + BK * 128;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = i * 16 + wid * 4;  // first LDS row of this wave-instruction
+      const bool mok = s_m + r + lrow < mend;
+      dma16(drs, ds + r * 128, (mok && nok) ? doff[i] * (int)sizeof(T) : -1);
+      doff[i] += BK * a.Ncol;
+      int off;
+      if constexpr (MODE == WG_PLAIN) {
+        off = (mok && kok) ? xo[i] * (int)sizeof(T) : -1;
+        xo[i] += BK * a.C;
+      } else {
+        const int hi = xoh[i] * a.sh - a.pt + kh, wi = xow[i] * a.sw - a.pl + kw;
+        const bool ok = mok && kok && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+        off = ok ? (((ximg[i] * a.H + hi) * a.W + wi) * a.C + cc) * (int)sizeof(T) : -1;
+        xow[i] += dr;
+        xoh[i] += dq;
+        if (xow[i] >= a.OW) { xow[i] -= a.OW; ++xoh[i]; }
+        while (xoh[i] >= a.OH) { xoh[i] -= a.OH; ++ximg[i]; }
+      }
+      dma16(xrs, xs + r * 128, off);
+    }
+    s_m += BK;
+  };
+
+  v4f acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int wn = wid >> 1, wm = wid & 1;
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  auto compute = [&](int stage) {
+    const T* ds = smem + stage * STAGE;
+    const T* xs = ds + BK * 128;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int r0 = kk * 32 + 8 * g;
+      v8s af[TN], bfr[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int cl = wn * (BMC / 2) + i * 16 + 4 * p;
+        v4s lo = ds_read_tr<T>(ds + tr_off(r0 + q, cl));
+        v4s hi = ds_read_tr<T>(ds + tr_off(r0 + 4 + q, cl));
+        af[i] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int cl = wm * (BNK / 2) + j * 16 + 4 * p;
+        v4s lo = ds_read_tr<T>(xs + tr_off(r0 + q, cl));
+        v4s hi = ds_read_tr<T>(xs + tr_off(r0 + 4 + q, cl));
+        bfr[j] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = Mfma<T>::run(af[i], bfr[j], acc[i][j]);
+    }
+  };
+
+  const int nsteps = (mend - mbeg + BK - 1) / BK;
+  if (nsteps > 0) issue(0);
+  int st = 0;
+  for (int s = 0; s < nsteps; ++s) {
+    wait_vmcnt<0>();  // this step's DMAs (the only ones outstanding)
+    lds_barrier();    // ... of every wave landed; stage st^1 (step s-1) fully read
+    if (s + 1 < nsteps) issue(st ^ 1);
+    compute(st);
+    st ^= 1;
+  }
+  __syncthreads();  // every fragment read done before the epilogue reuses the ring
+  // acc[i][j]: dW row c0 + wn*64 + i*16 + (lane>>4)*4 + r, col k0 + wm*64 + j*16 + (lane&15)
+  if (a.slab) {
+    constexpr int HR = BMC / 2, LDR = BNK;
+    static_assert(HR * LDR * 4 <= (int)sizeof(smem), "slab staging exceeds LDS");
+    float* stg = (float*)smem;
+    float* dst = a.slab + (long)split * a.Ncol * a.Ktot;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (wn == h) {
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              stg[(i * 16 + (lane >> 4) * 4 + r) * LDR + wm * (BNK / 2) + j * 16 + (lane & 15)] =
+                  acc[i][j][r];
+      }
+      __syncthreads();
+      constexpr int CPR = BNK / 4;
+#pragma unroll
+      for (int t = tid; t < HR * CPR; t += 256) {
+        const int row = t / CPR, cq = (t % CPR) * 4;
+        const int c = c0 + h * HR + row, kq = k0 + cq;
+        if (c < a.Ncol && kq < a.Ktot)
+          *(float4*)(dst + (long)c * a.Ktot + kq) = *(const float4*)(stg + row * LDR + cq);
+      }
+      __syncthreads();
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int kq = k0 + wm * (BNK / 2) + j * 16 + (lane & 15);
+      if (kq >= a.Ktot) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = c0 + wn * (BMC / 2) + i * 16 + (lane >> 4) * 4 + r;
+        if (c < a.Ncol) atomicAdd(a.dw + (long)c * a.Ktot + kq, acc[i][j][r]);
+      }
+    }
+}
+
 // dw[i] += sum_s slab[s][i]   (n4 = elements / 4), one thread per float4.
 __global__ void __launch_bounds__(256) wgrad_reduce_k(const float4* __restrict__ slab,
                                                       float4* __restrict__ dw, long n4,
@@ -2217,7 +2394,7 @@ KFB_API int kfb_conv_stats_spread() { return IG_SPREAD; }
 // slab workspace needs splits * Ncol * KH*KW*C floats).
 KFB_API int kfb_conv_wgrad_splits(int N, int OH, int OW, int KH, int KW, int C, int Ncol,
                                   int target_blocks) {
-  return wgrad_split(N * OH * OW, KH * KW * C, Ncol, target_blocks, nullptr);
+  return wgrad_split(N * OH * OW, KH * KW * C, Ncol, target_blocks & 0xFFFF, nullptr);
 }
 
 // Weight gradient: dw [Ncol][KH*KW*C] fp32 must be zeroed by the caller.
@@ -2226,6 +2403,9 @@ KFB_API hipError_t kfb_conv_wgrad(int dtype, const void* dy, const void* x, floa
                                   int sw, int pt, int pl, int Ncol, int target_blocks,
                                   float* slab, long slab_elems, hipStream_t stream) {
   if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
+  // target_blocks bits 16+: kernel (0 = wgrad_k, 1 = wgrad_glds_k where it applies)
+  const int algo = target_blocks >> 16;
+  target_blocks &= 0xFFFF;
   const long dybytes = (long)N * OH * OW * Ncol * 2, xbytes = (long)N * H * W * C * 2;
   WgArgs a{dy, x, dw, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
            N * OH * OW, 0, (int)(dybytes < (1L << 31) ? dybytes : 0),
@@ -2240,7 +2420,15 @@ KFB_API hipError_t kfb_conv_wgrad(int dtype, const void* dy, const void* x, floa
     mode = (KH == 1 && KW == 1 && sh == 1 && sw == 1 && pt == 0 && pl == 0 && OH == H && OW == W)
                ? WG_PLAIN : WG_GATHER;
   const dim3 grid(tiles * split);
-  if (dtype == BF16) {
+  if (algo == 1 && mode != WG_GENERIC && bmc == 128 && (dtype == BF16 || dtype == F16)) {
+    if (dtype == BF16) {
+      if (mode == WG_PLAIN) hipLaunchKernelGGL((wgrad_glds_k<bf16, WG_PLAIN>), grid, dim3(256), 0, stream, a);
+      else hipLaunchKernelGGL((wgrad_glds_k<bf16, WG_GATHER>), grid, dim3(256), 0, stream, a);
+    } else {
+      if (mode == WG_PLAIN) hipLaunchKernelGGL((wgrad_glds_k<f16, WG_PLAIN>), grid, dim3(256), 0, stream, a);
+      else hipLaunchKernelGGL((wgrad_glds_k<f16, WG_GATHER>), grid, dim3(256), 0, stream, a);
+    }
+  } else if (dtype == BF16) {
     if (bmc == 64) launch_wg<bf16, 64>(a, mode, grid, stream);
     else launch_wg<bf16, 128>(a, mode, grid, stream);
   } else if (dtype == F16) {

@@ -210,7 +210,8 @@ def _time_candidates(cands, run, rounds=2, reps=3, label=None):
             _ALGO_NAMES.update({v: k for k, v in IG_ALGOS.items()})
         ranked = sorted(best_t.items(), key=lambda kv: kv[1])
         print("[autotune] %s: %s" % (label, "  ".join(
-            "%s %.1f" % (_ALGO_NAMES.get(c, c), 1e3 * t / reps) for c, t in ranked)),
+            "%s %.1f" % ("glds/%d" % (c & 0xFFFF) if c >= (1 << 16) else _ALGO_NAMES.get(c, c),
+                         1e3 * t / reps) for c, t in ranked)),
             file=sys.stderr, flush=True)
     return best
 
@@ -392,7 +393,21 @@ def _wgrad_launch(dy, x, dw, geo, target):
 # KFB_CONV_AUTOTUNE=0 pins _WGRAD_TARGET_BLOCKS.
 _AUTOTUNE = os.environ.get("KFB_CONV_AUTOTUNE", "1") != "0" and "KFB_WGRAD_BLOCKS" not in os.environ
 _WGRAD_CANDIDATES = (384, 512, 768, 1024)
+# bit 16 of a candidate selects the LDS-DMA wgrad kernel (wgrad_glds_k: 128-wide
+# output-channel tiles, operands < 2 GiB); KFB_WGRAD_ALGO=classic|glds pins one
+_WGRAD_GLDS = 1 << 16
+_WGRAD_ALGO = os.environ.get("KFB_WGRAD_ALGO", "")
 _wgrad_tuned = {}
+
+
+def _wgrad_candidates(geo):
+    cout = geo[12]
+    glds = tuple(t | _WGRAD_GLDS for t in _WGRAD_CANDIDATES) if cout > 64 else ()
+    if _WGRAD_ALGO == "classic" or not glds:
+        return _WGRAD_CANDIDATES
+    if _WGRAD_ALGO == "glds":
+        return glds
+    return _WGRAD_CANDIDATES + glds
 
 
 def _tune_wgrad(dy, x, dw, geo):
@@ -403,7 +418,8 @@ def _tune_wgrad(dy, x, dw, geo):
     if torch.cuda.is_current_stream_capturing():
         return _WGRAD_TARGET_BLOCKS
     scratch = torch.zeros_like(dw)
-    best = _time_candidates(_WGRAD_CANDIDATES, lambda t: _wgrad_launch(dy, x, scratch, geo, t))
+    best = _time_candidates(_wgrad_candidates(geo), lambda t: _wgrad_launch(dy, x, scratch, geo, t),
+                            label="wgrad %s" % (geo,))
     _wgrad_tuned[key] = best
     return best
 

@@ -406,3 +406,40 @@ def test_act_link_fused_backward(cuda, relu, consumers, monkeypatch):
     for wa, wb in zip(w2a, w2b):
         torch.testing.assert_close(wa.grad.cpu(), wb.grad, rtol=3e-2,
                                    atol=2e-2 * wb.grad.abs().max().item())
+
+
+# (N, H, W, Cin, Cout, KH, KW, stride, mode): LDS-DMA wgrad geometries - 3x3
+# gathers with padding, a strided gather, plain 1x1, Cout / K not multiples of
+# 128, reduction lengths not multiples of the 64-row step
+WGRAD_SHAPES = [
+    (4, 14, 14, 64, 128, 3, 3, 1, "SAME_RESNET"),
+    (2, 13, 13, 128, 192, 3, 3, 1, "SAME_RESNET"),
+    (3, 15, 15, 64, 256, 1, 1, 2, "SAME"),
+    (5, 7, 7, 256, 128, 1, 1, 1, "SAME"),
+    (2, 9, 11, 32, 136, 3, 3, 2, "VALID"),
+]
+
+
+@pytest.mark.parametrize("shape", WGRAD_SHAPES, ids=[str(s) for s in WGRAD_SHAPES])
+@pytest.mark.parametrize("target", [1024, 64])
+def test_wgrad_glds_kernel(cuda, shape, target):
+    """wgrad_glds_k (forced: bit 16 of the launch target) vs the fp32
+    reference; target 1024 splits the reduction into slabs, 64 keeps one
+    split (fp32 atomics epilogue)."""
+    from kf_benchmarks_amd.ops import conv_hip
+    n, H, W, cin, cout, kh, kw, s, mode = shape
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(n, H, W, cin, generator=g).to(torch.bfloat16)
+    pads = F.resolve_pads(mode, H, W, kh, kw, s, s)
+    w = torch.randn(cout, kh, kw, cin, generator=g)
+    y = conv_ops.conv2d_reference(x.float(), w, (s, s), pads)
+    dy = torch.randn(y.shape, generator=g).to(torch.bfloat16)
+    xb = x.float().requires_grad_(True)
+    wb = w.clone().requires_grad_(True)
+    conv_ops.conv2d_reference(xb, wb, (s, s), pads).backward(dy.float())
+    want = wb.grad
+    geo = (n, H, W, cin, y.shape[1], y.shape[2], kh, kw, s, s, pads[0], pads[2], cout)
+    for t in (target, target | conv_hip._WGRAD_GLDS):
+        dw = torch.zeros(cout, kh, kw, cin, device=cuda)
+        conv_hip._wgrad_launch(dy.to(cuda), x.to(cuda), dw, geo, t)
+        torch.testing.assert_close(dw.cpu(), want, rtol=2e-3, atol=2e-3 * want.abs().max().item())
