@@ -220,10 +220,26 @@ __device__ __forceinline__ void coef_load(const float* __restrict__ p, int c, fl
   for (int k = 0; k < V; ++k) o[k] = p[c + k];
 }
 
+// ReLU bit mask of one 8-channel vector of a 2-byte output: bit k of byte
+// mb[i] = (stored y[8i + k] > 0), from the value as rounded to T, so it equals
+// the test a consumer would make on y itself.  A conv dgrad epilogue reads
+// this byte (1/16 of y's bytes) instead of y (IgArgs::maskbits).
+template <typename T, int V>
+__device__ __forceinline__ void relu_bits(uint8_t* __restrict__ mb, unsigned i, const float (&v)[V]) {
+  if constexpr (V == 8 && sizeof(T) == 2) {
+    if (!mb) return;
+    unsigned b = 0;
+#pragma unroll
+    for (int k = 0; k < V; ++k) b |= ((float)(T)v[k] > 0.f ? 1u : 0u) << k;
+    mb[i] = (uint8_t)b;
+  }
+}
+
 template <typename T, int V, bool RES, bool RELU, int U = 0>
 __global__ void __launch_bounds__(256)
 bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y, long nvec, int C,
-           const float* __restrict__ scale, const float* __restrict__ shift) {
+           const float* __restrict__ scale, const float* __restrict__ shift,
+           uint8_t* __restrict__ mb = nullptr) {
   // nvec < 2^31 is checked on the host: 32-bit index math avoids 64-bit division.
   const unsigned cv = (unsigned)(C / V);
   const unsigned n = (unsigned)nvec, stride = gridDim.x * blockDim.x;
@@ -259,6 +275,7 @@ bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y
       if (i < n) {
         apply(v[u], rr[u], sc, sf);
         store_vec<T, V>(y + (long)i * V, v[u]);
+        if (RELU) relu_bits<T, V>(mb, i, v[u]);
       }
     }
     return;
@@ -281,6 +298,10 @@ bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y
       apply(v1, r1, sc, sf);
       store_vec<T, V>(y + (long)i * V, v0);
       store_vec<T, V>(y + (long)(i + stride) * V, v1);
+      if (RELU) {
+        relu_bits<T, V>(mb, i, v0);
+        relu_bits<T, V>(mb, i + stride, v1);
+      }
     }
     if (i < n) {
       float v0[V], r0[V];
@@ -288,6 +309,7 @@ bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y
       if (RES) load_vec<T, V>(res + (long)i * V, r0);
       apply(v0, r0, sc, sf);
       store_vec<T, V>(y + (long)i * V, v0);
+      if (RELU) relu_bits<T, V>(mb, i, v0);
     }
     return;
   }
@@ -301,6 +323,7 @@ bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y
     coef_load<V>(shift, c, sf);
     apply(v, rr, sc, sf);
     store_vec<T, V>(y + e, v);
+    if (RELU) relu_bits<T, V>(mb, i, v);
   }
 }
 
@@ -312,7 +335,8 @@ template <typename T, int V, bool RELU, int U = 0>
 __global__ void __launch_bounds__(256)
 bn_apply2_k(const T* __restrict__ x, const T* __restrict__ xr, T* __restrict__ y, long nvec, int C,
             const float* __restrict__ scale, const float* __restrict__ shift,
-            const float* __restrict__ scale_r, const float* __restrict__ shift_r) {
+            const float* __restrict__ scale_r, const float* __restrict__ shift_r,
+            uint8_t* __restrict__ mb = nullptr) {
   const unsigned cv = (unsigned)(C / V);
   const unsigned n = (unsigned)nvec, stride = gridDim.x * blockDim.x;
   const unsigned i0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -347,6 +371,7 @@ bn_apply2_k(const T* __restrict__ x, const T* __restrict__ xr, T* __restrict__ y
       if (i < n) {
         apply(v[u], r[u], a, b, ar, br);
         store_vec<T, V>(y + (long)i * V, v[u]);
+        if (RELU) relu_bits<T, V>(mb, i, v[u]);
       }
     }
     return;
@@ -369,6 +394,10 @@ bn_apply2_k(const T* __restrict__ x, const T* __restrict__ xr, T* __restrict__ y
       apply(v1, r1, a, b, ar, br);
       store_vec<T, V>(y + (long)i * V, v0);
       store_vec<T, V>(y + (long)(i + stride) * V, v1);
+      if (RELU) {
+        relu_bits<T, V>(mb, i, v0);
+        relu_bits<T, V>(mb, i + stride, v1);
+      }
     }
     if (i < n) {
       float v0[V], r0[V];
@@ -376,6 +405,7 @@ bn_apply2_k(const T* __restrict__ x, const T* __restrict__ xr, T* __restrict__ y
       load_vec<T, V>(xr + (long)i * V, r0);
       apply(v0, r0, a, b, ar, br);
       store_vec<T, V>(y + (long)i * V, v0);
+      if (RELU) relu_bits<T, V>(mb, i, v0);
     }
     return;
   }
@@ -391,6 +421,7 @@ bn_apply2_k(const T* __restrict__ x, const T* __restrict__ xr, T* __restrict__ y
     coef_load<V>(shift_r, c, br);
     apply(v, r, a, b, ar, br);
     store_vec<T, V>(y + e, v);
+    if (RELU) relu_bits<T, V>(mb, i, v);
   }
 }
 
@@ -1028,13 +1059,13 @@ static void launch_bwd_apply(int gb, hipStream_t stream, const void* dy, const v
 
 template <typename T, int V, bool RES, bool RELU>
 static void launch_apply(hipStream_t stream, const void* x, const void* res, void* y, long nvec,
-                         int C, const float* scale, const float* shift) {
+                         int C, const float* scale, const float* shift, uint8_t* mb = nullptr) {
   if (flat_ok(nvec, C, V))
     hipLaunchKernelGGL((bn_apply_k<T, V, RES, RELU, 4>), dim3(flat_grid(nvec)), dim3(256), 0,
-                       stream, (const T*)x, (const T*)res, (T*)y, nvec, C, scale, shift);
+                       stream, (const T*)x, (const T*)res, (T*)y, nvec, C, scale, shift, mb);
   else
     hipLaunchKernelGGL((bn_apply_k<T, V, RES, RELU>), dim3(stream_grid(nvec)), dim3(256), 0,
-                       stream, (const T*)x, (const T*)res, (T*)y, nvec, C, scale, shift);
+                       stream, (const T*)x, (const T*)res, (T*)y, nvec, C, scale, shift, mb);
 }
 
 }  // namespace kfb
@@ -1055,7 +1086,9 @@ KFB_API hipError_t kfb_bn_fwd_train(int dtype, const void* x, const void* res, v
                                     float eps, float* run_mean, float* run_var, float* save_mean,
                                     float* save_invstd, float* scale, float* shift, float* psum,
                                     float* psq, int nslab, int relu, int have_partials,
-                                    float* kshift, hipStream_t stream) {
+                                    float* kshift, uint8_t* mbits, hipStream_t stream) {
+  // mbits (nullable, 2-byte dtypes with relu): also write y's ReLU bit mask
+  // [rows * C / 8] (see relu_bits)
   const int V = vec_width(C);
   KFB_DISPATCH_DTYPE(dtype, T, {
     KFB_DISPATCH_VEC(V, VV, {
@@ -1072,10 +1105,10 @@ KFB_API hipError_t kfb_bn_fwd_train(int dtype, const void* x, const void* res, v
                          save_mean, save_invstd, scale, shift, kshift);
       const long nvec = rows * C / VV;
       if (res) {
-        if (relu) launch_apply<T, VV, true, true>(stream, x, res, y, nvec, C, scale, shift);
+        if (relu) launch_apply<T, VV, true, true>(stream, x, res, y, nvec, C, scale, shift, mbits);
         else launch_apply<T, VV, true, false>(stream, x, res, y, nvec, C, scale, shift);
       } else {
-        if (relu) launch_apply<T, VV, false, true>(stream, x, nullptr, y, nvec, C, scale, shift);
+        if (relu) launch_apply<T, VV, false, true>(stream, x, nullptr, y, nvec, C, scale, shift, mbits);
         else launch_apply<T, VV, false, false>(stream, x, nullptr, y, nvec, C, scale, shift);
       }
     });
@@ -1093,7 +1126,7 @@ KFB_API hipError_t kfb_bn_fwd_train_dual(
     int nslab, const float* gamma_r, const float* beta_r, float decay_r, float eps_r,
     float* run_mean_r, float* run_var_r, float* save_mean_r, float* save_invstd_r,
     float* scale_r, float* shift_r, const float* psum_r, const float* psq_r, int nslab_r,
-    int relu, float* kshift, float* kshift_r, hipStream_t stream) {
+    int relu, float* kshift, float* kshift_r, uint8_t* mbits, hipStream_t stream) {
   const int V = vec_width(C);
   hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, psum_r,
                      psq_r, nslab_r, C, rows, gamma_r, beta_r, decay_r, eps_r, run_mean_r,
@@ -1110,11 +1143,11 @@ KFB_API hipError_t kfb_bn_fwd_train_dual(
         if (flat)
           hipLaunchKernelGGL((bn_apply2_k<T, VV, true, 4>), dim3(gb), dim3(256), 0, stream,
                              (const T*)x, (const T*)xr, (T*)y, nvec, C, scale, shift, scale_r,
-                             shift_r);
+                             shift_r, mbits);
         else
           hipLaunchKernelGGL((bn_apply2_k<T, VV, true>), dim3(gb), dim3(256), 0, stream,
                              (const T*)x, (const T*)xr, (T*)y, nvec, C, scale, shift, scale_r,
-                             shift_r);
+                             shift_r, mbits);
       } else {
         if (flat)
           hipLaunchKernelGGL((bn_apply2_k<T, VV, false, 4>), dim3(gb), dim3(256), 0, stream,

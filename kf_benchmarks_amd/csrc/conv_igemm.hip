@@ -113,6 +113,11 @@ struct IgArgs {
   // (kh, kw) = (8s + kc) / KW, (8s + kc) % KW of step s; the step advances
   // the rows by 8 / KW (c8_step elements)
   int c8, c8_step;
+  // mask != null: 1 = `mask` is the producer BN's ReLU bit mask (bit k of
+  // byte e/8 = y[e + k] > 0 for the 8-element chunk starting at element e,
+  // written by the BN apply pass, csrc/bn.hip relu_bits) instead of its
+  // output y - 1/16 of the bytes for the same test
+  int maskbits;
 };
 
 constexpr int IG_BK = 64;
@@ -273,8 +278,10 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
   } else if (EXTRAS && a.ybytes > 0) {
     const __amdgpu_buffer_rsrc_t rad = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.addend ? a.addend : a.y), (short)0, a.addend ? a.ybytes : 0, 0x00020000);
+    const bool mbits = a.maskbits != 0;
     const __amdgpu_buffer_rsrc_t rmk = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.mask ? a.mask : a.y), (short)0, (a.mask && a.xbn) ? a.ybytes : 0, 0x00020000);
+        (void*)(a.mask ? a.mask : a.y), (short)0,
+        (a.mask && a.xbn) ? (mbits ? a.ybytes / 16 : a.ybytes) : 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t rxb = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.xbn ? a.xbn : a.y), (short)0, a.xbn ? a.ybytes : 0, 0x00020000);
     // Passes go in groups of G: the extra-operand loads of group g+1 are
@@ -295,7 +302,12 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
         const int m = m0 + t / CPR, n = n0 + (t % CPR) * 8;
         offb[b][q] = (m < a.M && n < a.Ncol) ? (int)((row_offset(m) + n) * (long)sizeof(T)) : -1;
         ad[b][q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rad, offb[b][q], 0, 0));
-        mk[b][q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rmk, offb[b][q], 0, 0));
+        if (mbits)  // one byte per 16-byte chunk (offb < 0: out of range, reads 0)
+          mk[b][q] = make_uint4(
+              __builtin_amdgcn_raw_buffer_load_b8(rmk, offb[b][q] < 0 ? -1 : offb[b][q] >> 4, 0, 0),
+              0u, 0u, 0u);
+        else
+          mk[b][q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rmk, offb[b][q], 0, 0));
         xb[b][q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rxb, offb[b][q], 0, 0));
       }
     };
@@ -316,7 +328,10 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
         for (int k = 0; k < 8; ++k) {
           float v = (float)tv.v[k] + (float)av.v[k];  // zero addend when absent
           if (a.xbn) {
-            if (a.mask) v = (float)mv.v[k] > 0.f ? v : 0.f;
+            if (a.mask) {
+              if (mbits) v = (mk[b][q].x >> k) & 1u ? v : 0.f;
+              else v = (float)mv.v[k] > 0.f ? v : 0.f;
+            }
             // same expression as the BN apply (bn_apply_k), so the same sign
             else if (mrec) v = (float)xv.v[k] * msc[k] + msh[k] > 0.f ? v : 0.f;
             s1[k] += v;
@@ -358,7 +373,11 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
         for (int k = 0; k < 8; ++k) v[k] += (float)av.v[k];
       }
       if (a.xbn) {
-        if (a.mask) {
+        if (a.mask && a.maskbits) {
+          const unsigned mb = ((const uint8_t*)a.mask)[off >> 3];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = (mb >> k) & 1u ? v[k] : 0.f;
+        } else if (a.mask) {
           const Vec<T, 8> mv = *(const Vec<T, 8>*)((const T*)a.mask + off);
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[k] = (float)mv.v[k] > 0.f ? v[k] : 0.f;
@@ -2292,7 +2311,8 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
                                   const float* bias, int flags, int algo, const float* kshift,
                                   hipStream_t stream) {
   // flags: bit 0 = ReLU after the bias (forward epilogue), bit 1 = zero-fill
-  // the unsampled pixels of a stride-2 scatter (see IgArgs::zfill)
+  // the unsampled pixels of a stride-2 scatter (see IgArgs::zfill), bit 2 =
+  // `mask` is a ReLU bit mask (see IgArgs::maskbits)
   if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
   const int relu = flags & 1, zfill = (flags >> 1) & 1;
   if (zfill && !(ys == 2 && YH == 2 * OH && YW == 2 * OW)) return hipErrorInvalidValue;
@@ -2303,7 +2323,8 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
            (int)(xbytes < (1L << 31) ? xbytes : 0), (int)(wbytes < (1L << 31) ? wbytes : 0),
            (int)(ybytes < (1L << 31) ? ybytes : 0),
            (stats && !xbn && !addend) ? kshift : nullptr,
-           FastDiv(C), FastDiv(KW), FastDiv(sh), FastDiv(sw), zfill, 0, 0};
+           FastDiv(C), FastDiv(KW), FastDiv(sh), FastDiv(sw), zfill, 0, 0,
+           (mask && ((flags >> 2) & 1)) ? 1 : 0};
   const bool t = trans != 0;
   // IG_ALGO_GENERIC: the per-chunk division loader (autotune candidate for
   // the 8-channel geometry, where it can beat the FAST tap stepping)

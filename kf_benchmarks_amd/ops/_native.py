@@ -33,9 +33,9 @@ F = c_float
 # name -> argtypes (restype is int = hipError_t unless listed in _RESTYPES)
 _SIGS = {
     "kfb_bn_num_slabs": [L, I],
-    "kfb_bn_fwd_train": [I, P, P, P, L, I, P, P, F, F, P, P, P, P, P, P, P, P, I, I, I, P, P],
+    "kfb_bn_fwd_train": [I, P, P, P, L, I, P, P, F, F, P, P, P, P, P, P, P, P, I, I, I, P, P, P],
     "kfb_bn_fwd_train_dual": [I, P, P, P, L, I, P, P, F, F, P, P, P, P, P, P, P, P, I,
-                              P, P, F, F, P, P, P, P, P, P, P, P, I, I, P, P, P],
+                              P, P, F, F, P, P, P, P, P, P, P, P, I, I, P, P, P, P],
     "kfb_bn_bwd_dual": [I, P, P, P, P, P, L, I, P, P, P, P, P, P, P, I, P, P, P, I,
                         P, P, P, P, P, P, P, I, P, P, P, I, P],
     "kfb_bn_fwd_infer": [I, P, P, P, L, I, P, P, P, P, F, P, P, I, P],

@@ -291,7 +291,9 @@ def _igemm(x, wmat, y, N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW
     """``zfill``: stride-2 scatter whose epilogue also zeroes the unsampled
     pixels of each 2x2 block (the output needs no separate zero fill)."""
     geo = (N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy, int(trans))
-    flags = int(bool(relu)) | (2 if zfill else 0)
+    # a uint8 mask is the producer BN's ReLU bit mask (IgArgs::maskbits)
+    mbits = mask is not None and mask.dtype == torch.uint8
+    flags = int(bool(relu)) | (2 if zfill else 0) | (4 if mbits else 0)
     algo = _igemm_algo(x, wmat, y, geo, (stats, mask, xbn, mean, addend, mcoef), (bias, flags))
     _igemm_call(algo, x, wmat, y, geo, stats, mask, xbn, mean, addend, mcoef, bias, flags)
 
@@ -731,8 +733,11 @@ class _Conv2d(torch.autograd.Function):
                             # residual add (link.mcoef), else read from its output
                             rec = link.relu and link.mcoef is not None
                             xbn = link.x_bn if link.x_bn is not None else xp  # act link
-                            fuse = (parts, xp if link.relu and not rec else None, xbn,
-                                    link.mean, link.mcoef if rec else None)
+                            # (y's ReLU bit mask when the BN apply wrote one)
+                            mk = None
+                            if link.relu and not rec:
+                                mk = link.mbits if link.mbits is not None else xp
+                            fuse = (parts, mk, xbn, link.mean, link.mcoef if rec else None)
                         dx = conv_dgrad(dy, wp, xp.shape, stride, pads, fuse, addend=pend,
                                         wt=ctx.wt, addend_inplace=owned)
                         if fuse is not None:

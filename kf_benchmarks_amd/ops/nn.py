@@ -118,7 +118,7 @@ class BNLink:
 
     __slots__ = ("x_bn", "mean", "relu", "convs", "resid", "pools", "other", "accum", "partials",
                  "pending",
-                 "pending_owned", "arrived", "mcoef", "pending_sparse", "pending_event")
+                 "pending_owned", "arrived", "mcoef", "pending_sparse", "pending_event", "mbits")
 
     def __init__(self, x_bn, mean, relu, mcoef=None):
         self.x_bn, self.mean, self.relu = x_bn, mean, relu
@@ -126,6 +126,10 @@ class BNLink:
         # residual add: a consumer's dgrad epilogue recomputes the ReLU mask
         # from x_bn instead of reading y
         self.mcoef = mcoef
+        # y's ReLU bit mask (uint8 [rows * C / 8], bit k of byte e/8 = y[e+k] > 0)
+        # written by the BN apply pass when the mask cannot be recomputed from
+        # x_bn (residual add): a consumer's dgrad epilogue reads it instead of y
+        self.mbits = None
         self.convs, self.resid, self.pools, self.other = 0, 0, 0, False
         # accumulation-only link (a concat output, no BN behind it): the last
         # conv adds the pending gradient in its dgrad epilogue, nothing else
@@ -208,6 +212,19 @@ def _grad_ready(p):
         cb(p)
 
 
+# KFB_RELU_BITS=0: consumers' dgrad epilogues read the BN output itself for
+# the ReLU mask (16x the bytes of the bit mask)
+_RELU_BITS = os.environ.get("KFB_RELU_BITS", "1") != "0"
+
+
+def _relu_bits_buffer(x, rows, C):
+    """uint8 [rows * C / 8] for the BN apply pass's ReLU bit mask, or None
+    (2-byte dtypes with C % 8 == 0 only: one byte per 16-byte vector)."""
+    if not _RELU_BITS or x.element_size() != 2 or C % 8 or not _conv.FUSE_BN:
+        return None
+    return torch.empty((rows * C // 8,), dtype=torch.uint8, device=x.device)
+
+
 class _BatchNormTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, rm, rv, decay, eps, relu, stats):
@@ -228,17 +245,20 @@ class _BatchNormTrain(torch.autograd.Function):
         st = torch.empty((2, C), dtype=torch.float32, device=dev)  # mean, invstd
         y = torch.empty_like(x)
         res = residual.contiguous() if residual is not None else None
+        rec = relu and residual is None and _MASK_RECOMPUTE
+        mbits = _relu_bits_buffer(x, rows, C) if relu and not rec else None
         N.call("kfb_bn_fwd_train", N.dt(x), x.data_ptr(), N.ptr(res), y.data_ptr(), rows, C,
                N.ptr(gamma), N.ptr(beta), float(decay), float(eps), N.ptr(rm), N.ptr(rv),
                st[0].data_ptr(), st[1].data_ptr(), coef[:C].data_ptr(),
                coef[C:].data_ptr(), psum.data_ptr(), psq.data_ptr(), nslab, int(relu),
-               int(stats is not None), N.ptr(_conv_hip().stats_shift(stats)), N.stream(dev))
+               int(stats is not None), N.ptr(_conv_hip().stats_shift(stats)), N.ptr(mbits),
+               N.stream(dev))
         ctx.save_for_backward(x, y if relu else None, gamma, st)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.gamma, ctx.beta = gamma, beta
-        link = BNLink(x, st[0], relu,
-                      coef if (relu and residual is None and _MASK_RECOMPUTE) else None)
+        link = BNLink(x, st[0], relu, coef if rec else None)
+        link.mbits = mbits
         y._kfb_bn_link = link
         ctx.link = link
         ctx.res_link = getattr(residual, "_kfb_bn_link", None) if residual is not None else None
@@ -361,6 +381,7 @@ class _BatchNormTrainDual(torch.autograd.Function):
         nslab, nslab_r = stats.numel() // (2 * C), stats_r.numel() // (2 * C)
         ws = torch.empty((2, 4, C), dtype=torch.float32, device=dev)  # [bn][mean|invstd|scale|shift]
         y = torch.empty_like(x)
+        mbits = _relu_bits_buffer(x, rows, C) if relu else None
         N.call("kfb_bn_fwd_train_dual", N.dt(x), x.data_ptr(), xr.data_ptr(), y.data_ptr(),
                rows, C, N.ptr(gamma), N.ptr(beta), float(decay), float(eps), N.ptr(rm),
                N.ptr(rv), ws[0, 0].data_ptr(), ws[0, 1].data_ptr(), ws[0, 2].data_ptr(),
@@ -370,12 +391,13 @@ class _BatchNormTrainDual(torch.autograd.Function):
                ws[1, 3].data_ptr(), stats_r[:nslab_r * C].data_ptr(),
                stats_r[nslab_r * C:].data_ptr(), nslab_r, int(relu),
                N.ptr(_conv_hip().stats_shift(stats)), N.ptr(_conv_hip().stats_shift(stats_r)),
-               N.stream(dev))
+               N.ptr(mbits), N.stream(dev))
         st, st_r = ws[0, :2], ws[1, :2]
         ctx.save_for_backward(x, y if relu else None, gamma, st, xr, gamma_r, st_r)
         ctx.relu = relu
         ctx.params = (gamma, beta, gamma_r, beta_r)
         link = BNLink(x, st[0], relu)
+        link.mbits = mbits
         y._kfb_bn_link = link
         ctx.link = link
         return y

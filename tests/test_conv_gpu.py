@@ -148,14 +148,22 @@ FUSED_SHAPES = [
 ]
 
 
+def pack_relu_bits(y):
+    """Host form of the BN apply pass's ReLU bit mask (csrc/bn.hip relu_bits):
+    bit k of byte e/8 = y[e + k] > 0 over the flattened tensor."""
+    b = (y.float().reshape(-1, 8) > 0).to(torch.int32)
+    return (b * (1 << torch.arange(8, dtype=torch.int32))).sum(1).to(torch.uint8)
+
+
 @pytest.mark.parametrize("shape", FUSED_SHAPES, ids=[str(s) for s in FUSED_SHAPES])
 @pytest.mark.parametrize("with_addend", [False, True])
-@pytest.mark.parametrize("mask_src", ["read", "recompute"])
+@pytest.mark.parametrize("mask_src", ["read", "recompute", "bits"])
 def test_dgrad_fused_epilogue(cuda, shape, with_addend, ig_algo, mask_src):
     """dgrad epilogue: dX = (conv^T(dY) + addend) * [x > 0] and the producer
     BN's backward partials sum(dX), sum(dX * (x_bn - mean)) per channel.  The
-    ReLU mask is read from x (the BN output) or recomputed as
-    x_bn * scale + shift > 0 (BNs without a residual add)."""
+    ReLU mask is read from x (the BN output), from its bit mask (one byte
+    per 8 channels, IgArgs::maskbits) or recomputed as x_bn * scale + shift > 0
+    (BNs without a residual add)."""
     from kf_benchmarks_amd.ops import conv_hip
     n, H, W, cin, cout, kh, kw, s, mode = shape
     scatter = kh == 1 and s > 1
@@ -190,7 +198,9 @@ def test_dgrad_fused_epilogue(cuda, shape, with_addend, ig_algo, mask_src):
     if True:
         ref = ref * (x.float() > 0)
         parts = conv_hip.stats_buffer(cin, cuda).zero_()
-        if mcoef is None:
+        if mask_src == "bits":
+            fuse = (parts, pack_relu_bits(x).to(cuda), xb.to(cuda), mean.to(cuda))
+        elif mcoef is None:
             fuse = (parts, x.to(cuda), xb.to(cuda), mean.to(cuda))
         else:
             fuse = (parts, None, xb.to(cuda), mean.to(cuda), mcoef.to(cuda))
@@ -443,3 +453,37 @@ def test_wgrad_glds_kernel(cuda, shape, target):
         dw = torch.zeros(cout, kh, kw, cin, device=cuda)
         conv_hip._wgrad_launch(dy.to(cuda), x.to(cuda), dw, geo, t)
         torch.testing.assert_close(dw.cpu(), want, rtol=2e-3, atol=2e-3 * want.abs().max().item())
+
+
+@pytest.mark.parametrize("dual", [False, True])
+@pytest.mark.parametrize("shape", [(2, 7, 7, 64), (4, 14, 14, 256), (1, 3, 5, 8)])
+def test_bn_apply_writes_relu_bits(cuda, shape, dual):
+    """The residual / dual BN apply pass writes y's ReLU bit mask (the byte a
+    consumer dgrad epilogue reads instead of y): equal to packing y > 0."""
+    from kf_benchmarks_amd.ops import conv_hip
+    n, H, W, C = shape
+    g = torch.Generator().manual_seed(3)
+    dt = torch.bfloat16
+    x = torch.randn(n, H, W, C, generator=g).to(dt).to(cuda)
+    gamma = (torch.rand(C, generator=g).to(cuda) + 0.5).requires_grad_(True)
+    beta = torch.randn(C, generator=g).to(cuda).requires_grad_(True)
+    stats = conv_hip.stats_buffer(C, cuda).zero_()
+    xs = x.float().reshape(-1, C)
+    stats.view(2, conv_hip.STATS_SPREAD, C)[0, 0] = xs.sum(0)
+    stats.view(2, conv_hip.STATS_SPREAD, C)[1, 0] = (xs * xs).sum(0)
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    if dual:
+        xr = torch.randn(n, H, W, C, generator=g).to(dt).to(cuda)
+        sr = conv_hip.stats_buffer(C, cuda).zero_()
+        xrs = xr.float().reshape(-1, C)
+        sr.view(2, conv_hip.STATS_SPREAD, C)[0, 0] = xrs.sum(0)
+        sr.view(2, conv_hip.STATS_SPREAD, C)[1, 0] = (xrs * xrs).sum(0)
+        r = F.DeferredBN(xr, gamma, beta, rm.clone(), rv.clone(), 0.9, 1e-3, sr)
+        y = F.batch_norm_dual(x, gamma, beta, rm, rv, 0.9, 1e-3, True, stats, r)
+    else:
+        res = torch.randn(n, H, W, C, generator=g).to(dt).to(cuda)
+        y = F.batch_norm(x, gamma, beta, rm, rv, 0.9, 1e-3, True, True, res, stats=stats)
+    link = y._kfb_bn_link
+    assert link.mbits is not None and link.mbits.dtype == torch.uint8
+    torch.cuda.synchronize()
+    assert torch.equal(link.mbits.cpu(), pack_relu_bits(y.detach().cpu()))
