@@ -478,6 +478,13 @@ _WGRAD_SIDE = os.environ.get("KFB_WGRAD_STREAM", "1") != "0"
 _SIDE_STREAMS = {}
 
 
+# weight gradients with more dY rows (pixels) than this run on the compute stream
+# after their dgrad instead of beside the dgrad chain (large-grid layers fill
+# the chip alone; two compute-bound kernels sharing it can be slower than
+# the two back to back)
+_WGRAD_SIDE_MAX = int(float(os.environ.get("KFB_WGRAD_SIDE_MAX", "1e18")))
+
+
 def wgrad_stream(device):
     """The side stream weight gradients run on for ``device`` (None when
     disabled or on the CPU)."""
@@ -767,7 +774,8 @@ class _Conv2d(torch.autograd.Function):
             sink = getattr(w, "_kfb_grad_sink", None)
             direct = (sink is not None and cout_p == cout and wp.shape[-1] == cin
                       and _fuse_enabled())
-            side = wgrad_stream(dy.device) if direct else None
+            side = (wgrad_stream(dy.device)
+                    if direct and dy.numel() // dy.shape[-1] <= _WGRAD_SIDE_MAX else None)
             if side is not None:
                 # weight gradient off the critical path: the dgrad chain
                 # continues on the compute stream while this runs beside it
