@@ -989,6 +989,18 @@ bn_pool3s2_k(const T* __restrict__ dz, const T* __restrict__ z, const uint8_t* _
     const int ox = (int)(p % (unsigned)OWo); p /= (unsigned)OWo;
     const int oy = (int)(p % (unsigned)OHo);
     const int n = (int)(p / (unsigned)OHo);
+    // the block's 4 x loads go out first (clamped in-range addresses, masked
+    // below), so they fly with the window loads of the routing instead of
+    // after it (the partial pass was latency-bound at ~2 TB/s)
+    float xb[2][2][8];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int h = min(max(2 * oy - g.pt + a, 0), g.H - 1);
+        const int w = min(max(2 * ox - g.pl + b, 0), g.W - 1);
+        load_vec<T, 8>(x + (((long)n * g.H + h) * g.W + w) * g.C + c, xb[a][b]);
+      }
     float gr[2][2][8];
     route_block_3s2<T>(dz, z, idx, g, n, oy, ox, c, gr);
 #pragma unroll
@@ -1000,8 +1012,7 @@ bn_pool3s2_k(const T* __restrict__ dz, const T* __restrict__ z, const uint8_t* _
         const int w = 2 * ox - g.pl + b;
         if ((unsigned)w >= (unsigned)g.W) continue;
         const long e = (((long)n * g.H + h) * g.W + w) * g.C + c;
-        float xv[8];
-        load_vec<T, 8>(x + e, xv);
+        const float (&xv)[8] = xb[a][b];
         if (PASS == 0) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) { s[k] += gr[a][b][k]; q[k] += gr[a][b][k] * (xv[k] - m[k]); }

@@ -160,11 +160,77 @@ struct NoPrefetch {
   __device__ void operator()() const {}
 };
 
+// Output-row offset (elements) of GEMM row m in the y layout.
+__device__ __forceinline__ long ig_row_offset(const IgArgs& a, int m) {
+  if (a.ys == 1 && a.YH == a.OH && a.YW == a.OW) return (long)m * a.ldy;
+  const int OHW = a.OH * a.OW;
+  const int img = m / OHW, rem = m - img * OHW;
+  const int oh = rem / a.OW, ow = rem - oh * a.OW;
+  return ((long)(img * a.YH + oh * a.ys) * a.YW + ow * a.ys) * a.ldy;
+}
+
+// Range-checked buffer resources of the dgrad-style epilogue operands
+// (addend, mask / ReLU bits, xbn); a null operand gets a zero-size range.
+struct EpiRsrc {
+  __amdgpu_buffer_rsrc_t ad, mk, xb;
+};
+__device__ __forceinline__ EpiRsrc epi_rsrc(const IgArgs& a) {
+  EpiRsrc r;
+  r.ad = __builtin_amdgcn_make_buffer_rsrc((void*)(a.addend ? a.addend : a.y), (short)0,
+                                           a.addend ? a.ybytes : 0, 0x00020000);
+  r.mk = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.mask ? a.mask : a.y), (short)0,
+      (a.mask && a.xbn) ? (a.maskbits ? a.ybytes / 16 : a.ybytes) : 0, 0x00020000);
+  r.xb = __builtin_amdgcn_make_buffer_rsrc((void*)(a.xbn ? a.xbn : a.y), (short)0,
+                                           a.xbn ? a.ybytes : 0, 0x00020000);
+  return r;
+}
+
+// One pass group's epilogue operands (G 16-byte chunks of each of addend,
+// mask, xbn, and their byte offsets; -1 = outside the output).
+template <int G>
+struct EpiOps {
+  int offb[G];
+  uint4 ad[G], mk[G], xb[G];
+};
+
+template <typename T, int BN, int NT, int G>
+__device__ __forceinline__ void epi_load(const IgArgs& a, const EpiRsrc& r, int m0, int n0, int g,
+                                         EpiOps<G>& e) {
+  constexpr int CPR = BN / 8;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < G; ++q) {
+    const int t = tid + (g * G + q) * NT;
+    const int m = m0 + t / CPR, n = n0 + (t % CPR) * 8;
+    e.offb[q] = (m < a.M && n < a.Ncol) ? (int)((ig_row_offset(a, m) + n) * (long)sizeof(T)) : -1;
+    e.ad[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r.ad, e.offb[q], 0, 0));
+    if (a.maskbits)  // one byte per 16-byte chunk (offb < 0: out of range, reads 0)
+      e.mk[q] = make_uint4(
+          __builtin_amdgcn_raw_buffer_load_b8(r.mk, e.offb[q] < 0 ? -1 : e.offb[q] >> 4, 0, 0), 0u,
+          0u, 0u);
+    else
+      e.mk[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r.mk, e.offb[q], 0, 0));
+    e.xb[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r.xb, e.offb[q], 0, 0));
+  }
+}
+
+// Pass-group size of the dgrad-style epilogue of a BM x BN tile on NT threads.
+template <int BM, int BN, int NT>
+constexpr int epi_group() {
+  return BM * (BN / 8) / NT > 4 ? 4 : BM * (BN / 8) / NT;
+}
+
+// EARLY: the first pass group's operands were loaded by the kernel before
+// its K loop (`early`, valid only when the launch has addend / xbn): their
+// latency hides behind the GEMM instead of following it (short-K dgrads,
+// where the epilogue's three extra streams are most of the bytes).
 template <typename T, int BM, int BN, int NT, int WGM, int WGN, typename Pre = NoPrefetch,
-          bool EXTRAS = true>
+          bool EXTRAS = true, bool EARLY = false>
 __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN / 16][BM / WGM / 16],
                                             T* smem, int m0, int n0, int wm, int wn,
-                                            Pre pre = Pre()) {
+                                            Pre pre = Pre(),
+                                            const EpiOps<epi_group<BM, BN, NT>()>* early = nullptr) {
   constexpr int TN = BN / WGN / 16, TM = BM / WGM / 16;
   const int tid = threadIdx.x, lane = tid & 63;
   const int OHW = a.OH * a.OW;
@@ -276,60 +342,38 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
       }
     }
   } else if (EXTRAS && a.ybytes > 0) {
-    const __amdgpu_buffer_rsrc_t rad = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.addend ? a.addend : a.y), (short)0, a.addend ? a.ybytes : 0, 0x00020000);
     const bool mbits = a.maskbits != 0;
-    const __amdgpu_buffer_rsrc_t rmk = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.mask ? a.mask : a.y), (short)0,
-        (a.mask && a.xbn) ? (mbits ? a.ybytes / 16 : a.ybytes) : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rxb = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.xbn ? a.xbn : a.y), (short)0, a.xbn ? a.ybytes : 0, 0x00020000);
+    const EpiRsrc rs = epi_rsrc(a);
     // Passes go in groups of G: the extra-operand loads of group g+1 are
     // issued before group g is processed and stored, so they fly meanwhile
     // and a store never precedes the loads it would make wait (loads and
     // stores share the in-order vmcnt).  Small tiles (NPASS <= 4) form one
     // group: every load before any store.  Big tiles keep 2 groups of 3 x G
     // 16-byte operands in registers instead of 3 x NPASS.
-    constexpr int G = NPASS > 4 ? 4 : NPASS;
+    constexpr int G = epi_group<BM, BN, NT>();
     constexpr int NG = NPASS / G;
     static_assert(NPASS % G == 0, "pass groups");
-    int offb[2][G];
-    uint4 ad[2][G], mk[2][G], xb[2][G];
-    auto load_group = [&](int g, int b) {
-#pragma unroll
-      for (int q = 0; q < G; ++q) {
-        const int t = tid + (g * G + q) * NT;
-        const int m = m0 + t / CPR, n = n0 + (t % CPR) * 8;
-        offb[b][q] = (m < a.M && n < a.Ncol) ? (int)((row_offset(m) + n) * (long)sizeof(T)) : -1;
-        ad[b][q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rad, offb[b][q], 0, 0));
-        if (mbits)  // one byte per 16-byte chunk (offb < 0: out of range, reads 0)
-          mk[b][q] = make_uint4(
-              __builtin_amdgcn_raw_buffer_load_b8(rmk, offb[b][q] < 0 ? -1 : offb[b][q] >> 4, 0, 0),
-              0u, 0u, 0u);
-        else
-          mk[b][q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rmk, offb[b][q], 0, 0));
-        xb[b][q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rxb, offb[b][q], 0, 0));
-      }
-    };
-    load_group(0, 0);
+    EpiOps<G> ops[2];
+    if constexpr (EARLY) ops[0] = *early;
+    else epi_load<T, BN, NT, G>(a, rs, m0, n0, 0, ops[0]);
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const int b = g & 1;
-      if (g + 1 < NG) load_group(g + 1, b ^ 1);
+      if (g + 1 < NG) epi_load<T, BN, NT, G>(a, rs, m0, n0, g + 1, ops[b ^ 1]);
 #pragma unroll
       for (int q = 0; q < G; ++q) {
         const uint4 raw = lds_chunk(tid + (g * G + q) * NT);
         const Vec<T, 8> tv = __builtin_bit_cast(Vec<T, 8>, raw);
-        const Vec<T, 8> av = __builtin_bit_cast(Vec<T, 8>, ad[b][q]);
-        const Vec<T, 8> mv = __builtin_bit_cast(Vec<T, 8>, mk[b][q]);
-        const Vec<T, 8> xv = __builtin_bit_cast(Vec<T, 8>, xb[b][q]);
+        const Vec<T, 8> av = __builtin_bit_cast(Vec<T, 8>, ops[b].ad[q]);
+        const Vec<T, 8> mv = __builtin_bit_cast(Vec<T, 8>, ops[b].mk[q]);
+        const Vec<T, 8> xv = __builtin_bit_cast(Vec<T, 8>, ops[b].xb[q]);
         Vec<T, 8> ov;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           float v = (float)tv.v[k] + (float)av.v[k];  // zero addend when absent
           if (a.xbn) {
             if (a.mask) {
-              if (mbits) v = (mk[b][q].x >> k) & 1u ? v : 0.f;
+              if (mbits) v = (ops[b].mk[q].x >> k) & 1u ? v : 0.f;
               else v = (float)mv.v[k] > 0.f ? v : 0.f;
             }
             // same expression as the BN apply (bn_apply_k), so the same sign
@@ -342,8 +386,8 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
           }
           ov.v[k] = (T)v;
         }
-        if (offb[b][q] >= 0) {
-          char* yp = (char*)y + offb[b][q];
+        if (ops[b].offb[q] >= 0) {
+          char* yp = (char*)y + ops[b].offb[q];
           *(uint4*)yp = __builtin_bit_cast(uint4, ov);
           if (a.zfill) {
             const uint4 z = make_uint4(0, 0, 0, 0);
@@ -455,8 +499,10 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
 // workgroups (20 waves) per CU - more loads and stores in flight per CU, for
 // the short-K, write-heavy layers (e.g. 1x1 convs with K = 64).
 
-template <typename T, int BM, int BN, bool TRANS, bool FAST, int NBUF = 2>
-__global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : (NBUF == 1 ? 4 : 2))
+// (EARLY at 128 x 64: the early operands stay live through the K loop; 3
+// workgroups per CU, <= 168 VGPRs, no spills)
+template <typename T, int BM, int BN, bool TRANS, bool FAST, int NBUF = 2, bool EARLY = false>
+__global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : (EARLY ? 3 : (NBUF == 1 ? 4 : 2)))
     igemm_k(IgArgs a) {
   constexpr int XC = BM / 32;  // 16-byte X chunks per thread per K step
   constexpr int WC = BN / 32;  // 16-byte W chunks per thread per K step
@@ -628,6 +674,15 @@ __global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : (NBUF == 1 ? 4 : 2)
   // single set (a second set would spill at 128x128).
   load_x(xr0, 0);
   load_w(wr0, 0);
+  // EARLY: the epilogue's first group of extra operands, issued behind the
+  // first K step's operand loads (the in-order vmcnt lets the LDS store of
+  // those wait for them alone)
+  constexpr int EG = epi_group<BM, BN, 256>();
+  EpiOps<EG> early;
+  if constexpr (EARLY) {
+    if (a.ybytes > 0 && (a.addend || a.xbn))
+      epi_load<T, BN, 256, EG>(a, epi_rsrc(a), m0, n0, 0, early);
+  }
   store(xr0, wr0, 0);
   // Only the FAST 128x128 kernel takes the second X set: the generic gather
   // would spill, and at 128x64 the extra registers cost a workgroup per CU
@@ -662,7 +717,8 @@ __global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : (NBUF == 1 ? 4 : 2)
     __syncthreads();
   }
 
-  ig_epilogue<T, BM, BN, 256, 2, 2>(a, acc, smem, m0, n0, wm, wn);
+  ig_epilogue<T, BM, BN, 256, 2, 2, NoPrefetch, true, EARLY>(a, acc, smem, m0, n0, wm, wn,
+                                                             NoPrefetch(), &early);
 }
 
 // Multi-tile form of the FAST one-stage igemm_k: each workgroup computes TPW
@@ -2221,9 +2277,14 @@ static hipError_t launch_sk(const IgArgs& a, hipStream_t s) {
 }
 
 template <typename T, int BM, int BN>
-static void launch_ig(const IgArgs& a, bool trans, bool fast, hipStream_t s, bool onebuf = false) {
+static void launch_ig(const IgArgs& a, bool trans, bool fast, hipStream_t s, bool onebuf = false,
+                      bool early = false) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
-  if (onebuf && fast)
+  if (early && fast && onebuf)
+    hipLaunchKernelGGL((igemm_k<T, BM, BN, false, true, 1, true>), dim3(nwg), dim3(256), 0, s, a);
+  else if (early && fast)
+    hipLaunchKernelGGL((igemm_k<T, BM, BN, false, true, 2, true>), dim3(nwg), dim3(256), 0, s, a);
+  else if (onebuf && fast)
     hipLaunchKernelGGL((igemm_k<T, BM, BN, false, true, 1>), dim3(nwg), dim3(256), 0, s, a);
   else if (trans)
     hipLaunchKernelGGL((igemm_k<T, BM, BN, true, false>), dim3(nwg), dim3(256), 0, s, a);
@@ -2290,7 +2351,8 @@ enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_G
        IG_ALGO_GSHORT64_3 = 12, IG_ALGO_GSHORT128_3 = 13, IG_ALGO_MULTI2 = 14,
        IG_ALGO_MULTI4 = 15, IG_ALGO_SMALL_MULTI4 = 16, IG_ALGO_GMULTI64 = 17,
        IG_ALGO_GMULTI128 = 18, IG_ALGO_GBIG256 = 19, IG_ALGO_GBIG512 = 20,
-       IG_ALGO_GENERIC = 21, IG_ALGO_SK128 = 22, IG_ALGO_G8P = 23 };
+       IG_ALGO_GENERIC = 21, IG_ALGO_SK128 = 22, IG_ALGO_G8P = 23, IG_ALGO_ONEBUF_E = 24,
+       IG_ALGO_ONEBUF_N64_E = 25, IG_ALGO_CLASSIC_N64_E = 26 };
 
 static bool c8_geometry(int C, int KH, int KW) {
   return C == 8 && (KW == 1 || KW == 2 || KW == 4 || KW == 8) && (KH * KW) % 8 == 0;
@@ -2335,9 +2397,15 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
   }
   const bool fast = !t && (C % IG_BK == 0 || c8) && KH * KW <= 64 && xbytes < (1L << 31) &&
                     wbytes < (1L << 31) && !igemm_fast_disabled() && algo != IG_ALGO_GENERIC;
+  // (the early-epilogue forms exist at 128 x 64 only: 128 x 128 spills)
   const bool narrow = algo == IG_ALGO_CLASSIC_N64 || algo == IG_ALGO_GLDS_N64 ||
-                      algo == IG_ALGO_ONEBUF_N64;
-  const bool onebuf = algo == IG_ALGO_ONEBUF || algo == IG_ALGO_ONEBUF_N64;
+                      algo == IG_ALGO_ONEBUF_N64 || algo == IG_ALGO_ONEBUF_N64_E ||
+                      algo == IG_ALGO_CLASSIC_N64_E || algo == IG_ALGO_ONEBUF_E;
+  const bool onebuf = algo == IG_ALGO_ONEBUF || algo == IG_ALGO_ONEBUF_N64 ||
+                      algo == IG_ALGO_ONEBUF_E || algo == IG_ALGO_ONEBUF_N64_E;
+  // the early-epilogue forms (dgrad-style operands loaded before the K loop)
+  const bool early = algo == IG_ALGO_ONEBUF_E || algo == IG_ALGO_ONEBUF_N64_E ||
+                     algo == IG_ALGO_CLASSIC_N64_E;
   if ((algo == IG_ALGO_TALL512 || algo == IG_ALGO_TALL256) && fast) {
     if (dtype == BF16) launch_glds_tall<bf16>(a, algo == IG_ALGO_TALL512, stream);
     else if (dtype == F16) launch_glds_tall<f16>(a, algo == IG_ALGO_TALL512, stream);
@@ -2398,11 +2466,11 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
     return hipGetLastError();
   }
   if (dtype == BF16) {
-    if (Ncol <= 64 || narrow) launch_ig<bf16, 128, 64>(a, t, fast, stream, onebuf);
-    else launch_ig<bf16, 128, 128>(a, t, fast, stream, onebuf);
+    if (Ncol <= 64 || narrow) launch_ig<bf16, 128, 64>(a, t, fast, stream, onebuf, early);
+    else launch_ig<bf16, 128, 128>(a, t, fast, stream, onebuf, early);
   } else if (dtype == F16) {
-    if (Ncol <= 64 || narrow) launch_ig<f16, 128, 64>(a, t, fast, stream, onebuf);
-    else launch_ig<f16, 128, 128>(a, t, fast, stream, onebuf);
+    if (Ncol <= 64 || narrow) launch_ig<f16, 128, 64>(a, t, fast, stream, onebuf, early);
+    else launch_ig<f16, 128, 128>(a, t, fast, stream, onebuf, early);
   } else {
     return hipErrorInvalidValue;
   }

@@ -43,6 +43,11 @@ IG_GENERIC = 21  # the generic (per-chunk division) loader, forced
 IG_SK128 = 22
 # 256 x 256 LDS-DMA tile, 8-phase schedule with the two wave groups staggered
 IG_G8P = 23
+# register-staged 128x64 one- and two-stage kernels that load the dgrad-style
+# epilogue operands (addend, mask, x_bn) before their K loop, behind the first
+# K step's operand loads (offered with those operands; IG_ONEBUF_E = the
+# 128x64 one-stage form too, 128x128 would spill)
+IG_ONEBUF_E, IG_ONEBUF_N64_E, IG_CLASSIC_N64_E = 24, 25, 26
 IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N64,
             "glds_n64": IG_GLDS_N64, "onebuf": IG_ONEBUF, "onebuf_n64": IG_ONEBUF_N64,
             "tall512": IG_TALL512, "tall256": IG_TALL256, "small": IG_SMALL,
@@ -50,7 +55,8 @@ IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N6
             "gshort128_3": IG_GSHORT128_3, "multi2": IG_MULTI2, "multi4": IG_MULTI4,
             "small_multi4": IG_SMALL_MULTI4, "gmulti64": IG_GMULTI64,
             "gmulti128": IG_GMULTI128, "gbig256": IG_GBIG256, "gbig512": IG_GBIG512,
-            "generic": IG_GENERIC, "sk128": IG_SK128, "g8p": IG_G8P}
+            "generic": IG_GENERIC, "sk128": IG_SK128, "g8p": IG_G8P, "onebuf_e": IG_ONEBUF_E,
+            "onebuf_n64_e": IG_ONEBUF_N64_E, "classic_n64_e": IG_CLASSIC_N64_E}
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
@@ -59,6 +65,11 @@ _GSHORT3 = os.environ.get("KFB_IGEMM_GSHORT3", "1") != "0"  # A/B knob: the 3-st
 _NO_MULTI = os.environ.get("KFB_IGEMM_NOMULTI", "0") == "1"  # A/B knob: drop IG_*MULTI*
 _NO_BIG = os.environ.get("KFB_IGEMM_NOBIG", "0") == "1"  # A/B knob: drop IG_GBIG*
 _SK = os.environ.get("KFB_IGEMM_SK", "0") == "1"  # offer IG_SK128 to the autotune
+# KFB_IGEMM_EARLY=1: offer the early-epilogue-operand kernels (IG_*_E) to the
+# autotune.  Off: at 3 workgroups per CU (their early operands stay live
+# through the K loop) they lost to the 4-workgroup one-stage kernel on every
+# ResNet-50 dgrad geometry, by 5-20% (profiles/r8_early_epilogue.txt)
+_EARLY_EPI = os.environ.get("KFB_IGEMM_EARLY", "0") == "1"
 # largest K (= KH*KW*Cin) offered the multi-tile candidates (register-staged;
 # the LDS-DMA form gets twice that)
 _MULTI_K = int(os.environ.get("KFB_IGEMM_MULTI_K", "2304"))
@@ -267,6 +278,8 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
     if fast and C % 64 != 0:
         # 8-channel geometry: the generic loader competes with the FAST ones
         cands += (IG_GENERIC,)
+    if fast and _EARLY_EPI and (xbn is not None or addend is not None):
+        cands += (IG_ONEBUF_N64_E, IG_CLASSIC_N64_E)
     if ncol > 64:  # 64-wide tiles: more workgroups for small-M layers
         cands += (IG_CLASSIC_N64, IG_GLDS_N64, IG_ONEBUF_N64) if fast else (IG_CLASSIC_N64,)
     if len(cands) == 1:
