@@ -1356,6 +1356,134 @@ __global__ void __launch_bounds__(512, 1) igemm_8p_k(IgArgs a) {
   ig_epilogue<T, BM, BN, NT, 2, 4, NoPrefetch, EXTRAS>(a, acc, smem, m0, n0, wr, wc);
 }
 
+// ------------------------------------------------------------ direct-B igemm
+// The register-staged and LDS-DMA kernels above stage BOTH operands through
+// LDS; with 2x2 wave grids every pixel chunk is written once and read by two
+// waves, and the LDS pipe (not the MFMAs) bounds the 64- and 128-channel
+// layers (~1.1 KB of LDS traffic per 16x16x32 MFMA at 128x64).  Here only the
+// weight tile goes through LDS.  The four waves split the 256-pixel tile
+// along M (64 pixels each, 64 output channels), so no pixel chunk is shared
+// between waves and each lane loads its B fragments straight from global
+// memory in MFMA layout: the 16-byte chunk (lane >> 4) of K sub-step ks of
+// pixel (lane & 15) of subtile j - one buffer load per fragment, no LDS
+// round trip.  The 64 x 64 weight tile of a K step (8 KB) is double-
+// buffered in LDS (one 16-byte chunk per thread, two per step) and read as
+// the A fragments.  LDS traffic per MFMA: ~0.3 KB.  B fragments of step k+1
+// are loaded (two register sets) while step k computes.
+// FAST geometry only (C % 64 == 0: a K step is one tap, 64 channels).
+constexpr int DB_BM = 256, DB_BN = 64;
+
+template <typename T>
+__global__ void __launch_bounds__(256, 2) igemm_db_k(IgArgs a) {
+  __shared__ __attribute__((aligned(16))) T smem[DB_BM * DB_BN];  // 2 A stages, then the epilogue
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int mtiles = (a.M + DB_BM - 1) / DB_BM, ntiles = (a.Ncol + DB_BN - 1) / DB_BN;
+  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int m0 = (bid / ntiles) * DB_BM, n0 = (bid % ntiles) * DB_BN;
+  const int OHW = a.OH * a.OW;
+  const int kc = lane >> 4;  // this lane's 16-byte chunk of a 32-deep K sub-step
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.wbytes, 0x00020000);
+  // B: this lane's pixel of each of the wave's four 16-pixel subtiles
+  int xoff[4];
+  unsigned long long tapmask[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = m0 + wid * 64 + j * 16 + (lane & 15);
+    const bool ok = m < a.M;
+    const int mm = ok ? m : 0;
+    const int img = mm / OHW, rem = mm - img * OHW;
+    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+    const int ih = oh * a.sh - a.pt, iw = ow * a.sw - a.pl;
+    unsigned long long mk = 0;
+    for (int kh = 0; kh < a.KH; ++kh)
+      for (int kw = 0; kw < a.KW; ++kw) {
+        const bool in = (unsigned)(ih + kh) < (unsigned)a.H && (unsigned)(iw + kw) < (unsigned)a.W;
+        mk |= (unsigned long long)(in && ok) << (kh * a.KW + kw);
+      }
+    tapmask[j] = mk;
+    xoff[j] = img * a.H * a.W * a.C + (ih * a.W + iw) * a.C + kc * 8;
+  }
+  // A: weight rows n0 + (tid >> 3) and n0 + 32 + (tid >> 3), chunk tid & 7
+  const int ar = tid >> 3, ac = tid & 7;
+  const int woff0 = (n0 + ar) * a.Ktot + ac * 8, woff1 = (n0 + 32 + ar) * a.Ktot + ac * 8;
+  const bool wok0 = n0 + ar < a.Ncol, wok1 = n0 + 32 + ar < a.Ncol;
+  int s_k = 0;
+  auto load_a = [&](uint4 (&wr)[2]) {
+    wr[0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                          wrs, wok0 ? (woff0 + s_k) * (int)sizeof(T) : -1, 0, 0));
+    wr[1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                          wrs, wok1 ? (woff1 + s_k) * (int)sizeof(T) : -1, 0, 0));
+    s_k += IG_BK;
+  };
+  auto store_a = [&](const uint4 (&wr)[2], int buf) {
+    T* ws = smem + buf * (DB_BN * IG_BK);
+    *(uint4*)(ws + swz_off(ar, ac)) = wr[0];
+    *(uint4*)(ws + swz_off(ar + 32, ac)) = wr[1];
+  };
+  // B state: tap (kh, kw), its bit, element offset of the tap, channel block
+  int s_cc = 0, s_kh = 0, s_kw = 0, s_tap = 0, s_tapi = 0;
+  auto load_b = [&](v8s (&br)[4][2]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool ok = (tapmask[j] >> s_tapi) & 1ull;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int off = ok ? (xoff[j] + s_tap + s_cc + ks * 32) * (int)sizeof(T) : -1;
+        br[j][ks] = __builtin_bit_cast(v8s, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+      }
+    }
+    s_cc += IG_BK;
+    if (s_cc == a.C) {
+      s_cc = 0;
+      ++s_tapi;
+      if (++s_kw == a.KW) { s_kw = 0; ++s_kh; }
+      s_tap = (s_kh * a.W + s_kw) * a.C;
+    }
+  };
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](const v8s (&br)[4][2], int buf) {
+    const T* ws = smem + buf * (DB_BN * IG_BK);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      v8s af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i] = *(const v8s*)(ws + swz_off(i * 16 + (lane & 15), ks * 4 + kc));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = Mfma<T>::run(af[i], br[j][ks], acc[i][j]);
+    }
+  };
+  const int nk = a.Ktot / IG_BK;
+  uint4 wr[2];
+  v8s b0[4][2], b1[4][2];
+  load_a(wr);
+  load_b(b0);
+  store_a(wr, 0);
+  __syncthreads();
+  // step kt: A in LDS stage kt & 1, B in set (kt & 1 ? b1 : b0)
+  for (int kt = 0; kt < nk; kt += 2) {
+    if (kt + 1 < nk) { load_a(wr); load_b(b1); }
+    compute(b0, 0);
+    if (kt + 1 < nk) store_a(wr, 1);
+    __syncthreads();
+    if (kt + 1 >= nk) break;
+    if (kt + 2 < nk) { load_a(wr); load_b(b0); }
+    compute(b1, 1);
+    if (kt + 2 < nk) store_a(wr, 0);
+    __syncthreads();
+  }
+  ig_epilogue<T, DB_BM, DB_BN, 256, 4, 1>(a, acc, smem, m0, n0, wid, 0);
+}
+
 // ------------------------------------------------------------ stream-K igemm
 // Persistent form of the 4-wave 128 x 128 LDS-DMA tile whose workgroups
 // share the tail of the tile space along K.  A launch of T tiles on P
@@ -2352,7 +2480,7 @@ enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_G
        IG_ALGO_MULTI4 = 15, IG_ALGO_SMALL_MULTI4 = 16, IG_ALGO_GMULTI64 = 17,
        IG_ALGO_GMULTI128 = 18, IG_ALGO_GBIG256 = 19, IG_ALGO_GBIG512 = 20,
        IG_ALGO_GENERIC = 21, IG_ALGO_SK128 = 22, IG_ALGO_G8P = 23, IG_ALGO_ONEBUF_E = 24,
-       IG_ALGO_ONEBUF_N64_E = 25, IG_ALGO_CLASSIC_N64_E = 26 };
+       IG_ALGO_ONEBUF_N64_E = 25, IG_ALGO_CLASSIC_N64_E = 26, IG_ALGO_DB = 27 };
 
 static bool c8_geometry(int C, int KH, int KW) {
   return C == 8 && (KW == 1 || KW == 2 || KW == 4 || KW == 8) && (KH * KW) % 8 == 0;
@@ -2429,6 +2557,13 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
   if (algo == IG_ALGO_G8P && fast && !c8) {
     if (dtype == BF16) launch_8p<bf16>(a, stream);
     else if (dtype == F16) launch_8p<f16>(a, stream);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
+  if (algo == IG_ALGO_DB && fast && !c8) {
+    const int nwg = ((a.M + DB_BM - 1) / DB_BM) * ((a.Ncol + DB_BN - 1) / DB_BN);
+    if (dtype == BF16) hipLaunchKernelGGL(igemm_db_k<bf16>, dim3(nwg), dim3(256), 0, stream, a);
+    else if (dtype == F16) hipLaunchKernelGGL(igemm_db_k<f16>, dim3(nwg), dim3(256), 0, stream, a);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }

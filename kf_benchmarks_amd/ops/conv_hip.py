@@ -48,6 +48,9 @@ IG_G8P = 23
 # K step's operand loads (offered with those operands; IG_ONEBUF_E = the
 # 128x64 one-stage form too, 128x128 would spill)
 IG_ONEBUF_E, IG_ONEBUF_N64_E, IG_CLASSIC_N64_E = 24, 25, 26
+# 256x64 tile, four waves along M; only the weight tile goes through LDS, the
+# pixel operand is loaded straight into MFMA B-fragment layout (igemm_db_k)
+IG_DB = 27
 IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N64,
             "glds_n64": IG_GLDS_N64, "onebuf": IG_ONEBUF, "onebuf_n64": IG_ONEBUF_N64,
             "tall512": IG_TALL512, "tall256": IG_TALL256, "small": IG_SMALL,
@@ -56,7 +59,7 @@ IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N6
             "small_multi4": IG_SMALL_MULTI4, "gmulti64": IG_GMULTI64,
             "gmulti128": IG_GMULTI128, "gbig256": IG_GBIG256, "gbig512": IG_GBIG512,
             "generic": IG_GENERIC, "sk128": IG_SK128, "g8p": IG_G8P, "onebuf_e": IG_ONEBUF_E,
-            "onebuf_n64_e": IG_ONEBUF_N64_E, "classic_n64_e": IG_CLASSIC_N64_E}
+            "onebuf_n64_e": IG_ONEBUF_N64_E, "classic_n64_e": IG_CLASSIC_N64_E, "db": IG_DB}
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
@@ -70,6 +73,11 @@ _SK = os.environ.get("KFB_IGEMM_SK", "0") == "1"  # offer IG_SK128 to the autotu
 # through the K loop) they lost to the 4-workgroup one-stage kernel on every
 # ResNet-50 dgrad geometry, by 5-20% (profiles/r8_early_epilogue.txt)
 _EARLY_EPI = os.environ.get("KFB_IGEMM_EARLY", "0") == "1"
+# KFB_IGEMM_DB=1: offer IG_DB.  Off: 380-410 TF/s on every ResNet-50 shape (the
+# per-lane B-fragment loads touch 16 pixel rows per instruction; the LDS-staged
+# loaders read whole rows), 1.1-2x slower than the chosen kernels
+# (profiles/r8_direct_b.txt)
+_DB = os.environ.get("KFB_IGEMM_DB", "0") == "1"
 # largest K (= KH*KW*Cin) offered the multi-tile candidates (register-staged;
 # the LDS-DMA form gets twice that)
 _MULTI_K = int(os.environ.get("KFB_IGEMM_MULTI_K", "2304"))
@@ -278,6 +286,8 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
     if fast and C % 64 != 0:
         # 8-channel geometry: the generic loader competes with the FAST ones
         cands += (IG_GENERIC,)
+    if fast and _DB and C % 64 == 0:
+        cands += (IG_DB,)
     if fast and _EARLY_EPI and (xbn is not None or addend is not None):
         cands += (IG_ONEBUF_N64_E, IG_CLASSIC_N64_E)
     if ncol > 64:  # 64-wide tiles: more workgroups for small-M layers

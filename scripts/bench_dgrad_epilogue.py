@@ -19,7 +19,7 @@ from kf_benchmarks_amd.ops import conv_hip  # noqa: E402
 SHAPES = [(56, 64, 256), (28, 128, 512), (14, 256, 1024), (7, 512, 2048)]
 ALGOS = ["classic", "glds", "onebuf", "tall256", "small", "gshort64", "gshort128", "gmulti64",
          "gmulti128", "gbig256", "g8p", "classic_n64", "glds_n64", "onebuf_n64", "onebuf_n64_e",
-         "classic_n64_e"]
+         "classic_n64_e", "db"]
 
 
 def timeit(fn, reps=10, rounds=5):
