@@ -64,9 +64,11 @@ def main(argv=None):
                          "crop, flip, resize) instead of synthetic batches")
     ap.add_argument("--input_threads", type=int, default=0,
                     help="host preprocessing threads with --data_dir (0: the default)")
-    ap.add_argument("--launch_tape", type=int, default=0,
+    ap.add_argument("--launch_tape", type=int, default=-1,
                     help="1: record one step's native launches after warmup and replay them "
-                         "from C++ (ops/tape.py); falls back to eager where not eligible")
+                         "from C++ (ops/tape.py); falls back to eager where not eligible.  "
+                         "-1 (default): on for one GPU with synthetic data, off otherwise "
+                         "(multi-rank taped replay is exercised only as a 1-rank RCCL group)")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
@@ -112,7 +114,9 @@ def main(argv=None):
                       kernel_impl=a.kernel_impl, bucket_size_mb=a.bucket_size_mb,
                       gradient_wire_dtype=a.wire_dtype, display_every=10**9,
                       all_reduce_spec=a.all_reduce_spec, hierarchical_copy=a.hierarchical_copy,
-                      launch_tape=bool(a.launch_tape), data_dir=a.data_dir,
+                      launch_tape=(bool(a.launch_tape) if a.launch_tape >= 0 else
+                                   (a.gpus == 1 and cuda and not a.data_dir)),
+                      data_dir=a.data_dir,
                       datasets_num_private_threads=a.input_threads or None,
                       datasets_repeat_cached_sample=bool(a.data_dir),
                       synthetic_resample=not a.reuse_synthetic)
