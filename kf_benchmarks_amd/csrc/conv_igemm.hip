@@ -33,6 +33,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <type_traits>
 #include <utility>
 
 namespace kfb {
@@ -40,6 +41,7 @@ namespace kfb {
 typedef __attribute__((ext_vector_type(8))) short v8s;
 typedef __attribute__((ext_vector_type(4))) float v4f;
 typedef __attribute__((ext_vector_type(4))) short v4s;
+typedef __attribute__((ext_vector_type(16))) float v16f;
 
 template <typename T> struct Mfma;
 template <> struct Mfma<bf16> {
@@ -51,6 +53,24 @@ template <> struct Mfma<f16> {
   static __device__ __forceinline__ v4f run(v8s a, v8s b, v4f c) {
     typedef __attribute__((ext_vector_type(8))) _Float16 v8h;
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(v8h, a),
+                                                  __builtin_bit_cast(v8h, b), c, 0, 0, 0);
+  }
+};
+// 32x32x16 form: twice the MACs per instruction and ~15% more sustained
+// throughput than 16x16x32 on random operands (scripts/probes/mfma_rate.hip:
+// 1.79 vs 1.55 PFLOP/s); lane l holds rows 8g + 4(l/32) + r (g, r < 4) of
+// column l % 32 of the 32x32 result, and supplies row / column l % 32, K
+// elements 8(l/32) .. +8 of each operand.
+template <typename T> struct Mfma32;
+template <> struct Mfma32<bf16> {
+  static __device__ __forceinline__ v16f run(v8s a, v8s b, v16f c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Mfma32<f16> {
+  static __device__ __forceinline__ v16f run(v8s a, v8s b, v16f c) {
+    typedef __attribute__((ext_vector_type(8))) _Float16 v8h;
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(v8h, a),
                                                   __builtin_bit_cast(v8h, b), c, 0, 0, 0);
   }
 };
@@ -225,12 +245,15 @@ constexpr int epi_group() {
 // its K loop (`early`, valid only when the launch has addend / xbn): their
 // latency hides behind the GEMM instead of following it (short-K dgrads,
 // where the epilogue's three extra streams are most of the bytes).
+// ACC: v4f [BN/WGN/16][BM/WGM/16] (16x16x32 accumulators) or v16f
+// [BN/WGN/32][BM/WGM/32] (32x32x16); only the LDS staging differs.
 template <typename T, int BM, int BN, int NT, int WGM, int WGN, typename Pre = NoPrefetch,
-          bool EXTRAS = true, bool EARLY = false>
-__device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN / 16][BM / WGM / 16],
+          bool EXTRAS = true, bool EARLY = false, typename ACC>
+__device__ __forceinline__ void ig_epilogue(const IgArgs& a, ACC& acc,
                                             T* smem, int m0, int n0, int wm, int wn,
                                             Pre pre = Pre(),
                                             const EpiOps<epi_group<BM, BN, NT>()>* early = nullptr) {
+  constexpr bool M32 = std::is_same<std::decay_t<decltype(acc[0][0])>, v16f>::value;
   constexpr int TN = BN / WGN / 16, TM = BM / WGM / 16;
   const int tid = threadIdx.x, lane = tid & 63;
   const int OHW = a.OH * a.OW;
@@ -251,17 +274,38 @@ __device__ __forceinline__ void ig_epilogue(const IgArgs& a, v4f (&acc)[BN / WGN
     const int n = n0 + (tid % CPR) * 8 + k;
     kv[k] = (a.kshift && n < a.Ncol) ? a.kshift[n] : 0.f;
   }
+  if constexpr (!M32) {
 #pragma unroll
-  for (int j = 0; j < TM; ++j) {
-    const int ml = wm * (BM / WGM) + j * 16 + (lane & 15);
+    for (int j = 0; j < TM; ++j) {
+      const int ml = wm * (BM / WGM) + j * 16 + (lane & 15);
 #pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      const int nl = wn * (BN / WGN) + i * 16 + (lane >> 4) * 4;
-      Vec<T, 4> o;
+      for (int i = 0; i < TN; ++i) {
+        const int nl = wn * (BN / WGN) + i * 16 + (lane >> 4) * 4;
+        Vec<T, 4> o;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o.v[r] = (T)acc[i][j][r];
-      const int chunk = (nl >> 3) ^ (ml & (CPR - 1));
-      *reinterpret_cast<Vec<T, 4>*>(cs + ml * BN + chunk * 8 + (nl & 7)) = o;
+        for (int r = 0; r < 4; ++r) o.v[r] = (T)acc[i][j][r];
+        const int chunk = (nl >> 3) ^ (ml & (CPR - 1));
+        *reinterpret_cast<Vec<T, 4>*>(cs + ml * BN + chunk * 8 + (nl & 7)) = o;
+      }
+    }
+  } else {
+    // 32x32 tiles: register group g of lane l = channels 8g + 4(l/32) .. +3
+    // of pixel l % 32
+#pragma unroll
+    for (int j = 0; j < TM / 2; ++j) {
+      const int ml = wm * (BM / WGM) + j * 32 + (lane & 31);
+#pragma unroll
+      for (int i = 0; i < TN / 2; ++i) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int nl = wn * (BN / WGN) + i * 32 + g * 8 + (lane >> 5) * 4;
+          Vec<T, 4> o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o.v[r] = (T)acc[i][j][g * 4 + r];
+          const int chunk = (nl >> 3) ^ (ml & (CPR - 1));
+          *reinterpret_cast<Vec<T, 4>*>(cs + ml * BN + chunk * 8 + (nl & 7)) = o;
+        }
+      }
     }
   }
   __syncthreads();
@@ -909,8 +953,9 @@ constexpr int glds_occupancy() {
   return NT == 256 && BM == 128 ? (BN == 64 ? 3 : 2) : 1;
 }
 
+// MF32: 32x32x16 MFMAs (wave tiles must be multiples of 32 in both dims)
 template <typename T, int BM, int BN, int WGM, int WGN, int STAGES = GL_STAGES,
-          bool EXTRAS = true>
+          bool EXTRAS = true, bool MF32 = false>
 __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * WGN * 64>()))
     igemm_glds_k(IgArgs a) {
   constexpr int NT = WGM * WGN * 64;
@@ -986,29 +1031,57 @@ __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * 
     }
   };
 
-  v4f acc[TN][TM];
+  static_assert(!MF32 || (TN % 2 == 0 && TM % 2 == 0), "32x32 wave tiles");
+  constexpr int TN2 = MF32 ? TN / 2 : 1, TM2 = MF32 ? TM / 2 : 1;
+  v4f acc[MF32 ? 1 : TN][MF32 ? 1 : TM];
+  v16f acc32[TN2][TM2];
 #pragma unroll
-  for (int i = 0; i < TN; ++i)
+  for (int i = 0; i < (MF32 ? 1 : TN); ++i)
 #pragma unroll
-    for (int j = 0; j < TM; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < (MF32 ? 1 : TM); ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < TN2; ++i)
+#pragma unroll
+    for (int j = 0; j < TM2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc32[i][j][r] = 0.f;
   const int wm = wid % WGM, wn = wid / WGM;
   auto compute = [&](int stage) {
     const T* xs = smem + stage * STAGE;
     const T* ws = xs + BM * IG_BK;
+    if constexpr (MF32) {
+      // four 16-deep sub-steps; lane l reads chunk 2ks + l/32 of row l % 32
 #pragma unroll
-    for (int ks = 0; ks < IG_BK / 32; ++ks) {
-      const int chunk = ks * 4 + (lane >> 4);
-      v8s af[TN], bfr[TM];
+      for (int ks = 0; ks < IG_BK / 16; ++ks) {
+        const int chunk = ks * 2 + (lane >> 5);
+        v8s af[TN2], bfr[TM2];
 #pragma unroll
-      for (int i = 0; i < TN; ++i)
-        af[i] = *(const v8s*)(ws + swz_off(wn * (BN / WGN) + i * 16 + (lane & 15), chunk));
+        for (int i = 0; i < TN2; ++i)
+          af[i] = *(const v8s*)(ws + swz_off(wn * (BN / WGN) + i * 32 + (lane & 31), chunk));
 #pragma unroll
-      for (int j = 0; j < TM; ++j)
-        bfr[j] = *(const v8s*)(xs + swz_off(wm * (BM / WGM) + j * 16 + (lane & 15), chunk));
+        for (int j = 0; j < TM2; ++j)
+          bfr[j] = *(const v8s*)(xs + swz_off(wm * (BM / WGM) + j * 32 + (lane & 31), chunk));
 #pragma unroll
-      for (int i = 0; i < TN; ++i)
+        for (int i = 0; i < TN2; ++i)
 #pragma unroll
-        for (int j = 0; j < TM; ++j) acc[i][j] = Mfma<T>::run(af[i], bfr[j], acc[i][j]);
+          for (int j = 0; j < TM2; ++j) acc32[i][j] = Mfma32<T>::run(af[i], bfr[j], acc32[i][j]);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < IG_BK / 32; ++ks) {
+        const int chunk = ks * 4 + (lane >> 4);
+        v8s af[TN], bfr[TM];
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+          af[i] = *(const v8s*)(ws + swz_off(wn * (BN / WGN) + i * 16 + (lane & 15), chunk));
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+          bfr[j] = *(const v8s*)(xs + swz_off(wm * (BM / WGM) + j * 16 + (lane & 15), chunk));
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j) acc[i][j] = Mfma<T>::run(af[i], bfr[j], acc[i][j]);
+      }
     }
   };
 
@@ -1033,7 +1106,10 @@ __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * 
     }
   }
   __syncthreads();  // all fragment reads done before the epilogue reuses the ring
-  ig_epilogue<T, BM, BN, NT, WGM, WGN, NoPrefetch, EXTRAS>(a, acc, smem, m0, n0, wm, wn);
+  if constexpr (MF32)
+    ig_epilogue<T, BM, BN, NT, WGM, WGN, NoPrefetch, EXTRAS>(a, acc32, smem, m0, n0, wm, wn);
+  else
+    ig_epilogue<T, BM, BN, NT, WGM, WGN, NoPrefetch, EXTRAS>(a, acc, smem, m0, n0, wm, wn);
 }
 
 // Multi-tile form of the 4-wave 2-stage LDS-DMA kernel (128 x 64 / 128 x 128):
@@ -2284,10 +2360,15 @@ static void launch_glds(const IgArgs& a, bool narrow, hipStream_t s) {
 // ds_write pass (the register-staged igemm_k spends more LDS cycles on its
 // ds_write_b128 stores than on its fragment reads)
 template <typename T>
-static void launch_glds_short(const IgArgs& a, bool wide, bool three, hipStream_t s) {
+static void launch_glds_short(const IgArgs& a, bool wide, bool three, hipStream_t s,
+                              bool mf32 = false) {
   const int mt = (a.M + 127) / 128;
   const dim3 g128(mt * ((a.Ncol + 127) / 128)), g64(mt * ((a.Ncol + 63) / 64));
-  if (wide && three)
+  if (mf32 && wide)
+    hipLaunchKernelGGL((igemm_glds_k<T, 128, 128, 2, 2, 2, true, true>), g128, dim3(256), 0, s, a);
+  else if (mf32)
+    hipLaunchKernelGGL((igemm_glds_k<T, 128, 64, 2, 2, 2, true, true>), g64, dim3(256), 0, s, a);
+  else if (wide && three)
     hipLaunchKernelGGL((igemm_glds_k<T, 128, 128, 2, 2, 3>), g128, dim3(256), 0, s, a);
   else if (wide)
     hipLaunchKernelGGL((igemm_glds_k<T, 128, 128, 2, 2, 2>), g128, dim3(256), 0, s, a);
@@ -2303,8 +2384,11 @@ static void launch_glds_short(const IgArgs& a, bool wide, bool three, hipStream_
 // >= 256 output channels (2 x 64 KB ring), 512 x 128 for 128-channel layers
 // (2 x 80 KB ring, the whole 160 KB LDS).
 template <typename T>
-static void launch_glds_big(const IgArgs& a, bool wide, hipStream_t s) {
-  if (wide)
+static void launch_glds_big(const IgArgs& a, bool wide, hipStream_t s, bool mf32 = false) {
+  if (mf32)
+    hipLaunchKernelGGL((igemm_glds_k<T, 256, 256, 2, 4, 2, true, true>),
+                       dim3(((a.M + 255) / 256) * ((a.Ncol + 255) / 256)), dim3(512), 0, s, a);
+  else if (wide)
     hipLaunchKernelGGL((igemm_glds_k<T, 256, 256, 2, 4, 2>),
                        dim3(((a.M + 255) / 256) * ((a.Ncol + 255) / 256)), dim3(512), 0, s, a);
   else
@@ -2480,7 +2564,8 @@ enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_G
        IG_ALGO_MULTI4 = 15, IG_ALGO_SMALL_MULTI4 = 16, IG_ALGO_GMULTI64 = 17,
        IG_ALGO_GMULTI128 = 18, IG_ALGO_GBIG256 = 19, IG_ALGO_GBIG512 = 20,
        IG_ALGO_GENERIC = 21, IG_ALGO_SK128 = 22, IG_ALGO_G8P = 23, IG_ALGO_ONEBUF_E = 24,
-       IG_ALGO_ONEBUF_N64_E = 25, IG_ALGO_CLASSIC_N64_E = 26, IG_ALGO_DB = 27 };
+       IG_ALGO_ONEBUF_N64_E = 25, IG_ALGO_CLASSIC_N64_E = 26, IG_ALGO_DB = 27,
+       IG_ALGO_GBIG256_32 = 28, IG_ALGO_GSHORT128_32 = 29, IG_ALGO_GSHORT64_32 = 30 };
 
 static bool c8_geometry(int C, int KH, int KW) {
   return C == 8 && (KW == 1 || KW == 2 || KW == 4 || KW == 8) && (KH * KW) % 8 == 0;
@@ -2558,6 +2643,20 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
     if (dtype == BF16) launch_8p<bf16>(a, stream);
     else if (dtype == F16) launch_8p<f16>(a, stream);
     else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
+  if ((algo == IG_ALGO_GBIG256_32 || algo == IG_ALGO_GSHORT128_32 || algo == IG_ALGO_GSHORT64_32) &&
+      fast) {
+    if (algo == IG_ALGO_GBIG256_32) {
+      if (dtype == BF16) launch_glds_big<bf16>(a, true, stream, true);
+      else if (dtype == F16) launch_glds_big<f16>(a, true, stream, true);
+      else return hipErrorInvalidValue;
+    } else {
+      const bool wide = algo == IG_ALGO_GSHORT128_32;
+      if (dtype == BF16) launch_glds_short<bf16>(a, wide, false, stream, true);
+      else if (dtype == F16) launch_glds_short<f16>(a, wide, false, stream, true);
+      else return hipErrorInvalidValue;
+    }
     return hipGetLastError();
   }
   if (algo == IG_ALGO_DB && fast && !c8) {

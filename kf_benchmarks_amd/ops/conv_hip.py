@@ -51,6 +51,9 @@ IG_ONEBUF_E, IG_ONEBUF_N64_E, IG_CLASSIC_N64_E = 24, 25, 26
 # 256x64 tile, four waves along M; only the weight tile goes through LDS, the
 # pixel operand is loaded straight into MFMA B-fragment layout (igemm_db_k)
 IG_DB = 27
+# IG_GBIG256 / IG_GSHORT128 / IG_GSHORT64 on v_mfma_f32_32x32x16 (15% more
+# sustained MFMA throughput than the 16x16x32 form, scripts/probes/mfma_rate.hip)
+IG_GBIG256_32, IG_GSHORT128_32, IG_GSHORT64_32 = 28, 29, 30
 IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N64,
             "glds_n64": IG_GLDS_N64, "onebuf": IG_ONEBUF, "onebuf_n64": IG_ONEBUF_N64,
             "tall512": IG_TALL512, "tall256": IG_TALL256, "small": IG_SMALL,
@@ -59,7 +62,9 @@ IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N6
             "small_multi4": IG_SMALL_MULTI4, "gmulti64": IG_GMULTI64,
             "gmulti128": IG_GMULTI128, "gbig256": IG_GBIG256, "gbig512": IG_GBIG512,
             "generic": IG_GENERIC, "sk128": IG_SK128, "g8p": IG_G8P, "onebuf_e": IG_ONEBUF_E,
-            "onebuf_n64_e": IG_ONEBUF_N64_E, "classic_n64_e": IG_CLASSIC_N64_E, "db": IG_DB}
+            "onebuf_n64_e": IG_ONEBUF_N64_E, "classic_n64_e": IG_CLASSIC_N64_E, "db": IG_DB,
+            "gbig256_32": IG_GBIG256_32, "gshort128_32": IG_GSHORT128_32,
+            "gshort64_32": IG_GSHORT64_32}
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
@@ -78,6 +83,10 @@ _EARLY_EPI = os.environ.get("KFB_IGEMM_EARLY", "0") == "1"
 # loaders read whole rows), 1.1-2x slower than the chosen kernels
 # (profiles/r8_direct_b.txt)
 _DB = os.environ.get("KFB_IGEMM_DB", "0") == "1"
+# KFB_IGEMM_MF32=1: offer the *_32 kernels.  Off: within -4..+1% of their 16x16x32
+# forms on every ResNet-50 shape (the MFMA issue rate is not what binds these
+# kernels; profiles/r8_mfma_forms.txt)
+_MF32 = os.environ.get("KFB_IGEMM_MF32", "0") == "1"
 # largest K (= KH*KW*Cin) offered the multi-tile candidates (register-staged;
 # the LDS-DMA form gets twice that)
 _MULTI_K = int(os.environ.get("KFB_IGEMM_MULTI_K", "2304"))
@@ -260,6 +269,8 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
         cands += (IG_SMALL,)
     if fast and not _NO_GSHORT:
         cands += (IG_GSHORT64,) + ((IG_GSHORT128,) if ncol > 64 else ())
+        if _MF32:
+            cands += (IG_GSHORT64_32,) + ((IG_GSHORT128_32,) if ncol > 64 else ())
         if _GSHORT3:
             cands += (IG_GSHORT64_3,) + ((IG_GSHORT128_3,) if ncol > 64 else ())
     if fast and not _NO_MULTI and mask is None and xbn is None and addend is None \
@@ -275,6 +286,8 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
         M = geo[0] * geo[4] * geo[5]
         if ncol >= 256 and ((M + 255) // 256) * ((ncol + 255) // 256) >= 192:
             cands += (IG_GBIG256,) + ((IG_G8P,) if C % 64 == 0 else ())
+            if _MF32:
+                cands += (IG_GBIG256_32,)
         if 64 < ncol <= 256 and ((M + 511) // 512) * ((ncol + 127) // 128) >= 256:
             cands += (IG_GBIG512,)
     if fast and _SK and C % 64 == 0 and ncol > 64:
