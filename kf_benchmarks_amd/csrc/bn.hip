@@ -510,13 +510,17 @@ bn_finalize_grad_k(const float* __restrict__ pdy, const float* __restrict__ pdyx
                    const float* __restrict__ mean, const float* __restrict__ invstd,
                    float* __restrict__ dgamma, float* __restrict__ dbeta,
                    float* __restrict__ coefA, float* __restrict__ coefB,
-                   float* __restrict__ coefC, int accumulate) {
+                   float* __restrict__ coefC, int accumulate, int s2_over_scale = 0) {
   const int c = blockIdx.x * 64 + threadIdx.x;
   double s1, s2;
   fold_slabs(pdy, pdyx, nslab, C, c, s1, s2);
   if (threadIdx.y != 0 || c >= C) return;
   const float is = invstd[c];
   const float g = gamma ? gamma[c] : 1.f;
+  // s2_over_scale: the partials hold sum(dy' (y - beta)) over the BN output y
+  // (the stem pool's consumers, see kfb_bn_relu_maxpool_bwd), and
+  // x - mean = (y - beta) / (gamma * invstd) where the ReLU passed
+  if (s2_over_scale) s2 /= (double)g * (double)is;
   if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)(s2 * is);
   if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)s1;
   const double n = (double)rows;
@@ -1357,7 +1361,12 @@ KFB_API hipError_t kfb_bn_relu_maxpool_bwd(int dtype, const void* dz, const void
                                            const float* save_mean, const float* save_invstd,
                                            float* dgamma, float* dbeta, float* pdy, float* pdyx,
                                            int nslab, float* coefA, float* coefB, float* coefC,
-                                           int accumulate, hipStream_t stream) {
+                                           int accumulate, int have_partials, hipStream_t stream) {
+  // have_partials: pdy / pdyx already hold [nslab][C] slot sums of dz' and
+  // dz' (z - beta) over the pooled output z (accumulated by the dgrad epilogue
+  // of the convs that consume z, with z's ReLU mask): each window routes its
+  // gradient to one BN-output pixel p, whose x_p - mean = (z - beta) /
+  // (gamma * invstd), so the partial pass over x is skipped
   if (C % 8 || (long)N * H * W * C >= (1L << 31)) return hipErrorInvalidValue;
   const BPGeo g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
   const long rows = (long)N * H * W;
@@ -1369,12 +1378,13 @@ KFB_API hipError_t kfb_bn_relu_maxpool_bwd(int dtype, const void* dz, const void
     const long total = (long)N * OHo * OWo * cv;
     if (total >= (1L << 31)) return hipErrorInvalidValue;
     KFB_DISPATCH_DTYPE(dtype, T, {
-      hipLaunchKernelGGL((bn_pool3s2_k<T, 0>), dim3(nslab), dim3(256), 0, stream, (const T*)dz,
-                         (const T*)z, idx, (const T*)x, (T*)dx, g, OHo, OWo, save_mean, pdy, pdyx,
-                         nullptr, nullptr, nullptr);
+      if (!have_partials)
+        hipLaunchKernelGGL((bn_pool3s2_k<T, 0>), dim3(nslab), dim3(256), 0, stream, (const T*)dz,
+                           (const T*)z, idx, (const T*)x, (T*)dx, g, OHo, OWo, save_mean, pdy, pdyx,
+                           nullptr, nullptr, nullptr);
       hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, pdy,
                          pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta, coefA,
-                         coefB, coefC, accumulate);
+                         coefB, coefC, accumulate, have_partials);
       hipLaunchKernelGGL((bn_pool3s2_k<T, 1>), dim3(stream_grid(total)), dim3(256), 0, stream,
                          (const T*)dz, (const T*)z, idx, (const T*)x, (T*)dx, g, OHo, OWo, nullptr,
                          nullptr, nullptr, coefA, coefB, coefC);
@@ -1385,12 +1395,13 @@ KFB_API hipError_t kfb_bn_relu_maxpool_bwd(int dtype, const void* dz, const void
     Geo gg = make_geo<8>(C);
     const long slab_rows = (rows + nslab - 1) / nslab;
     const size_t lds = 2 * (size_t)gg.rpi * gg.tpr * 8 * sizeof(float);
-    hipLaunchKernelGGL((bn_pool_partial_grad_k<T, 8>), dim3(nslab, gg.nchunk), dim3(BN_THREADS),
-                       lds, stream, (const T*)dz, (const T*)z, idx, (const T*)x, save_mean, g,
-                       rows, gg.cw, gg.tpr, gg.rpi, slab_rows, pdy, pdyx);
+    if (!have_partials)
+      hipLaunchKernelGGL((bn_pool_partial_grad_k<T, 8>), dim3(nslab, gg.nchunk), dim3(BN_THREADS),
+                         lds, stream, (const T*)dz, (const T*)z, idx, (const T*)x, save_mean, g,
+                         rows, gg.cw, gg.tpr, gg.rpi, slab_rows, pdy, pdyx);
     hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, pdy,
                        pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta, coefA,
-                       coefB, coefC, accumulate);
+                       coefB, coefC, accumulate, have_partials);
     hipLaunchKernelGGL((bn_pool_bwd_apply_k<T, 8>), dim3(stream_grid(rows * C / 8)), dim3(256), 0,
                        stream, (const T*)dz, (const T*)z, idx, (const T*)x, (T*)dx, g, coefA,
                        coefB, coefC);

@@ -393,7 +393,9 @@ class ConvNetBuilder:
         autograd's separate adds.  Concat outputs only with KFB_CONCAT_LINKS=1
         (measured neutral there); ``always`` for the stem (one 103 MB add per
         ResNet step)."""
-        if (_CONCAT_LINKS or always) and y.is_cuda:
+        if (_CONCAT_LINKS or always) and y.is_cuda and getattr(y, "_kfb_bn_link", None) is None:
+            # (a tensor that already carries a link keeps it: the fused stem
+            # pool's BN-partials link, ops/nn.py _BNReluMaxPool)
             if conv_ops.FUSE_BN:
                 link = F.BNLink(None, None, False)
                 link.accum = True

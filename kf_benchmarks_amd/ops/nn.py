@@ -641,10 +641,17 @@ def _pool_link_grad(link, dx):
         return None
     if link.pending is not None:
         link.take_pending_stream()
-        if link.pending_owned:
-            dx = link.pending.add_(dx)
+        p = link.pending
+        if dx.is_cuda and dx.is_contiguous() and p.is_contiguous() and p.dtype == dx.dtype \
+                and p.shape == dx.shape:
+            # native in-place sum into the fresh pool gradient (recordable by a
+            # launch tape, unlike a torch add)
+            N.call("kfb_add", N.dt(dx), p.data_ptr(), dx.data_ptr(), dx.data_ptr(), dx.numel(), 0,
+                   N.stream(dx.device))
+        elif link.pending_owned:
+            dx = p.add_(dx)
         else:
-            dx = dx.add_(link.pending)
+            dx = dx.add_(p)
         link.pending = None
     return dx
 
@@ -702,7 +709,12 @@ N.register_optional("kfb_bn_relu_maxpool_fwd", [N.I, N.P, N.P, N.P] + [N.I] * 12
                     [N.P, N.P, N.F, N.F] + [N.P] * 8 + [N.I, N.P, N.P])
 N.register_optional("kfb_bn_pool_num_slabs", [N.I] * 8, N.c_int)
 N.register_optional("kfb_bn_relu_maxpool_bwd", [N.I, N.P, N.P, N.P, N.P, N.P] + [N.I] * 12 +
-                    [N.P] * 7 + [N.I] + [N.P] * 3 + [N.I, N.P])
+                    [N.P] * 7 + [N.I] + [N.P] * 3 + [N.I, N.I, N.P])
+
+# KFB_POOL_LINK=1: the stem BN+ReLU+max-pool backward takes its BN partials
+# from its consumers' dgrad epilogue (sum dz', sum dz' (z - beta), rescaled by
+# 1 / (gamma * invstd)) instead of its own pass over x
+_POOL_LINK = os.environ.get("KFB_POOL_LINK", "0") == "1"
 
 
 class _BNReluMaxPool(torch.autograd.Function):
@@ -728,6 +740,18 @@ class _BNReluMaxPool(torch.autograd.Function):
         ctx.save_for_backward(x, z, idx, gamma, st)
         ctx.geo = geo
         ctx.gamma, ctx.beta = gamma, beta
+        ctx.out_link = None
+        if _POOL_LINK and _conv.FUSE_BN:
+            # z's consumers (conv1 and the projection shortcut) sum their data
+            # gradients in the last one's dgrad epilogue, which also masks them
+            # with z > 0 (z * 1 + 0) and accumulates sum(dz') and
+            # sum(dz' (z - beta)): the BN partials of this backward
+            coef = _conv_hip()._act_link_consts(C, True, dev)[1]
+            mu = (beta.detach().float().contiguous() if beta is not None
+                  else torch.zeros(C, dtype=torch.float32, device=dev))
+            link = BNLink(None, mu, True, coef)
+            z._kfb_bn_link = link
+            ctx.out_link = link
         return z
 
     @staticmethod
@@ -736,8 +760,18 @@ class _BNReluMaxPool(torch.autograd.Function):
         dz = dz.contiguous()
         n, H, W, C = ctx.geo[:4]
         dev = x.device
-        nslab = N.query("kfb_bn_pool_num_slabs", n, H, W, C, *ctx.geo[6:10])
-        ws = torch.empty((2 * nslab * C + 3 * C,), dtype=torch.float32, device=dev)
+        link = ctx.out_link
+        parts = link.partials if link is not None else None
+        if link is not None:
+            link.partials = None
+        if parts is not None:
+            nslab = parts.numel() // (2 * C)
+            ws = torch.empty((3 * C,), dtype=torch.float32, device=dev)
+            pdy, pdyx, o = parts[:nslab * C], parts[nslab * C:], 0
+        else:
+            nslab = N.query("kfb_bn_pool_num_slabs", n, H, W, C, *ctx.geo[6:10])
+            ws = torch.empty((2 * nslab * C + 3 * C,), dtype=torch.float32, device=dev)
+            pdy, pdyx, o = ws[:nslab * C], ws[nslab * C:2 * nslab * C], 2 * nslab * C
         gsink, bsink = _grad_sink(ctx.gamma), _grad_sink(ctx.beta)
         direct = bsink is not None and (ctx.gamma is None or gsink is not None) and \
             _conv.FUSE_BN
@@ -747,13 +781,11 @@ class _BNReluMaxPool(torch.autograd.Function):
             dparams = torch.empty((2, C), dtype=torch.float32, device=dev)
             dgp, dbp = dparams[0].data_ptr(), dparams[1].data_ptr()
         dx = torch.empty_like(x)
-        o = 2 * nslab * C
         N.call("kfb_bn_relu_maxpool_bwd", N.dt(x), dz.data_ptr(), z.data_ptr(), idx.data_ptr(),
                x.data_ptr(), dx.data_ptr(), *ctx.geo, N.ptr(gamma), st[0].data_ptr(),
-               st[1].data_ptr(), dgp, dbp, ws[:nslab * C].data_ptr(),
-               ws[nslab * C:o].data_ptr(), nslab, ws[o:o + C].data_ptr(),
-               ws[o + C:o + 2 * C].data_ptr(), ws[o + 2 * C:].data_ptr(), int(direct),
-               N.stream(dev))
+               st[1].data_ptr(), dgp, dbp, pdy.data_ptr(), pdyx.data_ptr(), nslab,
+               ws[o:o + C].data_ptr(), ws[o + C:o + 2 * C].data_ptr(), ws[o + 2 * C:].data_ptr(),
+               int(direct), int(parts is not None), N.stream(dev))
         nones = (None,) * 12
         if direct:
             _grad_ready(ctx.gamma)
