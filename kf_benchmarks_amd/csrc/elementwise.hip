@@ -219,6 +219,36 @@ add_k(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ y, long 
   }
 }
 
+// Elementwise activations without a bias (KIND 1 = relu6, 2 = tanh); the
+// backward reads the forward output: relu6' = 0 < y < 6, tanh' = 1 - y^2.
+template <typename T, int V, int KIND>
+__global__ void __launch_bounds__(256)
+act_fwd_k(const T* __restrict__ x, T* __restrict__ y, long nvec) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
+       i += (long)gridDim.x * blockDim.x) {
+    float v[V];
+    load_vec<T, V>(x + i * V, v);
+#pragma unroll
+    for (int k = 0; k < V; ++k) v[k] = KIND == 1 ? fminf(fmaxf(v[k], 0.f), 6.f) : tanhf(v[k]);
+    store_vec<T, V>(y + i * V, v);
+  }
+}
+
+template <typename T, int V, int KIND>
+__global__ void __launch_bounds__(256)
+act_bwd_k(const T* __restrict__ dy, const T* __restrict__ y, T* __restrict__ dx, long nvec) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
+       i += (long)gridDim.x * blockDim.x) {
+    float g[V], o[V];
+    load_vec<T, V>(dy + i * V, g);
+    load_vec<T, V>(y + i * V, o);
+#pragma unroll
+    for (int k = 0; k < V; ++k)
+      g[k] = KIND == 1 ? ((o[k] > 0.f && o[k] < 6.f) ? g[k] : 0.f) : g[k] * (1.f - o[k] * o[k]);
+    store_vec<T, V>(dx + i * V, g);
+  }
+}
+
 static int egrid(long n) {
   long b = (n + 255) / 256;
   if (b > 256L * 16) b = 256L * 16;
@@ -241,6 +271,44 @@ KFB_API hipError_t kfb_bias_act(int dtype, const void* x, const float* b, void* 
       else
         hipLaunchKernelGGL((bias_act_k<T, VV, false>), dim3(egrid(nvec)), dim3(256), 0, stream,
                            (const T*)x, b, (T*)y, nvec, C);
+    });
+  });
+  return hipGetLastError();
+}
+
+// y = act(x) / dx = dy * act'(y) over n elements (n % vec width == 0 is not
+// required: the vector width is picked from n), kind 1 = relu6, 2 = tanh.
+KFB_API hipError_t kfb_act_fwd(int dtype, const void* x, void* y, long n, int kind,
+                               hipStream_t stream) {
+  if (kind != 1 && kind != 2) return hipErrorInvalidValue;
+  const int V = n % 8 == 0 ? 8 : n % 4 == 0 ? 4 : n % 2 == 0 ? 2 : 1;
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    KFB_DISPATCH_VEC(V, VV, {
+      const long nvec = n / VV;
+      if (kind == 1)
+        hipLaunchKernelGGL((act_fwd_k<T, VV, 1>), dim3(egrid(nvec)), dim3(256), 0, stream,
+                           (const T*)x, (T*)y, nvec);
+      else
+        hipLaunchKernelGGL((act_fwd_k<T, VV, 2>), dim3(egrid(nvec)), dim3(256), 0, stream,
+                           (const T*)x, (T*)y, nvec);
+    });
+  });
+  return hipGetLastError();
+}
+
+KFB_API hipError_t kfb_act_bwd(int dtype, const void* dy, const void* y, void* dx, long n, int kind,
+                               hipStream_t stream) {
+  if (kind != 1 && kind != 2) return hipErrorInvalidValue;
+  const int V = n % 8 == 0 ? 8 : n % 4 == 0 ? 4 : n % 2 == 0 ? 2 : 1;
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    KFB_DISPATCH_VEC(V, VV, {
+      const long nvec = n / VV;
+      if (kind == 1)
+        hipLaunchKernelGGL((act_bwd_k<T, VV, 1>), dim3(egrid(nvec)), dim3(256), 0, stream,
+                           (const T*)dy, (const T*)y, (T*)dx, nvec);
+      else
+        hipLaunchKernelGGL((act_bwd_k<T, VV, 2>), dim3(egrid(nvec)), dim3(256), 0, stream,
+                           (const T*)dy, (const T*)y, (T*)dx, nvec);
     });
   });
   return hipGetLastError();

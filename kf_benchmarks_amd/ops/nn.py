@@ -530,11 +530,42 @@ def relu(x):
     return bias_act(x, None, True)
 
 
+N.register_optional("kfb_act_fwd", [N.I, N.P, N.P, N.L, N.I, N.P])
+N.register_optional("kfb_act_bwd", [N.I, N.P, N.P, N.P, N.L, N.I, N.P])
+_ACT_KINDS = {"relu6": 1, "tanh": 2}
+
+
+class _Act(torch.autograd.Function):
+    """relu6 / tanh on the GPU (csrc/elementwise.hip act_fwd_k / act_bwd_k;
+    the backward reads the output)."""
+
+    @staticmethod
+    def forward(ctx, x, kind):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        N.call("kfb_act_fwd", N.dt(x), x.data_ptr(), y.data_ptr(), x.numel(), kind,
+               N.stream(x.device))
+        ctx.save_for_backward(y)
+        ctx.kind = kind
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        N.call("kfb_act_bwd", N.dt(dy), dy.data_ptr(), y.data_ptr(), dx.data_ptr(), dy.numel(),
+               ctx.kind, N.stream(dy.device))
+        return dx, None
+
+
 def activation(x, kind: Optional[str]):
     if kind in (None, "linear"):
         return x
     if kind == "relu":
         return relu(x)
+    if kind in _ACT_KINDS and _on_gpu(x) and x.numel() > 0:
+        return _Act.apply(x, _ACT_KINDS[kind])
     if kind == "tanh":
         return torch.tanh(x)
     if kind == "relu6":

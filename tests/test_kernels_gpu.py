@@ -497,3 +497,23 @@ def test_channel_pad(cuda, dt):
     g = torch.randn(y.shape).to(dt)
     y.backward(g.to(cuda))
     assert torch.equal(xa.grad.float().cpu(), g[..., 8:24].float())
+
+
+@pytest.mark.parametrize("kind", ["relu6", "tanh"])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(2, 7, 7, 96), (3, 5, 5, 3)])
+def test_activation_native(cuda, kind, dt, shape):
+    """relu6 / tanh forward and backward (csrc/elementwise.hip act_fwd_k /
+    act_bwd_k) against the fp32 torch ops."""
+    g = torch.Generator().manual_seed(5)
+    x = (torch.randn(shape, generator=g) * 4).to(dt)
+    dy = torch.randn(shape, generator=g).to(dt)
+    xa = x.to(cuda).requires_grad_(True)
+    ya = F.activation(xa, kind)
+    ya.backward(dy.to(cuda))
+    xr = x.float().requires_grad_(True)
+    yr = torch.clamp(xr, 0.0, 6.0) if kind == "relu6" else torch.tanh(xr)
+    yr.backward(dy.float())
+    tol = 2e-2 if dt == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(ya.float().cpu(), yr.detach(), rtol=tol, atol=tol)
+    torch.testing.assert_close(xa.grad.float().cpu(), xr.grad, rtol=tol, atol=tol)

@@ -110,6 +110,26 @@ def test_scatter_dgrad_bn_fusion_matches(cuda, monkeypatch):
     assert vals[len(vals) // 2] > 0.99 and vals[0] > 0.9, (vals[0], vals[len(vals) // 2])
 
 
+def test_stem_pool_link_partials_match(cuda, monkeypatch):
+    """ResNet-50 stem: the fused BN+ReLU+max-pool backward takes its BN
+    partials from the dgrad epilogue of the convs consuming the pooled output
+    z (sum dz', sum dz' (z - beta) / (gamma * invstd), ops/nn.py _POOL_LINK)
+    instead of its own pass over x.  The forward is unchanged and the
+    backward identical down to the stem BN, whose partials now come from the
+    bf16 z instead of the bf16 x: the stem gradients agree to bf16 rounding,
+    every other gradient to the atomics' order."""
+    from kf_benchmarks_amd.ops import nn as F
+    monkeypatch.setattr(F, "_POOL_LINK", True)
+    loss_new, new = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
+    monkeypatch.setattr(F, "_POOL_LINK", False)
+    loss_old, old = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
+    assert abs(loss_new - loss_old) < 1e-3 * abs(loss_old), (loss_new, loss_old)
+    cos = {k: _cos(new[k], ref) for k, ref in old.items() if ref.norm() > 0}
+    vals = sorted(cos.values())
+    print("pool-link cosines: min %.5f median %.5f" % (vals[0], vals[len(vals) // 2]))
+    assert vals[len(vals) // 2] > 0.999 and vals[0] > 0.98, (vals[0], vals[len(vals) // 2])
+
+
 def test_deferred_shortcut_bn_network(cuda, monkeypatch):
     """ResNet-50 v1 projection shortcuts take the deferred-BN path (the
     shortcut BN applied inside the block-output BN's apply pass) on the GPU:
