@@ -514,6 +514,11 @@ def test_activation_native(cuda, kind, dt, shape):
     xr = x.float().requires_grad_(True)
     yr = torch.clamp(xr, 0.0, 6.0) if kind == "relu6" else torch.tanh(xr)
     yr.backward(dy.float())
+    gref = xr.grad
+    if kind == "relu6":
+        # tf.nn.relu6's gradient: dy * (0 < x < 6), strict at both ends
+        # (torch.clamp's passes the gradient at x == 0 and x == 6)
+        gref = dy.float() * ((x.float() > 0) & (x.float() < 6)).float()
     tol = 2e-2 if dt == torch.bfloat16 else 1e-5
     torch.testing.assert_close(ya.float().cpu(), yr.detach(), rtol=tol, atol=tol)
-    torch.testing.assert_close(xa.grad.float().cpu(), xr.grad, rtol=tol, atol=tol)
+    torch.testing.assert_close(xa.grad.float().cpu(), gref, rtol=tol, atol=tol)
