@@ -940,6 +940,10 @@ def _gemm(mode, p, ldp, q, ldq, rows, cols, red, out, ldc, bias=None, relu=False
            slab.numel() if slab is not None else 0, nsplit, N.stream(dev))
 
 
+# KFB_LINEAR_WGRAD_SIDE=0: affine weight gradients on the compute stream
+_LINEAR_WGRAD_SIDE = os.environ.get("KFB_LINEAR_WGRAD_SIDE", "1") != "0"
+
+
 class _Linear(torch.autograd.Function):
     """y = act(x @ W + b) with W the fp32 master [Cin, Cout] (TF layout) and
     W_lp its compute copy, on the MFMA GEMM (csrc/gemm.hip): the forward
@@ -997,6 +1001,20 @@ class _Linear(torch.autograd.Function):
         wsink = _grad_sink(ctx.w)
         dw = None
         if wsink is not None:
+            ch = _conv_hip()
+            side = ch.wgrad_stream(dev) if _LINEAR_WGRAD_SIDE else None
+            if side is not None:
+                # like the conv weight gradients: off the dgrad chain, on the
+                # side stream (the classifier's wgrad is a small latency-bound
+                # GEMM at the head of the backward critical path)
+                N.stream_wait(side.cuda_stream, N.stream(dev))
+                ch._queue_join(dev)
+                with torch.cuda.stream(side):
+                    _gemm(_GEMM_WGRAD, x, K, dy, Nout, K, Nout, M, wsink, Nout, accumulate=True)
+                    x.record_stream(side)
+                    dy.record_stream(side)
+                    _grad_ready(ctx.w)
+                return dx, None, db, None, None
             _gemm(_GEMM_WGRAD, x, K, dy, Nout, K, Nout, M, wsink, Nout, accumulate=True)
             _grad_ready(ctx.w)
         else:
