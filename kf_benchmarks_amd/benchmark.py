@@ -580,7 +580,15 @@ class BenchmarkCNN:
         self.flat.zero_grad()
         step = self.global_step
         self.strategy.before_backward(step)
+        self._early_hi = 0
+        early_args = self._early_update_args(step)
+        if early_args is not None:
+            from .ops import nn as F
+            F._BACKWARD_TAIL_HOOK = lambda g, b: self._early_update(early_args, g, b)
         loss, acc = self.forward_backward(inputs, need_accuracy)
+        if early_args is not None:
+            from .ops import nn as F
+            F._BACKWARD_TAIL_HOOK = None
         self.strategy.after_backward(step)
         if need_loss and p.loss_type_to_report == "total_loss" and p.weight_decay:
             # the reported total loss uses the weights of this step's forward
@@ -615,13 +623,65 @@ class BenchmarkCNN:
                     wd = 0.0
                 mix, wout = self.strategy.fused_update()
                 self.optimizer.step(self.learning_rate(step), grad_scale=grad_scale,
-                                    weight_decay=wd, clip=p.gradient_clip, mix=mix, wout=wout)
+                                    weight_decay=wd, clip=p.gradient_clip, mix=mix, wout=wout,
+                                    lo=self._early_hi)
             except BaseException:
                 self.strategy.abort_update(step)
                 raise
             self.strategy.after_update(step)
         self.global_step += 1
         return loss, acc
+
+    # KFB_EARLY_UPDATE=1: the update of all but the stem's variables runs on
+    # the weight-gradient stream beside the stem's backward.  Off: both are
+    # HBM-bound (the update moves ~560 MB on ResNet-50), so the overlap saves
+    # nothing and the split costs 0.08 ms/step (profiles/r8_early_update_ab.txt)
+    _EARLY_UPDATE = os.environ.get("KFB_EARLY_UPDATE", "0") == "1"
+
+    def _early_update_args(self, step):
+        """The optimizer arguments of this step's update if part of it may run
+        early (one GPU, a plain synchronous strategy, no host-side gradient
+        logic), else None."""
+        from .parallel.variable_mgr import (IndependentStrategy, KungFuSyncSGD,
+                                            SumAllReduceStrategy)
+        p = self.params
+        s = self.strategy
+        if not self._EARLY_UPDATE or self.device_type != "cuda" or self.tower_mode \
+                or type(s) not in (KungFuSyncSGD, SumAllReduceStrategy, IndependentStrategy) \
+                or s.reducer is not None or self.world.communicates \
+                or self.enable_auto_loss_scale or self.loss_scale \
+                or self.l2_mask is not None or self.flat.master is not None:
+            return None
+        wd = (p.weight_decay or 0.0) * self._l2_multiplier()
+        return dict(lr=self.learning_rate(step), grad_scale=s.grad_scale, weight_decay=wd,
+                    clip=p.gradient_clip)
+
+    def _early_update(self, args, gamma, beta):
+        """Runs the update of every variable before the stem's in flat order
+        (their gradients are final: they come earlier in the backward) on the
+        weight-gradient stream, beside the stem's backward; the update after
+        the backward then covers the stem's variables only."""
+        from .ops import conv_hip
+        f = self.flat
+        offs = {id(q): o for q, o in zip(f.params, f.offsets)}
+        tail = [offs.get(id(t)) for t in (gamma, beta) if t is not None]
+        if not tail or None in tail:
+            return
+        hi = min(tail)
+        if sum(1 for o in f.offsets if o >= hi) > 3:  # stem BN gamma/beta + stem conv only
+            return
+        side = conv_hip.wgrad_stream(self.device)
+        if side is None:
+            return
+        # gradients of the range written on the compute stream are enqueued
+        # before this point; the side stream's own wgrads precede it in order
+        _native.stream_wait(side.cuda_stream, _native.stream(self.device))
+        conv_hip._queue_join(self.device)
+        with torch.cuda.stream(side):
+            self.optimizer.step(args["lr"], grad_scale=args["grad_scale"],
+                                weight_decay=args["weight_decay"], clip=args["clip"],
+                                lo=0, hi=hi, advance=False)
+        self._early_hi = hi
 
     def _l2_multiplier(self) -> float:
         """Copies of wd * w in the applied gradient.  The reference adds the

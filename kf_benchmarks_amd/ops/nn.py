@@ -748,6 +748,13 @@ N.register_optional("kfb_bn_relu_maxpool_bwd", [N.I, N.P, N.P, N.P, N.P, N.P] + 
 _POOL_LINK = os.environ.get("KFB_POOL_LINK", "0") == "1"
 
 
+# Called once at the top of the stem BN+ReLU+max-pool backward (the point
+# where every gradient but the stem's is complete or enqueued): the engine
+# starts the optimizer on those variables there, beside the stem's backward
+# (BenchmarkCNN._early_update)
+_BACKWARD_TAIL_HOOK = None
+
+
 class _BNReluMaxPool(torch.autograd.Function):
     """maxpool(relu(bn_train(x))) with the BN statistics already summed by
     the producing conv (the ResNet stem tail, csrc/bn.hip): neither the BN
@@ -787,6 +794,10 @@ class _BNReluMaxPool(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dz):
+        global _BACKWARD_TAIL_HOOK
+        hook, _BACKWARD_TAIL_HOOK = _BACKWARD_TAIL_HOOK, None
+        if hook is not None:
+            hook(ctx.gamma, ctx.beta)
         x, z, idx, gamma, st = ctx.saved_tensors
         dz = dz.contiguous()
         n, H, W, C = ctx.geo[:4]

@@ -170,13 +170,32 @@ class FusedOptimizer:
 
     def step(self, lr: float, grad_scale: float = 1.0, weight_decay: float = 0.0,
              clip: Optional[float] = None, grad: Optional[torch.Tensor] = None,
-             mix=None, wout: Optional[torch.Tensor] = None):
+             mix=None, wout: Optional[torch.Tensor] = None, lo: int = 0,
+             hi: Optional[int] = None, advance: bool = True):
         """One update of every variable. ``grad`` overrides the flat gradient
         buffer (e.g. an all-reduced copy).  ``mix = (src, a, b, ok)`` first
         sets w <- a*w + b*src (model averaging; skipped when the device flag
         ``ok`` (nullable) is 0); ``wout`` receives a copy of the updated
-        weights.  Both ride the same single pass over the model."""
+        weights.  Both ride the same single pass over the model.
+        ``lo`` / ``hi``: only flat elements [lo, hi) (GPU); ``advance=False``:
+        an early part of this step's update (the step counter and the
+        after-update hooks wait for the call that finishes the step)."""
+        if lo or hi is not None:
+            if self.flat.device.type != "cuda" or mix is not None or wout is not None \
+                    or grad is not None or self.flat.master is not None:
+                raise ValueError("ranged updates: plain GPU updates only")
+        if not advance:
+            t_saved = self.t
+            try:
+                self.t += 1
+                return self._step(lr, grad_scale, weight_decay, clip, grad, mix, wout, lo, hi,
+                                  False)
+            finally:
+                self.t = t_saved
         self.t += 1
+        return self._step(lr, grad_scale, weight_decay, clip, grad, mix, wout, lo, hi, True)
+
+    def _step(self, lr, grad_scale, weight_decay, clip, grad, mix, wout, lo, hi, finish):
         f = self.flat
         g = f.grad if grad is None else grad
         b1, b2, eps, lr_t, mom = 0.0, 0.0, 0.0, 0.0, self.momentum
@@ -197,14 +216,20 @@ class FusedOptimizer:
                                   or not t.is_contiguous()):
                 raise ValueError("mix / wout must be contiguous fp32 of the flat size")
         if f.device.type == "cuda":
-            N.call("kfb_opt_step", _KINDS[self.kind], w.data_ptr(), g.data_ptr(),
-                   N.ptr(self.s1), N.ptr(self.s2), N.ptr(lp),
-                   N.dt(lp) if lp is not None else 0, None, f.numel, N.dyn("lr", float(lr)),
-                   float(grad_scale), float(weight_decay), clipv, float(mom), float(b1),
-                   float(b2), float(eps), N.dyn("lr_t", float(lr_t)), int(self.nesterov),
-                   N.ptr(msrc),
-                   float(ma), float(mb), N.ptr(mok), N.ptr(wout), N.stream(f.device))
-            f.after_update()
+            hi_ = f.numel if hi is None else hi
+
+            def at(t):  # pointer to element lo of a flat-sized tensor (or None)
+                return None if t is None else t.data_ptr() + lo * t.element_size()
+            if hi_ > lo:
+                N.call("kfb_opt_step", _KINDS[self.kind], at(w), at(g),
+                       at(self.s1), at(self.s2), at(lp),
+                       N.dt(lp) if lp is not None else 0, None, hi_ - lo, N.dyn("lr", float(lr)),
+                       float(grad_scale), float(weight_decay), clipv, float(mom), float(b1),
+                       float(b2), float(eps), N.dyn("lr_t", float(lr_t)), int(self.nesterov),
+                       N.ptr(msrc),
+                       float(ma), float(mb), N.ptr(mok), N.ptr(wout), N.stream(f.device))
+            if finish:
+                f.after_update()
             return
         if msrc is not None and (mok is None or int(mok.reshape(-1)[0]) != 0):
             with torch.no_grad():

@@ -65,3 +65,32 @@ def test_tape_refuses_torch_ops_in_step(cuda):
     t = StepTape(cuda)
     with pytest.raises(TapeError, match="torch device ops"):
         t.record(lambda: x.mul_(2))
+
+
+@pytest.mark.parametrize("optimizer", ["momentum", "adam"])
+def test_early_update_matches_late(cuda, optimizer, monkeypatch):
+    """The update of every variable but the stem's runs on the weight-gradient
+    stream at the top of the stem's backward (BenchmarkCNN._early_update);
+    the trajectory must match the all-after-backward update up to the
+    run-to-run spread of the BN-statistics atomics, eager and taped."""
+    from kf_benchmarks_amd.benchmark import BenchmarkCNN
+    monkeypatch.setattr(BenchmarkCNN, "_EARLY_UPDATE", False)
+    le, we, _ = _run("resnet50", optimizer, False)
+    le2, we2, _ = _run("resnet50", optimizer, False)
+    monkeypatch.setattr(BenchmarkCNN, "_EARLY_UPDATE", True)
+    calls = []
+    orig = BenchmarkCNN._early_update
+    monkeypatch.setattr(BenchmarkCNN, "_early_update",
+                        lambda self, *a: calls.append(1) or orig(self, *a))
+    lx, wx, _ = _run("resnet50", optimizer, False)
+    assert len(calls) == 6
+    lt, wt, replays = _run("resnet50", optimizer, True)
+    assert replays == 3
+    spread = 0.0
+    for a, a2, b, c in zip(le, le2, lx, lt):
+        spread = max(spread, abs(a - a2))
+        bound = max(4 * spread, 2.5e-2 * max(1.0, abs(a2)))
+        assert abs(a2 - b) <= bound and abs(a2 - c) <= bound, (le, le2, lx, lt)
+    ref = (we - we2).abs().max().item()
+    assert (wx - we2).abs().max().item() <= max(4 * ref, 1e-3), ref
+    assert (wt - we2).abs().max().item() <= max(4 * ref, 1e-3), ref
