@@ -170,6 +170,11 @@ def main(argv=None):
     elapsed = time.perf_counter() - start
     final_loss = float(loss)
 
+    tp = getattr(bench, "_tape", None)
+    if os.environ.get("KFB_TAPE_PROFILE") and tp is not None and tp.replays > 0 \
+            and world.is_chief:
+        print(tp.recorder.host_profile(tp.replays), file=sys.stderr)
+
     # replica consistency (outside the timed region): every rank's fp32
     # master-weight checksum; synchronous strategies must agree bit for bit
     w = bench.strategy.flat.flat

@@ -28,6 +28,8 @@
 
 #include <dlfcn.h>
 
+#include <chrono>
+
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -100,6 +102,8 @@ struct Op {
 
 struct Tape {
   std::vector<Op> ops;
+  // KFB_TAPE_PROFILE: accumulated host seconds per op over all replays
+  std::vector<double> host_s;
   std::unordered_map<std::string, Sig*> sigs;
   ~Tape() {
     for (auto& kv : sigs) delete kv.second;
@@ -157,6 +161,15 @@ KFB_API void kfb_tape_free(void* h) { delete (Tape*)h; }
 
 KFB_API int kfb_tape_size(void* h) { return h ? (int)((Tape*)h)->ops.size() : 0; }
 
+// Host seconds spent in each op over all replays so far (KFB_TAPE_PROFILE
+// set; zeros otherwise); out has kfb_tape_size entries.
+KFB_API int kfb_tape_host_times(void* h, double* out) {
+  Tape* t = (Tape*)h;
+  if (!t) return -1;
+  for (size_t i = 0; i < t->ops.size(); ++i) out[i] = i < t->host_s.size() ? t->host_s[i] : 0.0;
+  return 0;
+}
+
 // Appends fn(args...) with ``types`` (one code per argument) and the raw
 // 64-bit argument slots; returns the op index or -1.
 KFB_API int kfb_tape_add(void* h, void* fn, const char* types, const uint64_t* slots, int n) {
@@ -192,6 +205,8 @@ KFB_API int kfb_tape_replay(void* h, const int* pop, const int* parg, const uint
   for (int k = 0; k < npatch; ++k)
     if (kfb_tape_patch(h, pop[k], parg[k], pval[k]) != 0) return -2;
   call_fn call = ffi().call;
+  static const bool prof = getenv("KFB_TAPE_PROFILE") != nullptr;
+  if (prof && t->host_s.size() != t->ops.size()) t->host_s.assign(t->ops.size(), 0.0);
   for (size_t i = 0; i < t->ops.size(); ++i) {
     Op& op = t->ops[i];
     if (op.argp.size() != op.slots.size()) {
@@ -199,7 +214,13 @@ KFB_API int kfb_tape_replay(void* h, const int* pop, const int* parg, const uint
       for (size_t k = 0; k < op.slots.size(); ++k) op.argp[k] = &op.slots[k];
     }
     int64_t rc = 0;  // ffi widens an int return to a full register
-    call((void*)&op.sig->cif, op.fn, &rc, op.argp.data());
+    if (prof) {
+      const auto t0 = std::chrono::steady_clock::now();
+      call((void*)&op.sig->cif, op.fn, &rc, op.argp.data());
+      t->host_s[i] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    } else {
+      call((void*)&op.sig->cif, op.fn, &rc, op.argp.data());
+    }
     if ((int)rc != 0) {
       if (failed_op) *failed_op = (int)i;
       return (int)rc;

@@ -54,6 +54,7 @@ _SIGS = {
     "kfb_tape_add": [P, P, ctypes.c_char_p, P, I],
     "kfb_tape_patch": [P, I, I, ctypes.c_uint64],
     "kfb_tape_replay": [P, P, P, P, I, P],
+    "kfb_tape_host_times": [P, P],
     "kfb_host_register": [P, ctypes.c_size_t, P],
     "kfb_host_unregister": [P],
     "kfb_nonfinite": [P, L, P, P],

@@ -134,6 +134,23 @@ class Recorder:
     def __len__(self):
         return len(self.names)
 
+    def host_profile(self, replays: int, top: int = 12) -> str:
+        """Host time per replayed step by native entry point (KFB_TAPE_PROFILE)."""
+        n = len(self.names)
+        buf = (ctypes.c_double * n)()
+        N.load().kfb_tape_host_times(self.h, buf)
+        by: Dict[str, List[float]] = {}
+        for name, t in zip(self.names, buf):
+            by.setdefault(name, []).append(t)
+        tot = sum(buf) / max(replays, 1)
+        rows = sorted(by.items(), key=lambda kv: -sum(kv[1]))[:top]
+        out = ["tape host time per replayed step: %.3f ms over %d calls" % (1e3 * tot, n)]
+        for name, ts in rows:
+            out.append("  %-28s %5d calls %8.3f ms  %6.2f us/call" % (
+                name, len(ts), 1e3 * sum(ts) / max(replays, 1),
+                1e6 * sum(ts) / max(replays, 1) / len(ts)))
+        return "\n".join(out)
+
     def close(self):
         if self.h:
             N.load().kfb_tape_free(self.h)
