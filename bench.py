@@ -192,17 +192,21 @@ def main(argv=None):
     comm.all_reduce(t, op="max")
     elapsed = float(t[0].item())
     exposed_ms = float(t[1].item())
+    taped_steps = getattr(getattr(bench, "_tape", None), "replays", 0) > 0
     comm_info = {
         "backend": world.device_backend,
         "buckets": reducer.num_buckets if reducer is not None else 0,
-        "collectives_per_step": ((reducer.launch_count - launches0) / a.steps
+        # replayed steps skip the reducer's Python bookkeeping: not measured
+        "collectives_per_step": (None if taped_steps else
+                                 (reducer.launch_count - launches0) / a.steps
                                  if reducer is not None else 0),
         "wire_dtype": a.wire_dtype,
         "bucket_size_mb": a.bucket_size_mb,
         "rccl_channels": os.environ.get("NCCL_MAX_NCHANNELS", "auto"),
         "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
         # all-reduce time per step that backward did not hide (max over ranks)
-        "exposed_allreduce_ms": round(exposed_ms, 3) if (reducer is not None and cuda) else None,
+        "exposed_allreduce_ms": (round(exposed_ms, 3) if (reducer is not None and cuda
+                                                          and not taped_steps) else None),
     }
     n = world.size
     images = a.batch_size * n * a.steps

@@ -535,7 +535,10 @@ class BenchmarkCNN:
             self.net.tape_begin_recording()
             t = StepTape(self.device)
             try:
-                loss, acc = t.record(lambda: self._eager_train_step(False, False))
+                try:
+                    loss, acc = t.record(lambda: self._eager_train_step(False, False))
+                finally:
+                    self.net.tape_end_recording()
                 if l2 is not None:
                     loss = loss + len(self.devices) * p.weight_decay * l2
             except TapeError as e:

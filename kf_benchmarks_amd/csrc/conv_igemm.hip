@@ -28,6 +28,7 @@
 // with 32-byte units XOR-swizzled so the 8 rows a 32-lane half reads land in
 // 8 distinct 32-byte bank windows.
 #include "common.h"
+#include "igemm_args.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -75,79 +76,12 @@ template <> struct Mfma32<f16> {
   }
 };
 
-struct IgArgs {
-  const void* x;  // gathered operand (NHWC [N,H,W,C])
-  const void* w;  // [Ncol][Ktot]
-  void* y;        // output rows
-  int N, H, W, C;
-  int OH, OW;     // GEMM row space (M = N*OH*OW)
-  int KH, KW, sh, sw, pt, pl;
-  int Ncol, Ktot, M;
-  int YH, YW, ys, ldy;  // row m=(img,oh,ow) -> ((img*YH + oh*ys)*YW + ow*ys)*ldy
-  // Fused epilogue (optional):
-  //   stats != null, mask == null : BN forward statistics of the output,
-  //       stats[slot][0][n] += sum y, stats[slot][1][n] += sum y^2
-  //   stats != null, xbn != null  : BN backward partials of the *producer* BN
-  //       of this conv's input: y' = y * (mask > 0) (mask may be null = no
-  //       ReLU), stats[slot][0][n] += sum y', stats[slot][1][n] += sum y'(xbn - mean)
-  //   layout [2][IG_SPREAD][Ncol]; slot = pixel-tile index % IG_SPREAD (spreads
-  //   the atomics over 32 copies; the BN finalize folds the 32 slots).  Keyed
-  //   by the pixel tile, not the workgroup: the pixel tiles of one channel
-  //   tile land in distinct slots, so with <= 32 pixel tiles every slot takes
-  //   one add and the statistics are bitwise run-to-run deterministic.
-  float* stats;
-  const void* mask;
-  const void* xbn;
-  const float* mean;
-  // addend != null: y = conv(...) + addend (same layout as y) before the
-  // mask / statistics - the gradient other consumers of the conv input
-  // already produced (residual / second-branch accumulation).
-  const void* addend;
-  // mcoef != null (with xbn, mask == null): the producer BN's ReLU mask is
-  // recomputed as xbn * scale + shift > 0 (mcoef = [scale | shift], [2][Ncol])
-  // instead of read from its output - BNs without a residual add.
-  const float* mcoef;
-  // Forward epilogue of a conv without BN (VGG / AlexNet / GoogLeNet
-  // style): y = act(conv + bias[n]), bias nullable, relu 0/1; never combined
-  // with the statistics or the dgrad-style operands.
-  const float* bias;
-  int relu;
-  // FAST path only: byte sizes of x and w (buffer-descriptor range checks)
-  int xbytes, wbytes;
-  // byte size of the output layout (= that of addend / mask / xbn), or 0 if
-  // >= 2 GiB (the epilogue then uses plain loads instead of buffer loads)
-  int ybytes;
-  // forward statistics only: per-channel shift K (nullable); the partials
-  // are sums of (y - K) and (y - K)^2 (see bn_finalize_stats_k)
-  const float* kshift;
-  // generic (non-FAST) loader: k -> (tap, channel) -> (kh, kw) and the
-  // transposed gather's stride divisions as multiply-high divisions
-  FastDiv fd_c, fd_kw, fd_sh, fd_sw;
-  // stride-2 scatter (ys == 2, YH == 2*OH, YW == 2*OW): every output chunk
-  // also writes zeros to the three unsampled pixels of its 2x2 block, so the
-  // output needs no separate zero fill
-  int zfill;
-  // 8-channel geometry (C == 8, KW | 8, KH*KW % 8 == 0; e.g. the stem's
-  // pixel-pair conv, csrc/stem.hip): a 64-deep K step spans 8 taps, one
-  // 16-byte chunk each, so each lane's chunk kc is its own tap
-  // (kh, kw) = (8s + kc) / KW, (8s + kc) % KW of step s; the step advances
-  // the rows by 8 / KW (c8_step elements)
-  int c8, c8_step;
-  // mask != null: 1 = `mask` is the producer BN's ReLU bit mask (bit k of
-  // byte e/8 = y[e + k] > 0 for the 8-element chunk starting at element e,
-  // written by the BN apply pass, csrc/bn.hip relu_bits) instead of its
-  // output y - 1/16 of the bytes for the same test
-  int maskbits;
-};
-
-constexpr int IG_BK = 64;
 
 // offset (elements) of chunk kc's tap within step 0 (8-channel geometry) or
 // of the 16-byte channel chunk kc (C % 64 == 0)
 __device__ __forceinline__ int fast_lane_off(const IgArgs& a, int kc) {
   return a.c8 ? ((kc / a.KW) * a.W + kc % a.KW) * a.C : kc * 8;
 }
-constexpr int IG_SPREAD = 32;
 
 __device__ __forceinline__ int swz_off(int row, int chunk) {
   // element offset of 16-byte chunk `chunk` (0..7) of 128-byte row `row`
@@ -2565,7 +2499,8 @@ enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_G
        IG_ALGO_GMULTI128 = 18, IG_ALGO_GBIG256 = 19, IG_ALGO_GBIG512 = 20,
        IG_ALGO_GENERIC = 21, IG_ALGO_SK128 = 22, IG_ALGO_G8P = 23, IG_ALGO_ONEBUF_E = 24,
        IG_ALGO_ONEBUF_N64_E = 25, IG_ALGO_CLASSIC_N64_E = 26, IG_ALGO_DB = 27,
-       IG_ALGO_GBIG256_32 = 28, IG_ALGO_GSHORT128_32 = 29, IG_ALGO_GSHORT64_32 = 30 };
+       IG_ALGO_GBIG256_32 = 28, IG_ALGO_GSHORT128_32 = 29, IG_ALGO_GSHORT64_32 = 30,
+       IG_ALGO_S3 = 31 };
 
 static bool c8_geometry(int C, int KH, int KW) {
   return C == 8 && (KW == 1 || KW == 2 || KW == 4 || KW == 8) && (KH * KW) % 8 == 0;
@@ -2619,6 +2554,9 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
   // the early-epilogue forms (dgrad-style operands loaded before the K loop)
   const bool early = algo == IG_ALGO_ONEBUF_E || algo == IG_ALGO_ONEBUF_N64_E ||
                      algo == IG_ALGO_CLASSIC_N64_E;
+  // IG_ALGO_S3: the streaming 3x3 64-channel kernel (conv_stream.hip); off
+  // its geometry the default kernel below runs
+  if (algo == IG_ALGO_S3 && fast && !c8 && conv_s3_fits(a)) return launch_conv_s3(dtype, a, stream);
   if ((algo == IG_ALGO_TALL512 || algo == IG_ALGO_TALL256) && fast) {
     if (dtype == BF16) launch_glds_tall<bf16>(a, algo == IG_ALGO_TALL512, stream);
     else if (dtype == F16) launch_glds_tall<f16>(a, algo == IG_ALGO_TALL512, stream);

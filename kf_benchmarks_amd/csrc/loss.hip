@@ -86,7 +86,9 @@ in_top_k_k(const T* __restrict__ logits, const int* __restrict__ labels, int K,
   const long row = blockIdx.x;
   const T* lr = logits + row * K;
   const int lab = labels[row];
-  const float t = to_f32(lr[lab]);
+  // an out-of-range label (e.g. -1) is never "in the top k" (as xent_fwd_k,
+  // which gives it a NaN loss) and reads nothing outside the row
+  const float t = (lab >= 0 && lab < K) ? to_f32(lr[lab]) : NAN;
   float cnt = 0.f;
   for (int j = threadIdx.x; j < K; j += 256) cnt += (to_f32(lr[j]) > t) ? 1.f : 0.f;
   cnt = block_sum<256>(cnt, red);

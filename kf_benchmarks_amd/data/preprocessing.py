@@ -513,7 +513,13 @@ def _batched(pre, records: Iterator[bytes], threads: int):
             while True:
                 recs = [next(records) for _ in range(bs)]
                 seeds = base.spawn(1)[0].generate_state(bs, dtype=np.uint64)
-                imgs, prms, labels, _ = pipe.run(recs, seeds)
+                imgs, prms, labels, bad = pipe.run(recs, seeds)
+                if bad > 0:
+                    # the native decoder substitutes a grey image with label -1
+                    # for a record it cannot parse; the PIL path raises on the
+                    # same record, and a -1 label would poison the loss
+                    raise ValueError("%d of %d image records in this batch could not be "
+                                     "decoded (corrupt TFRecord / JPEG data)" % (bad, bs))
                 yield imgs, labels, prms
         finally:
             pipe.close()

@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..ops import _native as N
 from ..ops import conv as conv_ops
 from ..ops import nn as F
 from .layers import AffineLayer, BatchNormLayer, ConvLayer, DepthwiseConvLayer
@@ -121,7 +122,7 @@ class ConvNetBuilder:
             return
         main = torch.cuda.current_stream(x.device)
         side = _branch_stream(x.device)
-        side.wait_stream(main)
+        N.stream_wait(side.cuda_stream, main.cuda_stream)  # recordable (launch tape)
         with torch.cuda.stream(side):
             yield
 
@@ -135,7 +136,7 @@ class ConvNetBuilder:
         side = _BRANCH_STREAMS.get(x.device.index)
         cur = torch.cuda.current_stream(x.device)
         if side is not None and side != cur:
-            cur.wait_stream(side)
+            N.stream_wait(cur.cuda_stream, side.cuda_stream)
             x.record_stream(cur)
         return t
 

@@ -223,12 +223,20 @@ class Network(nn.Module):
 
     def tape_begin_recording(self):
         self._dropout_calls = 0
+        self._tape_dropouts = None
+
+    def tape_end_recording(self):
+        """Freezes the recorded step's dropout count: eager steps after the
+        recording (accuracy / display steps) still advance _dropout_calls,
+        but a replayed step holds exactly the recorded dropouts."""
+        self._tape_dropouts = getattr(self, "_dropout_calls", 0)
 
     def tape_dropout_values(self):
         """The dropout seeds of the next replayed step: the generator
         advanced exactly as an eager step advances it."""
         out = {}
-        for k in range(getattr(self, "_dropout_calls", 0)):
+        n = getattr(self, "_tape_dropouts", None)
+        for k in range(n if n is not None else getattr(self, "_dropout_calls", 0)):
             self._dropout_seed = (self._dropout_seed * 1103515245 + 12345) & 0x7FFFFFFF
             out["dropout%d" % k] = self._dropout_seed & 0xFFFFFFFF
         return out

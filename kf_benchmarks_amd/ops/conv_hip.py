@@ -25,6 +25,8 @@ _SIG = ([N.I, N.P, N.P, N.P] + [N.I] * 17 + [N.I, N.P, N.P, N.P, N.P, N.P, N.P]
         + [N.P, N.I] + [N.I, N.P, N.P])  # ... mcoef, bias, relu, algo, kshift, stream
 N.register_optional("kfb_conv_igemm", _SIG)
 N.register_optional("kfb_conv_igemm_fast", [N.I] * 4, N.c_int)
+N.register_optional("kfb_conv_s3_applicable", [N.I] * 12, N.c_int)
+N.register_optional("kfb_conv_s3_set_grid", [N.I], None)
 
 # igemm kernel choice (csrc/conv_igemm.hip): 1 = register-staged 128-tile
 # igemm_k, 2 = LDS-DMA ring igemm_glds_k (FAST geometries only).
@@ -54,6 +56,9 @@ IG_DB = 27
 # IG_GBIG256 / IG_GSHORT128 / IG_GSHORT64 on v_mfma_f32_32x32x16 (15% more
 # sustained MFMA throughput than the 16x16x32 form, scripts/probes/mfma_rate.hip)
 IG_GBIG256_32, IG_GSHORT128_32, IG_GSHORT64_32 = 28, 29, 30
+# streaming 3x3 64-channel kernel (csrc/conv_stream.hip): persistent, weights
+# resident in LDS, input read once through an LDS ring
+IG_S3 = 31
 IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N64,
             "glds_n64": IG_GLDS_N64, "onebuf": IG_ONEBUF, "onebuf_n64": IG_ONEBUF_N64,
             "tall512": IG_TALL512, "tall256": IG_TALL256, "small": IG_SMALL,
@@ -64,10 +69,11 @@ IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N6
             "generic": IG_GENERIC, "sk128": IG_SK128, "g8p": IG_G8P, "onebuf_e": IG_ONEBUF_E,
             "onebuf_n64_e": IG_ONEBUF_N64_E, "classic_n64_e": IG_CLASSIC_N64_E, "db": IG_DB,
             "gbig256_32": IG_GBIG256_32, "gshort128_32": IG_GSHORT128_32,
-            "gshort64_32": IG_GSHORT64_32}
+            "gshort64_32": IG_GSHORT64_32, "s3": IG_S3}
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
+_NO_S3 = os.environ.get("KFB_IGEMM_NOS3", "0") == "1"  # A/B knob: drop IG_S3
 _NO_GSHORT = os.environ.get("KFB_IGEMM_NOGSHORT", "0") == "1"  # A/B knob: drop IG_GSHORT*
 _GSHORT3 = os.environ.get("KFB_IGEMM_GSHORT3", "1") != "0"  # A/B knob: the 3-stage forms
 _NO_MULTI = os.environ.get("KFB_IGEMM_NOMULTI", "0") == "1"  # A/B knob: drop IG_*MULTI*
@@ -303,6 +309,10 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
         cands += (IG_DB,)
     if fast and _EARLY_EPI and (xbn is not None or addend is not None):
         cands += (IG_ONEBUF_N64_E, IG_CLASSIC_N64_E)
+    if fast and not _NO_S3 and N.load().kfb_conv_s3_applicable(
+            C, ncol, KH, KW, geo[8], geo[9], geo[10], geo[11], geo[1], geo[2], geo[4], geo[5]) \
+            and geo[13] == geo[4] and geo[14] == geo[5] and geo[15] == 1 and geo[16] == ncol:
+        cands += (IG_S3,)
     if ncol > 64:  # 64-wide tiles: more workgroups for small-M layers
         cands += (IG_CLASSIC_N64, IG_GLDS_N64, IG_ONEBUF_N64) if fast else (IG_CLASSIC_N64,)
     if len(cands) == 1:

@@ -231,8 +231,31 @@ class StepTape:
             return orig_rs(t, s)
 
         probe = _TorchKernelProbe() if check_torch_ops else None
+        # torch's stream-ordering calls are neither native calls nor
+        # dispatcher ops: recorded silently they would vanish at replay and
+        # leave a consumer stream unordered behind its producer, so any made
+        # while recording refuses the tape (use _native.stream_wait)
+        waits: List[str] = []
+        orig_ws, orig_we = torch.cuda.Stream.wait_stream, torch.cuda.Stream.wait_event
+
+        def _flag(kind):
+            import traceback
+            where = [f for f in traceback.extract_stack()
+                     if "kf_benchmarks_amd" in f.filename and "tape.py" not in f.filename]
+            waits.append("%s@%s" % (kind, ("%s:%d" % (where[-1].filename.split(
+                "kf_benchmarks_amd/")[-1], where[-1].lineno)) if where else "?"))
+
+        def wait_stream(s, other):
+            _flag("Stream.wait_stream")
+            return orig_ws(s, other)
+
+        def wait_event(s, ev):
+            _flag("Stream.wait_event")
+            return orig_we(s, ev)
+
         torch._C._cuda_beginAllocateToPool(dev, self.pool.id)
         torch.Tensor.record_stream = record_stream
+        torch.cuda.Stream.wait_stream, torch.cuda.Stream.wait_event = wait_stream, wait_event
         N._TAPE = rec
         try:
             if probe is not None:
@@ -243,9 +266,14 @@ class StepTape:
         finally:
             N._TAPE = None
             torch.Tensor.record_stream = orig_rs
+            torch.cuda.Stream.wait_stream, torch.cuda.Stream.wait_event = orig_ws, orig_we
             torch._C._cuda_endAllocateToPool(dev, self.pool.id)
         torch.cuda.synchronize(self.device)
         del keep
+        if waits:
+            rec.close()
+            raise TapeError("torch stream waits inside the recorded step (not replayable): %s"
+                            % sorted(set(waits)), outputs=out)
         if probe is not None and probe.ops:
             rec.close()
             raise TapeError("torch device ops inside the recorded step (not replayable): %s"

@@ -131,7 +131,11 @@ def _side_stream(buf):
     st = _SIDE.get(buf.device)
     if st is None:
         st = _SIDE[buf.device] = torch.cuda.Stream(buf.device)
-    st.wait_stream(torch.cuda.current_stream(buf.device))
+    # the native (recordable) wait, not torch's Stream.wait_stream: a launch
+    # tape replays this edge, so the chained collective never reads a bucket
+    # before backward has written it
+    from ..ops import _native as N
+    N.stream_wait(st.cuda_stream, N.stream(buf.device))
     return torch.cuda.stream(st)
 
 
@@ -178,19 +182,40 @@ class Hierarchical:
         gsize = max(1, min(gsize, world_size))
         self.rank, self.size, self.gsize = rank, world_size, gsize
         groups = [list(range(i, min(i + gsize, world_size))) for i in range(0, world_size, gsize)]
-        # device tensors need RCCL subgroups even when the default group is
-        # the host-side gloo group of a native-communicator world
-        from . import comm as _comm
-        be = "nccl" if _comm.get_world().device_backend in ("rccl", "nccl") else None
-        self.groups = [dist.new_group(g, backend=be) for g in groups]  # collective: all ranks
         self.my = rank // gsize
         self.members = groups[self.my]
         self.leader = self.members[0]
         leaders = [g[0] for g in groups]
-        self.leaders = dist.new_group(leaders, backend=be)
         self.is_leader = rank == self.leader
+        from . import comm as _comm
+        world = _comm.get_world()
+        self.native = None
+        if world.native is not None:
+            # one RCCL communicator family: the subgroups are native
+            # communicators like the world one (no ProcessGroupNCCL beside it)
+            from . import rccl as _rccl
+            store = dist.distributed_c10d._get_default_store()
+            self.native = (_rccl.subgroup(world.native, self.members, store, "hier%d" % self.my),
+                           _rccl.subgroup(world.native, leaders, store, "hier_leaders")
+                           if len(groups) > 1 else None)
+            return
+        # device tensors need RCCL subgroups when the world's device backend
+        # is RCCL; gloo (CPU rehearsals) otherwise
+        be = "nccl" if world.device_backend in ("rccl", "nccl") else None
+        self.groups = [dist.new_group(g, backend=be) for g in groups]  # collective: all ranks
+        self.leaders = dist.new_group(leaders, backend=be)
+
+    def _launch_native(self, buf, op):
+        g, lead = self.native
+        with _side_stream(buf):
+            g.reduce(buf, dst=0, op=op).wait()  # the leader is member 0
+            if self.is_leader and lead is not None:
+                lead.all_reduce(buf, op=op).wait()
+            return [g.broadcast(buf, src=0)]
 
     def launch(self, buf, op: str = "sum"):
+        if self.native is not None:
+            return self._launch_native(buf, op)
         import torch.distributed as dist
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX}[op]
         g = self.groups[self.my]

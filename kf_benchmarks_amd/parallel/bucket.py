@@ -270,7 +270,8 @@ class BucketReducer:
         cur = torch.cuda.current_stream(g.device)
         ev = torch.cuda.Event(enable_timing=True)
         if side is not None and side != cur:
-            side.wait_stream(cur)
+            from ..ops import _native as N
+            N.stream_wait(side.cuda_stream, cur.cuda_stream)
             ev.record(side)
         else:
             ev.record(cur)

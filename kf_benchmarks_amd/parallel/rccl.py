@@ -59,8 +59,25 @@ def available() -> bool:
 
 
 def enabled() -> bool:
-    """KFB_NATIVE_COMM=0 selects torch's ProcessGroupNCCL instead."""
-    return os.environ.get("KFB_NATIVE_COMM", "1") != "0"
+    """KFB_NATIVE_COMM=1 selects this communicator for the device
+    collectives of a multi-process run; the default is torch's
+    ProcessGroupNCCL (the path every multi-GPU run takes until the native one
+    has a recorded multi-GPU run with matching losses).  With it on, no
+    ProcessGroupNCCL is created at all: subgroups are native communicators
+    too (:func:`subgroup`)."""
+    return os.environ.get("KFB_NATIVE_COMM", "0") == "1"
+
+
+def subgroup(world_native: "NativeComm", ranks, store, tag: str):
+    """A native communicator over ``ranks`` (global ranks, ascending) for
+    this process if it is a member, else None.  Collective over the members
+    only: the first member publishes the RCCL unique id under ``tag`` in the
+    job's TCP store (the same rendezvous as the world communicator)."""
+    ranks = list(ranks)
+    if world_native.rank not in ranks:
+        return None
+    return NativeComm(ranks.index(world_native.rank), len(ranks), world_native.device.index,
+                      store, tag="sub/%s/%s" % (tag, ",".join(map(str, ranks))))
 
 
 class Work:
