@@ -507,8 +507,6 @@ class BenchmarkCNN:
             return "dynamic loss scaling reads the gradients on the host"
         if p.staged_vars or self.l2_mask is not None:
             return "staged variables / masked L2 use torch ops in the update"
-        if self.model.get_model_name().startswith("nasnet"):
-            return "NASNet's drop-path schedule follows the host step"
         return None
 
     def _tape_values(self, step):
@@ -560,6 +558,7 @@ class BenchmarkCNN:
         if need_loss and p.loss_type_to_report == "total_loss" and p.weight_decay:
             l2 = self.l2_loss_value()  # of the weights this step's forward reads
         self.input.tape_advance()
+        self.net.global_step = step  # NASNet drop-path schedule (tape_dropout_values)
         vals = self._tape_values(step)
         t.replay(vals)
         self.global_step += 1

@@ -62,8 +62,7 @@ constexpr int RING = BLK * NBLK;    // 640 positions (80 KB)
 constexpr int ROWB = CH * 2;        // bytes per position / weight row
 constexpr int W_BYTES = 9 * CH * ROWB;     // 73728
 constexpr int R_BYTES = RING * ROWB;       // 81920
-constexpr int NPRM = 5 * CH;               // kshift | mean | scale | shift | bias
-constexpr int LDS_BYTES = W_BYTES + R_BYTES + NPRM * 4;  // 156928
+constexpr int LDS_BYTES = W_BYTES + R_BYTES;  // 155648
 
 struct Geo {
   int W1, H1;       // W + 1, H + 1
@@ -86,13 +85,13 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, int o
 __device__ __forceinline__ void barrier_lds() { asm volatile("s_barrier" ::: "memory"); }
 
 // byte offset of the pixel at padded position P in the NHWC tensor, or -1 for
-// a pad position / outside the batch
+// a pad position / outside the batch (branch-free: selects only)
 __device__ __forceinline__ int pix_off(int P, const Geo& g, const IgArgs& a) {
-  if (P < 0) return -1;
-  const int r = g.fw1.div(P), c = P - r * g.W1;
+  const int Pc = P < 0 ? 0 : P;
+  const int r = g.fw1.div(Pc), c = Pc - r * g.W1;
   const int img = g.fh1.div(r), rr = r - img * g.H1;
-  if (c == 0 || rr == 0 || img >= a.N) return -1;
-  return ((img * a.H + rr - 1) * a.W + c - 1) * ROWB;
+  const int off = ((img * a.H + rr - 1) * a.W + c - 1) * ROWB;
+  return (P < 0 || c == 0 || rr == 0 || img >= a.N) ? -1 : off;
 }
 
 __device__ __forceinline__ unsigned f2u(float f) { return __builtin_bit_cast(unsigned, f); }
@@ -111,15 +110,36 @@ __device__ __forceinline__ v16f mfma32<f16>(v8s a, v8s b, v16f c) {
                                                 __builtin_bit_cast(v8h, b), c, 0, 0, 0);
 }
 
-// MODE 0: forward-style epilogue (bias / ReLU / statistics of the output);
-// MODE 1: dgrad-style (addend, producer-BN ReLU mask from bits / values /
-// recomputed from xbn, BN backward partials).
-template <typename T, int MODE>
+// Epilogue variants (compile time, so the epilogue is branch-free and can be
+// scheduled between the next tile's MFMAs):
+//   EPI_STATS : forward, BN statistics of the output (sum (y-K), sum (y-K)^2)
+//   EPI_ACT   : forward, y = act(conv + bias) (bias / ReLU), no statistics
+//   EPI_DGRAD : dX = conv + addend, masked by the producer BN's ReLU
+//               (MASK: 0 none, 1 bit mask, 2 mask values, 3 recomputed from
+//               xbn * scale + shift), BN backward partials sum dX,
+//               sum dX * (xbn - mean) (sum dX^2 without xbn)
+enum { EPI_STATS = 0, EPI_ACT = 1, EPI_DGRAD = 2 };
+
+// chunk q of a tile's epilogue (q = 4j + 2i + p): position subtile j, channel
+// subtile i, register-group pair p -> this lane's 16-byte chunk c = 4i + 2p + hh
+// of position 32j + l32
+template <int EPI>
+__host__ __device__ constexpr int chunk_tap(int q) {
+  // tap of the next tile at which chunk q is finished: from tap 1 on; the
+  // dgrad form loads the operands of position subtile j = 0 at the tile start
+  // (chunks 0-3 at taps 2-5) and those of j = 1 after tap 3 (taps 6-8)
+  return EPI == EPI_DGRAD ? (q < 4 ? q + 2 : (q < 7 ? q + 2 : 8)) : q + 1;
+}
+template <int EPI>
+__host__ __device__ constexpr int load_tap(int j) {
+  return j == 0 ? -1 : 3;  // dgrad operands of subtile j issued after this tap
+}
+
+template <typename T, int EPI, int MASK>
 __global__ void __launch_bounds__(256, 1) conv_s3_k(IgArgs a, Geo g) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   char* const wl = smem;
   char* const ring = smem + W_BYTES;
-  float* const prm = (float*)(smem + W_BYTES + R_BYTES);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -129,7 +149,7 @@ __global__ void __launch_bounds__(256, 1) conv_s3_k(IgArgs a, Geo g) {
   const int ntile = t1 - t0;
   if (ntile <= 0) return;  // (workgroup-uniform)
   const int Qa = g.Qlo + t0 * BM;
-  const int halo = g.W1 + 1;  // W + 2: the largest tap shift
+  const int halo = g.W1 + 1;    // W + 2: the largest tap shift
   const int Pbase = Qa - halo;  // position of stream index 0
 
   const __amdgpu_buffer_rsrc_t xrs =
@@ -138,15 +158,36 @@ __global__ void __launch_bounds__(256, 1) conv_s3_k(IgArgs a, Geo g) {
       __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.wbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t yrs =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, a.ybytes, 0x00020000);
+  // dgrad-form operands (a null operand gets a zero-size range: reads 0)
+  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.addend ? a.addend : a.y), (short)0, a.addend ? a.ybytes : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xbrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.xbn ? a.xbn : a.y), (short)0, a.xbn ? a.ybytes : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.mask ? a.mask : a.y), (short)0,
+      a.mask ? (MASK == 1 ? a.ybytes / 16 : a.ybytes) : 0, 0x00020000);
+  const unsigned xbn_mask = a.xbn != nullptr ? ~0u : 0u;  // (wave-uniform)
+  const float relu_floor = a.relu ? 0.f : -INFINITY;
 
-  // per-channel epilogue parameters
-  if (tid < CH) {
-    prm[tid] = a.kshift ? a.kshift[tid] : 0.f;
-    prm[CH + tid] = (MODE == 1 && a.mean) ? a.mean[tid] : 0.f;
-    prm[2 * CH + tid] = (MODE == 1 && a.mcoef) ? a.mcoef[tid] : 0.f;
-    prm[3 * CH + tid] = (MODE == 1 && a.mcoef) ? a.mcoef[CH + tid] : 0.f;
-    prm[4 * CH + tid] = (MODE == 0 && a.bias) ? a.bias[tid] : 0.f;
-  }
+  // per-lane channel parameters of the 32 channels this lane finishes:
+  // 8c + k, c = 4i + 2p + hh
+  float pa[2][2][8], pb[2][2][8], pc[2][2][8];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int ch = 8 * (4 * i + 2 * p + hh) + k;
+        if constexpr (EPI == EPI_STATS) pa[i][p][k] = a.kshift ? a.kshift[ch] : 0.f;
+        if constexpr (EPI == EPI_ACT) pa[i][p][k] = a.bias ? a.bias[ch] : 0.f;
+        if constexpr (EPI == EPI_DGRAD) pa[i][p][k] = a.mean ? a.mean[ch] : 0.f;
+        if constexpr (EPI == EPI_DGRAD && MASK == 3) {
+          pb[i][p][k] = a.mcoef[ch];
+          pc[i][p][k] = a.mcoef[CH + ch];
+        }
+      }
+
   // weight slab: row R = tap * 64 + cout (128 B), chunk-swizzled by cout
 #pragma unroll
   for (int q0 = 0; q0 < 9 * CH / 8; q0 += 4) {
@@ -173,9 +214,6 @@ __global__ void __launch_bounds__(256, 1) conv_s3_k(IgArgs a, Geo g) {
   wait_vm<0>();
   __syncthreads();
 
-  // statistics / partials: lane-local sums over this workgroup's positions of
-  // channels 8c + k, c = 4i + 2a + hh (the channels this lane owns after the
-  // epilogue's swaps)
   float s1[2][2][8], s2[2][2][8];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -183,182 +221,184 @@ __global__ void __launch_bounds__(256, 1) conv_s3_k(IgArgs a, Geo g) {
     for (int p = 0; p < 2; ++p)
 #pragma unroll
       for (int k = 0; k < 8; ++k) { s1[i][p][k] = 0.f; s2[i][p][k] = 0.f; }
-  const bool want_stats = a.stats != nullptr;
   const int fw = (l32 >> 1) & 7;  // weight-row swizzle of this lane's channel rows
+  const char* const wlane = wl + l32 * ROWB;
 
-  for (int t = 0; t < ntile; ++t) {
+  // dgrad-form operands of the tile being finished, one position subtile
+  // (4 chunks) at a time: [q & 3]
+  uint4 ad[4], xb[4];
+  unsigned mk[4];
+  uint4 mv[4];
+  auto epi_loads = [&](const int (&po)[2], int j) {
+    if constexpr (EPI == EPI_DGRAD) {
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int i = qq >> 1, p = qq & 1;
+        const int c = 4 * i + 2 * p + hh;
+        const int off = po[j] < 0 ? -1 : po[j] + c * 16;
+        ad[qq] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ars, off, 0, 0));
+        xb[qq] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xbrs, off, 0, 0));
+        if constexpr (MASK == 1)
+          mk[qq] = __builtin_amdgcn_raw_buffer_load_b8(mrs, off < 0 ? -1 : off >> 4, 0, 0);
+        if constexpr (MASK == 2)
+          mv[qq] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(mrs, off, 0, 0));
+      }
+    }
+  };
+
+  // finishes chunk q of the tile held in acc (positions po)
+  auto epi_chunk = [&](int q, const v16f (&acc)[2][2], const int (&po)[2]) {
+    const int j = q >> 2, i = (q >> 1) & 1, p = q & 1;
+    const int c = 4 * i + 2 * p + hh;
+    const bool valid = po[j] >= 0;
+    // selects as bit masks (a ?: on per-lane data becomes an exec-mask
+    // branch, which would split the MFMA block the epilogue is scheduled in)
+    const unsigned vmask = valid ? ~0u : 0u;
+    auto keep_if = [](float x, unsigned m) { return u2f(f2u(x) & m); };
+    float v[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const auto sw = __builtin_amdgcn_permlane32_swap(f2u(acc[i][j][8 * p + r]),
+                                                       f2u(acc[i][j][8 * p + 4 + r]), false,
+                                                       false);
+      v[r] = u2f(sw[0]);
+      v[4 + r] = u2f(sw[1]);
+    }
+    Vec<T, 8> ov;
+    if constexpr (EPI == EPI_STATS) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        ov.v[k] = (T)v[k];
+        const float d = keep_if(v[k] - pa[i][p][k], vmask);
+        s1[i][p][k] += d;
+        s2[i][p][k] = fmaf(d, d, s2[i][p][k]);
+      }
+    } else if constexpr (EPI == EPI_ACT) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ov.v[k] = (T)fmaxf(v[k] + pa[i][p][k], relu_floor);
+    } else {
+      const Vec<T, 8> av = __builtin_bit_cast(Vec<T, 8>, ad[q & 3]);
+      const Vec<T, 8> xv = __builtin_bit_cast(Vec<T, 8>, xb[q & 3]);
+      const Vec<T, 8> mvv = __builtin_bit_cast(Vec<T, 8>, mv[q & 3]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float x = v[k] + (float)av.v[k];
+        if constexpr (MASK == 1) x = keep_if(x, 0u - ((mk[q & 3] >> k) & 1u));
+        if constexpr (MASK == 2) x = keep_if(x, 0u - (unsigned)((float)mvv.v[k] > 0.f));
+        if constexpr (MASK == 3)
+          x = keep_if(x, 0u - (unsigned)((float)xv.v[k] * pb[i][p][k] + pc[i][p][k] > 0.f));
+        const float xd = keep_if(x, vmask);
+        s1[i][p][k] += xd;
+        // (xbn - mean) with xbn, else x (sum of squares); xbn reads 0 when absent
+        const float dx = (float)xv.v[k] - pa[i][p][k];
+        s2[i][p][k] = fmaf(xd, u2f((f2u(dx) & xbn_mask) | (f2u(x) & ~xbn_mask)), s2[i][p][k]);
+        ov.v[k] = (T)x;
+      }
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u_t, ov), yrs,
+                                           valid ? po[j] + c * 16 : -1, 0, 0);
+  };
+
+  int po_prev[2] = {-1, -1};
+  v16f accA[2][2], accB[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { accA[i][j][r] = 0.f; accB[i][j][r] = 0.f; }
+
+  // one tile into acc, finishing the previous tile (accp, po_prev) between its MFMAs
+  auto tile = [&](int t, v16f (&acc)[2][2], const v16f (&accp)[2][2]) {
+    epi_loads(po_prev, 0);  // (older than the DMAs below: waiting for them skips those)
     load_block(2 * t + 3);
     load_block(2 * t + 4);
     const int Q0 = Qa + t * BM;
-    // this lane's two output positions (subtile j), their pixel offsets
     int po[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int Q = Q0 + 64 * wid + 32 * j + l32;
       po[j] = Q < g.Qhi ? pix_off(Q, g, a) : -1;
     }
-    // dgrad-style operands of this tile (in flight during the MFMAs)
-    uint4 ad[2][2][2], xb[2][2][2];
-    unsigned mk[2][2][2];
-    if constexpr (MODE == 1) {
-      const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(a.addend ? a.addend : a.y), (short)0, a.addend ? a.ybytes : 0, 0x00020000);
-      const __amdgpu_buffer_rsrc_t xbrs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(a.xbn ? a.xbn : a.y), (short)0, a.xbn ? a.ybytes : 0, 0x00020000);
-      const int mlen = a.mask ? (a.maskbits ? a.ybytes / 16 : a.ybytes) : 0;
-      const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(a.mask ? a.mask : a.y), (short)0, mlen, 0x00020000);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int p = 0; p < 2; ++p) {
-            const int c = 4 * i + 2 * p + hh;
-            const int off = po[j] < 0 ? -1 : po[j] + c * 16;
-            ad[j][i][p] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ars, off, 0, 0));
-            xb[j][i][p] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xbrs, off, 0, 0));
-            if (a.maskbits)
-              mk[j][i][p] = __builtin_amdgcn_raw_buffer_load_b8(mrs, off < 0 ? -1 : off >> 4, 0, 0);
-            else {
-              const uint4 m = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(mrs, off, 0, 0));
-              // one bit per channel: value > 0
-              const Vec<T, 8> mv = __builtin_bit_cast(Vec<T, 8>, m);
-              unsigned bits = 0;
-#pragma unroll
-              for (int k = 0; k < 8; ++k) bits |= ((float)mv.v[k] > 0.f ? 1u : 0u) << k;
-              mk[j][i][p] = bits;
-            }
-          }
-    }
-
-    v16f acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
     // stream index of this wave's first position at tap shift 0
     const int sw0 = t * BM + halo + 64 * wid;
-#pragma unroll 1
-    for (int tap = 0; tap < 9; ++tap) {
-      const int kh = tap / 3, kw = tap - 3 * (tap / 3);
-      const int shift = (kh - 1) * g.W1 + (kw - 1);
-      const int sb = (sw0 + shift) % RING;  // wave-uniform ring slot of lane 0, subtile 0
-      int rowb[2], fx[2];
+    // operand fragments are double-buffered by groups of KG k steps (16 deep
+    // each): the reads of group gi + 1 are issued before the MFMAs of group
+    // gi.  KG = 4 (a whole tap) for the forward forms; the dgrad form holds
+    // its epilogue operands in registers too and uses half taps
+    constexpr int KG = EPI == EPI_DGRAD ? 2 : 4;
+    constexpr int NG = 36 / KG;
+    v8s fa[2][KG][2], fb[2][KG][2];  // [buffer][k step][i / j]
+    auto frags = [&](int gi, v8s (&af)[KG][2], v8s (&bf)[KG][2]) {
+      const int tap = gi * KG / 4, ks0 = gi * KG % 4;
+      const int kh = tap / 3, kw = tap % 3;
+      const int sb = (sw0 + (kh - 1) * g.W1 + (kw - 1)) % RING;
+      unsigned x0 = (unsigned)(sb + l32), x1 = x0 + 32u;
+      x0 = min(x0, x0 - (unsigned)RING);
+      x1 = min(x1, x1 - (unsigned)RING);
+      const int fx = (x0 >> 1) & 7;  // same for x1 (32 is a multiple of 16)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        unsigned x = (unsigned)(sb + 32 * j + l32);
-        x = min(x, x - (unsigned)RING);  // wrap (x < 2 * RING)
-        rowb[j] = (int)x * ROWB;
-        fx[j] = (x >> 1) & 7;  // == fx[0]: 32 is a multiple of 16
-      }
-      const char* wrow = wl + (tap * CH + l32) * ROWB;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int ch = 2 * ks + hh;
-        v8s af[2], bf[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          af[i] = *(const v8s*)(wrow + i * 32 * ROWB + ((ch ^ fw) << 4));
-#pragma unroll
-        for (int j = 0; j < 2; ++j) bf[j] = *(const v8s*)(ring + rowb[j] + ((ch ^ fx[j]) << 4));
+      for (int kk = 0; kk < KG; ++kk) {
+        const int ks = ks0 + kk;
+        const int cw = ((2 * ks + hh) ^ fw) << 4, cx = ((2 * ks + hh) ^ fx) << 4;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
+          af[kk][i] = *(const v8s*)(wlane + (tap * CH + 32 * i) * ROWB + cw);
+        bf[kk][0] = *(const v8s*)(ring + (int)x0 * ROWB + cx);
+        bf[kk][1] = *(const v8s*)(ring + (int)x1 * ROWB + cx);
+      }
+    };
+    frags(0, fa[0], fb[0]);
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mfma32<T>(af[i], bf[j], acc[i][j]);
+    for (int gi = 0; gi < NG; ++gi) {
+      const int cb = gi & 1;
+      if (gi + 1 < NG) frags(gi + 1, fa[cb ^ 1], fb[cb ^ 1]);
+#pragma unroll
+      for (int kk = 0; kk < KG; ++kk)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = mfma32<T>(fa[cb][kk][i], fb[cb][kk][j], acc[i][j]);
+      if ((gi + 1) * KG % 4 == 0) {  // end of a tap
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (chunk_tap<EPI>(q) == (gi * KG / 4)) epi_chunk(q, accp, po_prev);
+        if (load_tap<EPI>(1) == gi * KG / 4) epi_loads(po_prev, 1);
       }
     }
-
-    // ---- epilogue: acc[i][j] reg 4g + r = channel 32i + 8g + 4hh + r of
-    // position 32j + l32; swap groups (2p, 2p+1) across the lane halves so
-    // this lane holds channels 8c .. 8c+7, c = 4i + 2p + hh
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const bool valid = po[j] >= 0;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const int c = 4 * i + 2 * p + hh;
-          float v[8];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const auto sw = __builtin_amdgcn_permlane32_swap(f2u(acc[i][j][8 * p + r]),
-                                                             f2u(acc[i][j][8 * p + 4 + r]),
-                                                             false, false);
-            v[r] = u2f(sw[0]);
-            v[4 + r] = u2f(sw[1]);
-          }
-          const float4* pp = (const float4*)prm;
-          Vec<T, 8> ov;
-          if constexpr (MODE == 0) {
-            if (a.bias || a.relu) {
-              const float4 b0 = pp[(4 * CH + 8 * c) / 4], b1 = pp[(4 * CH + 8 * c) / 4 + 1];
-              const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-              for (int k = 0; k < 8; ++k) {
-                v[k] += bb[k];
-                if (a.relu) v[k] = fmaxf(v[k], 0.f);
-              }
-            }
-#pragma unroll
-            for (int k = 0; k < 8; ++k) ov.v[k] = (T)v[k];
-            if (want_stats) {
-              const float4 k0 = pp[(8 * c) / 4], k1 = pp[(8 * c) / 4 + 1];
-              const float kk[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
-#pragma unroll
-              for (int k = 0; k < 8; ++k) {
-                const float d = valid ? (float)ov.v[k] - kk[k] : 0.f;
-                s1[i][p][k] += d;
-                s2[i][p][k] += d * d;
-              }
-            }
-          } else {
-            const Vec<T, 8> av = __builtin_bit_cast(Vec<T, 8>, ad[j][i][p]);
-            const Vec<T, 8> xv = __builtin_bit_cast(Vec<T, 8>, xb[j][i][p]);
-            const float4 m0 = pp[(CH + 8 * c) / 4], m1 = pp[(CH + 8 * c) / 4 + 1];
-            const float mu[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
-            float sc[8], sh[8];
-            const bool mrec = a.xbn && !a.mask && a.mcoef;
-            if (mrec) {
-              const float4 c0 = pp[(2 * CH + 8 * c) / 4], c1 = pp[(2 * CH + 8 * c) / 4 + 1];
-              const float4 d0 = pp[(3 * CH + 8 * c) / 4], d1 = pp[(3 * CH + 8 * c) / 4 + 1];
-              const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-              const float ds[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
-#pragma unroll
-              for (int k = 0; k < 8; ++k) { sc[k] = cs[k]; sh[k] = ds[k]; }
-            }
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              float x = v[k] + (float)av.v[k];  // zero addend when absent
-              if (a.xbn) {
-                if (a.mask) x = (mk[j][i][p] >> k) & 1u ? x : 0.f;
-                else if (mrec) x = (float)xv.v[k] * sc[k] + sh[k] > 0.f ? x : 0.f;
-                if (want_stats && valid) {
-                  s1[i][p][k] += x;
-                  s2[i][p][k] += x * ((float)xv.v[k] - mu[k]);
-                }
-              } else if (want_stats && valid) {
-                s1[i][p][k] += x;
-                s2[i][p][k] += x * x;
-              }
-              ov.v[k] = (T)x;
-            }
-          }
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u_t, ov), yrs,
-                                                 valid ? po[j] + c * 16 : -1, 0, 0);
-        }
-    }
-    // the blocks issued at the top of this tile (older than its 8 stores)
-    // landed for every wave; every wave is done reading blocks 2t, 2t+1
+    po_prev[0] = po[0];
+    po_prev[1] = po[1];
+    // this tile's DMAs (older than the previous tile's 8 stores) landed for
+    // every wave; every wave is done reading blocks 2t, 2t+1
     wait_vm<8>();
     barrier_lds();
+  };
+
+  for (int t = 0; t < ntile; t += 2) {
+    tile(t, accA, accB);
+    if (t + 1 < ntile) tile(t + 1, accB, accA);
+  }
+  // the last tile's epilogue
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    epi_loads(po_prev, j);
+    if (ntile & 1) {
+#pragma unroll
+      for (int q = 4 * j; q < 4 * j + 4; ++q) epi_chunk(q, accA, po_prev);
+    } else {
+#pragma unroll
+      for (int q = 4 * j; q < 4 * j + 4; ++q) epi_chunk(q, accB, po_prev);
+    }
   }
 
-  if (!want_stats) return;
+  if (EPI == EPI_ACT || !a.stats) return;
   // reduce the lane sums over the 32 lanes of each half (same channels),
   // then over the 4 waves through LDS (the ring is free now), then one
   // atomic add per channel into statistics slot blockIdx % IG_SPREAD
@@ -430,7 +470,10 @@ bool conv_s3_fits(const IgArgs& a) {
                      a.YW, a.ys, a.ldy) &&
          a.xbytes > 0 && a.wbytes > 0 && a.ybytes > 0 && !a.zfill && !a.c8 &&
          (long)a.N * (a.H + 1) * (a.W + 1) + 4L * s3::BLK < (1L << 31) &&
-         !(a.relu && (a.addend || a.xbn));
+         !(a.relu && (a.addend || a.xbn)) && !(a.stats && !(a.addend || a.xbn) && (a.bias || a.relu)) &&
+         // producer-BN ReLU mask: none or the bit mask (mask values / the
+         // recomputed mask stay on the tiled kernels)
+         !(a.xbn && ((a.mask && !a.maskbits) || (!a.mask && a.mcoef)));
 }
 
 // Launch for an igemm_k-style argument block (forward / stride-1 dgrad with
@@ -447,15 +490,30 @@ hipError_t launch_conv_s3(int dtype, const IgArgs& a, hipStream_t stream) {
   g.tiles = (g.Qhi - g.Qlo + s3::BM - 1) / s3::BM;
   const int grid = s3_grid(g.tiles);
   const bool dg = a.addend || a.xbn;
+  // epilogue variant and mask source (see conv_s3_k)
+  const int epi = dg ? s3::EPI_DGRAD : (a.stats ? s3::EPI_STATS : s3::EPI_ACT);
+  int mask = 0;
+  if (dg && a.xbn) {
+    if (a.mask) mask = a.maskbits ? 1 : 2;
+    else if (a.mcoef) mask = 3;
+  }
+  if (epi == s3::EPI_STATS && (a.bias || a.relu)) return hipErrorInvalidValue;
+#define KFB_S3_LAUNCH(T)                                                                      \
+  switch (epi * 4 + mask) {                                                                   \
+    case 0: hipLaunchKernelGGL((s3::conv_s3_k<T, 0, 0>), dim3(grid), dim3(256), 0, stream, a, g); break; \
+    case 4: hipLaunchKernelGGL((s3::conv_s3_k<T, 1, 0>), dim3(grid), dim3(256), 0, stream, a, g); break; \
+    case 8: hipLaunchKernelGGL((s3::conv_s3_k<T, 2, 0>), dim3(grid), dim3(256), 0, stream, a, g); break; \
+    case 9: hipLaunchKernelGGL((s3::conv_s3_k<T, 2, 1>), dim3(grid), dim3(256), 0, stream, a, g); break; \
+    default: return hipErrorInvalidValue;                                                      \
+  }
   if (dtype == BF16) {
-    if (dg) hipLaunchKernelGGL((s3::conv_s3_k<bf16, 1>), dim3(grid), dim3(256), 0, stream, a, g);
-    else hipLaunchKernelGGL((s3::conv_s3_k<bf16, 0>), dim3(grid), dim3(256), 0, stream, a, g);
+    KFB_S3_LAUNCH(bf16)
   } else if (dtype == F16) {
-    if (dg) hipLaunchKernelGGL((s3::conv_s3_k<f16, 1>), dim3(grid), dim3(256), 0, stream, a, g);
-    else hipLaunchKernelGGL((s3::conv_s3_k<f16, 0>), dim3(grid), dim3(256), 0, stream, a, g);
+    KFB_S3_LAUNCH(f16)
   } else {
     return hipErrorInvalidValue;
   }
+#undef KFB_S3_LAUNCH
   return hipGetLastError();
 }
 

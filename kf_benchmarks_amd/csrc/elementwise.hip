@@ -380,6 +380,32 @@ KFB_API hipError_t kfb_dropout(int dtype, const void* x, void* y, long n, float 
   return hipGetLastError();
 }
 
+// NASNet drop path (tcb/models/nasnet_utils.py drop_path): every sample n of
+// x [N][per] is kept with probability kp and scaled by 1/kp, or zeroed:
+// y = x * floor(kp + u_n) / kp, u_n uniform from (seed, n).  The backward
+// is the same call on dy (same seed, same kp).  kp = 1 is the identity.
+template <typename T>
+__global__ void __launch_bounds__(256)
+drop_path_k(const T* __restrict__ x, T* __restrict__ y, long n, long per, float kp,
+            uint32_t seed) {
+  const float inv = 1.f / kp;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    const float u = u01(seed, (uint64_t)(i / per), 11u);
+    y[i] = from_f32<T>(floorf(kp + u) * inv * to_f32(x[i]));
+  }
+}
+
+KFB_API hipError_t kfb_drop_path(int dtype, const void* x, void* y, long n, long per, float kp,
+                                 uint32_t seed, hipStream_t stream) {
+  if (per <= 0 || !(kp > 0.f)) return hipErrorInvalidValue;
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((drop_path_k<T>), dim3(egrid(n)), dim3(256), 0, stream, (const T*)x, (T*)y,
+                       n, per, kp, seed);
+  });
+  return hipGetLastError();
+}
+
 KFB_API hipError_t kfb_synthetic_images(int dtype, void* x, long n, float mean, float std,
                                         uint32_t seed, hipStream_t stream) {
   const bool vec8 = n % 8 == 0 && n / 8 < (1L << 31) && ((uintptr_t)x & 15) == 0;
@@ -461,5 +487,62 @@ KFB_API hipError_t kfb_unpad_accum_f32(const float* src, float* dst, int R, long
   const long total = (long)R * K * C;
   hipLaunchKernelGGL(unpad_accum_f32_k, dim3(egrid(total)), dim3(256), 0, stream, src, dst, total,
                      (int)K, C, Cp);
+  return hipGetLastError();
+}
+
+// dst [R][K][C] = the leading block of src [Rp][K][Cp] (r < R, c < C): the
+// inverse of pad_rkc, for a channel-padded conv's output / input gradient
+template <typename T>
+__global__ void __launch_bounds__(256)
+crop_rkc_k(const T* __restrict__ src, T* __restrict__ dst, long total, int K, int C, int Cp) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const long rk = i / C;
+    dst[i] = src[rk * Cp + c];
+  }
+}
+
+KFB_API hipError_t kfb_crop_rkc(int dtype, const void* src, void* dst, int R, long K, int C,
+                                int Cp, hipStream_t stream) {
+  if (C > Cp) return hipErrorInvalidValue;
+  const long total = (long)R * K * C;
+  if (total == 0) return hipSuccess;
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((crop_rkc_k<T>), dim3(egrid(total)), dim3(256), 0, stream, (const T*)src,
+                       (T*)dst, total, (int)K, C, Cp);
+  });
+  return hipGetLastError();
+}
+
+// Conv weight relayouts for the dgrad GEMMs (tcb's conv2d_backprop_input
+// filter use): dst[ci][kh][kw][co] = src[co][kh'][kw'][ci] with (kh', kw') =
+// (KH-1-kh, KW-1-kw) when flip (stride-1 transposed conv), else (kh, kw);
+// a 1x1 conv's case is the plain [Cout][Cin] -> [Cin][Cout] transpose.
+template <typename T>
+__global__ void __launch_bounds__(256)
+wrelayout_k(const T* __restrict__ src, T* __restrict__ dst, int cout, int KH, int KW, int cin,
+            int flip) {
+  const long total = (long)cout * KH * KW * cin;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    // i indexes dst [ci][kh][kw][co]
+    const int co = (int)(i % cout);
+    long r = i / cout;
+    const int kw = (int)(r % KW);
+    r /= KW;
+    const int kh = (int)(r % KH);
+    const int ci = (int)(r / KH);
+    const int sh = flip ? KH - 1 - kh : kh, sw = flip ? KW - 1 - kw : kw;
+    dst[i] = src[(((long)co * KH + sh) * KW + sw) * cin + ci];
+  }
+}
+
+KFB_API hipError_t kfb_wrelayout(int dtype, const void* src, void* dst, int cout, int KH, int KW,
+                                 int cin, int flip, hipStream_t stream) {
+  const long total = (long)cout * KH * KW * cin;
+  if (total == 0) return hipSuccess;
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((wrelayout_k<T>), dim3(egrid(total)), dim3(256), 0, stream, (const T*)src,
+                       (T*)dst, cout, KH, KW, cin, flip);
+  });
   return hipGetLastError();
 }

@@ -68,6 +68,12 @@ class MobilenetModel(model.CNNModel):
     def _expanded_conv(cnn, t, out_depth, stride, std):
         x = cnn.top_layer
         in_depth = cnn.top_size
+        if stride == 1 and in_depth == out_depth and not cnn.meta:
+            # the block input feeds the expansion and the residual add: two
+            # aliases whose gradients a native add sums (autograd's own sum
+            # is a torch kernel a launch tape cannot replay)
+            from ..ops import nn as F
+            cnn.top_layer, x = F.fanout(x, 2, force=True)
         inner = make_divisible(in_depth * t) if t != 1 else in_depth
         if inner > in_depth:
             with cnn.scope("expand"):

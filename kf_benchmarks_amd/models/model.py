@@ -221,6 +221,27 @@ class Network(nn.Module):
         self._dropout_calls = k + 1
         return self._dropout_seed, "dropout%d" % k
 
+    def drop_path_kp(self, base, layer_ratio, total_steps, step=None):
+        """NASNet drop-path keep probability of a cell at ``step`` (default:
+        the current global step)."""
+        kp = 1 - layer_ratio * (1 - base)
+        step = float(getattr(self, "global_step", 0) if step is None else step)
+        ratio = min(1.0, step / total_steps)
+        return 1 - ratio * (1 - kp)
+
+    def drop_path_key(self, base, layer_ratio, total_steps):
+        """Per-step tape argument name of a drop-path keep probability (the
+        schedule parameters are kept to re-derive it at every replay)."""
+        if not hasattr(self, "_drop_paths"):
+            self._drop_paths = {}
+        spec = (base, layer_ratio, total_steps)
+        for k, v in self._drop_paths.items():
+            if v == spec:
+                return k
+        key = "droppath_kp_%d" % len(self._drop_paths)
+        self._drop_paths[key] = spec
+        return key
+
     def tape_begin_recording(self):
         self._dropout_calls = 0
         self._tape_dropouts = None
@@ -235,6 +256,9 @@ class Network(nn.Module):
         """The dropout seeds of the next replayed step: the generator
         advanced exactly as an eager step advances it."""
         out = {}
+        for key, (base, ratio, total) in getattr(self, "_drop_paths", {}).items():
+            # the step the replay trains (global_step is advanced after it)
+            out[key] = self.drop_path_kp(base, ratio, total)
         n = getattr(self, "_tape_dropouts", None)
         for k in range(n if n is not None else getattr(self, "_dropout_calls", 0)):
             self._dropout_seed = (self._dropout_seed * 1103515245 + 12345) & 0x7FFFFFFF

@@ -114,18 +114,22 @@ class _Builder:
         return fn(k, k, stride, stride, mode="SAME", input_layer=x, num_channels_in=x.shape[-1])
 
     def drop_path(self, x, cell_num):
-        kp = self.cfg["drop_path_keep_prob"]
-        if kp >= 1.0 or not self.cnn.phase_train or self.cnn.meta:
+        """tcb/models/nasnet_model.py _apply_drop_path: the keep probability
+        falls linearly with the cell index and ramps in over the first
+        total_training_steps steps.  The GPU form always runs (kp = 1 is the
+        identity), with kp and the seed as per-step launch-tape arguments:
+        a taped step follows the schedule (Network.tape_dropout_values)."""
+        base = self.cfg["drop_path_keep_prob"]
+        if base >= 1.0 or not self.cnn.phase_train or self.cnn.meta:
             return x
         layer_ratio = (cell_num + 1) / float(self.total_cells)
-        kp = 1 - layer_ratio * (1 - kp)
-        step = float(getattr(self.net, "global_step", 0))
-        ratio = min(1.0, step / self.cfg["total_training_steps"])
-        kp = 1 - ratio * (1 - kp)
-        if kp >= 1.0:
+        kp = self.net.drop_path_kp(base, layer_ratio, self.cfg["total_training_steps"])
+        if kp >= 1.0 and not x.is_cuda:
             return x
-        mask = torch.floor(kp + torch.rand((x.shape[0], 1, 1, 1), device=x.device))
-        return x * (mask / kp).to(x.dtype)
+        seed, key = self.net.next_dropout_seed(with_key=True)
+        kp_key = self.net.drop_path_key(base, layer_ratio, self.cfg["total_training_steps"])
+        from ..ops import nn as F
+        return F.drop_path(x, kp, seed, kp_key, key)
 
     # ---- cell
     def cell(self, spec, net, filters, stride, prev, cell_num):

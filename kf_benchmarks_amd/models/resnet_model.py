@@ -64,10 +64,11 @@ def bottleneck_block_v2(cnn, depth, depth_bottleneck, stride):
     input_layer, in_size = cnn.top_layer, cnn.top_size
     name = "resnet_v2%d" % cnn.counts["resnet_v2"]
     cnn.counts["resnet_v2"] += 1
-    if depth == in_size and stride == 1 and not cnn.meta:
+    if depth == in_size and not cnn.meta:
         # the block input feeds the pre-activation BN and the identity
-        # shortcut: two aliases whose gradients a native add sums (autograd's
-        # own sum is a torch kernel a launch tape cannot replay)
+        # shortcut (or its strided average pool): two aliases whose gradients
+        # a native add sums (autograd's own sum is a torch kernel a launch
+        # tape cannot replay)
         from ..ops import nn as F
         cnn.top_layer, input_layer = F.fanout(input_layer, 2)
     preact = cnn.batch_norm(relu=True)

@@ -384,14 +384,14 @@ def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None, addend=None, wt=None,
     sh, sw = stride
     pt, pb, pl, pr = pads
     if KH == 1 and KW == 1 and pt == 0 and pl == 0:
-        wt = wl.reshape(cout, C).t().contiguous() if wt is None else wt  # [Cin][Cout]
+        wt = _wrelayout(wl, False).view(C, cout) if wt is None else wt  # [Cin][Cout]
         if sh == 1 and sw == 1 and OH == H and OW == W:
             dx = torch.empty((n, H, W, C), dtype=dy.dtype, device=dy.device)
         elif addend is not None:
             # unsampled pixels keep the addend; sampled ones accumulate in place
             # (with ``fuse`` the caller guarantees the addend is zero at every
             # unsampled pixel, so the BN partials over sampled pixels are complete)
-            dx = addend if addend_inplace else addend.clone()
+            dx = addend if addend_inplace else _copy(addend)
             fz = f5[:4] + (dx, f5[4])
         else:
             dx = None
@@ -411,12 +411,12 @@ def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None, addend=None, wt=None,
             and KW - 1 - pl >= 0 and KW - 1 - pr >= 0:
         # stride-1 transposed conv == forward conv of dY with the spatially
         # flipped, channel-transposed kernel and complementary padding.
-        wf = wl.flip(1, 2).permute(3, 1, 2, 0).contiguous() if wt is None else wt
+        wf = _wrelayout(wl, True) if wt is None else wt
         dx = torch.empty((n, H, W, C), dtype=dy.dtype, device=dy.device)
         _igemm(dy, wf, dx, n, OH, OW, cout, H, W, KH, KW, 1, 1, KH - 1 - pt, KW - 1 - pl, C,
                H, W, 1, C, False, *fz)
         return dx
-    wd = wl.permute(3, 1, 2, 0).contiguous() if wt is None else wt  # [Cin][KH][KW][Cout]
+    wd = _wrelayout(wl, False) if wt is None else wt  # [Cin][KH][KW][Cout]
     dx = torch.empty((n, H, W, C), dtype=dy.dtype, device=dy.device)
     _igemm(dy, wd, dx, n, OH, OW, cout, H, W, KH, KW, sh, sw, pt, pl, C, H, W, 1, C, True, *fz)
     return dx
@@ -494,6 +494,46 @@ def conv_wgrad(dy, x, w_shape, stride, pads, out=None):
 
 N.register_optional("kfb_pad_rkc", [N.I, N.P, N.P, N.I, N.L, N.I, N.I, N.I, N.P])
 N.register_optional("kfb_unpad_accum_f32", [N.P, N.P, N.I, N.L, N.I, N.I, N.P])
+N.register_optional("kfb_crop_rkc", [N.I, N.P, N.P, N.I, N.L, N.I, N.I, N.P])
+N.register_optional("kfb_wrelayout", [N.I, N.P, N.P, N.I, N.I, N.I, N.I, N.I, N.P])
+
+
+def _crop_channels(t, c):
+    """[..., Cp] -> a new contiguous [..., c] holding the leading c channels
+    (native on the GPU: recordable in a launch tape, unlike a slice copy)."""
+    cp = t.shape[-1]
+    if not t.is_cuda:
+        return t[..., :c].contiguous()
+    t = t.contiguous()
+    out = torch.empty(tuple(t.shape[:-1]) + (c,), dtype=t.dtype, device=t.device)
+    N.call("kfb_crop_rkc", N.dt(t), t.data_ptr(), out.data_ptr(), 1, t.numel() // cp, c, cp,
+           N.stream(t.device))
+    return out
+
+
+def _copy(t):
+    """Device copy of a contiguous tensor (native memcpy on the GPU)."""
+    if not t.is_cuda:
+        return t.clone()
+    t = t.contiguous()
+    out = torch.empty_like(t)
+    N.call("kfb_memcpy_d2d", out.data_ptr(), t.data_ptr(), t.numel() * t.element_size(),
+           N.stream(t.device))
+    return out
+
+
+def _wrelayout(wl, flip):
+    """[Cout][KH][KW][Cin] -> [Cin][KH][KW][Cout], spatially flipped if
+    ``flip`` (native on the GPU)."""
+    cout, KH, KW, cin = wl.shape
+    if not wl.is_cuda:
+        w = wl.flip(1, 2) if flip else wl
+        return w.permute(3, 1, 2, 0).contiguous()
+    wl = wl.contiguous()
+    out = torch.empty((cin, KH, KW, cout), dtype=wl.dtype, device=wl.device)
+    N.call("kfb_wrelayout", N.dt(wl), wl.data_ptr(), out.data_ptr(), cout, KH, KW, cin, int(flip),
+           N.stream(wl.device))
+    return out
 
 
 def _pad_rkc(t, R, K, C, Rp, Cp):
@@ -705,11 +745,12 @@ class _Conv2d(torch.autograd.Function):
         if cout_p != cout:
             stats = None
             if bd is not None:
-                bd = torch.nn.functional.pad(bd, (0, cout_p - cout))
+                bd = (_pad_rkc(bd.contiguous(), 1, 1, cout, 1, cout_p) if bd.is_cuda
+                      else torch.nn.functional.pad(bd, (0, cout_p - cout)))
         wp = wp.contiguous()
         y = conv_fwd(xp, wp, stride, pads, stats, bd, relu)
         if cout_p != cout:
-            y = y[..., :cout].contiguous()
+            y = _crop_channels(y, cout)
         ctx.save_for_backward(xp, wp, y if relu else None)
         ctx.meta = (stride, pads, cin, cout, x.shape)
         ctx.x_needs_grad = ctx.needs_input_grad[0]
@@ -766,8 +807,13 @@ class _Conv2d(torch.autograd.Function):
                     pend, owned = link.pending, link.pending_owned
                     link.pending = None
                     if padded:
-                        dx = conv_dgrad(dy, wp, xp.shape, stride, pads)[..., :cin]
-                        dx = (dx + pend if pend is not None else dx).contiguous()
+                        dx = _crop_channels(conv_dgrad(dy, wp, xp.shape, stride, pads), cin)
+                        if pend is not None:
+                            if dx.is_cuda:
+                                N.call("kfb_add", N.dt(dx), dx.data_ptr(), pend.contiguous().data_ptr(),
+                                       dx.data_ptr(), dx.numel(), 0, N.stream(dx.device))
+                            else:
+                                dx = dx + pend
                     else:
                         fuse = None
                         scatter = is_scatter_dgrad(wp.shape, stride, pads)
@@ -809,11 +855,11 @@ class _Conv2d(torch.autograd.Function):
                             link.accumulated(g, sparse)
                     if g is None:
                         g = conv_dgrad(dy, wp, xp.shape, stride, pads, wt=ctx.wt)
-                        link.deposit(g[..., :cin].contiguous() if padded else g, sparse=sparse)
+                        link.deposit(_crop_channels(g, cin) if padded else g, sparse=sparse)
             else:
                 dx = conv_dgrad(dy, wp, xp.shape, stride, pads, wt=ctx.wt)
                 if dx is not None and padded:
-                    dx = dx[..., :cin].contiguous()
+                    dx = _crop_channels(dx, cin)
         dw = None
         if ctx.needs_input_grad[1]:
             w = ctx.w

@@ -622,10 +622,14 @@ class _FanOut(torch.autograd.Function):
         return acc, None
 
 
-def fanout(x, k: int):
-    """``k`` aliases of ``x`` for ``k`` consumers (GPU: native gradient sum)."""
-    if k <= 1 or not _on_gpu(x) or getattr(x, "_kfb_bn_link", None) is not None \
-            or not x.requires_grad:
+def fanout(x, k: int, force: bool = False):
+    """``k`` aliases of ``x`` for ``k`` consumers (GPU: native gradient sum).
+    A BN output keeps its link (its conv consumers finish the BN backward)
+    unless ``force``: then the aliases carry no link, the BN backward runs
+    unfused, and the gradient sum is still native (a consumer that is not a
+    conv, e.g. a residual add, makes the link unfusable anyway)."""
+    if k <= 1 or not _on_gpu(x) or not x.requires_grad or \
+            (getattr(x, "_kfb_bn_link", None) is not None and not force):
         return [x] * k
     return list(_FanOut.apply(x, k))
 
@@ -1074,6 +1078,46 @@ def dropout(x, keep_prob: float, training: bool, seed: int, key=None):
     if not _on_gpu(x):
         return F.dropout(x, p=1.0 - keep_prob, training=True)
     return _Dropout.apply(x, keep_prob, seed, key)
+
+
+# ------------------------------------------------------------------- drop path
+N.register_optional("kfb_drop_path", [N.I, N.P, N.P, N.L, N.L, N.c_float, N.c_uint32, N.P])
+
+
+class _DropPath(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, kp, seed, kp_key, seed_key):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        ctx.args = (kp, seed, kp_key, seed_key, x.numel() // x.shape[0])
+        _DropPath._call(x, y, *ctx.args)
+        return y
+
+    @staticmethod
+    def _call(x, y, kp, seed, kp_key, seed_key, per):
+        seed = int(seed) & 0xFFFFFFFF
+        N.call("kfb_drop_path", N.dt(x), x.data_ptr(), y.data_ptr(), x.numel(), per,
+               N.dyn(kp_key, float(kp)) if kp_key else float(kp),
+               N.dyn(seed_key, seed) if seed_key else seed, N.stream(x.device))
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        _DropPath._call(dy, dx, *ctx.args)
+        return dx, None, None, None, None
+
+
+def drop_path(x, kp: float, seed: int, kp_key=None, seed_key=None):
+    """Per-sample drop path: y = x * floor(kp + u_n) / kp.  On the GPU one
+    native kernel whose keep probability and seed are per-step launch-tape
+    arguments (``kp_key`` / ``seed_key``), so a taped step follows the
+    step-dependent schedule; kp = 1 is the identity."""
+    if not _on_gpu(x):
+        g = torch.Generator().manual_seed(int(seed) & 0x7FFFFFFF)
+        u = torch.rand((x.shape[0],) + (1,) * (x.dim() - 1), generator=g).to(x.device)
+        return x * (torch.floor(kp + u) / kp).to(x.dtype)
+    return _DropPath.apply(x, kp, seed, kp_key, seed_key)
 
 
 # ------------------------------------------------------------------------- LRN
