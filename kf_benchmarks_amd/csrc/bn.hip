@@ -1122,6 +1122,19 @@ static void launch_apply(hipStream_t stream, const void* x, const void* res, voi
 using namespace kfb;
 
 // Number of slab partial rows the caller must allocate (per output array).
+namespace kfb {
+hipError_t bn_finalize_stats_launch(const float* psum, const float* psq, int nslab, int C,
+                                    long rows, const float* gamma, const float* beta, float decay,
+                                    float eps, float* run_mean, float* run_var, float* save_mean,
+                                    float* save_invstd, float* scale, float* shift, float* kshift,
+                                    hipStream_t stream) {
+  hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, psum,
+                     psq, nslab, C, rows, gamma, beta, decay, eps, run_mean, run_var, save_mean,
+                     save_invstd, scale, shift, kshift);
+  return hipGetLastError();
+}
+}  // namespace kfb
+
 KFB_API int kfb_bn_num_slabs(long rows, int C) {
   const int V = vec_width(C);
   int n = 0;
@@ -1149,9 +1162,10 @@ KFB_API hipError_t kfb_bn_fwd_train(int dtype, const void* x, const void* res, v
         hipLaunchKernelGGL((bn_partial_stats_k<T, VV>), grid, dim3(BN_THREADS), lds, stream,
                            (const T*)x, rows, C, g.cw, g.tpr, g.rpi, slab_rows, psum, psq,
                            kshift);
-      hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, psum,
-                         psq, nslab, C, rows, gamma, beta, decay, eps, run_mean, run_var,
-                         save_mean, save_invstd, scale, shift, kshift);
+      if (have_partials != 2)  // 2: the producing conv's last workgroup finalized (BnFin)
+        hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,
+                           psum, psq, nslab, C, rows, gamma, beta, decay, eps, run_mean, run_var,
+                           save_mean, save_invstd, scale, shift, kshift);
       const long nvec = rows * C / VV;
       if (res) {
         if (relu) launch_apply<T, VV, true, true>(stream, x, res, y, nvec, C, scale, shift, mbits);

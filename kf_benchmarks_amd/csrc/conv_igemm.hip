@@ -697,6 +697,7 @@ __global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : (EARLY ? 3 : (NBUF 
 
   ig_epilogue<T, BM, BN, 256, 2, 2, NoPrefetch, true, EARLY>(a, acc, smem, m0, n0, wm, wn,
                                                              NoPrefetch(), &early);
+  bn_fin_tail(a, (int*)smem);
 }
 
 // Multi-tile form of the FAST one-stage igemm_k: each workgroup computes TPW
@@ -837,6 +838,7 @@ __global__ void __launch_bounds__(256, BM * BN <= 4096 ? 5 : 4) igemm_mt_k(IgArg
         a, acc, smem, (tile / ntiles) * BM, (tile % ntiles) * BN, wm, wn, next);
     if (more) __syncthreads();  // the epilogue's LDS reads precede the next tile's store
   }
+  bn_fin_tail(a, (int*)smem);
 }
 
 // ------------------------------------------------------------ LDS-DMA igemm
@@ -1044,6 +1046,7 @@ __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * 
     ig_epilogue<T, BM, BN, NT, WGM, WGN, NoPrefetch, EXTRAS>(a, acc32, smem, m0, n0, wm, wn);
   else
     ig_epilogue<T, BM, BN, NT, WGM, WGN, NoPrefetch, EXTRAS>(a, acc, smem, m0, n0, wm, wn);
+  bn_fin_tail(a, (int*)smem);
 }
 
 // Multi-tile form of the 4-wave 2-stage LDS-DMA kernel (128 x 64 / 128 x 128):
@@ -1177,6 +1180,7 @@ __global__ void __launch_bounds__(256, (glds_occupancy<BM, BN, 256>()))
     ig_epilogue<T, BM, BN, NT, WGM, WGN, decltype(next)>(
         a, acc, smem + STAGE, (tile / ntiles) * BM, (tile % ntiles) * BN, wm, wn, next);
   }
+  bn_fin_tail(a, (int*)smem);
 }
 
 // ------------------------------------------------------------ 8-phase igemm
@@ -1364,6 +1368,7 @@ __global__ void __launch_bounds__(512, 1) igemm_8p_k(IgArgs a) {
   if (!wr) barrier();  // group 0 matches group 1's extra barrier
   __syncthreads();     // every fragment read done before the epilogue reuses the buffers
   ig_epilogue<T, BM, BN, NT, 2, 4, NoPrefetch, EXTRAS>(a, acc, smem, m0, n0, wr, wc);
+  bn_fin_tail(a, (int*)smem);
 }
 
 // ------------------------------------------------------------ direct-B igemm
@@ -1492,6 +1497,7 @@ __global__ void __launch_bounds__(256, 2) igemm_db_k(IgArgs a) {
     __syncthreads();
   }
   ig_epilogue<T, DB_BM, DB_BN, 256, 4, 1>(a, acc, smem, m0, n0, wid, 0);
+  bn_fin_tail(a, (int*)smem);
 }
 
 // ------------------------------------------------------------ stream-K igemm
@@ -2519,7 +2525,14 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
                                   int trans, float* stats, const void* mask, const void* xbn,
                                   const float* mean, const void* addend, const float* mcoef,
                                   const float* bias, int flags, int algo, const float* kshift,
+                                  int* fin_counter, const float* fin_gamma,
+                                  const float* fin_beta, float* fin_rm, float* fin_rv,
+                                  float* fin_mean, float* fin_invstd, float* fin_scale,
+                                  float* fin_shift, float fin_decay, float fin_eps,
                                   hipStream_t stream) {
+  // fin_counter != null (forward statistics epilogue only): the consuming
+  // BN's finalize runs in the last workgroup (BnFin); the BN forward then
+  // skips its finalize launch
   // flags: bit 0 = ReLU after the bias (forward epilogue), bit 1 = zero-fill
   // the unsampled pixels of a stride-2 scatter (see IgArgs::zfill), bit 2 =
   // `mask` is a ReLU bit mask (see IgArgs::maskbits)
@@ -2535,6 +2548,12 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
            (stats && !xbn && !addend) ? kshift : nullptr,
            FastDiv(C), FastDiv(KW), FastDiv(sh), FastDiv(sw), zfill, 0, 0,
            (mask && ((flags >> 2) & 1)) ? 1 : 0};
+  if (fin_counter) {
+    if (!stats || xbn || addend || ys != 1) return hipErrorInvalidValue;
+    a.fin = BnFin{fin_counter, fin_gamma, fin_beta, fin_rm, fin_rv, fin_mean, fin_invstd,
+                  fin_scale, fin_shift, const_cast<float*>(kshift), fin_decay, fin_eps,
+                  (long)N * OH * OW};
+  }
   const bool t = trans != 0;
   // IG_ALGO_GENERIC: the per-chunk division loader (autotune candidate for
   // the 8-channel geometry, where it can beat the FAST tap stepping)
@@ -2605,9 +2624,16 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
     return hipGetLastError();
   }
   if (algo == IG_ALGO_SK128 && fast && !c8) {
-    if (dtype == BF16) return launch_sk<bf16>(a, stream);
-    if (dtype == F16) return launch_sk<f16>(a, stream);
-    return hipErrorInvalidValue;
+    // (no finalize tail in the stream-K kernel: a separate finalize launch)
+    hipError_t e = hipErrorInvalidValue;
+    if (dtype == BF16) e = launch_sk<bf16>(a, stream);
+    if (dtype == F16) e = launch_sk<f16>(a, stream);
+    if (e == hipSuccess && a.fin.counter)
+      e = bn_finalize_stats_launch(stats, stats + (long)IG_SPREAD * Ncol, IG_SPREAD, Ncol,
+                                   a.fin.rows, fin_gamma, fin_beta, fin_decay, fin_eps, fin_rm,
+                                   fin_rv, fin_mean, fin_invstd, fin_scale, fin_shift,
+                                   const_cast<float*>(kshift), stream);
+    return e;
   }
   if ((algo == IG_ALGO_GMULTI64 || algo == IG_ALGO_GMULTI128) && fast && !c8) {
     const bool wide = algo == IG_ALGO_GMULTI128;
@@ -2655,6 +2681,10 @@ KFB_API int kfb_conv_stats_spread() { return IG_SPREAD; }
 // slab workspace needs splits * Ncol * KH*KW*C floats).
 KFB_API int kfb_conv_wgrad_splits(int N, int OH, int OW, int KH, int KW, int C, int Ncol,
                                   int target_blocks) {
+  if ((target_blocks >> 16) == 2) {  // streaming wgrad: stride 1, SAME (OH == H)
+    const int sp = wgrad_s3_splits(N, OH, OW, C, OH, OW, KH, KW, 1, 1, 1, 1, Ncol);
+    if (sp > 0) return sp;
+  }
   return wgrad_split(N * OH * OW, KH * KW * C, Ncol, target_blocks & 0xFFFF, nullptr);
 }
 
@@ -2667,6 +2697,10 @@ KFB_API hipError_t kfb_conv_wgrad(int dtype, const void* dy, const void* x, floa
   // target_blocks bits 16+: kernel (0 = wgrad_k, 1 = wgrad_glds_k where it applies)
   const int algo = target_blocks >> 16;
   target_blocks &= 0xFFFF;
+  // algo 2: the streaming 3x3 64-channel wgrad (conv_stream.hip)
+  if (algo == 2 && wgrad_s3_splits(N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol) > 0)
+    return launch_wgrad_s3(dtype, dy, x, dw, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol,
+                           slab, slab_elems, stream);
   const long dybytes = (long)N * OH * OW * Ncol * 2, xbytes = (long)N * H * W * C * 2;
   WgArgs a{dy, x, dw, N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, KH * KW * C,
            N * OH * OW, 0, (int)(dybytes < (1L << 31) ? dybytes : 0),

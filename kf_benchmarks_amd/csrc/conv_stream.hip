@@ -147,7 +147,10 @@ __global__ void __launch_bounds__(256, 1) conv_s3_k(IgArgs a, Geo g) {
   const int G = gridDim.x, b = blockIdx.x;
   const int t0 = (int)((long)b * g.tiles / G), t1 = (int)((long)(b + 1) * g.tiles / G);
   const int ntile = t1 - t0;
-  if (ntile <= 0) return;  // (workgroup-uniform)
+  if (ntile <= 0) {  // (workgroup-uniform) nothing to compute; still arrives
+    bn_fin_tail(a, (int*)smem);
+    return;
+  }
   const int Qa = g.Qlo + t0 * BM;
   const int halo = g.W1 + 1;    // W + 2: the largest tap shift
   const int Pbase = Qa - halo;  // position of stream index 0
@@ -398,7 +401,7 @@ __global__ void __launch_bounds__(256, 1) conv_s3_k(IgArgs a, Geo g) {
     }
   }
 
-  if (EPI == EPI_ACT || !a.stats) return;
+  if (EPI == EPI_ACT || !a.stats) return;  // (no statistics: no finalize either)
   // reduce the lane sums over the 32 lanes of each half (same channels),
   // then over the 4 waves through LDS (the ring is free now), then one
   // atomic add per channel into statistics slot blockIdx % IG_SPREAD
@@ -435,9 +438,172 @@ __global__ void __launch_bounds__(256, 1) conv_s3_k(IgArgs a, Geo g) {
     for (int w = 0; w < 4; ++w) v += red[(w * 2 + st) * CH + ch];
     atomicAdd(a.stats + ((long)st * IG_SPREAD + b % IG_SPREAD) * CH + ch, v);
   }
+  bn_fin_tail(a, (int*)smem);
 }
 
 }  // namespace s3
+
+// ---------------------------------------------------------------------------
+// Streaming weight gradient of the same 3x3 64 -> 64 conv:
+//   dW[co][tap][ci] = sum_Q dy[Q][co] * x[Q + shift(tap)][ci]
+// over the output positions Q of the padded position space (dy is zero at
+// pad positions: the DMA loads zeros there).  Each persistent workgroup owns
+// a run of 256-position tiles, streams x through the same 640-position ring
+// as the forward kernel and dy tiles through two 32 KB stages, and keeps its
+// whole partial dW (64 x 576 fp32) in accumulators: wave w computes output
+// channels 32 (w & 1) .. +32 x input channels 32 (w >> 1) .. +32 for all 9
+// taps (nine 32x32 tiles, 144 AGPRs).  The reduction index (positions) is
+// the MFMA K: both operands are read column-major with ds_read_b64_tr_b16
+// from [position][channel] images whose 16-byte chunks are swizzled by
+// c ^ 4 ((p >> 1) & 1), which puts any 4 consecutive positions in 4 distinct
+// 64-byte quarters of the bank row (every transposed read conflict-free).
+// The workgroup's partial dW goes to its slab; wgrad_reduce_k-style fixed-
+// order summation folds the slabs into dW (deterministic).
+namespace s3w {
+
+using s3::CH;
+using s3::BM;
+using s3::BLK;
+using s3::NBLK;
+using s3::RING;
+using s3::ROWB;
+typedef __attribute__((ext_vector_type(4))) short v4s;
+typedef s3::v8s v8s;
+typedef s3::v16f v16f;
+
+constexpr int R_BYTES = RING * ROWB;        // 81920
+constexpr int D_BYTES = BM * ROWB;          // 32768 per dy stage
+constexpr int LDS_BYTES = R_BYTES + 2 * D_BYTES;  // 147456
+
+__device__ __forceinline__ int swz(int pos, int chunk) {
+  return pos * ROWB + ((chunk ^ (((pos >> 1) & 1) << 2)) << 4);
+}
+
+__device__ __forceinline__ v4s read_tr(const char* p) {
+  typedef __attribute__((address_space(3))) v4s lds_v4s;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256, 1) wgrad_s3_k(const void* dyp, const void* xp,
+                                                     float* __restrict__ slab, int N, int H,
+                                                     int W, int dybytes, int xbytes, s3::Geo g) {
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+  char* const ring = smem;
+  char* const dys = smem + R_BYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5, l32 = lane & 31;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int t0 = (int)((long)b * g.tiles / G), t1 = (int)((long)(b + 1) * g.tiles / G);
+  const int ntile = t1 - t0;
+  const int Qa = g.Qlo + t0 * BM;
+  const int halo = g.W1 + 1;
+  const int Pbase = Qa - halo;
+  IgArgs a{};  // pix_off reads N, H, W
+  a.N = N;
+  a.H = H;
+  a.W = W;
+
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)xp, (short)0, xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t drs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)dyp, (short)0, dybytes, 0x00020000);
+
+  auto load_block = [&](int blk) {
+    const int slot = blk % NBLK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int sp = blk * BLK + 32 * wid + 8 * i + (lane >> 3);
+      const int po = s3::pix_off(Pbase + sp, g, a);
+      const int off = po < 0 ? -1 : po + (((lane & 7) ^ (((sp >> 1) & 1) << 2)) << 4);
+      s3::dma16(xrs, ring + (slot * BLK + 32 * wid + 8 * i) * ROWB, off);
+    }
+  };
+  auto load_dy = [&](int t, int stage) {
+    const int Q0 = Qa + t * BM;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int u = 64 * wid + 8 * i + (lane >> 3);
+      const int Q = Q0 + u;
+      const int po = Q < g.Qhi ? s3::pix_off(Q, g, a) : -1;
+      const int off = po < 0 ? -1 : po + (((lane & 7) ^ (((u >> 1) & 1) << 2)) << 4);
+      s3::dma16(drs, dys + stage * D_BYTES + (64 * wid + 8 * i) * ROWB, off);
+    }
+  };
+
+  v16f acc[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[k][r] = 0.f;
+
+  if (ntile > 0) {
+    load_block(0);
+    load_block(1);
+    load_block(2);
+    load_dy(0, 0);
+    s3::wait_vm<0>();
+    __syncthreads();
+  }
+  // this lane's part of a transposed read: row q of a 4-row block, columns
+  // 4p .. 4p+3 of its 16-column group gq
+  const int q = (lane & 15) >> 2, pq = lane & 3, gq = (lane >> 4) & 1;
+  const int co_col = 32 * (wid & 1) + 16 * gq + 4 * pq;  // dy column (output channel)
+  const int ci_col = 32 * (wid >> 1) + 16 * gq + 4 * pq;  // x column (input channel)
+  const int co_chunk = co_col >> 3, co_half = (co_col & 7) * 2;   // byte offset in chunk
+  const int ci_chunk = ci_col >> 3, ci_half = (ci_col & 7) * 2;
+
+  for (int t = 0; t < ntile; ++t) {
+    const int st = t & 1;
+    load_block(2 * t + 3);
+    load_block(2 * t + 4);
+    if (t + 1 < ntile) load_dy(t + 1, st ^ 1);
+    const char* dyb = dys + st * D_BYTES;
+    const int sw0 = t * BM + halo;  // stream index of the tile's position 0
+#pragma unroll 2
+    for (int ks = 0; ks < BM / 16; ++ks) {
+      // A: dy^T, rows = positions 16 ks + 8 hh + 4 e + q
+      v8s af;
+      {
+        const int u0 = 16 * ks + 8 * hh + q;
+        const v4s lo = read_tr(dyb + swz(u0, co_chunk) + co_half);
+        const v4s hi = read_tr(dyb + swz(u0 + 4, co_chunk) + co_half);
+        af = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int kh = tap / 3, kw = tap % 3;
+        const int sb = (sw0 + 16 * ks + (kh - 1) * g.W1 + (kw - 1)) % RING;  // wave-uniform
+        unsigned x0 = (unsigned)(sb + 8 * hh + q), x1 = x0 + 4u;
+        x0 = min(x0, x0 - (unsigned)RING);
+        x1 = min(x1, x1 - (unsigned)RING);
+        const v4s lo = read_tr(ring + swz((int)x0, ci_chunk) + ci_half);
+        const v4s hi = read_tr(ring + swz((int)x1, ci_chunk) + ci_half);
+        const v8s bf = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc[tap] = s3::mfma32<T>(af, bf, acc[tap]);
+      }
+    }
+    // this tile's x blocks and the next tile's dy stage landed for every
+    // wave; every wave is done reading blocks 2t, 2t+1 and dy stage st
+    s3::wait_vm<0>();
+    s3::barrier_lds();
+  }
+
+  // partial dW -> slab[b][co][tap][ci] (acc[tap] reg 4gg + r = row co =
+  // 32 (w & 1) + 8 gg + 4 hh + r, column ci = 32 (w >> 1) + l32)
+  float* const out = slab + (long)b * CH * 9 * CH;
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = 32 * (wid & 1) + 8 * (r >> 2) + 4 * hh + (r & 3);
+      out[(co * 9 + tap) * CH + 32 * (wid >> 1) + l32] = acc[tap][r];
+    }
+}
+
+}  // namespace s3w
 
 // Geometry the streaming kernel computes (see file comment).
 static bool s3_geometry(int C, int Ncol, int KH, int KW, int sh, int sw, int pt, int pl, int H,
@@ -514,6 +680,82 @@ hipError_t launch_conv_s3(int dtype, const IgArgs& a, hipStream_t stream) {
     return hipErrorInvalidValue;
   }
 #undef KFB_S3_LAUNCH
+  return hipGetLastError();
+}
+
+}  // namespace kfb
+
+namespace kfb {
+namespace s3w {
+// dw[i] += sum_s slab[s][i] in split order (float4 per thread)
+__global__ void __launch_bounds__(256) reduce_k(const float4* __restrict__ slab,
+                                                float4* __restrict__ dw, int n4, int nsplit) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  float4 acc = dw[i];
+  int sp = 0;
+  for (; sp + 4 <= nsplit; sp += 4) {
+    const float4 v0 = slab[(long)sp * n4 + i], v1 = slab[(long)(sp + 1) * n4 + i];
+    const float4 v2 = slab[(long)(sp + 2) * n4 + i], v3 = slab[(long)(sp + 3) * n4 + i];
+    acc.x += (v0.x + v1.x) + (v2.x + v3.x);
+    acc.y += (v0.y + v1.y) + (v2.y + v3.y);
+    acc.z += (v0.z + v1.z) + (v2.z + v3.z);
+    acc.w += (v0.w + v1.w) + (v2.w + v3.w);
+  }
+  for (; sp < nsplit; ++sp) {
+    const float4 v = slab[(long)sp * n4 + i];
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  dw[i] = acc;
+}
+}  // namespace s3w
+
+static bool s3w_geo(int N, int H, int W, int C, int OH, int OW, int KH, int KW, int sh, int sw,
+                    int pt, int pl, int Ncol, s3::Geo* g) {
+  if (!s3_geometry(C, Ncol, KH, KW, sh, sw, pt, pl, H, W, OH, OW, OH, OW, 1, Ncol)) return false;
+  if ((long)N * (H + 1) * (W + 1) + 4L * s3::BLK >= (1L << 31)) return false;
+  if ((long)N * H * W * C * 2 >= (1L << 31)) return false;
+  g->W1 = W + 1;
+  g->H1 = H + 1;
+  g->fw1 = FastDiv(g->W1);
+  g->fh1 = FastDiv(g->H1);
+  g->Qlo = g->W1;
+  g->Qhi = N * g->H1 * g->W1;
+  g->tiles = (g->Qhi - g->Qlo + s3::BM - 1) / s3::BM;
+  return true;
+}
+
+// Splits (= workgroups, one partial dW slab each) of the streaming wgrad, or
+// 0 off its geometry.
+int wgrad_s3_splits(int N, int H, int W, int C, int OH, int OW, int KH, int KW, int sh, int sw,
+                    int pt, int pl, int Ncol) {
+  s3::Geo g;
+  if (!s3w_geo(N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, &g)) return 0;
+  return s3_grid(g.tiles);
+}
+
+hipError_t launch_wgrad_s3(int dtype, const void* dy, const void* x, float* dw, int N, int H,
+                           int W, int C, int OH, int OW, int KH, int KW, int sh, int sw, int pt,
+                           int pl, int Ncol, float* slab, long slab_elems, hipStream_t stream) {
+  s3::Geo g;
+  if (!s3w_geo(N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, Ncol, &g)) return hipErrorInvalidValue;
+  const int grid = s3_grid(g.tiles);
+  const long per = (long)s3::CH * 9 * s3::CH;
+  if (!slab || (long)grid * per > slab_elems) return hipErrorInvalidValue;
+  const int bytes = (int)((long)N * H * W * C * 2);
+  if (dtype == BF16)
+    hipLaunchKernelGGL((s3w::wgrad_s3_k<bf16>), dim3(grid), dim3(256), 0, stream, dy, x, slab, N,
+                       H, W, bytes, bytes, g);
+  else if (dtype == F16)
+    hipLaunchKernelGGL((s3w::wgrad_s3_k<f16>), dim3(grid), dim3(256), 0, stream, dy, x, slab, N,
+                       H, W, bytes, bytes, g);
+  else
+    return hipErrorInvalidValue;
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int n4 = (int)(per / 4);
+  hipLaunchKernelGGL(s3w::reduce_k, dim3((n4 + 255) / 256), dim3(256), 0, stream,
+                     (const float4*)slab, (float4*)dw, n4, grid);
   return hipGetLastError();
 }
 

@@ -6,6 +6,27 @@
 
 namespace kfb {
 
+// BN forward finalize of a conv whose epilogue accumulated the statistics
+// (counter == null: off): the last workgroup to finish folds the
+// [2][IG_SPREAD][Ncol] slots into mean / invstd, scale / shift, the running
+// statistics and the next step's statistics shift - the work of
+// bn.hip's bn_finalize_stats_k, without its launch
+// (tcb/convnet_builder.py:437-461 batch_norm in training mode).
+struct BnFin {
+  int* counter;  // zeroed with the statistics slots
+  const float* gamma;
+  const float* beta;
+  float* run_mean;
+  float* run_var;
+  float* save_mean;
+  float* save_invstd;
+  float* scale;
+  float* shift;
+  float* kshift;  // the shift the partials are centered on (updated to this mean)
+  float decay, eps;
+  long rows;
+};
+
 struct IgArgs {
   const void* x;  // gathered operand (NHWC [N,H,W,C])
   const void* w;  // [Ncol][Ktot]
@@ -69,13 +90,87 @@ struct IgArgs {
   // written by the BN apply pass, csrc/bn.hip relu_bits) instead of its
   // output y - 1/16 of the bytes for the same test
   int maskbits;
+  BnFin fin;
 };
 
 constexpr int IG_BK = 64;
 constexpr int IG_SPREAD = 32;
 
+// One channel's finalize from its summed partials (double): the math of
+// bn_finalize_stats_k.
+__device__ __forceinline__ void bn_fin_channel(const BnFin& f, int c, double s, double q) {
+  const double n = (double)f.rows;
+  const double k = f.kshift ? (double)f.kshift[c] : 0.0;
+  const double dm = s / n;
+  const double mean = k + dm;
+  double var = q / n - dm * dm;
+  if (var < 0.0) var = 0.0;
+  if (f.kshift) f.kshift[c] = (float)mean;
+  const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+  const float g = f.gamma ? f.gamma[c] : 1.f;
+  const float b = f.beta ? f.beta[c] : 0.f;
+  f.save_mean[c] = (float)mean;
+  f.save_invstd[c] = invstd;
+  f.scale[c] = g * invstd;
+  f.shift[c] = b - (float)mean * g * invstd;
+  if (f.run_mean) {
+    const double unbiased = f.rows > 1 ? var * n / (n - 1.0) : var;
+    f.run_mean[c] = f.run_mean[c] * f.decay + (float)mean * (1.f - f.decay);
+    f.run_var[c] = f.run_var[c] * f.decay + (float)unbiased * (1.f - f.decay);
+  }
+}
+
+// Called once by every workgroup of the launch, at its very end, after its
+// statistics atomics: the last one to arrive finalizes (split-K arrival
+// protocol of the MI355X guide: vmcnt drain, barrier, agent release, ticket;
+// the last arriver's agent acquire, then agent-scope loads of the slots).
+// `flag`: one int of the kernel's LDS (dead by now).
+__device__ __forceinline__ void bn_fin_tail(const IgArgs& a, int* flag) {
+  if (!a.fin.counter || !a.stats) return;  // (uniform)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int total = (int)(gridDim.x * gridDim.y * gridDim.z);
+    const int prev = __hip_atomic_fetch_add(a.fin.counter, 1, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+    *flag = prev == total - 1;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < a.Ncol; c += blockDim.x) {
+    double s = 0.0, q = 0.0;
+    for (int k = 0; k < IG_SPREAD; ++k) {
+      s += __hip_atomic_load(a.stats + (long)k * a.Ncol + c, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      q += __hip_atomic_load(a.stats + (long)(IG_SPREAD + k) * a.Ncol + c, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    }
+    bn_fin_channel(a.fin, c, s, q);
+  }
+}
+
+// bn.hip: the separate finalize launch (kernels without the tail)
+hipError_t bn_finalize_stats_launch(const float* psum, const float* psq, int nslab, int C,
+                                    long rows, const float* gamma, const float* beta, float decay,
+                                    float eps, float* run_mean, float* run_var, float* save_mean,
+                                    float* save_invstd, float* scale, float* shift, float* kshift,
+                                    hipStream_t stream);
+
 // conv_stream.hip: the streaming 3x3 64-channel kernel (IG_ALGO_S3)
 bool conv_s3_fits(const IgArgs& a);
 hipError_t launch_conv_s3(int dtype, const IgArgs& a, hipStream_t stream);
+// ... and its streaming weight gradient (slab per workgroup + fixed-order fold)
+int wgrad_s3_splits(int N, int H, int W, int C, int OH, int OW, int KH, int KW, int sh, int sw,
+                    int pt, int pl, int Ncol);
+hipError_t launch_wgrad_s3(int dtype, const void* dy, const void* x, float* dw, int N, int H,
+                           int W, int C, int OH, int OW, int KH, int KW, int sh, int sw, int pt,
+                           int pl, int Ncol, float* slab, long slab_elems, hipStream_t stream);
 
 }  // namespace kfb

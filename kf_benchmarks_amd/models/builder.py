@@ -189,9 +189,15 @@ class ConvNetBuilder:
             from ..ops import conv_hip
             # partials centered on the BN's previous batch mean (the BN this
             # conv feeds is created under the same scope right below)
-            stats = conv_hip.stats_buffer(num_out_channels, x.device,
-                                          shift=self._peek_bn_layer(name, num_out_channels)
-                                          .stat_shift)
+            bnl = self._peek_bn_layer(name, num_out_channels)
+            stats = conv_hip.stats_buffer(num_out_channels, x.device, shift=bnl.stat_shift)
+            # the plain BN forward (not the dual / fused-pool forms, which
+            # finalize on their own) takes the conv's in-kernel finalize
+            if not (defer_bn and activation is None and residual is None and pool is None) \
+                    and pool is None and not isinstance(residual, F.DeferredBN):
+                conv_hip.attach_bn_finalize(stats, bnl.gamma, bnl.beta, bnl.moving_mean,
+                                            bnl.moving_variance, bnl.decay, bnl.eps,
+                                            bnl.fin_st, bnl.fin_coef)
         layer.stride = (d_height, d_width)
         relu = activation == "relu"
         # conv + bias (+ ReLU) without BN: applied in the conv's epilogue

@@ -133,6 +133,13 @@ class BatchNormLayer(Layer):
         # batch mean; csrc/bn.hip bn_finalize_stats_k) - not a TF variable
         self.register_buffer("stat_shift", torch.zeros(channels, device=device),
                              persistent=False)
+        # the training-mode finalize's outputs (mean | invstd, scale | shift)
+        # when the producing conv's last workgroup computes them
+        # (ops/conv_hip.attach_bn_finalize): persistent, so a launch tape
+        # replays stable addresses
+        self.register_buffer("fin_st", torch.zeros(2, channels, device=device), persistent=False)
+        self.register_buffer("fin_coef", torch.zeros(2 * channels, device=device),
+                             persistent=False)
 
     def tf_variables(self):
         out = {"beta": self.beta.detach(), "moving_mean": self.moving_mean,

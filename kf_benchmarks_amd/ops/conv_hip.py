@@ -22,7 +22,8 @@ import torch
 from . import _native as N
 
 _SIG = ([N.I, N.P, N.P, N.P] + [N.I] * 17 + [N.I, N.P, N.P, N.P, N.P, N.P, N.P]
-        + [N.P, N.I] + [N.I, N.P, N.P])  # ... mcoef, bias, relu, algo, kshift, stream
+        + [N.P, N.I] + [N.I, N.P]  # ... mcoef, bias, relu, algo, kshift
+        + [N.P] * 9 + [N.c_float, N.c_float] + [N.P])  # BN finalize (BnFin), stream
 N.register_optional("kfb_conv_igemm", _SIG)
 N.register_optional("kfb_conv_igemm_fast", [N.I] * 4, N.c_int)
 N.register_optional("kfb_conv_s3_applicable", [N.I] * 12, N.c_int)
@@ -188,7 +189,9 @@ def stats_buffer(channels, device, shift=None):
     """Zeroed [2][STATS_SPREAD][C] fp32 buffer for fused BN partial sums.
     ``shift`` (fp32 [C], the consuming BN's stat_shift): the conv epilogue
     sums y - shift and (y - shift)^2, and the BN finalize undoes it; the
-    buffer carries it (``_kfb_shift``) so producer and consumer agree."""
+    buffer carries it (``_kfb_shift``) so producer and consumer agree.
+    The zeroed 64 floats after it hold the arrival counter of the in-kernel
+    BN finalize (``attach_bn_finalize``)."""
     global _SPREAD_CHECKED
     if not _SPREAD_CHECKED:
         lib_spread = N.query("kfb_conv_stats_spread")
@@ -196,10 +199,39 @@ def stats_buffer(channels, device, shift=None):
             raise N.NativeError("stats spread mismatch: library %d, Python %d"
                                 % (lib_spread, STATS_SPREAD))
         _SPREAD_CHECKED = True
-    buf = STATS_ARENA.take(2 * STATS_SPREAD * channels, device)[:2 * STATS_SPREAD * channels]
+    full = STATS_ARENA.take(2 * STATS_SPREAD * channels + 64, device)
+    buf = full[:2 * STATS_SPREAD * channels]
+    buf._kfb_counter = full[2 * STATS_SPREAD * channels:]
     if shift is not None and _STATS_SHIFT:
         buf._kfb_shift = shift
     return buf
+
+
+# KFB_BN_FIN=0: the consuming BN finalizes with its own launch (A/B switch)
+_BN_FIN = os.environ.get("KFB_BN_FIN", "1") != "0"
+
+
+def attach_bn_finalize(stats, gamma, beta, rm, rv, decay, eps, st, coef):
+    """Asks the conv that fills ``stats`` to also run the consuming BN's
+    finalize in its last workgroup (csrc/igemm_args.h BnFin): mean / invstd
+    into ``st`` [2][C], scale / shift into ``coef`` [2][C], the running
+    statistics and the statistics shift.  The BN forward then sees
+    ``stats._kfb_finalized`` and skips its finalize launch."""
+    if stats is None or not _BN_FIN or not stats.is_cuda:
+        return
+    stats._kfb_fin = (gamma, beta, rm, rv, float(decay), float(eps), st, coef)
+    stats._kfb_finalized = False
+
+
+def _fin_args(stats):
+    fin = getattr(stats, "_kfb_fin", None) if stats is not None else None
+    if fin is None:
+        return (None,) * 9 + (0.0, 0.0)
+    gamma, beta, rm, rv, decay, eps, st, coef = fin
+    C = st.shape[-1]
+    return (stats._kfb_counter.data_ptr(), N.ptr(gamma), N.ptr(beta), N.ptr(rm), N.ptr(rv),
+            st[0].data_ptr(), st[1].data_ptr(), coef[:C].data_ptr(), coef[C:2 * C].data_ptr(),
+            decay, eps)
 
 
 def stats_shift(stats):
@@ -209,9 +241,14 @@ def stats_shift(stats):
 
 def _igemm_call(algo, x, wmat, y, geo, stats=None, mask=None, xbn=None, mean=None, addend=None,
                 mcoef=None, bias=None, relu=False):
+    fin = (None,) * 9 + (0.0, 0.0)
+    if (stats is not None and xbn is None and addend is None and geo[15] == 1
+            and getattr(stats, "_kfb_fin", None) is not None):
+        fin = _fin_args(stats)
+        stats._kfb_finalized = True
     N.call("kfb_conv_igemm", N.dt(x), x.data_ptr(), wmat.data_ptr(), y.data_ptr(), *geo,
            N.ptr(stats), N.ptr(mask), N.ptr(xbn), N.ptr(mean), N.ptr(addend), N.ptr(mcoef),
-           N.ptr(bias), int(relu), algo, N.ptr(stats_shift(stats)), N.stream(x.device))
+           N.ptr(bias), int(relu), algo, N.ptr(stats_shift(stats)), *fin, N.stream(x.device))
 
 
 _TUNE_LOG = os.environ.get("KFB_AUTOTUNE_LOG", "0") == "1"  # print every timed choice
@@ -244,7 +281,8 @@ def _time_candidates(cands, run, rounds=2, reps=3, label=None):
             _ALGO_NAMES.update({v: k for k, v in IG_ALGOS.items()})
         ranked = sorted(best_t.items(), key=lambda kv: kv[1])
         print("[autotune] %s: %s" % (label, "  ".join(
-            "%s %.1f" % ("glds/%d" % (c & 0xFFFF) if c >= (1 << 16) else _ALGO_NAMES.get(c, c),
+            "%s %.1f" % (("s3w" if c >> 16 == 2 else "glds/%d" % (c & 0xFFFF)) if c >= (1 << 16)
+                         else _ALGO_NAMES.get(c, c),
                          1e3 * t / reps) for c, t in ranked)),
             file=sys.stderr, flush=True)
     return best
@@ -425,7 +463,7 @@ def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None, addend=None, wt=None,
 def _wgrad_launch(dy, x, dw, geo, target):
     n, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, cout = geo
     slab, slab_elems = None, 0
-    if _WGRAD_SLAB:
+    if _WGRAD_SLAB or (target >> 16) == 2:  # (the streaming wgrad always folds slabs)
         splits = N.load().kfb_conv_wgrad_splits(n, OH, OW, KH, KW, C, cout, target)
         if splits > 1:
             slab_elems = splits * cout * KH * KW * C
@@ -448,14 +486,21 @@ _WGRAD_ALGO = os.environ.get("KFB_WGRAD_ALGO", "")
 _wgrad_tuned = {}
 
 
+_WGRAD_S3 = 2 << 16  # the streaming 3x3 64-channel wgrad (csrc/conv_stream.hip)
+
+
 def _wgrad_candidates(geo):
-    cout = geo[12]
+    n, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, cout = geo
+    if _WGRAD_ALGO == "s3":
+        return (_WGRAD_S3,)
+    s3 = ((_WGRAD_S3,) if not _NO_S3 and N.load().kfb_conv_s3_applicable(
+        C, cout, KH, KW, sh, sw, pt, pl, H, W, OH, OW) else ())
     glds = tuple(t | _WGRAD_GLDS for t in _WGRAD_CANDIDATES) if cout > 64 else ()
     if _WGRAD_ALGO == "classic" or not glds:
-        return _WGRAD_CANDIDATES
+        return _WGRAD_CANDIDATES + s3
     if _WGRAD_ALGO == "glds":
         return glds
-    return _WGRAD_CANDIDATES + glds
+    return _WGRAD_CANDIDATES + glds + s3
 
 
 def _tune_wgrad(dy, x, dw, geo):

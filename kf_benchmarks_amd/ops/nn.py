@@ -232,17 +232,25 @@ class _BatchNormTrain(torch.autograd.Function):
         C = x.shape[-1]
         rows = x.numel() // C
         dev = x.device
+        fin = None
+        if stats is not None and getattr(stats, "_kfb_finalized", False):
+            # the producing conv's last workgroup already finalized into the
+            # BN layer's persistent st / coef (conv_hip.attach_bn_finalize)
+            fin = stats._kfb_fin
         if stats is not None:  # partial sums from the producing conv's epilogue
             nslab = stats.numel() // (2 * C)
             psum, psq = stats[:nslab * C], stats[nslab * C:]
-            ws = torch.empty((4 * C,), dtype=torch.float32, device=dev)
-            coef = ws[:2 * C]
+            if fin is not None:
+                coef = fin[7]
+            else:
+                ws = torch.empty((4 * C,), dtype=torch.float32, device=dev)
+                coef = ws[:2 * C]
         else:
             nslab = N.query("kfb_bn_num_slabs", rows, C)
             ws = torch.empty((2 * nslab * C + 4 * C,), dtype=torch.float32, device=dev)
             psum, psq = ws[:nslab * C], ws[nslab * C:2 * nslab * C]
             coef = ws[2 * nslab * C:2 * nslab * C + 2 * C]
-        st = torch.empty((2, C), dtype=torch.float32, device=dev)  # mean, invstd
+        st = fin[6] if fin is not None else torch.empty((2, C), dtype=torch.float32, device=dev)
         y = torch.empty_like(x)
         res = residual.contiguous() if residual is not None else None
         rec = relu and residual is None and _MASK_RECOMPUTE
@@ -251,8 +259,8 @@ class _BatchNormTrain(torch.autograd.Function):
                N.ptr(gamma), N.ptr(beta), float(decay), float(eps), N.ptr(rm), N.ptr(rv),
                st[0].data_ptr(), st[1].data_ptr(), coef[:C].data_ptr(),
                coef[C:].data_ptr(), psum.data_ptr(), psq.data_ptr(), nslab, int(relu),
-               int(stats is not None), N.ptr(_conv_hip().stats_shift(stats)), N.ptr(mbits),
-               N.stream(dev))
+               2 if fin is not None else int(stats is not None),
+               N.ptr(_conv_hip().stats_shift(stats)), N.ptr(mbits), N.stream(dev))
         ctx.save_for_backward(x, y if relu else None, gamma, st)
         ctx.relu = relu
         ctx.has_res = residual is not None

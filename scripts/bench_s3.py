@@ -36,7 +36,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--algos", default="onebuf,s3")
-    ap.add_argument("--passes", default="fwd,dgrad")
+    ap.add_argument("--passes", default="fwd,dgrad,wgrad")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     n, H = a.batch, a.hw
@@ -57,13 +57,20 @@ def main():
         "fwd": lambda: conv_hip.conv_fwd(x, w, (1, 1), pads, st.zero_()),
         "dgrad": lambda: conv_hip.conv_dgrad(dy, w, x.shape, (1, 1), pads,
                                              (st.zero_(), bits, xb, mean)),
+        "wgrad": lambda: conv_hip.conv_wgrad(dy, x, (64, 3, 3, 64), (1, 1), pads, out=dwb),
     }
+    dwb = torch.zeros(64, 3, 3, 64, device=dev)
+    sol["wgrad"] = max(2 * act / 6e12, flops / 2.5e15) * 1e6
     passes = {k: v for k, v in passes.items() if k in a.passes.split(",")}
     algos = a.algos.split(",")
     res = {}
     for _ in range(a.rounds):
         for al in algos:
             conv_hip._IG_FORCE = conv_hip.IG_ALGOS[al]
+            # wgrad: the streaming kernel vs the autotuned tiled kernels
+            conv_hip._WGRAD_ALGO = "s3" if al == "s3" else ""
+            conv_hip._NO_S3 = al != "s3"
+            conv_hip._wgrad_tuned.clear()
             for pn, fn in passes.items():
                 res.setdefault((al, pn), []).append(timeit(fn, a.iters))
     conv_hip._IG_FORCE = None

@@ -125,3 +125,34 @@ def test_s3_matches_tiled_kernel_at_resnet_shape(cuda, monkeypatch):
     b = conv_hip.conv_fwd(x, w, (1, 1), pads).float()
     err = (a - b).abs().max().item()
     assert err <= 1e-2 * b.abs().max().item(), err
+
+
+@pytest.fixture
+def s3w(monkeypatch, cuda):
+    from kf_benchmarks_amd.ops import conv_hip
+    monkeypatch.setattr(conv_hip, "_WGRAD_ALGO", "s3")
+    monkeypatch.setattr(conv_hip, "_wgrad_tuned", {})
+    yield
+    N.load().kfb_conv_s3_set_grid(0)
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+@pytest.mark.parametrize("grid", GRIDS)
+def test_s3_wgrad(s3w, cuda, shape, grid):
+    """Streaming weight gradient vs the fp32 reference, and bitwise
+    repeatable (fixed-order slab fold, no atomics)."""
+    from kf_benchmarks_amd.ops import conv_hip
+    N.load().kfb_conv_s3_set_grid(grid)
+    n, H, W = shape
+    g = torch.Generator().manual_seed(11)
+    dt = torch.bfloat16
+    x = torch.randn(n, H, W, 64, generator=g).to(dt)
+    dy = torch.randn(n, H, W, 64, generator=g).to(dt)
+    pads = F.resolve_pads("SAME_RESNET", H, W, 3, 3, 1, 1)
+    wr = torch.zeros(64, 3, 3, 64, requires_grad=True)
+    conv_ops.conv2d_reference(x.float(), wr, (1, 1), pads).backward(dy.float())
+    dw = conv_hip.conv_wgrad(dy.to(cuda), x.to(cuda), (64, 3, 3, 64), (1, 1), pads)
+    ref = wr.grad
+    torch.testing.assert_close(dw.float().cpu(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+    dw2 = conv_hip.conv_wgrad(dy.to(cuda), x.to(cuda), (64, 3, 3, 64), (1, 1), pads)
+    assert torch.equal(dw, dw2)
