@@ -2265,6 +2265,10 @@ __global__ void __launch_bounds__(256) wgrad_reduce_grouped_k(const float* __res
   atomicAdd(dw + i, (a0 + a1) + (a2 + a3));
 }
 
+// kfb_set_deterministic(1): weight-gradient slab folds run in one fixed
+// order (no grouped atomic fold); for bitwise run-to-run comparisons
+static int g_deterministic = 0;
+
 static bool igemm_fast_disabled() {
   static const bool off = getenv("KFB_IGEMM_NOFAST") != nullptr;  // A/B switch
   return off;
@@ -2677,6 +2681,8 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
 
 KFB_API int kfb_conv_stats_spread() { return IG_SPREAD; }
 
+KFB_API void kfb_set_deterministic(int on) { g_deterministic = on ? 1 : 0; }
+
 // Number of reduction splits kfb_conv_wgrad uses for this geometry (the
 // slab workspace needs splits * Ncol * KH*KW*C floats).
 KFB_API int kfb_conv_wgrad_splits(int N, int OH, int OW, int KH, int KW, int C, int Ncol,
@@ -2747,6 +2753,7 @@ KFB_API hipError_t kfb_conv_wgrad(int dtype, const void* dy, const void* x, floa
       long groups = (1024 + blocks - 1) / blocks;
       if (groups < (split + 15) / 16) groups = (split + 15) / 16;
       if (groups > split) groups = split;
+      if (g_deterministic) groups = 1;  // one atomic add per element into zeroed / fixed dW
       hipLaunchKernelGGL(wgrad_reduce_grouped_k, dim3((unsigned)blocks, (unsigned)groups),
                          dim3(256), 0, stream, (const float*)slab, dw, per_split, split);
     }

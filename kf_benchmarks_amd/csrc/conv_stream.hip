@@ -126,13 +126,14 @@ enum { EPI_STATS = 0, EPI_ACT = 1, EPI_DGRAD = 2 };
 template <int EPI>
 __host__ __device__ constexpr int chunk_tap(int q) {
   // tap of the next tile at which chunk q is finished: from tap 1 on; the
-  // dgrad form loads the operands of position subtile j = 0 at the tile start
-  // (chunks 0-3 at taps 2-5) and those of j = 1 after tap 3 (taps 6-8)
-  return EPI == EPI_DGRAD ? (q < 4 ? q + 2 : (q < 7 ? q + 2 : 8)) : q + 1;
+  // dgrad form loads the operands of position subtile j = 0 at the tile
+  // start (chunks 0-3 at taps 2-3) and those of j = 1 after tap 1 (chunks
+  // 4-7 at taps 5-8), each subtile in its own registers
+  return EPI == EPI_DGRAD ? (q < 4 ? 2 + (q >> 1) : q + 1) : q + 1;
 }
 template <int EPI>
 __host__ __device__ constexpr int load_tap(int j) {
-  return j == 0 ? -1 : 3;  // dgrad operands of subtile j issued after this tap
+  return j == 0 ? -1 : 1;  // dgrad operands of subtile j issued after this tap
 }
 
 template <typename T, int EPI, int MASK>
@@ -227,11 +228,10 @@ __global__ void __launch_bounds__(256, 1) conv_s3_k(IgArgs a, Geo g) {
   const int fw = (l32 >> 1) & 7;  // weight-row swizzle of this lane's channel rows
   const char* const wlane = wl + l32 * ROWB;
 
-  // dgrad-form operands of the tile being finished, one position subtile
-  // (4 chunks) at a time: [q & 3]
-  uint4 ad[4], xb[4];
-  unsigned mk[4];
-  uint4 mv[4];
+  // dgrad-form operands of the tile being finished: [position subtile j][q & 3]
+  uint4 ad[2][4], xb[2][4];
+  unsigned mk[2][4];
+  uint4 mv[2][4];
   auto epi_loads = [&](const int (&po)[2], int j) {
     if constexpr (EPI == EPI_DGRAD) {
 #pragma unroll
@@ -239,12 +239,12 @@ __global__ void __launch_bounds__(256, 1) conv_s3_k(IgArgs a, Geo g) {
         const int i = qq >> 1, p = qq & 1;
         const int c = 4 * i + 2 * p + hh;
         const int off = po[j] < 0 ? -1 : po[j] + c * 16;
-        ad[qq] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ars, off, 0, 0));
-        xb[qq] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xbrs, off, 0, 0));
+        ad[j][qq] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ars, off, 0, 0));
+        xb[j][qq] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xbrs, off, 0, 0));
         if constexpr (MASK == 1)
-          mk[qq] = __builtin_amdgcn_raw_buffer_load_b8(mrs, off < 0 ? -1 : off >> 4, 0, 0);
+          mk[j][qq] = __builtin_amdgcn_raw_buffer_load_b8(mrs, off < 0 ? -1 : off >> 4, 0, 0);
         if constexpr (MASK == 2)
-          mv[qq] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(mrs, off, 0, 0));
+          mv[j][qq] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(mrs, off, 0, 0));
       }
     }
   };
@@ -280,13 +280,13 @@ __global__ void __launch_bounds__(256, 1) conv_s3_k(IgArgs a, Geo g) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) ov.v[k] = (T)fmaxf(v[k] + pa[i][p][k], relu_floor);
     } else {
-      const Vec<T, 8> av = __builtin_bit_cast(Vec<T, 8>, ad[q & 3]);
-      const Vec<T, 8> xv = __builtin_bit_cast(Vec<T, 8>, xb[q & 3]);
-      const Vec<T, 8> mvv = __builtin_bit_cast(Vec<T, 8>, mv[q & 3]);
+      const Vec<T, 8> av = __builtin_bit_cast(Vec<T, 8>, ad[q >> 2][q & 3]);
+      const Vec<T, 8> xv = __builtin_bit_cast(Vec<T, 8>, xb[q >> 2][q & 3]);
+      const Vec<T, 8> mvv = __builtin_bit_cast(Vec<T, 8>, mv[q >> 2][q & 3]);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float x = v[k] + (float)av.v[k];
-        if constexpr (MASK == 1) x = keep_if(x, 0u - ((mk[q & 3] >> k) & 1u));
+        if constexpr (MASK == 1) x = keep_if(x, 0u - ((mk[q >> 2][q & 3] >> k) & 1u));
         if constexpr (MASK == 2) x = keep_if(x, 0u - (unsigned)((float)mvv.v[k] > 0.f));
         if constexpr (MASK == 3)
           x = keep_if(x, 0u - (unsigned)((float)xv.v[k] * pb[i][p][k] + pc[i][p][k] > 0.f));

@@ -546,3 +546,67 @@ KFB_API hipError_t kfb_wrelayout(int dtype, const void* src, void* dst, int cout
   });
   return hipGetLastError();
 }
+
+// Strided / shifted window of an NHWC tensor and its adjoint:
+//   adjoint = 0: y[n][oh][ow][c] = x[n][oh*sh + oh0][ow*sw + ow0][c] (0 outside x)
+//   adjoint = 1: dx[n][h][w][c] = dy[n][(h-oh0)/sh][(w-ow0)/sw][c] where that
+//                is an exact, in-range sample (0 elsewhere): the gradient
+// The 1x1 strided average pool of ResNet shortcuts (tcb/convnet_builder.py
+// apool with a 1x1 window) and NASNet's one-pixel shift before its second
+// factorized-reduction path (tcb/models/nasnet_utils.py
+// _factorized_reduction: pad + slice).  V channels per thread.
+template <typename T, int V>
+__global__ void __launch_bounds__(256)
+window_k(const T* __restrict__ src, T* __restrict__ dst, long total, int H, int W, int C,
+         int OH, int OW, int sh, int sw, int oh0, int ow0, int adjoint) {
+  const int CV = C / V;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int cv = (int)(i % CV);
+    long r = i / CV;
+    Vec<T, V> v;
+    bool ok;
+    long so;
+    if (!adjoint) {  // i indexes y [N][OH][OW][CV]
+      const int ow = (int)(r % OW);
+      r /= OW;
+      const int oh = (int)(r % OH);
+      const long n = r / OH;
+      const int h = oh * sh + oh0, w = ow * sw + ow0;
+      ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      so = ((n * H + h) * W + w) * C + (long)cv * V;
+    } else {  // i indexes dx [N][H][W][CV]
+      const int w = (int)(r % W);
+      r /= W;
+      const int h = (int)(r % H);
+      const long n = r / H;
+      const int hh = h - oh0, ww = w - ow0;
+      const int oh = hh / sh, ow = ww / sw;
+      ok = hh >= 0 && ww >= 0 && oh * sh == hh && ow * sw == ww && oh < OH && ow < OW;
+      so = ((n * OH + oh) * OW + ow) * C + (long)cv * V;
+    }
+    if (ok) {
+      v = *(const Vec<T, V>*)(src + so);
+    } else {
+#pragma unroll
+      for (int k = 0; k < V; ++k) v.v[k] = (T)0.f;
+    }
+    *(Vec<T, V>*)(dst + i * V) = v;
+  }
+}
+
+KFB_API hipError_t kfb_window(int dtype, const void* src, void* dst, int N, int H, int W, int C,
+                              int OH, int OW, int sh, int sw, int oh0, int ow0, int adjoint,
+                              hipStream_t stream) {
+  if (sh < 1 || sw < 1) return hipErrorInvalidValue;
+  const int V = (C % 8 == 0 && dtype != F32) ? 8 : (C % 4 == 0 ? 4 : 1);
+  const long total = (long)N * (adjoint ? (long)H * W : (long)OH * OW) * (C / V);
+  if (total == 0) return hipSuccess;
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    KFB_DISPATCH_VEC(V, VV, {
+      hipLaunchKernelGGL((window_k<T, VV>), dim3(egrid(total)), dim3(256), 0, stream,
+                         (const T*)src, (T*)dst, total, H, W, C, OH, OW, sh, sw, oh0, ow0,
+                         adjoint);
+    });
+  });
+  return hipGetLastError();
+}

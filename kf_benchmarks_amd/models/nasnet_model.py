@@ -90,7 +90,8 @@ class _Builder:
                       stddev=_std(1, filters // 2))
         # shift by one pixel (pad bottom/right, drop the first row/col)
         cnn._use(x)
-        x2 = torch.nn.functional.pad(x, (0, 0, 0, 1, 0, 1))[:, 1:, 1:, :].contiguous()
+        from ..ops import nn as F
+        x2 = F.window(x, 1, 1, 1, 1, x.shape[1], x.shape[2])  # pad bottom/right, drop row/col 0
         p2 = cnn.apool(1, 1, stride, stride, input_layer=x2, num_channels_in=x.shape[-1])
         p2 = cnn.conv(filters // 2, 1, 1, input_layer=p2, num_channels_in=x.shape[-1],
                       use_batch_norm=False, bias=None, activation=None,

@@ -28,6 +28,7 @@ N.register_optional("kfb_conv_igemm", _SIG)
 N.register_optional("kfb_conv_igemm_fast", [N.I] * 4, N.c_int)
 N.register_optional("kfb_conv_s3_applicable", [N.I] * 12, N.c_int)
 N.register_optional("kfb_conv_s3_set_grid", [N.I], None)
+N.register_optional("kfb_set_deterministic", [N.I], None)
 
 # igemm kernel choice (csrc/conv_igemm.hip): 1 = register-staged 128-tile
 # igemm_k, 2 = LDS-DMA ring igemm_glds_k (FAST geometries only).
@@ -465,7 +466,7 @@ def _wgrad_launch(dy, x, dw, geo, target):
     slab, slab_elems = None, 0
     if _WGRAD_SLAB or (target >> 16) == 2:  # (the streaming wgrad always folds slabs)
         splits = N.load().kfb_conv_wgrad_splits(n, OH, OW, KH, KW, C, cout, target)
-        if splits > 1:
+        if splits > 1 or (target >> 16) == 2:
             slab_elems = splits * cout * KH * KW * C
             slab = torch.empty((slab_elems,), dtype=torch.float32, device=x.device)
     N.call("kfb_conv_wgrad", N.dt(x), dy.data_ptr(), x.data_ptr(), dw.data_ptr(), n, H, W, C, OH,

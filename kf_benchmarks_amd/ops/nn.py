@@ -866,10 +866,8 @@ def bn_relu_max_pool(x, gamma, beta, running_mean, running_var, decay, eps, stat
 def pool_takes_link(x, kh, kw, sh, sw, mode, kind):
     """True if max_pool / avg_pool of x runs the pool autograd Function
     (which follows the BNLink protocol) rather than a CPU or subsample path."""
-    if not _on_gpu(x):
-        return False
-    pads = pool_geometry(x.shape, kh, kw, sh, sw, mode)[0]
-    return not (kind == "avg" and kh == 1 and kw == 1 and pads == (0, 0, 0, 0))
+    # (the 1x1 subsample's native window op follows the protocol too)
+    return _on_gpu(x)
 
 
 def max_pool(x, kh, kw, sh, sw, mode="VALID"):
@@ -879,13 +877,53 @@ def max_pool(x, kh, kw, sh, sw, mode="VALID"):
     return _MaxPool.apply(x, kh, kw, sh, sw, pads, OH, OW)
 
 
+N.register_optional("kfb_window", [N.I, N.P, N.P] + [N.I] * 11 + [N.P])
+
+
+class _Window(torch.autograd.Function):
+    """y[n, oh, ow] = x[n, oh*sh + oh0, ow*sw + ow0] (zero outside x), one
+    native kernel each way (csrc/elementwise.hip window_k); its input
+    gradient follows the BNLink protocol like a pool's."""
+
+    @staticmethod
+    def forward(ctx, x, sh, sw, oh0, ow0, OH, OW):
+        x = x.contiguous()
+        n, H, W, C = x.shape
+        y = torch.empty((n, OH, OW, C), dtype=x.dtype, device=x.device)
+        N.call("kfb_window", N.dt(x), x.data_ptr(), y.data_ptr(), n, H, W, C, OH, OW, sh, sw,
+               oh0, ow0, 0, N.stream(x.device))
+        ctx.geo = (n, H, W, C, OH, OW, sh, sw, oh0, ow0)
+        ctx.link = getattr(x, "_kfb_bn_link", None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, H, W, C, OH, OW, sh, sw, oh0, ow0 = ctx.geo
+        dy = dy.contiguous()
+        dx = torch.empty((n, H, W, C), dtype=dy.dtype, device=dy.device)
+        N.call("kfb_window", N.dt(dy), dy.data_ptr(), dx.data_ptr(), n, H, W, C, OH, OW, sh, sw,
+               oh0, ow0, 1, N.stream(dy.device))
+        return _pool_link_grad(ctx.link, dx), None, None, None, None, None, None
+
+
+def window(x, sh, sw, oh0, ow0, OH, OW):
+    """Strided / shifted window of an NHWC tensor (see _Window)."""
+    if not _on_gpu(x):
+        n, H, W, C = x.shape
+        xp = torch.nn.functional.pad(x, (0, 0, 0, max(0, (OW - 1) * sw + ow0 + 1 - W),
+                                         0, max(0, (OH - 1) * sh + oh0 + 1 - H)))
+        return xp[:, oh0:oh0 + (OH - 1) * sh + 1:sh, ow0:ow0 + (OW - 1) * sw + 1:sw, :] \
+            .contiguous()
+    return _Window.apply(x, sh, sw, oh0, ow0, OH, OW)
+
+
 def avg_pool(x, kh, kw, sh, sw, mode="VALID"):
     pads, OH, OW = pool_geometry(x.shape, kh, kw, sh, sw, mode)
     if not _on_gpu(x):
         return _pool_cpu(x, kh, kw, sh, sw, pads, "avg")
     if kh == 1 and kw == 1 and pads == (0, 0, 0, 0):
-        # 1x1 average pool == strided subsample (ResNet v1 shortcut).
-        return x[:, ::sh, ::sw, :].contiguous()
+        # 1x1 average pool == strided subsample (ResNet v1 shortcut)
+        return window(x, sh, sw, 0, 0, OH, OW)
     return _AvgPool.apply(x, kh, kw, sh, sw, pads, OH, OW)
 
 

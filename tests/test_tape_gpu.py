@@ -132,10 +132,12 @@ def _run_exact(tape, steps=6, bs=4):
 
 
 def _same(a, b):
-    """Names of the state entries that differ (bitwise)."""
+    """Names of the state entries that differ (bitwise; the reported losses
+    to 1e-6 relative: a replayed step's total loss adds the L2 term on the
+    host, in a different order than the eager step)."""
     bad = []
-    if a["losses"] != b["losses"]:
-        bad.append("losses")
+    if any(abs(x - y) > 1e-6 * max(1.0, abs(y)) for x, y in zip(a["losses"], b["losses"])):
+        bad.append("losses %s vs %s" % (a["losses"], b["losses"]))
     if not torch.equal(a["w"], b["w"]):
         bad.append("weights")
     for k in a["bufs"]:
@@ -149,8 +151,12 @@ def _same(a, b):
 
 @pytest.fixture
 def _deterministic(monkeypatch):
+    from kf_benchmarks_amd.ops import _native as N
     from kf_benchmarks_amd.ops import conv_hip
     monkeypatch.setattr(conv_hip, "_NO_S3", True)
+    N.load().kfb_set_deterministic(1)  # fixed-order weight-gradient folds
+    yield
+    N.load().kfb_set_deterministic(0)
 
 
 def test_tape_bitwise_matches_eager(cuda, _deterministic):
