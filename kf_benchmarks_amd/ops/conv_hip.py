@@ -208,8 +208,19 @@ def stats_buffer(channels, device, shift=None):
     return buf
 
 
-# KFB_BN_FIN=0: the consuming BN finalizes with its own launch (A/B switch)
-_BN_FIN = os.environ.get("KFB_BN_FIN", "1") != "0"
+# In-kernel BN finalize (attach_bn_finalize): KFB_BN_FIN=1 in every igemm
+# kernel, "persistent" (default) only in the persistent streaming kernel,
+# 0 never.  Every workgroup of a kernel with the tail drains its stores
+# before its arrival ticket; on the one-tile kernels (thousands of short
+# workgroups) that drain costs more than the finalize launch it saves
+# (ResNet-50 bs256: 19.64-19.70 vs 19.45-19.50 ms/step, gpurun_out/r9d),
+# in a persistent kernel it is one drain per CU.
+_BN_FIN_MODE = os.environ.get("KFB_BN_FIN", "persistent")
+_BN_FIN = _BN_FIN_MODE != "0"
+# KFB_S3_DGRAD=0: the streaming 3x3 kernel for forward convs only (its dgrad
+# form runs beside the weight-gradient side stream, which can hold CUs its
+# one-workgroup-per-CU grid waits for)
+_S3_DGRAD = os.environ.get("KFB_S3_DGRAD", "1") != "0"
 
 
 def attach_bn_finalize(stats, gamma, beta, rm, rv, decay, eps, st, coef):
@@ -244,7 +255,8 @@ def _igemm_call(algo, x, wmat, y, geo, stats=None, mask=None, xbn=None, mean=Non
                 mcoef=None, bias=None, relu=False):
     fin = (None,) * 9 + (0.0, 0.0)
     if (stats is not None and xbn is None and addend is None and geo[15] == 1
-            and getattr(stats, "_kfb_fin", None) is not None):
+            and getattr(stats, "_kfb_fin", None) is not None
+            and (_BN_FIN_MODE == "1" or algo == IG_S3)):
         fin = _fin_args(stats)
         stats._kfb_finalized = True
     N.call("kfb_conv_igemm", N.dt(x), x.data_ptr(), wmat.data_ptr(), y.data_ptr(), *geo,
@@ -348,7 +360,8 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
         cands += (IG_DB,)
     if fast and _EARLY_EPI and (xbn is not None or addend is not None):
         cands += (IG_ONEBUF_N64_E, IG_CLASSIC_N64_E)
-    if fast and not _NO_S3 and N.load().kfb_conv_s3_applicable(
+    if fast and not _NO_S3 and (_S3_DGRAD or (xbn is None and addend is None)) \
+            and N.load().kfb_conv_s3_applicable(
             C, ncol, KH, KW, geo[8], geo[9], geo[10], geo[11], geo[1], geo[2], geo[4], geo[5]) \
             and geo[13] == geo[4] and geo[14] == geo[5] and geo[15] == 1 and geo[16] == ncol:
         cands += (IG_S3,)

@@ -30,6 +30,7 @@ CASES = [
 def test_conv_finalizes_bn(cuda, monkeypatch, case):
     (n, H, W, cin, cout, kh, kw), algo = case
     monkeypatch.setattr(conv_hip, "_IG_FORCE", conv_hip.IG_ALGOS[algo])
+    monkeypatch.setattr(conv_hip, "_BN_FIN_MODE", "1")
     g = torch.Generator().manual_seed(4)
     x = torch.randn(n, H, W, cin, generator=g).to(torch.bfloat16).to(cuda)
     w = (torch.randn(cout, kh, kw, cin, generator=g) / (kh * kw * cin) ** 0.5).to(torch.bfloat16)
@@ -79,6 +80,7 @@ def test_resnet_trains_same_with_in_kernel_finalize(cuda, monkeypatch):
 
     def run(fin):
         monkeypatch.setattr(conv_hip, "_BN_FIN", fin)
+        monkeypatch.setattr(conv_hip, "_BN_FIN_MODE", "1" if fin else "0")
         p = P.make_params(model="resnet50", batch_size=8, num_gpus=1, use_bf16=True,
                           optimizer="momentum", data_format="NHWC", variable_update="kungfu",
                           init_learning_rate=0.002, display_every=10 ** 9)
