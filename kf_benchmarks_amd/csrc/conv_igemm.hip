@@ -2510,7 +2510,7 @@ enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_G
        IG_ALGO_GENERIC = 21, IG_ALGO_SK128 = 22, IG_ALGO_G8P = 23, IG_ALGO_ONEBUF_E = 24,
        IG_ALGO_ONEBUF_N64_E = 25, IG_ALGO_CLASSIC_N64_E = 26, IG_ALGO_DB = 27,
        IG_ALGO_GBIG256_32 = 28, IG_ALGO_GSHORT128_32 = 29, IG_ALGO_GSHORT64_32 = 30,
-       IG_ALGO_S3 = 31 };
+       IG_ALGO_S3 = 31, IG_ALGO_S1 = 32 };
 
 static bool c8_geometry(int C, int KH, int KW) {
   return C == 8 && (KW == 1 || KW == 2 || KW == 4 || KW == 8) && (KH * KW) % 8 == 0;
@@ -2580,6 +2580,8 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
   // IG_ALGO_S3: the streaming 3x3 64-channel kernel (conv_stream.hip); off
   // its geometry the default kernel below runs
   if (algo == IG_ALGO_S3 && fast && !c8 && conv_s3_fits(a)) return launch_conv_s3(dtype, a, stream);
+  // IG_ALGO_S1: the streaming 1x1 64 -> 256-channel kernel (conv_s1.hip)
+  if (algo == IG_ALGO_S1 && fast && !c8 && conv_s1_fits(a)) return launch_conv_s1(dtype, a, stream);
   if ((algo == IG_ALGO_TALL512 || algo == IG_ALGO_TALL256) && fast) {
     if (dtype == BF16) launch_glds_tall<bf16>(a, algo == IG_ALGO_TALL512, stream);
     else if (dtype == F16) launch_glds_tall<f16>(a, algo == IG_ALGO_TALL512, stream);

@@ -167,7 +167,10 @@ hipError_t bn_finalize_stats_launch(const float* psum, const float* psq, int nsl
 // conv_stream.hip: the streaming 3x3 64-channel kernel (IG_ALGO_S3)
 bool conv_s3_fits(const IgArgs& a);
 hipError_t launch_conv_s3(int dtype, const IgArgs& a, hipStream_t stream);
-// ... and its streaming weight gradient (slab per workgroup + fixed-order fold)
+// conv_s1.hip: the streaming 1x1 64 -> 256-channel kernel (IG_ALGO_S1)
+bool conv_s1_fits(const IgArgs& a);
+hipError_t launch_conv_s1(int dtype, const IgArgs& a, hipStream_t stream);
+// conv_stream.hip: the streaming 3x3 kernel's streaming weight gradient (slab per workgroup + fixed-order fold)
 int wgrad_s3_splits(int N, int H, int W, int C, int OH, int OW, int KH, int KW, int sh, int sw,
                     int pt, int pl, int Ncol);
 hipError_t launch_wgrad_s3(int dtype, const void* dy, const void* x, float* dw, int N, int H,

@@ -1,0 +1,144 @@
+"""Streaming 1x1 K -> 4K-channel conv kernel (csrc/conv_s1.hip, IG_ALGO_S1,
+K = 64 .. 512) vs a PyTorch fp32 reference: forward with the (shifted)
+BN-statistics epilogue and the in-kernel BN finalize, and the 4K <- K data
+gradient with the producer BN's fused backward epilogue (ReLU bit mask,
+addend, partial sums) - at pixel counts that leave a partial last tile, and
+with the grid forced small so every workgroup streams many tiles through its
+LDS ring (and, for K >= 128, several channel slices share a pixel run)."""
+
+import pytest
+import torch
+
+from kf_benchmarks_amd.ops import _native as N
+from kf_benchmarks_amd.ops import conv_hip
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(2, 14, 14), (3, 9, 11), (4, 56, 56), (1, 5, 3)]
+GRIDS = [0, 7, 1]
+KS = [64, 128, 256, 512]
+
+
+@pytest.fixture
+def s1(monkeypatch, cuda):
+    monkeypatch.setattr(conv_hip, "_IG_FORCE", conv_hip.IG_S1)
+    yield
+    N.load().kfb_conv_s1_set_grid(0)
+
+
+def test_s1_applicability():
+    lib = N.load()
+    assert lib.kfb_conv_s1_applicable(64, 256, 1, 1, 1, 1, 0, 0, 56, 56, 56, 56) == 1
+    assert lib.kfb_conv_s1_applicable(64, 128, 1, 1, 1, 1, 0, 0, 56, 56, 56, 56) == 0
+    assert lib.kfb_conv_s1_applicable(128, 512, 1, 1, 1, 1, 0, 0, 28, 28, 28, 28) == 1
+    assert lib.kfb_conv_s1_applicable(256, 1024, 1, 1, 1, 1, 0, 0, 14, 14, 14, 14) == 1
+    assert lib.kfb_conv_s1_applicable(512, 2048, 1, 1, 1, 1, 0, 0, 7, 7, 7, 7) == 1
+    assert lib.kfb_conv_s1_applicable(96, 384, 1, 1, 1, 1, 0, 0, 56, 56, 56, 56) == 0
+    assert lib.kfb_conv_s1_applicable(64, 256, 1, 1, 2, 2, 0, 0, 56, 56, 28, 28) == 0
+
+
+def _bits(y):
+    b = (y.float().reshape(-1, 8) > 0).to(torch.int32)
+    return (b * (1 << torch.arange(8, dtype=torch.int32))).sum(1).to(torch.uint8)
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+@pytest.mark.parametrize("grid", GRIDS)
+@pytest.mark.parametrize("K", KS)
+def test_s1_fwd_stats(s1, cuda, shape, grid, K):
+    N.load().kfb_conv_s1_set_grid(grid)
+    n, H, W = shape
+    C = 4 * K
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(n, H, W, K, generator=g).to(torch.bfloat16)
+    w = (torch.randn(C, 1, 1, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    shift = torch.randn(C, generator=g) * 0.3
+    ref = x.float().reshape(-1, K) @ w.float().reshape(C, K).t()
+    st = conv_hip.stats_buffer(C, cuda, shift=shift.to(cuda)).zero_()
+    y = conv_hip.conv_fwd(x.to(cuda), w.to(cuda), (1, 1), (0, 0, 0, 0), st)
+    yf = y.float().cpu().reshape(-1, C)
+    torch.testing.assert_close(yf, ref, rtol=2e-2, atol=2e-2)
+    p = st.view(2, conv_hip.STATS_SPREAD, C).sum(1).cpu()
+    d = yf - shift
+    tol = 4e-3 * (d.abs() + d * d).sum(0).max().item()
+    torch.testing.assert_close(p[0], d.sum(0), rtol=1e-2, atol=tol)
+    torch.testing.assert_close(p[1], (d * d).sum(0), rtol=1e-2, atol=tol)
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+@pytest.mark.parametrize("mask_src", ["bits", "none"])
+@pytest.mark.parametrize("with_addend", [False, True])
+@pytest.mark.parametrize("grid", [0, 5, 17])
+@pytest.mark.parametrize("K", KS)
+def test_s1_dgrad_fused_epilogue(s1, cuda, shape, mask_src, with_addend, grid, K):
+    N.load().kfb_conv_s1_set_grid(grid)
+    n, H, W = shape
+    C = 4 * K
+    g = torch.Generator().manual_seed(5)
+    dt = torch.bfloat16
+    # the 1x1 conv C -> K whose data gradient this is: dX[C] = dY[K] W
+    w = (torch.randn(K, 1, 1, C, generator=g) / K ** 0.5).to(dt)
+    dy = torch.randn(n, H, W, K, generator=g).to(dt)
+    xb = torch.randn(n, H, W, C, generator=g).to(dt)
+    mean = torch.randn(C, generator=g)
+    x = torch.randn(n, H, W, C, generator=g).to(dt)
+    add = torch.randn(n, H, W, C, generator=g).to(dt) if with_addend else None
+    r = (dy.float().reshape(-1, K) @ w.float().reshape(K, C)).reshape(n, H, W, C)
+    if add is not None:
+        r = r + add.float()
+    if mask_src == "bits":
+        r = r * (x.float() > 0)
+    parts = conv_hip.stats_buffer(C, cuda).zero_()
+    fuse = (parts, _bits(x).to(cuda) if mask_src == "bits" else None, xb.to(cuda), mean.to(cuda))
+    dx = conv_hip.conv_dgrad(dy.to(cuda), w.to(cuda), x.shape, (1, 1), (0, 0, 0, 0), fuse,
+                             addend=add.to(cuda) if add is not None else None)
+    torch.testing.assert_close(dx.float().cpu(), r, rtol=3e-2, atol=3e-2)
+    p = parts.view(2, conv_hip.STATS_SPREAD, C).sum(1).cpu()
+    o = dx.float().cpu()
+    s1_ = o.sum((0, 1, 2))
+    s2_ = (o * (xb.float() - mean)).sum((0, 1, 2))
+    tol = 4e-3 * (o.abs() * (1 + (xb.float() - mean).abs())).sum((0, 1, 2)).max().item()
+    torch.testing.assert_close(p[0], s1_, rtol=1e-2, atol=tol)
+    torch.testing.assert_close(p[1], s2_, rtol=1e-2, atol=tol)
+
+
+def test_s1_finalizes_bn(s1, cuda):
+    n, H, W = 8, 28, 28
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(n, H, W, 64, generator=g).to(torch.bfloat16).to(cuda)
+    w = (torch.randn(256, 1, 1, 64, generator=g) / 8.0).to(torch.bfloat16).to(cuda)
+    gamma = (torch.rand(256, generator=g) + 0.5).to(cuda)
+    beta = torch.randn(256, generator=g).to(cuda)
+    kshift = (torch.randn(256, generator=g) * 0.1).to(cuda)
+    rm0, rv0 = torch.zeros(256, device=cuda), torch.ones(256, device=cuda)
+    rm, rv = rm0.clone(), rv0.clone()
+    st = torch.zeros(2, 256, device=cuda)
+    coef = torch.zeros(512, device=cuda)
+    stats = conv_hip.stats_buffer(256, cuda, shift=kshift).zero_()
+    stats._kfb_counter.zero_()
+    conv_hip.attach_bn_finalize(stats, gamma, beta, rm, rv, 0.9, 1e-3, st, coef)
+    y = conv_hip.conv_fwd(x, w, (1, 1), (0, 0, 0, 0), stats)
+    torch.cuda.synchronize()
+    assert stats._kfb_finalized
+    yd = y.double().reshape(-1, 256)
+    mean, var = yd.mean(0), yd.var(0, unbiased=False)
+    invstd = 1.0 / torch.sqrt(var + 1e-3)
+    torch.testing.assert_close(st[0].double(), mean, rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(st[1].double(), invstd, rtol=5e-3, atol=5e-3)
+    torch.testing.assert_close(coef[:256].double(), gamma.double() * invstd, rtol=5e-3, atol=5e-3)
+    torch.testing.assert_close(kshift.double(), mean, rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(rm.double(), mean * 0.1, rtol=2e-3, atol=2e-3)
+
+
+def test_s1_matches_tiled_kernel_at_resnet_shape(cuda, monkeypatch):
+    """ResNet-50 conv2_x expand shape at batch 32: the streaming kernel and
+    the tiled kernel agree to bf16 output rounding."""
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(32, 56, 56, 64, generator=g).to(torch.bfloat16).to(cuda)
+    w = (torch.randn(256, 1, 1, 64, generator=g) / 8.0).to(torch.bfloat16).to(cuda)
+    monkeypatch.setattr(conv_hip, "_IG_FORCE", conv_hip.IG_S1)
+    a = conv_hip.conv_fwd(x, w, (1, 1), (0, 0, 0, 0)).float()
+    monkeypatch.setattr(conv_hip, "_IG_FORCE", conv_hip.IG_ONEBUF)
+    b = conv_hip.conv_fwd(x, w, (1, 1), (0, 0, 0, 0)).float()
+    err = (a - b).abs().max().item()
+    assert err <= 1e-2 * b.abs().max().item(), err
