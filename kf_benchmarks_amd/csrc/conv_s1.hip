@@ -29,6 +29,7 @@
 #include "common.h"
 #include "igemm_args.h"
 
+#include <cstdlib>
 #include <mutex>
 
 namespace kfb {
@@ -43,8 +44,9 @@ constexpr int LDS_CAP = 160 * 1024;  // per CU
 
 enum { EPI_STATS = 0, EPI_DGRAD = 2 };
 
-// per input-channel count K: WCH channels per wave (4 waves along channels)
-template <int K, int EPI>
+// per input-channel count K: WCH channels per wave (4 waves along channels);
+// WPC workgroups per CU share its LDS
+template <int K, int EPI, int WPC>
 struct Cfg {
   static constexpr int WCH = K <= 128 ? 64 : 32;
   static constexpr int NS = 4 * WCH;            // channels per workgroup
@@ -63,7 +65,7 @@ struct Cfg {
   static constexpr int YD = YB / 4096;          // per epilogue operand per wave
   static constexpr bool DG = EPI == EPI_DGRAD;
   static constexpr int STB = XB + (DG ? 2 * YB + MBA : 0);  // ring stage
-  static constexpr int NST0 = LDS_CAP / STB;
+  static constexpr int NST0 = LDS_CAP / WPC / STB;
   static constexpr int NST = NST0 > 7 ? 7 : NST0;
   static constexpr int D = NST - 1;             // prefetch distance (tiles)
   static constexpr int DMAS = XD + (DG ? 2 * YD + 1 : 0);  // DMAs per wave per tile
@@ -71,7 +73,7 @@ struct Cfg {
   static constexpr int WAIT = ST * D + (D - 1) * DMAS;
   static_assert(XD >= 1 && (!DG || YD >= 1), "tile split");
   static_assert(MB <= MBA, "bits area");
-  static_assert(D >= 2 && WAIT < 64, "pipeline depth");
+  static_assert(D >= 1 && WAIT < 64, "pipeline depth");
 };
 
 template <int N>
@@ -117,9 +119,9 @@ __device__ __forceinline__ int xsw(int p) {
 }
 
 // MASK (EPI_DGRAD): 0 none, 1 the producer BN's ReLU bit mask
-template <typename T, int K, int EPI, int MASK>
-__global__ void __launch_bounds__(256, 1) conv_s1_k(IgArgs a, int tiles, int nsl) {
-  using C = Cfg<K, EPI>;
+template <typename T, int K, int EPI, int MASK, int WPC>
+__global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int nsl) {
+  using C = Cfg<K, EPI, WPC>;
   constexpr int NS = C::NS, CT = C::CT, KS = C::KS, D = C::D, NST = C::NST;
   constexpr int STB = C::STB;
   __shared__ __attribute__((aligned(16))) char ring[NST * STB];
@@ -400,7 +402,20 @@ bool conv_s1_fits(const IgArgs& a) {
 
 static int g_s1_grid_force = 0;  // test hook: workgroups per launch (0 = one per CU)
 
-static int s1_grid(int tiles, int nsl) {
+// workgroups per CU: 2 where two fit (LDS ring and registers: the variants
+// below 256 VGPR + AGPR at one workgroup per CU) - the second workgroup's
+// waves hide the first's MFMA / LDS / epilogue latencies, which one wave per
+// SIMD leaves exposed; KFB_S1_WPC=1 forces one
+static int s1_wpc(int K, bool dg) {
+  static const int force = [] {
+    const char* e = getenv("KFB_S1_WPC");
+    return e ? atoi(e) : 0;
+  }();
+  const bool two = dg ? (K == 64 || K == 256) : (K <= 256);
+  return (force == 1 || !two) ? 1 : 2;
+}
+
+static int s1_grid(int tiles, int nsl, int wpc) {
   static std::once_flag once;
   static int cus = 256;
   std::call_once(once, [] {
@@ -412,7 +427,7 @@ static int s1_grid(int tiles, int nsl) {
         cus = n;
     }
   });
-  int g = g_s1_grid_force > 0 ? g_s1_grid_force : cus;
+  int g = g_s1_grid_force > 0 ? g_s1_grid_force : cus * wpc;
   // whole pixel groups (one workgroup per slice each), at most one tile each
   int groups = g / nsl;
   if (groups > tiles) groups = tiles;
@@ -420,18 +435,39 @@ static int s1_grid(int tiles, int nsl) {
   return groups * nsl;
 }
 
+template <typename T, int K, int WPC>
+static void launch_s1_w(const IgArgs& a, int tiles, int nsl, bool dg, int mask, hipStream_t s) {
+  const int grid = s1_grid(tiles, nsl, WPC);
+  if (!dg)
+    hipLaunchKernelGGL((s1::conv_s1_k<T, K, s1::EPI_STATS, 0, WPC>), dim3(grid), dim3(256), 0, s,
+                       a, tiles, nsl);
+  else if (mask)
+    hipLaunchKernelGGL((s1::conv_s1_k<T, K, s1::EPI_DGRAD, 1, WPC>), dim3(grid), dim3(256), 0, s,
+                       a, tiles, nsl);
+  else
+    hipLaunchKernelGGL((s1::conv_s1_k<T, K, s1::EPI_DGRAD, 0, WPC>), dim3(grid), dim3(256), 0, s,
+                       a, tiles, nsl);
+}
+
 template <typename T, int K>
 static void launch_s1(const IgArgs& a, int tiles, int nsl, bool dg, int mask, hipStream_t s) {
-  const int grid = s1_grid(tiles, nsl);
-  if (!dg)
-    hipLaunchKernelGGL((s1::conv_s1_k<T, K, s1::EPI_STATS, 0>), dim3(grid), dim3(256), 0, s, a,
-                       tiles, nsl);
-  else if (mask)
-    hipLaunchKernelGGL((s1::conv_s1_k<T, K, s1::EPI_DGRAD, 1>), dim3(grid), dim3(256), 0, s, a,
-                       tiles, nsl);
-  else
-    hipLaunchKernelGGL((s1::conv_s1_k<T, K, s1::EPI_DGRAD, 0>), dim3(grid), dim3(256), 0, s, a,
-                       tiles, nsl);
+  if (s1_wpc(K, dg) == 2) {
+    if constexpr (K <= 256) {
+      if (!dg)
+        hipLaunchKernelGGL((s1::conv_s1_k<T, K, s1::EPI_STATS, 0, 2>),
+                           dim3(s1_grid(tiles, nsl, 2)), dim3(256), 0, s, a, tiles, nsl);
+      else if constexpr (K != 128) {
+        if (mask)
+          hipLaunchKernelGGL((s1::conv_s1_k<T, K, s1::EPI_DGRAD, 1, 2>),
+                             dim3(s1_grid(tiles, nsl, 2)), dim3(256), 0, s, a, tiles, nsl);
+        else
+          hipLaunchKernelGGL((s1::conv_s1_k<T, K, s1::EPI_DGRAD, 0, 2>),
+                             dim3(s1_grid(tiles, nsl, 2)), dim3(256), 0, s, a, tiles, nsl);
+      }
+      return;
+    }
+  }
+  launch_s1_w<T, K, 1>(a, tiles, nsl, dg, mask, s);
 }
 
 template <typename T>
