@@ -1133,6 +1133,17 @@ hipError_t bn_finalize_stats_launch(const float* psum, const float* psq, int nsl
                      save_invstd, scale, shift, kshift);
   return hipGetLastError();
 }
+
+hipError_t bn_finalize_grad_launch(const float* slots, int C, long rows, const float* gamma,
+                                   const float* mean, const float* invstd, float* dgamma,
+                                   float* dbeta, float* coefA, float* coefB, float* coefC,
+                                   int accumulate, hipStream_t stream) {
+  constexpr int NSLOT = 32;  // IG_SPREAD
+  hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, slots,
+                     slots + (long)NSLOT * C, NSLOT, C, rows, gamma, mean, invstd, dgamma, dbeta,
+                     coefA, coefB, coefC, accumulate);
+  return hipGetLastError();
+}
 }  // namespace kfb
 
 KFB_API int kfb_bn_num_slabs(long rows, int C) {
@@ -1277,9 +1288,10 @@ KFB_API hipError_t kfb_bn_bwd(int dtype, const void* dy, const void* y, const vo
         hipLaunchKernelGGL((bn_partial_grad_k<T, VV, false>), grid, dim3(BN_THREADS), lds,
                            stream, (const T*)dy, (const T*)y, (const T*)x, save_mean, rows, C,
                            g.cw, g.tpr, g.rpi, slab_rows, pdy, pdyx);
-      hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, pdy,
-                         pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta,
-                         coefA, coefB, coefC, accumulate);
+      if (have_partials != 2)  // 2: the producing dgrad's last workgroup finalized (BnGFin)
+        hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,
+                           pdy, pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta,
+                           coefA, coefB, coefC, accumulate);
       const long nvec = rows * C / VV;
       const int gb = stream_grid(nvec);
       if (relu) {

@@ -2552,7 +2552,17 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
            (stats && !xbn && !addend) ? kshift : nullptr,
            FastDiv(C), FastDiv(KW), FastDiv(sh), FastDiv(sw), zfill, 0, 0,
            (mask && ((flags >> 2) & 1)) ? 1 : 0};
-  if (fin_counter) {
+  // With a dgrad-style epilogue (xbn != null) the fin_* arguments carry the
+  // producer BN's backward finalize instead (BnGFin): fin_gamma = gamma,
+  // fin_invstd = its saved invstd, fin_rm / fin_rv = dgamma / dbeta,
+  // fin_scale / fin_shift / fin_mean = coefA / coefB / coefC, fin_decay != 0:
+  // accumulate into dgamma / dbeta.
+  const bool gfin = fin_counter && xbn;
+  if (gfin) {
+    if (!stats || ys != 1) return hipErrorInvalidValue;
+    a.gfin = BnGFin{fin_counter, fin_gamma, fin_invstd, fin_rm, fin_rv, fin_scale, fin_shift,
+                    fin_mean, fin_decay != 0.f ? 1 : 0};
+  } else if (fin_counter) {
     if (!stats || xbn || addend || ys != 1) return hipErrorInvalidValue;
     a.fin = BnFin{fin_counter, fin_gamma, fin_beta, fin_rm, fin_rv, fin_mean, fin_invstd,
                   fin_scale, fin_shift, const_cast<float*>(kshift), fin_decay, fin_eps,
@@ -2580,8 +2590,22 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
   // IG_ALGO_S3: the streaming 3x3 64-channel kernel (conv_stream.hip); off
   // its geometry the default kernel below runs
   if (algo == IG_ALGO_S3 && fast && !c8 && conv_s3_fits(a)) return launch_conv_s3(dtype, a, stream);
-  // IG_ALGO_S1: the streaming 1x1 64 -> 256-channel kernel (conv_s1.hip)
+  // IG_ALGO_S1: the streaming 1x1 K -> 4K-channel kernel (conv_s1.hip)
   if (algo == IG_ALGO_S1 && fast && !c8 && conv_s1_fits(a)) return launch_conv_s1(dtype, a, stream);
+  if (gfin) {
+    // only the persistent kernels above carry the backward finalize tail:
+    // any other kernel runs without it and the finalize is launched after
+    a.gfin = BnGFin{};
+    const hipError_t e = kfb_conv_igemm(dtype, x, w, y, N, H, W, C, OH, OW, KH, KW, sh, sw, pt,
+                                        pl, Ncol, YH, YW, ys, ldy, trans, stats, mask, xbn, mean,
+                                        addend, mcoef, bias, flags, algo, kshift, nullptr, nullptr,
+                                        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                        nullptr, 0.f, 0.f, stream);
+    if (e != hipSuccess) return e;
+    return bn_finalize_grad_launch(stats, Ncol, (long)N * OH * OW, fin_gamma, mean, fin_invstd,
+                                   fin_rm, fin_rv, fin_scale, fin_shift, fin_mean,
+                                   fin_decay != 0.f ? 1 : 0, stream);
+  }
   if ((algo == IG_ALGO_TALL512 || algo == IG_ALGO_TALL256) && fast) {
     if (dtype == BF16) launch_glds_tall<bf16>(a, algo == IG_ALGO_TALL512, stream);
     else if (dtype == F16) launch_glds_tall<f16>(a, algo == IG_ALGO_TALL512, stream);

@@ -379,7 +379,7 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
           }
     }
   }
-  bn_fin_tail(a, (int*)ring);
+  bn_tail(a, (int*)ring);
 }
 
 static int slice_width(int K) { return K <= 128 ? 256 : 128; }
@@ -427,7 +427,14 @@ static int s1_grid(int tiles, int nsl, int wpc) {
         cus = n;
     }
   });
-  int g = g_s1_grid_force > 0 ? g_s1_grid_force : cus * wpc;
+  // KFB_S1_OVERSUB=k: k workgroups per slot, the hardware dispatcher then
+  // balances the runs over CUs a concurrent kernel holds (A/B knob)
+  static const int over = [] {
+    const char* e = getenv("KFB_S1_OVERSUB");
+    const int v = e ? atoi(e) : 1;
+    return v > 0 ? v : 1;
+  }();
+  int g = g_s1_grid_force > 0 ? g_s1_grid_force : cus * wpc * over;
   // whole pixel groups (one workgroup per slice each), at most one tile each
   int groups = g / nsl;
   if (groups > tiles) groups = tiles;

@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(256, 1) conv_s3_k(IgArgs a, Geo g) {
   const int t0 = (int)((long)b * g.tiles / G), t1 = (int)((long)(b + 1) * g.tiles / G);
   const int ntile = t1 - t0;
   if (ntile <= 0) {  // (workgroup-uniform) nothing to compute; still arrives
-    bn_fin_tail(a, (int*)smem);
+    bn_tail(a, (int*)smem);
     return;
   }
   const int Qa = g.Qlo + t0 * BM;
@@ -438,7 +438,7 @@ __global__ void __launch_bounds__(256, 1) conv_s3_k(IgArgs a, Geo g) {
     for (int w = 0; w < 4; ++w) v += red[(w * 2 + st) * CH + ch];
     atomicAdd(a.stats + ((long)st * IG_SPREAD + b % IG_SPREAD) * CH + ch, v);
   }
-  bn_fin_tail(a, (int*)smem);
+  bn_tail(a, (int*)smem);
 }
 
 }  // namespace s3

@@ -27,6 +27,23 @@ struct BnFin {
   long rows;
 };
 
+// BN backward finalize of a dgrad whose epilogue accumulated the producer
+// BN's backward partials (counter == null: off): the last workgroup folds the
+// [2][IG_SPREAD][Ncol] slots into dgamma / dbeta and the apply coefficients
+// dx = dy' * A + x * B + Cc - the work of bn.hip's bn_finalize_grad_k
+// without its launch (the BN's saved mean is IgArgs::mean).
+struct BnGFin {
+  int* counter;  // zeroed with the partial-sum slots
+  const float* gamma;
+  const float* invstd;
+  float* dgamma;
+  float* dbeta;
+  float* coefA;
+  float* coefB;
+  float* coefC;
+  int accumulate;  // add into dgamma / dbeta (flat gradient buffer) instead of writing
+};
+
 struct IgArgs {
   const void* x;  // gathered operand (NHWC [N,H,W,C])
   const void* w;  // [Ncol][Ktot]
@@ -91,6 +108,7 @@ struct IgArgs {
   // output y - 1/16 of the bytes for the same test
   int maskbits;
   BnFin fin;
+  BnGFin gfin;
 };
 
 constexpr int IG_BK = 64;
@@ -121,43 +139,112 @@ __device__ __forceinline__ void bn_fin_channel(const BnFin& f, int c, double s, 
 }
 
 // Called once by every workgroup of the launch, at its very end, after its
-// statistics atomics: the last one to arrive finalizes.  The slots are only
+// statistics atomics: true in the last one to arrive.  The slots are only
 // ever written by float atomics, which execute at the memory side (MI355X
 // guide, Global float atomics), so there are no dirty L2 lines to publish:
 // a workgroup's vmcnt drain (its atomics acknowledged) orders them before
 // its ticket, with no agent release (a buffer_wbl2 per workgroup measured
 // +35 % on the 56x56 convs); the last arriver acquires and reads the slots
 // with agent-scope loads.  `flag`: one int of the kernel's LDS (dead by now).
-__device__ __forceinline__ void bn_fin_tail(const IgArgs& a, int* flag) {
-  if (!a.fin.counter || !a.stats) return;  // (uniform)
+__device__ __forceinline__ bool last_arriver(int* counter, int* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const int total = (int)(gridDim.x * gridDim.y * gridDim.z);
-    const int prev = __hip_atomic_fetch_add(a.fin.counter, 1, __ATOMIC_RELAXED,
+    const int prev = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
     *flag = prev == total - 1;
   }
   __syncthreads();
-  if (!*flag) return;
+  if (!*flag) return false;
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < a.Ncol; c += blockDim.x) {
-    double s = 0.0, q = 0.0;
-    for (int k = 0; k < IG_SPREAD; ++k) {
-      s += __hip_atomic_load(a.stats + (long)k * a.Ncol + c, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      q += __hip_atomic_load(a.stats + (long)(IG_SPREAD + k) * a.Ncol + c, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+// Folds the [2][IG_SPREAD][Ncol] slots of channels 4 g .. 4 g + 3 (after the
+// last arriver's acquire): 16 independent 16-byte loads per batch, so the
+// serial tail costs four memory round trips per channel group rather than
+// one per few slots.
+__device__ __forceinline__ void fold_slots4(const IgArgs& a, int g, double (&s)[4],
+                                            double (&q)[4]) {
+  typedef __attribute__((ext_vector_type(4))) float f4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { s[j] = 0.0; q[j] = 0.0; }
+  const f4* p = (const f4*)a.stats + g;
+  const long row = a.Ncol / 4;
+#pragma unroll
+  for (int kb = 0; kb < IG_SPREAD; kb += 8) {
+    f4 vs[8], vq[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      vs[k] = p[(kb + k) * row];
+      vq[k] = p[(IG_SPREAD + kb + k) * row];
     }
-    bn_fin_channel(a.fin, c, s, q);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[j] += vs[k][j];
+        q[j] += vq[k][j];
+      }
   }
 }
 
-// bn.hip: the separate finalize launch (kernels without the tail)
+__device__ __forceinline__ void bn_fin_tail(const IgArgs& a, int* flag) {
+  if (!a.fin.counter || !a.stats) return;  // (uniform)
+  if (!last_arriver(a.fin.counter, flag)) return;
+  for (int g = threadIdx.x; g < a.Ncol / 4; g += blockDim.x) {
+    double s[4], q[4];
+    fold_slots4(a, g, s, q);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bn_fin_channel(a.fin, 4 * g + j, s[j], q[j]);
+  }
+}
+
+// the dgrad form (bn_finalize_grad_k's math): dgamma = invstd * S2,
+// dbeta = S1, A = g * invstd, B = -A * invstd^2 * S2 / n,
+// Cc = -A * S1 / n - mean * B
+__device__ __forceinline__ void bn_gfin_tail(const IgArgs& a, int* flag) {
+  if (!a.gfin.counter || !a.stats) return;  // (uniform)
+  if (!last_arriver(a.gfin.counter, flag)) return;
+  const double n = (double)a.M;
+  for (int g4 = threadIdx.x; g4 < a.Ncol / 4; g4 += blockDim.x) {
+    double s[4], q[4];
+    fold_slots4(a, g4, s, q);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = 4 * g4 + j;
+      const double s1 = s[j], s2 = q[j];
+      const float is = a.gfin.invstd[c];
+      const float g = a.gfin.gamma ? a.gfin.gamma[c] : 1.f;
+      if (a.gfin.dgamma)
+        a.gfin.dgamma[c] = (a.gfin.accumulate ? a.gfin.dgamma[c] : 0.f) + (float)(s2 * is);
+      if (a.gfin.dbeta)
+        a.gfin.dbeta[c] = (a.gfin.accumulate ? a.gfin.dbeta[c] : 0.f) + (float)s1;
+      const double A = (double)g * is;
+      const double B = -A * (double)is * (double)is * s2 / n;
+      a.gfin.coefA[c] = (float)A;
+      a.gfin.coefB[c] = (float)B;
+      a.gfin.coefC[c] = (float)(-A * s1 / n - (double)a.mean[c] * B);
+    }
+  }
+}
+
+// the tail of a kernel that can carry either finalize
+__device__ __forceinline__ void bn_tail(const IgArgs& a, int* flag) {
+  if (a.gfin.counter) bn_gfin_tail(a, flag);
+  else bn_fin_tail(a, flag);
+}
+
+// bn.hip: the separate finalize launches (kernels without the tail)
+hipError_t bn_finalize_grad_launch(const float* slots, int C, long rows, const float* gamma,
+                                   const float* mean, const float* invstd, float* dgamma,
+                                   float* dbeta, float* coefA, float* coefB, float* coefC,
+                                   int accumulate, hipStream_t stream);
 hipError_t bn_finalize_stats_launch(const float* psum, const float* psq, int nslab, int C,
                                     long rows, const float* gamma, const float* beta, float decay,
                                     float eps, float* run_mean, float* run_var, float* save_mean,

@@ -214,14 +214,20 @@ def stats_buffer(channels, device, shift=None):
     return buf
 
 
-# In-kernel BN finalize (attach_bn_finalize): KFB_BN_FIN=1 in every igemm
-# kernel, "persistent" (default) only in the persistent streaming kernel,
-# 0 never.  Every workgroup of a kernel with the tail drains its stores
+# In-kernel BN finalize (attach_bn_finalize, attach_bn_grad_finalize):
+# KFB_BN_FIN=1 in every igemm kernel, "persistent" (default) only in the
+# persistent streaming kernels (forward statistics and the dgrad's backward
+# partials), "grad" only the dgrad form there, 0 never.  Every workgroup of a kernel with the tail drains its stores
 # before its arrival ticket; on the one-tile kernels (thousands of short
 # workgroups) that drain costs more than the finalize launch it saves
 # (ResNet-50 bs256: 19.64-19.70 vs 19.45-19.50 ms/step, gpurun_out/r9d),
 # in a persistent kernel it is one drain per CU.
-_BN_FIN_MODE = os.environ.get("KFB_BN_FIN", "persistent")
+# Default "grad": ResNet-50 bs256 A/B (profiles/r10_bn_finalize_tails.txt):
+# persistent 19.25-19.40, grad 18.84-19.02, off 18.87-18.88 ms/step - the
+# forward tails cost more than the launches they replace (the last arriver's
+# fold and parameter round trips are one serial post-step per kernel), the
+# dgrad tails about break even and remove ~17 launches per step.
+_BN_FIN_MODE = os.environ.get("KFB_BN_FIN", "grad")
 _BN_FIN = _BN_FIN_MODE != "0"
 # KFB_S3_DGRAD=0: the streaming 3x3 kernel for forward convs only (its dgrad
 # form runs beside the weight-gradient side stream, which can hold CUs its
@@ -239,6 +245,27 @@ def attach_bn_finalize(stats, gamma, beta, rm, rv, decay, eps, st, coef):
         return
     stats._kfb_fin = (gamma, beta, rm, rv, float(decay), float(eps), st, coef)
     stats._kfb_finalized = False
+
+
+def attach_bn_grad_finalize(parts, link, C, device):
+    """Asks the dgrad that fills the BN backward partials ``parts`` (the
+    last consumer of a BNLink) to also run the BN's backward finalize in
+    its last workgroup (csrc/igemm_args.h BnGFin): dgamma / dbeta into the
+    BN's gradient targets and the apply coefficients.  The BN backward then
+    sees ``parts._kfb_gfinalized`` and only runs the apply pass."""
+    if _BN_FIN_MODE not in ("persistent", "1", "grad") or link.gfin is None \
+            or device.type != "cuda":
+        return
+    from .nn import _bn_grad_targets
+    gamma, st, beta = link.gfin
+    coef = torch.empty((3 * C,), dtype=torch.float32, device=device)
+    targets = _bn_grad_targets(gamma, beta, C, device)
+    direct, dgp, dbp, _ = targets
+    parts._kfb_gfin = (parts._kfb_counter.data_ptr(), N.ptr(gamma), N.ptr(None), dgp, dbp,
+                       coef[2 * C:].data_ptr(), st[1].data_ptr(), coef[:C].data_ptr(),
+                       coef[C:2 * C].data_ptr(), 1.0 if direct else 0.0, 0.0)
+    parts._kfb_gfin_out = (coef, targets)
+    parts._kfb_gfinalized = False
 
 
 def _fin_args(stats):
@@ -262,9 +289,16 @@ def _igemm_call(algo, x, wmat, y, geo, stats=None, mask=None, xbn=None, mean=Non
     fin = (None,) * 9 + (0.0, 0.0)
     if (stats is not None and xbn is None and addend is None and geo[15] == 1
             and getattr(stats, "_kfb_fin", None) is not None
-            and (_BN_FIN_MODE == "1" or algo in (IG_S3, IG_S1))):
+            and (_BN_FIN_MODE == "1" or (_BN_FIN_MODE != "grad" and algo in (IG_S3, IG_S1)))):
         fin = _fin_args(stats)
         stats._kfb_finalized = True
+    elif (stats is not None and xbn is not None and geo[15] == 1 and algo in (IG_S3, IG_S1)
+            and getattr(stats, "_kfb_gfin", None) is not None):
+        # (the kfb_conv_igemm fin_* slots in their BnGFin meaning, in order:
+        # counter, gamma, -, dgamma, dbeta, coefC, invstd, coefA, coefB,
+        # accumulate, -; kernels without the tail launch the finalize after)
+        fin = stats._kfb_gfin
+        stats._kfb_gfinalized = True
     N.call("kfb_conv_igemm", N.dt(x), x.data_ptr(), wmat.data_ptr(), y.data_ptr(), *geo,
            N.ptr(stats), N.ptr(mask), N.ptr(xbn), N.ptr(mean), N.ptr(addend), N.ptr(mcoef),
            N.ptr(bias), int(relu), algo, N.ptr(stats_shift(stats)), *fin, N.stream(x.device))
@@ -908,6 +942,7 @@ class _Conv2d(torch.autograd.Function):
                             if link.relu and not rec:
                                 mk = link.mbits if link.mbits is not None else xp
                             fuse = (parts, mk, xbn, link.mean, link.mcoef if rec else None)
+                            attach_bn_grad_finalize(parts, link, cin, dy.device)
                         dx = conv_dgrad(dy, wp, xp.shape, stride, pads, fuse, addend=pend,
                                         wt=ctx.wt, addend_inplace=owned)
                         if fuse is not None:

@@ -118,7 +118,8 @@ class BNLink:
 
     __slots__ = ("x_bn", "mean", "relu", "convs", "resid", "pools", "other", "accum", "partials",
                  "pending",
-                 "pending_owned", "arrived", "mcoef", "pending_sparse", "pending_event", "mbits")
+                 "pending_owned", "arrived", "mcoef", "pending_sparse", "pending_event", "mbits",
+                 "gfin")
 
     def __init__(self, x_bn, mean, relu, mcoef=None):
         self.x_bn, self.mean, self.relu = x_bn, mean, relu
@@ -142,6 +143,10 @@ class BNLink:
         # contributors may run on different streams (side branches): the
         # pending gradient is complete once this event has fired
         self.pending_event = None
+        # (gamma, st = [mean | invstd], beta) of a plain training BN: the
+        # last consumer's dgrad may run the BN's backward finalize in its
+        # last workgroup (conv_hip.attach_bn_grad_finalize)
+        self.gfin = None
 
     @property
     def fusable(self):
@@ -267,6 +272,7 @@ class _BatchNormTrain(torch.autograd.Function):
         ctx.gamma, ctx.beta = gamma, beta
         link = BNLink(x, st[0], relu, coef if rec else None)
         link.mbits = mbits
+        link.gfin = (gamma, st, beta)
         y._kfb_bn_link = link
         ctx.link = link
         ctx.res_link = getattr(residual, "_kfb_bn_link", None) if residual is not None else None
@@ -309,18 +315,28 @@ def _bn_backward(x, y, gamma, st, dy, relu, has_res, link, res_link, gamma_p, be
     rows = x.numel() // C
     dev = x.device
     pre = link is not None and link.partials is not None
+    gdone = None
     if pre:
         parts = link.partials
         nslab = parts.numel() // (2 * C)
         pdy, pdyx = parts[:nslab * C], parts[nslab * C:]
-        coef = torch.empty((3 * C,), dtype=torch.float32, device=dev)
+        if getattr(parts, "_kfb_gfinalized", False):
+            # the dgrad that filled the partials finalized in its last
+            # workgroup (dgamma / dbeta and the apply coefficients)
+            gdone = parts._kfb_gfin_out
+            coef = gdone[0]
+        else:
+            coef = torch.empty((3 * C,), dtype=torch.float32, device=dev)
         link.partials = None
     else:
         nslab = N.query("kfb_bn_num_slabs", rows, C)
         ws = torch.empty((2 * nslab * C + 3 * C,), dtype=torch.float32, device=dev)
         pdy, pdyx = ws[:nslab * C], ws[nslab * C:2 * nslab * C]
         coef = ws[2 * nslab * C:]
-    direct, dgp, dbp, dparams = _bn_grad_targets(gamma_p, beta_p, C, dev)
+    if gdone is not None:
+        direct, dgp, dbp, dparams = gdone[1]
+    else:
+        direct, dgp, dbp, dparams = _bn_grad_targets(gamma_p, beta_p, C, dev)
     dx = torch.empty_like(x)
     rl = res_link
     res_fused = has_res and rl is not None and rl.fusable
@@ -331,7 +347,7 @@ def _bn_backward(x, y, gamma, st, dy, relu, has_res, link, res_link, gamma_p, be
            N.ptr(dres), rows, C, N.ptr(gamma), st[0].data_ptr(), st[1].data_ptr(),
            dgp, dbp, pdy.data_ptr(), pdyx.data_ptr(),
            nslab, coef[:C].data_ptr(), coef[C:2 * C].data_ptr(), coef[2 * C:].data_ptr(),
-           int(relu), int(direct), int(pre), N.stream(dev))
+           int(relu), int(direct), 2 if gdone is not None else int(pre), N.stream(dev))
     if has_res and dres is None:
         dres = dy
     if res_fused:

@@ -71,12 +71,18 @@ def test_conv_finalizes_bn(cuda, monkeypatch, case):
     torch.testing.assert_close(kshift.double(), mean, **tol)  # next step's shift
 
 
-def test_resnet_trains_same_with_in_kernel_finalize(cuda, monkeypatch):
+@pytest.mark.parametrize("force", [None, "s1"])
+def test_resnet_trains_same_with_in_kernel_finalize(cuda, monkeypatch, force):
     """ResNet-50 at batch 8: the finalize in the conv's last workgroup and
     the BN's own finalize launch give the same training trajectory (up to
-    the run-to-run spread of the statistics atomics)."""
+    the run-to-run spread of the statistics atomics).  force="s1": every
+    eligible 1x1 conv on the streaming kernel, whose dgrad form also runs the
+    producer BN's backward finalize in its last workgroup (BnGFin)."""
     from kf_benchmarks_amd import params as P
     from kf_benchmarks_amd.benchmark import BenchmarkCNN
+
+    if force is not None:
+        monkeypatch.setattr(conv_hip, "_IG_FORCE", conv_hip.IG_ALGOS[force])
 
     def run(fin):
         monkeypatch.setattr(conv_hip, "_BN_FIN", fin)

@@ -142,3 +142,52 @@ def test_s1_matches_tiled_kernel_at_resnet_shape(cuda, monkeypatch):
     b = conv_hip.conv_fwd(x, w, (1, 1), (0, 0, 0, 0)).float()
     err = (a - b).abs().max().item()
     assert err <= 1e-2 * b.abs().max().item(), err
+
+
+@pytest.mark.parametrize("K", [64, 256])
+@pytest.mark.parametrize("algo", ["s1", "onebuf"])
+def test_dgrad_finalizes_bn_backward(cuda, monkeypatch, K, algo):
+    """The dgrad that fills a BN's backward partials also runs the BN's
+    backward finalize (BnGFin): in the streaming kernel's last workgroup, or
+    (any other kernel) as a launch right after it - dgamma / dbeta and the
+    apply coefficients match the finalize math on the summed partials."""
+    from kf_benchmarks_amd.ops.nn import BNLink
+    monkeypatch.setattr(conv_hip, "_IG_FORCE", conv_hip.IG_ALGOS[algo])
+    n, H, W = 4, 14, 14
+    C = 4 * K
+    g = torch.Generator().manual_seed(13)
+    dt = torch.bfloat16
+    w = (torch.randn(K, 1, 1, C, generator=g) / K ** 0.5).to(dt).to(cuda)
+    dy = torch.randn(n, H, W, K, generator=g).to(dt).to(cuda)
+    xb = torch.randn(n, H, W, C, generator=g).to(dt).to(cuda)
+    x = torch.randn(n, H, W, C, generator=g).to(dt)
+    mean = torch.randn(C, generator=g).to(cuda)
+    invstd = (torch.rand(C, generator=g) + 0.5).to(cuda)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(cuda)
+    beta = torch.randn(C, generator=g).to(cuda)
+    st = torch.stack([mean, invstd])
+    link = BNLink(xb, mean, True)
+    link.gfin = (gamma, st, beta)
+    parts = conv_hip.stats_buffer(C, cuda).zero_()
+    parts._kfb_counter.zero_()
+    conv_hip.attach_bn_grad_finalize(parts, link, C, cuda)
+    conv_hip.conv_dgrad(dy, w, x.shape, (1, 1), (0, 0, 0, 0),
+                        (parts, _bits(x).to(cuda), xb, mean))
+    torch.cuda.synchronize()
+    assert parts._kfb_gfinalized == (algo == "s1")
+    coef, (direct, _, _, dparams) = parts._kfb_gfin_out
+    if algo != "s1":
+        return  # (the BN backward then finalizes itself; covered end to end)
+    p = parts.view(2, conv_hip.STATS_SPREAD, C).sum(1).double()
+    s1, s2 = p[0], p[1]
+    rows = n * H * W
+    A = gamma.double() * invstd.double()
+    B = -A * invstd.double() ** 2 * s2 / rows
+    Cc = -A * s1 / rows - mean.double() * B
+    tol = dict(rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(coef[:C].double(), A, **tol)
+    torch.testing.assert_close(coef[C:2 * C].double(), B, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(coef[2 * C:].double(), Cc, rtol=1e-4, atol=1e-5)
+    assert not direct
+    torch.testing.assert_close(dparams[0].double(), s2 * invstd.double(), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dparams[1].double(), s1, rtol=1e-4, atol=1e-4)
