@@ -2510,7 +2510,7 @@ enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_G
        IG_ALGO_GENERIC = 21, IG_ALGO_SK128 = 22, IG_ALGO_G8P = 23, IG_ALGO_ONEBUF_E = 24,
        IG_ALGO_ONEBUF_N64_E = 25, IG_ALGO_CLASSIC_N64_E = 26, IG_ALGO_DB = 27,
        IG_ALGO_GBIG256_32 = 28, IG_ALGO_GSHORT128_32 = 29, IG_ALGO_GSHORT64_32 = 30,
-       IG_ALGO_S3 = 31, IG_ALGO_S1 = 32 };
+       IG_ALGO_S3 = 31, IG_ALGO_S1 = 32, IG_ALGO_S7 = 33 };
 
 static bool c8_geometry(int C, int KH, int KW) {
   return C == 8 && (KW == 1 || KW == 2 || KW == 4 || KW == 8) && (KH * KW) % 8 == 0;
@@ -2592,6 +2592,8 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
   if (algo == IG_ALGO_S3 && fast && !c8 && conv_s3_fits(a)) return launch_conv_s3(dtype, a, stream);
   // IG_ALGO_S1: the streaming 1x1 K -> 4K-channel kernel (conv_s1.hip)
   if (algo == IG_ALGO_S1 && fast && !c8 && conv_s1_fits(a)) return launch_conv_s1(dtype, a, stream);
+  // IG_ALGO_S7: the streaming stem conv over the pixel-pair view (conv_s7.hip)
+  if (algo == IG_ALGO_S7 && !t && conv_s7_fits(a)) return launch_conv_s7(dtype, a, stream);
   if (gfin) {
     // only the persistent kernels above carry the backward finalize tail:
     // any other kernel runs without it and the finalize is launched after

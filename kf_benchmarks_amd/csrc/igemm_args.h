@@ -257,6 +257,9 @@ hipError_t launch_conv_s3(int dtype, const IgArgs& a, hipStream_t stream);
 // conv_s1.hip: the streaming 1x1 64 -> 256-channel kernel (IG_ALGO_S1)
 bool conv_s1_fits(const IgArgs& a);
 hipError_t launch_conv_s1(int dtype, const IgArgs& a, hipStream_t stream);
+// conv_s7.hip: the streaming stem conv (IG_ALGO_S7)
+bool conv_s7_fits(const IgArgs& a);
+hipError_t launch_conv_s7(int dtype, const IgArgs& a, hipStream_t stream);
 // conv_stream.hip: the streaming 3x3 kernel's streaming weight gradient (slab per workgroup + fixed-order fold)
 int wgrad_s3_splits(int N, int H, int W, int C, int OH, int OW, int KH, int KW, int sh, int sw,
                     int pt, int pl, int Ncol);

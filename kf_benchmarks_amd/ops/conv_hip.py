@@ -30,6 +30,7 @@ N.register_optional("kfb_conv_s3_applicable", [N.I] * 12, N.c_int)
 N.register_optional("kfb_conv_s3_set_grid", [N.I], None)
 N.register_optional("kfb_conv_s1_applicable", [N.I] * 12, N.c_int)
 N.register_optional("kfb_conv_s1_set_grid", [N.I], None)
+N.register_optional("kfb_conv_s7_applicable", [N.I] * 12, N.c_int)
 N.register_optional("kfb_set_deterministic", [N.I], None)
 
 # igemm kernel choice (csrc/conv_igemm.hip): 1 = register-staged 128-tile
@@ -66,6 +67,9 @@ IG_S3 = 31
 # streaming 1x1 64 -> 256-channel kernel (csrc/conv_s1.hip): persistent,
 # weights resident in LDS, every operand streamed through an LDS-DMA ring
 IG_S1 = 32
+# streaming stem conv over the pixel-pair view (csrc/conv_s7.hip): one image
+# band per CU, input rows through an LDS ring, weights in VGPRs
+IG_S7 = 33
 IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N64,
             "glds_n64": IG_GLDS_N64, "onebuf": IG_ONEBUF, "onebuf_n64": IG_ONEBUF_N64,
             "tall512": IG_TALL512, "tall256": IG_TALL256, "small": IG_SMALL,
@@ -76,12 +80,14 @@ IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N6
             "generic": IG_GENERIC, "sk128": IG_SK128, "g8p": IG_G8P, "onebuf_e": IG_ONEBUF_E,
             "onebuf_n64_e": IG_ONEBUF_N64_E, "classic_n64_e": IG_CLASSIC_N64_E, "db": IG_DB,
             "gbig256_32": IG_GBIG256_32, "gshort128_32": IG_GSHORT128_32,
-            "gshort64_32": IG_GSHORT64_32, "s3": IG_S3, "s1": IG_S1}
+            "gshort64_32": IG_GSHORT64_32, "s3": IG_S3, "s1": IG_S1,
+            "s7": IG_S7}
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
 _NO_S3 = os.environ.get("KFB_IGEMM_NOS3", "0") == "1"  # A/B knob: drop IG_S3
 _NO_S1 = os.environ.get("KFB_IGEMM_NOS1", "0") == "1"  # A/B knob: drop IG_S1
+_NO_S7 = os.environ.get("KFB_IGEMM_NOS7", "0") == "1"  # A/B knob: drop IG_S7
 _NO_GSHORT = os.environ.get("KFB_IGEMM_NOGSHORT", "0") == "1"  # A/B knob: drop IG_GSHORT*
 _GSHORT3 = os.environ.get("KFB_IGEMM_GSHORT3", "1") != "0"  # A/B knob: the 3-stage forms
 _NO_MULTI = os.environ.get("KFB_IGEMM_NOMULTI", "0") == "1"  # A/B knob: drop IG_*MULTI*
@@ -289,7 +295,7 @@ def _igemm_call(algo, x, wmat, y, geo, stats=None, mask=None, xbn=None, mean=Non
     fin = (None,) * 9 + (0.0, 0.0)
     if (stats is not None and xbn is None and addend is None and geo[15] == 1
             and getattr(stats, "_kfb_fin", None) is not None
-            and (_BN_FIN_MODE == "1" or (_BN_FIN_MODE != "grad" and algo in (IG_S3, IG_S1)))):
+            and (_BN_FIN_MODE == "1" or (_BN_FIN_MODE != "grad" and algo in (IG_S3, IG_S1, IG_S7)))):
         fin = _fin_args(stats)
         stats._kfb_finalized = True
     elif (stats is not None and xbn is not None and geo[15] == 1 and algo in (IG_S3, IG_S1)
@@ -411,6 +417,11 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
             C, ncol, KH, KW, geo[8], geo[9], geo[10], geo[11], geo[1], geo[2], geo[4], geo[5]) \
             and geo[13] == geo[4] and geo[14] == geo[5] and geo[15] == 1 and geo[16] == ncol:
         cands += (IG_S1,)
+    if not _NO_S7 and xbn is None and addend is None and mask is None and bact[0] is None \
+            and not (int(bact[1]) & 3) and not trans and N.load().kfb_conv_s7_applicable(
+            C, ncol, KH, KW, geo[8], geo[9], geo[10], geo[11], geo[1], geo[2], geo[4], geo[5]) \
+            and geo[13] == geo[4] and geo[14] == geo[5] and geo[15] == 1 and geo[16] == ncol:
+        cands += (IG_S7,)
     if ncol > 64:  # 64-wide tiles: more workgroups for small-M layers
         cands += (IG_CLASSIC_N64, IG_GLDS_N64, IG_ONEBUF_N64) if fast else (IG_CLASSIC_N64,)
     if len(cands) == 1:

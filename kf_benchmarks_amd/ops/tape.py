@@ -184,6 +184,15 @@ class _TorchKernelProbe:
         class Mode(TorchDispatchMode):
             def __torch_dispatch__(self, func, types, args=(), kwargs=None):
                 name = func.__name__.split(".")[0]
+                if name in ("add", "add_"):
+                    # the autograd engine's own sums of a multi-use tensor's
+                    # incoming gradients (no Python frame of ours): run as
+                    # the native add, a recorded call, instead of a torch
+                    # kernel the tape would miss
+                    y = _native_add(func, args, kwargs)
+                    if y is not None:
+                        probe.native_adds += 1
+                        return y
                 out = func(*args, **(kwargs or {}))
                 if name not in probe._HOST_ONLY:
                     flat = [out] if isinstance(out, torch.Tensor) else (
@@ -200,6 +209,30 @@ class _TorchKernelProbe:
 
         self.mode = Mode()
         self.ops: List[str] = []
+        self.native_adds = 0
+
+
+def _native_add(func, args, kwargs):
+    """``a + b`` / ``a += b`` as kfb_add when it is a plain same-shape sum of
+    contiguous, 16-byte aligned CUDA tensors of a native dtype (None: leave
+    it to torch)."""
+    aten = torch.ops.aten
+    inplace = func is aten.add_.Tensor
+    if not (inplace or func is aten.add.Tensor) or len(args) != 2:
+        return None
+    a, b = args
+    if (kwargs or {}).get("alpha", 1) != 1 or not isinstance(a, torch.Tensor) \
+            or not isinstance(b, torch.Tensor):
+        return None
+    if not (a.is_cuda and b.is_cuda and a.device == b.device and a.dtype == b.dtype
+            and a.dtype in (torch.bfloat16, torch.float16, torch.float32)
+            and a.shape == b.shape and a.is_contiguous() and b.is_contiguous()
+            and a.numel() > 0 and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0):
+        return None
+    y = a if inplace else torch.empty_like(a)
+    N.call("kfb_add", N.dt(a), a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), 0,
+           N.stream(a.device))
+    return y
 
 
 class StepTape:

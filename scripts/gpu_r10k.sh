@@ -1,0 +1,20 @@
+#!/bin/bash
+# bench A/B knobs: compute-stream priority, S3 dgrad form
+set -u
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$ROOT"
+OUT="$ROOT/gpurun_out/${1:-r10k}"
+mkdir -p "$OUT"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+run() {
+  local name="$1"; shift
+  env "$@" timeout -k 10 300 python bench.py --steps 20 --warmup 8 > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc $(grep -o '"ms_per_step": [0-9.]*' "$OUT/$name.log")"
+  case $rc in 0) ;; *) exit $rc;; esac
+}
+for r in 1 2; do
+  run base_$r KFB_BN_FIN=grad
+  run prio_$r KFB_COMPUTE_PRIORITY=1
+  run nos3dg_$r KFB_S3_DGRAD=0
+done

@@ -65,8 +65,30 @@ def main():
         bench.strategy.reducer.reduce_now()
         torch.cuda.synchronize()
         reduce_identity = bool(torch.equal(g0, bench.flat.grad)) and bool(g0.abs().sum() > 0)
+    hier_identity = None
+    if os.environ.get("KFB_TEST_HIER"):
+        # a hierarchical (HierarchicalCopy) reducer over the same world: in a
+        # native-communicator run its subgroups are native communicators too
+        from kf_benchmarks_amd.parallel import allreduce as _ar
+        h = _ar.Hierarchical(comm.get_world().size, comm.get_world().rank)
+        t = torch.arange(4096, dtype=torch.float32, device="cuda")
+        for w in h.launch(t):
+            w.wait()
+        torch.cuda.synchronize()
+        hier_identity = bool(torch.equal(t, torch.arange(4096, dtype=torch.float32,
+                                                         device="cuda")))
+    import torch.distributed as dist
+    nccl_pgs = 0
+    if dist.is_initialized():
+        for pg in list(dist.distributed_c10d._world.pg_map.keys()):
+            try:
+                if dist.get_backend(pg) == "nccl":
+                    nccl_pgs += 1
+            except Exception:  # noqa: BLE001 - a group this rank is not in
+                pass
     flat = bench.flat.flat.detach()
-    res = {"reduce_identity": reduce_identity, "losses": losses, "w0": w0, "wsum": flat.double().sum().item(),
+    res = {"reduce_identity": reduce_identity, "hier_identity": hier_identity,
+           "nccl_pgs": nccl_pgs, "losses": losses, "w0": w0, "wsum": flat.double().sum().item(),
            "wabs": flat.double().abs().sum().item(), "head": flat[:64].cpu().tolist(),
            "tail": flat[-64:].cpu().tolist(), "rank": comm.get_world().rank,
            "gsegs": gsegs, "trace": trace,

@@ -111,10 +111,17 @@ def test_one_rank_rccl_is_identity(cuda, tmp_path, native):
     kw = dict(model="trivial", batch_size=16, num_gpus=1, use_bf16=True, optimizer="momentum",
               data_format="NHWC", variable_update="kungfu", kungfu_option="sync_sgd",
               bucket_size_mb=8.0)
-    env = dict(_RCCL, KFB_TEST_REDUCE_IDENTITY="1", KFB_NATIVE_COMM=native)
+    env = dict(_RCCL, KFB_TEST_REDUCE_IDENTITY="1", KFB_NATIVE_COMM=native, KFB_TEST_HIER="1")
     (a,) = _run(kw, 3, tmp_path, n=1, env_extra=env, tag="rccl")
     (b,) = _run(kw, 3, tmp_path, n=1, env_extra=_NOCOMM, tag="nocomm")
     assert a["backend"] == ("rccl" if native == "1" else "nccl") and a["size"] == 1
+    assert a["hier_identity"] is True
+    # one RCCL communicator family: a native-communicator run (world and the
+    # hierarchical subgroups) creates no ProcessGroupNCCL at all
+    if native == "1":
+        assert a["nccl_pgs"] == 0, a["nccl_pgs"]
+    else:
+        assert a["nccl_pgs"] >= 1
     # 3 steps + the identity check's synchronous reduction
     assert a["bucket_launches"] == 4 * a["num_buckets"] > 0
     assert b["bucket_launches"] == 0

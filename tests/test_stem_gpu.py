@@ -141,3 +141,47 @@ def test_c8_fast_conv_every_kernel(cuda, shape, algo, monkeypatch):
     ref = conv_ops.conv2d_reference(x, w, stride, (0, 0, 0, 0))
     assert y.shape == ref.shape
     torch.testing.assert_close(y.float().cpu(), ref, rtol=2e-2, atol=2e-2)
+
+
+S7_SHAPES = [(2, 112, 112), (3, 19, 15), (1, 9, 40), (4, 56, 128)]  # (N, OH, OW)
+
+
+@pytest.mark.parametrize("shape", S7_SHAPES, ids=[str(s) for s in S7_SHAPES])
+def test_s7_streaming_stem_conv(cuda, shape, monkeypatch):
+    """The streaming stem kernel (csrc/conv_s7.hip, IG_ALGO_S7) on the
+    pixel-pair view: 8x4 taps, stride (2, 1), 64 channels, with the shifted
+    BN statistics, vs the fp32 reference - full rows (112), rows shorter
+    than a wave's 32 pixels, the 128-pixel maximum, and bands of a few rows
+    (small batches split each image over several workgroups)."""
+    from kf_benchmarks_amd.ops import conv_hip
+    n, OH, OW = shape
+    Hp, Wp2 = 2 * (OH - 1) + 8, OW + 3
+    g = torch.Generator().manual_seed(17)
+    dt = torch.bfloat16
+    xv = torch.randn(n, Hp, Wp2, 8, generator=g).to(dt)
+    w2 = (torch.randn(64, 8, 4, 8, generator=g) / 16.0).to(dt)
+    shift = torch.randn(64, generator=g) * 0.2
+    ref = conv_ops.conv2d_reference(xv.float(), w2.float(), (2, 1), (0, 0, 0, 0))
+    assert ref.shape == (n, OH, OW, 64)
+    monkeypatch.setattr(conv_hip, "_IG_FORCE", conv_hip.IG_S7)
+    st = conv_hip.stats_buffer(64, cuda, shift=shift.to(cuda)).zero_()
+    y = conv_hip.conv_fwd(xv.to(cuda), w2.to(cuda), (2, 1), (0, 0, 0, 0), st)
+    yf = y.float().cpu()
+    torch.testing.assert_close(yf, ref, rtol=2e-2, atol=2e-2)
+    p = st.view(2, conv_hip.STATS_SPREAD, 64).sum(1).cpu()
+    d = yf.reshape(-1, 64) - shift
+    tol = 4e-3 * (d.abs() + d * d).sum(0).max().item()
+    torch.testing.assert_close(p[0], d.sum(0), rtol=1e-2, atol=tol)
+    torch.testing.assert_close(p[1], (d * d).sum(0), rtol=1e-2, atol=tol)
+    # the same through the tiled kernel agrees to output rounding
+    monkeypatch.setattr(conv_hip, "_IG_FORCE", conv_hip.IG_CLASSIC)
+    y2 = conv_hip.conv_fwd(xv.to(cuda), w2.to(cuda), (2, 1), (0, 0, 0, 0)).float().cpu()
+    assert (yf - y2).abs().max().item() <= 1e-2 * y2.abs().max().item()
+
+
+def test_s7_applicability():
+    from kf_benchmarks_amd.ops import _native as N
+    lib = N.load()
+    assert lib.kfb_conv_s7_applicable(8, 64, 8, 4, 2, 1, 0, 0, 230, 115, 112, 112) == 1
+    assert lib.kfb_conv_s7_applicable(8, 32, 8, 4, 2, 1, 0, 0, 230, 115, 112, 112) == 0
+    assert lib.kfb_conv_s7_applicable(8, 64, 8, 4, 2, 1, 0, 0, 230, 200, 112, 197) == 0

@@ -15,6 +15,7 @@ def _strict(monkeypatch):
 
 
 def _run(model, optimizer, tape, steps=6, bs=8, **kw):
+    steps = kw.pop("steps", steps)
     from kf_benchmarks_amd import params as P
     from kf_benchmarks_amd.benchmark import BenchmarkCNN
     p = P.make_params(model=model, batch_size=bs, num_gpus=1, use_bf16=True,
@@ -55,6 +56,49 @@ def test_tape_matches_eager(cuda, model, optimizer):
     assert (wt - we2).abs().max().item() <= max(4 * ref, 1e-3), ref
     # the replayed steps changed the weights (they ran at all)
     assert lt[-1] != lt[2]
+
+
+def test_tape_records_gradient_sums_natively(cuda):
+    """A plain same-shape add inside the recorded step - the autograd
+    engine's sum of a multi-use tensor's incoming gradients is one, with no
+    Python frame of ours - is recorded as the native add: the tape records,
+    and a replay recomputes the sum from the inputs' new contents."""
+    from kf_benchmarks_amd.ops import tape as T
+    a = torch.randn(4096, device=cuda).to(torch.bfloat16)
+    b = torch.randn(4096, device=cuda).to(torch.bfloat16)
+    t = T.StepTape(cuda)
+    y = t.record(lambda: torch.add(a, b))
+    torch.testing.assert_close(y.float(), (a.float() + b.float()), rtol=1e-2, atol=1e-2)
+    a.copy_(torch.randn(4096, device=cuda))
+    b.copy_(torch.randn(4096, device=cuda))
+    y2 = t.replay({})
+    torch.cuda.synchronize()
+    assert torch.equal(y2, a + b)
+    x = torch.randn(1000, device=cuda)
+    assert T._native_add(torch.ops.aten.add.Tensor, (x, x), {"alpha": 2}) is None
+    assert T._native_add(torch.ops.aten.add.Tensor, (x, x[:999]), {}) is None
+    assert torch.equal(T._native_add(torch.ops.aten.add.Tensor, (x, x), {}), x + x)
+
+
+def test_nasnet_tapes_and_tracks_eager(cuda, monkeypatch):
+    """NASNet (CIFAR form, drop path on): its cells read every hidden state
+    several times, so the autograd engine sums gradients between our native
+    backward ops; recorded as native adds the step tapes, and the replayed
+    steps track eager (drop-path keep probability and seeds as per-step
+    values)."""
+    from kf_benchmarks_amd.ops import conv_hip
+    monkeypatch.setattr(conv_hip, "_AUTOTUNE", False)  # (hundreds of geometries)
+    kw = dict(data_name="cifar10", steps=5)
+    le, we, _ = _run("nasnet", "momentum", False, **kw)
+    le2, we2, _ = _run("nasnet", "momentum", False, **kw)
+    lt, wt, replays = _run("nasnet", "momentum", True, **kw)
+    assert replays == 2
+    spread = 0.0
+    for a, a2, b in zip(le, le2, lt):
+        spread = max(spread, abs(a - a2))
+        assert abs(a2 - b) <= max(4 * spread, 2.5e-2 * max(1.0, abs(a2))), (le, le2, lt)
+    ref = (we - we2).abs().max().item()
+    assert (wt - we2).abs().max().item() <= max(4 * ref, 1e-3), ref
 
 
 def test_tape_refuses_torch_ops_in_step(cuda):
