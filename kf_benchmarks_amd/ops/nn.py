@@ -230,6 +230,14 @@ def _relu_bits_buffer(x, rows, C):
     return torch.empty((rows * C // 8,), dtype=torch.uint8, device=x.device)
 
 
+def _foldable(stats):
+    """A conv epilogue's stats_buffer (its zeroed counter tail follows the
+    slots): the BN forward may fold its finalize into the apply pass
+    (csrc/bn.hip bn_apply_fold_k; have_partials = 3)."""
+    return (stats is not None and getattr(stats, "_kfb_counter", None) is not None
+            and stats.is_cuda)
+
+
 class _BatchNormTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, rm, rv, decay, eps, relu, stats):
@@ -264,7 +272,7 @@ class _BatchNormTrain(torch.autograd.Function):
                N.ptr(gamma), N.ptr(beta), float(decay), float(eps), N.ptr(rm), N.ptr(rv),
                st[0].data_ptr(), st[1].data_ptr(), coef[:C].data_ptr(),
                coef[C:].data_ptr(), psum.data_ptr(), psq.data_ptr(), nslab, int(relu),
-               2 if fin is not None else int(stats is not None),
+               2 if fin is not None else (3 if _foldable(stats) else int(stats is not None)),
                N.ptr(_conv_hip().stats_shift(stats)), N.ptr(mbits), N.stream(dev))
         ctx.save_for_backward(x, y if relu else None, gamma, st)
         ctx.relu = relu
@@ -764,6 +772,7 @@ class _AvgPool(torch.autograd.Function):
         return _pool_link_grad(ctx.link, dx), None, None, None, None, None, None, None
 
 
+N.register_optional("kfb_bn_set_fold", [N.I], None)
 N.register_optional("kfb_bn_relu_maxpool_fwd", [N.I, N.P, N.P, N.P] + [N.I] * 12 +
                     [N.P, N.P, N.F, N.F] + [N.P] * 8 + [N.I, N.P, N.P])
 N.register_optional("kfb_bn_pool_num_slabs", [N.I] * 8, N.c_int)

@@ -17,6 +17,7 @@ step() {
 step s7test 300 python -u -m pytest tests/test_stem_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
 step s7bench 200 python -u scripts/bench_s7.py
 step tapetest 500 python -u -m pytest tests/test_tape_gpu.py -x -q -p no:cacheprovider --timeout 400 --timeout-method thread -k "natively or nasnet"
+step foldtest 400 python -u -m pytest tests/test_bn_fin_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread
 step disttest 300 python -u -m pytest tests/test_dist_gpu.py -x -q -p no:cacheprovider --timeout 250 --timeout-method thread -k one_rank_rccl_is_identity
 run() {
   local name="$1"; shift
@@ -26,6 +27,7 @@ run() {
   case $rc in 0) ;; *) exit $rc;; esac
 }
 for r in 1 2; do
-  run base_$r KFB_IGEMM_NOS7=1
-  run s7_$r KFB_IGEMM_NOS7=0
+  run base_$r KFB_IGEMM_NOS7=1 KFB_BN_FOLD=0
+  run s7_$r KFB_IGEMM_NOS7=0 KFB_BN_FOLD=0
+  run s7fold_$r KFB_IGEMM_NOS7=0 KFB_BN_FOLD=1
 done
