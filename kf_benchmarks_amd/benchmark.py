@@ -492,15 +492,11 @@ class BenchmarkCNN:
         if self.tower_mode:
             return "tower processes average the reported loss on the host"
         if self.world.communicates:
-            if self.world.native is None:
+            if self.world.native is None and self.strategy.steps_use_collectives():
                 return "device collectives go through torch.distributed (not recordable)"
-            from .parallel.variable_mgr import KungFuSyncSGD, SumAllReduceStrategy
-            s = self.strategy
-            r = getattr(s, "reducer", None)
-            if not isinstance(s, (KungFuSyncSGD, SumAllReduceStrategy)) or r is None:
-                return "%s runs host-side logic every step" % s.name
-            if r.relaxed or r.hierarchical is not None:
-                return "relaxed / hierarchical reductions keep host-side state"
+            why = self.strategy.tape_blocker()
+            if why is not None:
+                return why
         if not self.dataset.use_synthetic_gpu_inputs() or getattr(self, "fake_data", None):
             return "host-side input pipeline"
         if self.enable_auto_loss_scale:
@@ -510,7 +506,8 @@ class BenchmarkCNN:
         return None
 
     def _tape_values(self, step):
-        vals = {"lr": self.learning_rate(step)}
+        vals = self.strategy.tape_pre(step)
+        vals["lr"] = self.learning_rate(step)
         vals.update(self.optimizer.tape_values(vals["lr"]))
         vals.update(self.input.tape_values())
         vals.update(self.net.tape_dropout_values())
@@ -521,10 +518,24 @@ class BenchmarkCNN:
         if need_accuracy:
             return None
         t = getattr(self, "_tape", None)
+        phase = self.strategy.tape_phase(self.global_step)
+        if t is not None and phase != self._tape_phase:
+            # (e.g. ada_sgd's switch from model averaging to S-SGD): the
+            # step's launch sequence changed, record it again
+            t.close()
+            t = self._tape = None
+            log_fn("launch tape: strategy phase changed at step %d, re-recording"
+                   % self.global_step)
         if t is None:
             if self._tape_warm < 2:  # autotune / arena sizing settle first
                 self._tape_warm += 1
                 return None
+            why = self.strategy.tape_blocker()  # (state created after build)
+            if why is not None:
+                self._tape_reason = why
+                log_fn("launch tape: not used (%s)" % why)
+                return None
+            self._tape_phase = phase
             from .ops.tape import StepTape, TapeError
             p = self.params
             l2 = None
@@ -561,6 +572,7 @@ class BenchmarkCNN:
         self.net.global_step = step  # NASNet drop-path schedule (tape_dropout_values)
         vals = self._tape_values(step)
         t.replay(vals)
+        self.strategy.tape_post(step)
         self.global_step += 1
         loss = self._tape_loss
         if l2 is not None:

@@ -255,7 +255,7 @@ template <typename T, int V, bool RES, bool RELU, int U = 0>
 __global__ void __launch_bounds__(256)
 bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y, long nvec, int C,
            const float* __restrict__ scale, const float* __restrict__ shift,
-           uint8_t* __restrict__ mb = nullptr) {
+           uint8_t* __restrict__ mb) {
   // nvec < 2^31 is checked on the host: 32-bit index math avoids 64-bit division.
   const unsigned cv = (unsigned)(C / V);
   const unsigned n = (unsigned)nvec, stride = gridDim.x * blockDim.x;
@@ -352,7 +352,7 @@ __global__ void __launch_bounds__(256)
 bn_apply2_k(const T* __restrict__ x, const T* __restrict__ xr, T* __restrict__ y, long nvec, int C,
             const float* __restrict__ scale, const float* __restrict__ shift,
             const float* __restrict__ scale_r, const float* __restrict__ shift_r,
-            uint8_t* __restrict__ mb = nullptr) {
+            uint8_t* __restrict__ mb) {
   const unsigned cv = (unsigned)(C / V);
   const unsigned n = (unsigned)nvec, stride = gridDim.x * blockDim.x;
   const unsigned i0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -510,7 +510,7 @@ bn_finalize_grad_k(const float* __restrict__ pdy, const float* __restrict__ pdyx
                    const float* __restrict__ mean, const float* __restrict__ invstd,
                    float* __restrict__ dgamma, float* __restrict__ dbeta,
                    float* __restrict__ coefA, float* __restrict__ coefB,
-                   float* __restrict__ coefC, int accumulate, int s2_over_scale = 0) {
+                   float* __restrict__ coefC, int accumulate, int s2_over_scale) {
   const int c = blockIdx.x * 64 + threadIdx.x;
   double s1, s2;
   fold_slabs(pdy, pdyx, nslab, C, c, s1, s2);
@@ -1411,7 +1411,7 @@ hipError_t bn_finalize_grad_launch(const float* slots, int C, long rows, const f
   constexpr int NSLOT = 32;  // IG_SPREAD
   hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream, slots,
                      slots + (long)NSLOT * C, NSLOT, C, rows, gamma, mean, invstd, dgamma, dbeta,
-                     coefA, coefB, coefC, accumulate);
+                     coefA, coefB, coefC, accumulate, 0);
   return hipGetLastError();
 }
 }  // namespace kfb
@@ -1524,11 +1524,11 @@ KFB_API hipError_t kfb_bn_fwd_train_dual(
         if (flat)
           hipLaunchKernelGGL((bn_apply2_k<T, VV, false, 4>), dim3(gb), dim3(256), 0, stream,
                              (const T*)x, (const T*)xr, (T*)y, nvec, C, scale, shift, scale_r,
-                             shift_r);
+                             shift_r, (uint8_t*)nullptr);
         else
           hipLaunchKernelGGL((bn_apply2_k<T, VV, false>), dim3(gb), dim3(256), 0, stream,
                              (const T*)x, (const T*)xr, (T*)y, nvec, C, scale, shift, scale_r,
-                             shift_r);
+                             shift_r, (uint8_t*)nullptr);
       }
     });
   });
@@ -1616,7 +1616,7 @@ KFB_API hipError_t kfb_bn_bwd(int dtype, const void* dy, const void* y, const vo
       if (have_partials != 2)  // 2: the producing dgrad's last workgroup finalized (BnGFin)
         hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,
                            pdy, pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta,
-                           coefA, coefB, coefC, accumulate);
+                           coefA, coefB, coefC, accumulate, 0);
       const int gb = stream_grid(nvec);
       if (relu) {
         if (dres) launch_bwd_apply<T, VV, true, true>(gb, stream, dy, y, x, dx, dres, nvec, C, coefA, coefB, coefC);
@@ -1654,10 +1654,10 @@ KFB_API hipError_t kfb_bn_bwd_dual(
                          pdy_r, pdyx_r);
       hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,
                          pdy, pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta,
-                         coefA, coefB, coefC, accumulate);
+                         coefA, coefB, coefC, accumulate, 0);
       hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,
                          pdy_r, pdyx_r, nslab_r, C, rows, gamma_r, save_mean_r, save_invstd_r,
-                         dgamma_r, dbeta_r, coefA_r, coefB_r, coefC_r, accumulate_r);
+                         dgamma_r, dbeta_r, coefA_r, coefB_r, coefC_r, accumulate_r, 0);
       const long nvec = rows * C / VV;
       if (flat_ok(nvec, C, VV))
         hipLaunchKernelGGL((bn_bwd_apply2_k<T, VV, 4>), dim3(flat_grid(nvec)), dim3(256), 0,

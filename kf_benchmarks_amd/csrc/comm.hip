@@ -101,7 +101,10 @@ static bool valid_op(int op) { return op >= 0 && op <= 3; }
 
 // RCCL results are returned offset by 1000 so they cannot be mistaken for
 // hipError_t codes by the caller (0 stays success).
-static int rc(ncclResult_t r) { return r == 0 ? 0 : 1000 + r; }
+static int rc(ncclResult_t r) {
+  kfb::raw_taint();  // a recorded op that talks to RCCL replays through its entry point
+  return r == 0 ? 0 : 1000 + r;
+}
 
 }  // namespace rccl
 }  // namespace kfb

@@ -10,6 +10,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+#include <tuple>
+#include <type_traits>
+#include <utility>
+
 #define KFB_API extern "C" __attribute__((visibility("default")))
 
 namespace kfb {
@@ -73,7 +78,50 @@ inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 // Largest vector width (elements) in {8,4,2,1} dividing C.
 inline int vec_width(int C) { return (C % 8 == 0) ? 8 : (C % 4 == 0) ? 4 : (C % 2 == 0) ? 2 : 1; }
 
+// ---- kernel launches (recorded for the launch tape's raw replay) ---------
+// Every kernel of the library is launched through kfb::launch (the
+// hipLaunchKernelGGL macro below): the arguments are converted to the
+// kernel's parameter types, laid out as hipLaunchKernel's argument table, and
+// while the launch tape records an entry point (tape.hip) the launch is also
+// appended to that tape op - function, grid, block, LDS bytes, stream and a
+// copy of the argument bytes - so a replay can re-issue it with
+// hipLaunchKernel directly instead of calling the entry point again.
+extern std::atomic<int> g_raw_rec;  // nonzero while a tape op records
+void raw_record_launch(const void* fn, dim3 grid, dim3 block, unsigned shm, hipStream_t s,
+                       void* const* argv, const size_t* sizes, int n);
+void raw_record_memset(void* p, int value, size_t bytes, hipStream_t s);
+void raw_taint();  // the op did device work a raw replay cannot repeat
+
+template <typename Tup, size_t... I>
+inline void launch_argv(Tup& t, void** argv, size_t* sz, std::index_sequence<I...>) {
+  ((argv[I] = (void*)&std::get<I>(t), sz[I] = sizeof(std::tuple_element_t<I, Tup>)), ...);
+}
+
+template <typename... P, typename... A>
+inline void launch(void (*k)(P...), dim3 grid, dim3 block, size_t shm, hipStream_t s,
+                   A&&... a) {
+  static_assert(sizeof...(P) == sizeof...(A), "kernel argument count");
+  std::tuple<std::decay_t<P>...> t(static_cast<std::decay_t<P>>(std::forward<A>(a))...);
+  constexpr size_t n = sizeof...(P);
+  void* argv[n > 0 ? n : 1];
+  size_t sz[n > 0 ? n : 1];
+  launch_argv(t, argv, sz, std::index_sequence_for<P...>{});
+  (void)hipLaunchKernel((const void*)k, grid, block, argv, shm, s);
+  if (g_raw_rec.load(std::memory_order_relaxed))
+    raw_record_launch((const void*)k, grid, block, (unsigned)shm, s, argv, sz, (int)n);
+}
+
+inline hipError_t memset_async(void* p, int value, size_t bytes, hipStream_t s) {
+  const hipError_t e = hipMemsetAsync(p, value, bytes, s);
+  if (g_raw_rec.load(std::memory_order_relaxed)) raw_record_memset(p, value, bytes, s);
+  return e;
+}
+
 }  // namespace kfb
+
+#undef hipLaunchKernelGGL
+#define hipLaunchKernelGGL(k, grid, block, shm, stream, ...) \
+  ::kfb::launch(k, dim3(grid), dim3(block), (size_t)(shm), (hipStream_t)(stream), ##__VA_ARGS__)
 
 // Dispatch a templated launcher over the element type.
 #define KFB_DISPATCH_DTYPE(code, T, ...)            \

@@ -2403,7 +2403,7 @@ static hipError_t launch_sk(const IgArgs& a, hipStream_t s) {
       if (e != hipSuccess) return e;
       e = hipMalloc((void**)&c.cnt, (size_t)2 * P * sizeof(int));
       if (e != hipSuccess) return e;
-      e = hipMemsetAsync(c.cnt, 0, (size_t)2 * P * sizeof(int), s);
+      e = kfb::memset_async(c.cnt, 0, (size_t)2 * P * sizeof(int), s);
       if (e != hipSuccess) return e;
       c.P = P;
     }

@@ -33,10 +33,13 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
 namespace kfb {
+std::atomic<int> g_raw_rec{0};
+
 namespace tape {
 
 // ---- minimal libffi ABI (libffi >= 3.3, x86-64 SysV) -----------------------
@@ -93,11 +96,33 @@ struct Sig {
   std::vector<ffi_type_t*> types;
 };
 
+// What an entry point did on the device while it was recorded, for the raw
+// replay: kernel launches (function, shape, stream, argument bytes), memsets,
+// cross-stream waits and device copies.
+struct Raw {
+  int kind = 0;  // 0 launch, 1 memset, 2 stream wait, 3 device-to-device copy
+  const void* fn = nullptr;
+  dim3 grid, block;
+  unsigned shm = 0;
+  hipStream_t s = nullptr, s2 = nullptr;
+  hipEvent_t ev = nullptr;
+  std::vector<uint64_t> blob;  // the kernel's argument bytes
+  std::vector<void*> argv;     // hipLaunchKernel's table into blob
+  void* p = nullptr;
+  const void* q = nullptr;
+  int value = 0;
+  size_t bytes = 0;
+};
+
 struct Op {
   void (*fn)(void);
   const Sig* sig;
   std::vector<uint64_t> slots;  // one 64-bit slot per argument (value in the low bytes)
   std::vector<void*> argp;      // ffi avalue: &slots[k]
+  // raw replay: the recorded device work stands in for the entry point
+  // when nothing else happened in it (raw_ok) and no argument is patched
+  std::vector<Raw> raw;
+  bool tainted = false, patched = false, raw_ok = false;
 };
 
 struct Tape {
@@ -145,10 +170,97 @@ static const Sig* get_sig(Tape* t, const char* types) {
   return s;
 }
 
+// argv points into blob: element moves must keep the buffers where they are
+static_assert(std::is_nothrow_move_constructible<Raw>::value, "Raw moves must not copy");
+static_assert(std::is_nothrow_move_constructible<Op>::value, "Op moves must not copy");
+
+// the op being recorded (one at a time, by the thread that added it)
+static Tape* g_rt = nullptr;
+static int g_rop = -1;
+static std::thread::id g_rtid;
+
+static Op* cur_op() {
+  if (!g_rt || g_rop < 0 || g_rop >= (int)g_rt->ops.size() ||
+      std::this_thread::get_id() != g_rtid)
+    return nullptr;
+  return &g_rt->ops[g_rop];
+}
+
+static hipError_t replay_raw(const Raw& r) {
+  switch (r.kind) {
+    case 0:
+      return hipLaunchKernel(r.fn, r.grid, r.block, const_cast<void**>(r.argv.data()), r.shm,
+                             r.s);
+    case 1: return hipMemsetAsync(r.p, r.value, r.bytes, r.s);
+    case 2: {
+      const hipError_t e = hipEventRecord(r.ev, r.s2);
+      return e != hipSuccess ? e : hipStreamWaitEvent(r.s, r.ev, 0);
+    }
+    default: return hipMemcpyAsync(r.p, r.q, r.bytes, hipMemcpyDeviceToDevice, r.s);
+  }
+}
+
 }  // namespace tape
+
+void raw_record_launch(const void* fn, dim3 grid, dim3 block, unsigned shm, hipStream_t s,
+                       void* const* argv, const size_t* sizes, int n) {
+  tape::Op* op = tape::cur_op();
+  if (!op) return;
+  tape::Raw r;
+  r.kind = 0;
+  r.fn = fn;
+  r.grid = grid;
+  r.block = block;
+  r.shm = shm;
+  r.s = s;
+  std::vector<size_t> off(n);
+  size_t total = 0;
+  for (int i = 0; i < n; ++i) {
+    total = (total + 7) & ~(size_t)7;  // (every argument 8-byte aligned in the copy)
+    const size_t al = sizes[i] >= 16 ? 16 : 8;
+    total = (total + al - 1) & ~(al - 1);
+    off[i] = total;
+    total += sizes[i];
+  }
+  r.blob.assign((total + 15) / 8 + 2, 0);
+  char* base = (char*)r.blob.data();
+  base = (char*)(((uintptr_t)base + 15) & ~(uintptr_t)15);
+  r.argv.resize(n);
+  for (int i = 0; i < n; ++i) {
+    memcpy(base + off[i], argv[i], sizes[i]);
+    r.argv[i] = base + off[i];
+  }
+  op->raw.push_back(std::move(r));  // (vector moves keep blob's storage in place)
+}
+
+void raw_record_memset(void* p, int value, size_t bytes, hipStream_t s) {
+  tape::Op* op = tape::cur_op();
+  if (!op) return;
+  tape::Raw r;
+  r.kind = 1;
+  r.p = p;
+  r.value = value;
+  r.bytes = bytes;
+  r.s = s;
+  op->raw.push_back(std::move(r));
+}
+
+void raw_taint() {
+  tape::Op* op = tape::cur_op();
+  if (op) op->tainted = true;
+}
+
 }  // namespace kfb
 
 using namespace kfb::tape;
+
+// KFB_TAPE_RAW=0 (or kfb_tape_set_raw(0)): every op replays through its entry point
+static int g_raw_replay = [] {
+  const char* e = getenv("KFB_TAPE_RAW");
+  return (e && atoi(e) == 0) ? 0 : 1;
+}();
+
+KFB_API void kfb_tape_set_raw(int on) { g_raw_replay = on ? 1 : 0; }
 
 KFB_API int kfb_tape_available() { return ffi().ok ? 1 : 0; }
 
@@ -192,7 +304,41 @@ KFB_API int kfb_tape_patch(void* h, int op, int arg, uint64_t value) {
       arg >= (int)t->ops[op].slots.size())
     return -1;
   t->ops[op].slots[arg] = value;
+  t->ops[op].patched = true;  // (a per-step argument: always the entry point)
   return 0;
+}
+
+// Brackets the eager execution of a just-added op while recording: its kernel
+// launches, memsets, waits and copies are captured (Raw); allow_raw = 0 keeps
+// the op on the entry-point call at replay (an entry with host-side effects).
+KFB_API int kfb_tape_begin_op(void* h, int op) {
+  Tape* t = (Tape*)h;
+  if (!t || op < 0 || op >= (int)t->ops.size()) return -1;
+  g_rt = t;
+  g_rop = op;
+  g_rtid = std::this_thread::get_id();
+  kfb::g_raw_rec.store(1);
+  return 0;
+}
+
+KFB_API int kfb_tape_end_op(void* h, int op, int allow_raw) {
+  Tape* t = (Tape*)h;
+  kfb::g_raw_rec.store(0);
+  g_rt = nullptr;
+  g_rop = -1;
+  if (!t || op < 0 || op >= (int)t->ops.size()) return -1;
+  Op& o = t->ops[op];
+  o.raw_ok = allow_raw && !o.tainted && !o.raw.empty();
+  return o.raw_ok ? 1 : 0;
+}
+
+// Number of ops a replay re-issues raw (the rest call their entry point).
+KFB_API int kfb_tape_raw_ops(void* h) {
+  Tape* t = (Tape*)h;
+  if (!t) return -1;
+  int n = 0;
+  for (const Op& o : t->ops) n += o.raw_ok && !o.patched;
+  return n;
 }
 
 // Re-issues every recorded call in order: patches first (npatch triples
@@ -214,13 +360,21 @@ KFB_API int kfb_tape_replay(void* h, const int* pop, const int* parg, const uint
       for (size_t k = 0; k < op.slots.size(); ++k) op.argp[k] = &op.slots[k];
     }
     int64_t rc = 0;  // ffi widens an int return to a full register
-    if (prof) {
-      const auto t0 = std::chrono::steady_clock::now();
-      call((void*)&op.sig->cif, op.fn, &rc, op.argp.data());
-      t->host_s[i] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const auto t0 = prof ? std::chrono::steady_clock::now()
+                         : std::chrono::steady_clock::time_point();
+    if (op.raw_ok && !op.patched && g_raw_replay) {
+      for (const Raw& r : op.raw) {
+        const hipError_t e = replay_raw(r);
+        if (e != hipSuccess) {
+          rc = (int64_t)e;
+          break;
+        }
+      }
     } else {
       call((void*)&op.sig->cif, op.fn, &rc, op.argp.data());
     }
+    if (prof)
+      t->host_s[i] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if ((int)rc != 0) {
       if (failed_op) *failed_op = (int)i;
       return (int)rc;
@@ -241,16 +395,33 @@ KFB_API hipError_t kfb_event_destroy(hipEvent_t ev) { return hipEventDestroy(ev)
 
 // dst waits for everything enqueued on src so far (ev: scratch event).
 KFB_API hipError_t kfb_stream_wait(hipStream_t dst, hipStream_t src, hipEvent_t ev) {
+  if (Op* op = cur_op()) {
+    Raw r;
+    r.kind = 2;
+    r.s = dst;
+    r.s2 = src;
+    r.ev = ev;
+    op->raw.push_back(std::move(r));
+  }
   hipError_t e = hipEventRecord(ev, src);
   if (e != hipSuccess) return e;
   return hipStreamWaitEvent(dst, ev, 0);
 }
 
 KFB_API hipError_t kfb_memset(void* p, int byte, size_t bytes, hipStream_t s) {
-  return hipMemsetAsync(p, byte, bytes, s);
+  return kfb::memset_async(p, byte, bytes, s);
 }
 
 KFB_API hipError_t kfb_memcpy_d2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (Op* op = cur_op()) {
+    Raw r;
+    r.kind = 3;
+    r.p = dst;
+    r.q = src;
+    r.bytes = bytes;
+    r.s = s;
+    op->raw.push_back(std::move(r));
+  }
   return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s);
 }
 

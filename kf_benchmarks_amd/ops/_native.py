@@ -55,6 +55,10 @@ _SIGS = {
     "kfb_tape_patch": [P, I, I, ctypes.c_uint64],
     "kfb_tape_replay": [P, P, P, P, I, P],
     "kfb_tape_host_times": [P, P],
+    "kfb_tape_begin_op": [P, I],
+    "kfb_tape_end_op": [P, I, I],
+    "kfb_tape_raw_ops": [P],
+    "kfb_tape_set_raw": [I],
     "kfb_host_register": [P, ctypes.c_size_t, P],
     "kfb_host_unregister": [P],
     "kfb_nonfinite": [P, L, P, P],
@@ -101,7 +105,7 @@ _SIGS = {
 }
 _RESTYPES = {"kfb_bn_num_slabs": c_int, "kfb_colsum_num_slabs": c_int,
              "kfb_gemm_splits": c_int, "kfb_ctc_max_states": c_int, "kfb_tape_new": c_void_p,
-             "kfb_tape_free": None}
+             "kfb_tape_free": None, "kfb_tape_set_raw": None}
 # Optional symbols (added by later kernel files); bound if present.
 _OPTIONAL = {}
 
@@ -187,8 +191,9 @@ def call(name, *args):
     if fn is None:
         fn = _FN[name] = getattr(load(), name)
     if _TAPE is not None:
-        args = _TAPE.add(name, fn, args)
-    err = fn(*args)
+        err = _TAPE.call(name, fn, args)
+    else:
+        err = fn(*args)
     if err != 0:
         raise NativeError("%s failed with hipError %d" % (name, err))
     return err

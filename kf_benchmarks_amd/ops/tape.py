@@ -66,8 +66,22 @@ def _pack(v, code, keep=None):
     return int(v) & _MASK
 
 
+# Entry points whose work is not only kernel launches on the given streams
+# (collectives, host registration, events, stream creation): a replay always
+# calls them, never the raw launches recorded under them.
+_NO_RAW_PREFIX = ("kfb_rccl_", "kfb_host_", "kfb_event_", "kfb_stream_create", "kfb_tape_",
+                  "kfb_seqlock_")
+
+
 class Recorder:
-    """One native launch tape: ``add`` appends calls, ``replay`` re-issues them."""
+    """One native launch tape: ``add`` appends calls, ``replay`` re-issues them.
+
+    Calls recorded through ``call`` also capture the device work they issued
+    (kernel function + grid + argument bytes, memsets, stream waits, copies):
+    a replay re-issues that with ``hipLaunchKernel`` directly, skipping the
+    entry point's host logic (shape checks, algorithm choice, argument
+    packing), unless the op has a per-step argument (Dyn) or did something
+    else (an RCCL call) while recorded.  KFB_TAPE_RAW=0 turns this off."""
 
     def __init__(self):
         lib = N.load()
@@ -110,6 +124,27 @@ class Recorder:
         self.dyn.extend(dyn)
         return out
 
+    def call(self, name, fn, args):
+        """Records ``name(*args)`` and executes it, capturing its device work."""
+        n0 = len(self.names)
+        out = self.add(name, fn, args)
+        if len(self.names) != n0 + 1:  # (not appended: a test's dropped op)
+            return fn(*out)
+        op = n0
+        lib = N.load()
+        lib.kfb_tape_begin_op(self.h, op)
+        err = -1
+        try:
+            err = fn(*out)
+        finally:
+            allow = 0 if (err != 0 or name.startswith(_NO_RAW_PREFIX)) else 1
+            lib.kfb_tape_end_op(self.h, op, allow)
+        return err
+
+    def raw_ops(self) -> int:
+        """Ops a replay re-issues as raw launches (the rest call their entry point)."""
+        return N.load().kfb_tape_raw_ops(self.h)
+
     def keys(self):
         return sorted({k for _, _, k, _ in self.dyn})
 
@@ -144,7 +179,8 @@ class Recorder:
             by.setdefault(name, []).append(t)
         tot = sum(buf) / max(replays, 1)
         rows = sorted(by.items(), key=lambda kv: -sum(kv[1]))[:top]
-        out = ["tape host time per replayed step: %.3f ms over %d calls" % (1e3 * tot, n)]
+        out = ["tape host time per replayed step: %.3f ms over %d calls (%d raw)"
+               % (1e3 * tot, n, self.raw_ops())]
         for name, ts in rows:
             out.append("  %-28s %5d calls %8.3f ms  %6.2f us/call" % (
                 name, len(ts), 1e3 * sum(ts) / max(replays, 1),

@@ -227,7 +227,10 @@ class FusedOptimizer:
                        float(grad_scale), float(weight_decay), clipv, float(mom), float(b1),
                        float(b2), float(eps), N.dyn("lr_t", float(lr_t)), int(self.nesterov),
                        N.ptr(msrc),
-                       float(ma), float(mb), N.ptr(mok), N.ptr(wout), N.stream(f.device))
+                       float(ma), float(mb), N.ptr(mok),
+                       # (launch tape: the publish slot may change per step)
+                       N.dyn("wout", wout.data_ptr()) if wout is not None else None,
+                       N.stream(f.device))
             if finish:
                 f.after_update()
             return

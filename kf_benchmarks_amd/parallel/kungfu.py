@@ -54,6 +54,8 @@ import struct
 import uuid
 import warnings
 
+from typing import Optional
+
 import numpy as np
 import torch
 
@@ -263,26 +265,39 @@ class ModelStore:
                 return slot, v
         raise TornReadError("peer %d's latest slot stayed mid-write" % peer)
 
-    def begin_pull(self, peer: int, out: torch.Tensor):
-        """Start copying ``peer``'s latest committed model into ``out``
-        (side stream on the GPU; the owner does not participate)."""
+    def pull_values(self, peer: int) -> dict:
+        """The per-step values of a pull of ``peer``'s latest committed model
+        (launch tape: the recorded copy and seqlock check read them)."""
         slot, v = self._snapshot_header(peer)
-        ev = None
-        if self.cuda:
-            cur = torch.cuda.current_stream(out.device)
-            self.pull_stream.wait_stream(cur)  # ``out`` is free to overwrite
-            with torch.cuda.stream(self.pull_stream):
-                out.copy_(self.peer_slots[peer][slot], non_blocking=True)
-                if self.device_check:
-                    from ..ops import _native as N
-                    N.call("kfb_seqlock_check", self.hdr.device_word(peer, slot), v,
-                           self.ok.data_ptr(), self.torn.data_ptr(),
-                           self.pull_stream.cuda_stream)
-                ev = torch.cuda.Event()
-                ev.record(self.pull_stream)
-        else:
+        return {"pa_src": self.peer_slots[peer][slot].data_ptr(),
+                "pa_word": self.hdr.device_word(peer, slot) or 0, "pa_seq": v,
+                "_pa": (peer, slot)}
+
+    def begin_pull(self, peer: int, out: torch.Tensor, vals: Optional[dict] = None):
+        """Start copying ``peer``'s latest committed model into ``out``
+        (side stream on the GPU; the owner does not participate).  On the GPU
+        every operation is a native call (recordable in a launch tape):
+        stream waits, the device copy and the device-side seqlock check."""
+        if not self.cuda:
+            slot, v = self._snapshot_header(peer)
             out.copy_(self.peer_slots[peer][slot])
-        self._inflight = (peer, slot, v, ev, out)
+            self._inflight = (peer, slot, v, None, out)
+            return
+        from ..ops import _native as N
+        vals = vals or self.pull_values(peer)
+        ps = self.pull_stream.cuda_stream
+        N.stream_wait(ps, N.stream(out.device))  # ``out`` is free to overwrite
+        N.call("kfb_memcpy_d2d", out.data_ptr(), N.dyn("pa_src", vals["pa_src"]),
+               out.numel() * out.element_size(), ps)
+        if self.device_check:
+            N.call("kfb_seqlock_check", N.dyn("pa_word", vals["pa_word"]),
+                   N.dyn("pa_seq", vals["pa_seq"]), self.ok.data_ptr(), self.torn.data_ptr(), ps)
+        ev = None
+        if not self.device_check:
+            ev = torch.cuda.Event()
+            ev.record(self.pull_stream)
+        peer, slot = vals["_pa"]
+        self._inflight = (peer, slot, vals["pa_seq"], ev, out)
 
     def finish_pull_async(self):
         """Device-validated pull: the current stream waits for the copy and
@@ -290,7 +305,8 @@ class ModelStore:
         optimizer gates the averaging on.  The host never blocks."""
         peer, slot, v, ev, out = self._inflight
         self._inflight = None
-        torch.cuda.current_stream(out.device).wait_event(ev)
+        from ..ops import _native as N
+        N.stream_wait(N.stream(out.device), self.pull_stream.cuda_stream)
         return self.ok
 
     def finish_pull(self) -> int:
@@ -398,6 +414,33 @@ class PairAveraging(Strategy):
         self._mix = self._wout = None
         if self.store is not None:
             self.store.abort_publish()
+
+    # launch tape: the pull (copy + device seqlock check) and the update into
+    # the publish slot are recorded native calls whose peer-slot address,
+    # sequence word and publish slot are per-step values; the host halves
+    # (peer choice, header snapshot, publish bookkeeping) run around a replay
+    def steps_use_collectives(self):
+        return False  # one-sided pulls over HIP IPC; no collective per step
+
+    def tape_blocker(self):
+        if self.world.size > 1 and not self.flat.flat.is_cuda:
+            return "host-memory model store"
+        if self.store is not None and not self.store.device_check:
+            return "peer headers not mappable for the device seqlock check"
+        return None
+
+    def tape_pre(self, step):
+        if self.store is None:
+            return {}
+        self.store.poll()
+        vals = self.store.pull_values(self._pick_peer())
+        vals.pop("_pa")
+        vals["wout"] = self.store.begin_publish().data_ptr()
+        return vals
+
+    def tape_post(self, step):
+        if self.store is not None:
+            self.store.end_publish()
 
     def close(self):
         """Collective: every rank stops reading before any slot is freed."""

@@ -107,6 +107,39 @@ class Strategy:
         --variable_consistency=relaxed (no weight decay either)."""
         return self.reducer is not None and self.reducer.deferred_empty
 
+    # ---------------------------------------------------- launch tape hooks
+    def tape_blocker(self) -> Optional[str]:
+        """Why a step of this strategy cannot be replayed from a launch tape
+        (None: it can).  A taped step replays the recorded native calls; the
+        strategy's per-step host logic runs in tape_pre / tape_post around
+        the replay and feeds it per-step values."""
+        if not self.world.communicates:
+            return None
+        r = self.reducer
+        if not self.reduces_gradients or r is None:
+            return "%s runs host-side logic every step" % self.name
+        if r.relaxed or r.hierarchical is not None:
+            return "relaxed / hierarchical reductions keep host-side state"
+        return None
+
+    def steps_use_collectives(self) -> bool:
+        """Whether every step issues device collectives (then a launch tape
+        needs them as native calls: the native communicator)."""
+        return self.reducer is not None
+
+    def tape_phase(self, step: int):
+        """Steps in different phases record different launch sequences (a
+        recorded tape is re-recorded when the phase changes)."""
+        return 0
+
+    def tape_pre(self, step: int) -> dict:
+        """Host half of the strategy's step before a replay; returns the
+        per-step values (native.dyn keys) of the replay."""
+        return {}
+
+    def tape_post(self, step: int):
+        """Host half of the strategy's step after a replay was enqueued."""
+
     def describe(self) -> str:
         return self.name
 
@@ -116,6 +149,9 @@ class Strategy:
 
 class IndependentStrategy(Strategy):
     name = "independent"
+
+    def tape_blocker(self):
+        return None  # no per-step communication at all
 
 
 class SumAllReduceStrategy(Strategy):
@@ -187,6 +223,18 @@ class KungFuSMA(Strategy):
         if self.world.communicates and self._avg is not None:
             self._launch()
 
+    def steps_use_collectives(self):
+        return True
+
+    def tape_blocker(self):
+        # the model all-reduce and its stream waits are native calls on
+        # fixed buffers: a recorded step replays them (the all-reduce a
+        # replay enqueues at its end is the one the next replay waits for)
+        return None
+
+    def tape_pre(self, step):
+        return {"wout": self._avg.data_ptr()} if self._avg is not None else {}
+
     def abort_update(self, step):
         self._work = None
 
@@ -239,6 +287,24 @@ class KungFuAdaSGD(Strategy):
         # launch the next average only if the next step still averages
         if step + 1 < self.switch_step:
             self.sma.after_update(step)
+
+    def tape_blocker(self):
+        r = self.reducer
+        if self.world.communicates and r is not None and (r.relaxed or
+                                                          r.hierarchical is not None):
+            return "relaxed / hierarchical reductions keep host-side state"
+        return None
+
+    def steps_use_collectives(self):
+        return True
+
+    def tape_phase(self, step):
+        # averaging steps, the last averaging step (launches no next
+        # average), synchronous-SGD steps: three launch sequences
+        return (step < self.switch_step, step + 1 < self.switch_step)
+
+    def tape_pre(self, step):
+        return self.sma.tape_pre(step) if step < self.switch_step else {}
 
     def close(self):
         self.sma.close()

@@ -187,3 +187,43 @@ def test_two_ranks_pair_averaging_training(cuda, tmp_path):
     for r in (r0, r1):
         assert r["wsum"] != r["w0"] and r["wsum"] == r["wsum"]
         assert all(l == l and abs(l) < 1e3 for l in r["losses"])
+
+
+@pytest.mark.parametrize("option", ["sma", "ada_sgd"])
+def test_one_rank_rccl_model_averaging_taped(cuda, tmp_path, option):
+    """KungFu SMA / ada_sgd through the native 1-rank RCCL communicator from
+    a launch tape: the model all-reduce (launched after each update, waited
+    for by the next) is replayed with the step; ada_sgd re-records the tape
+    when it switches phase (last averaging step, then S-SGD).  The taped run
+    tracks the eager one."""
+    kw = dict(model="resnet50", batch_size=8, num_gpus=1, use_bf16=True, optimizer="momentum",
+              data_format="NHWC", variable_update="kungfu", kungfu_option=option,
+              kungfu_sma_alpha=0.5, kungfu_ada_switch_step=4, bucket_size_mb=4.0)
+    env = dict(_RCCL, KFB_NATIVE_COMM="1", KFB_TAPE_STRICT="1", KFB_TEST_GRAD_SEGS=None)
+    (a,) = _run(dict(kw, launch_tape=True), 8, tmp_path, n=1, env_extra=env, tag="taped")
+    (b,) = _run(dict(kw, launch_tape=False), 8, tmp_path, n=1, env_extra=env, tag="eager")
+    assert a["backend"] == "rccl" and a["nccl_pgs"] == 0
+    # sma: 2 eager, 1 recorded, 5 replayed; ada_sgd: recorded again at steps
+    # 3 and 4 (phase changes), then 3 replays
+    assert a["taped"] == (5 if option == "sma" else 3), a["taped"]
+    assert a["w0"] == b["w0"]
+    for la, lb in zip(a["losses"], b["losses"]):
+        assert la == la and abs(la - lb) <= 0.05 * max(1.0, abs(lb)), (a["losses"], b["losses"])
+
+
+def test_two_ranks_pair_averaging_taped(cuda, tmp_path):
+    """KungFu async_sgd from a launch tape, two ranks on the GPU: the peer
+    pull (device copy from the peer's IPC slot + device seqlock check) and
+    the update into the publish slot are replayed with per-step peer-slot
+    addresses, sequence words and publish slots; every step publishes."""
+    kw = dict(model="resnet50", batch_size=8, num_gpus=1, use_bf16=True, optimizer="momentum",
+              data_format="NHWC", variable_update="kungfu", kungfu_option="async_sgd",
+              launch_tape=True)
+    env = dict(KFB_TAPE_STRICT="1", KFB_TEST_GRAD_SEGS=None)
+    r0, r1 = _run(kw, 6, tmp_path, env_extra=env)
+    assert r0["w0"] == r1["w0"]
+    for r in (r0, r1):
+        assert r["taped"] == 3, r["taped"]
+        assert r["pa_publishes"] == 6
+        assert r["wsum"] != r["w0"] and r["wsum"] == r["wsum"]
+        assert all(l == l and abs(l) < 1e3 for l in r["losses"])

@@ -171,8 +171,10 @@ def _run_exact(tape, steps=6, bs=4):
     torch.cuda.synchronize()
     w = b.flat.flat.detach().float().cpu().clone()
     bufs, slots = _state(b)
-    replays = b._tape.replays if getattr(b, "_tape", None) is not None else 0
-    return dict(losses=losses, w=w, bufs=bufs, slots=slots, replays=replays)
+    tp = getattr(b, "_tape", None)
+    replays = tp.replays if tp is not None else 0
+    raw = (tp.recorder.raw_ops(), len(tp.recorder)) if tp is not None else (0, 0)
+    return dict(losses=losses, w=w, bufs=bufs, slots=slots, replays=replays, raw=raw)
 
 
 def _same(a, b):
@@ -203,7 +205,17 @@ def _deterministic(monkeypatch):
     N.load().kfb_set_deterministic(0)
 
 
-def test_tape_bitwise_matches_eager(cuda, _deterministic):
+@pytest.fixture(params=["raw", "entry"])
+def _replay_mode(request):
+    """raw: ops replay as the recorded hipLaunchKernel calls (the default);
+    entry: every op calls its native entry point again (KFB_TAPE_RAW=0)."""
+    from kf_benchmarks_amd.ops import _native as N
+    N.load().kfb_tape_set_raw(1 if request.param == "raw" else 0)
+    yield request.param
+    N.load().kfb_tape_set_raw(1)
+
+
+def test_tape_bitwise_matches_eager(cuda, _deterministic, _replay_mode):
     e1 = _run_exact(False)
     e2 = _run_exact(False)
     assert not _same(e1, e2), "eager run is not bitwise repeatable: %s" % _same(e1, e2)[:8]
@@ -211,6 +223,28 @@ def test_tape_bitwise_matches_eager(cuda, _deterministic):
     t = _run_exact(True)
     assert t["replays"] == 3
     assert not _same(e1, t), _same(e1, t)[:8]
+    raw, ops = t["raw"]
+    # everything but the ops with per-step arguments (optimizer step, seeds)
+    # replays raw
+    assert raw >= 0.8 * ops, (raw, ops)
+
+
+def test_raw_tape_records_launch_arguments(cuda):
+    """The raw replay re-issues the kernel with the argument bytes captured
+    at record time (pointers included): new input contents, same buffers."""
+    from kf_benchmarks_amd.ops import tape as T
+    a = torch.randn(1 << 16, device=cuda).to(torch.bfloat16)
+    b = torch.randn(1 << 16, device=cuda).to(torch.bfloat16)
+    t = T.StepTape(cuda)
+    y = t.record(lambda: torch.add(a, b))
+    assert t.recorder.raw_ops() == len(t.recorder) >= 1
+    for _ in range(3):
+        a.copy_(torch.randn(1 << 16, device=cuda))
+        b.copy_(torch.randn(1 << 16, device=cuda))
+        y2 = t.replay({})
+        torch.cuda.synchronize()
+        assert y2.data_ptr() == y.data_ptr()
+        assert torch.equal(y2, a + b)
 
 
 def test_tape_oracle_catches_a_dropped_op(cuda, _deterministic, monkeypatch):
