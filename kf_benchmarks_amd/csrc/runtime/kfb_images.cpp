@@ -33,6 +33,8 @@ extern "C" {
 }
 #endif
 
+#include "jpeg_recon.h"
+
 #define API extern "C" __attribute__((visibility("default")))
 
 extern "C" long kfbrt_parse_example(const uint8_t* data, size_t n, uint8_t* out, size_t cap);
@@ -207,6 +209,7 @@ struct Jpeg {
   JDIMENSION (*read_scanlines)(j_decompress_ptr, JSAMPARRAY, JDIMENSION) = nullptr;
   void (*abort_)(j_decompress_ptr) = nullptr;
   void (*destroy)(j_decompress_ptr) = nullptr;
+  jvirt_barray_ptr* (*read_coefficients)(j_decompress_ptr) = nullptr;  // (optional)
 };
 
 Jpeg& jpeg() {
@@ -228,6 +231,7 @@ Jpeg& jpeg() {
     KFB_J(read_scanlines, "jpeg_read_scanlines");
     KFB_J(abort_, "jpeg_abort_decompress");
     KFB_J(destroy, "jpeg_destroy_decompress");
+    KFB_J(read_coefficients, "jpeg_read_coefficients");
 #undef KFB_J
     j.ok = j.std_error && j.create && j.mem_src && j.read_header && j.start &&
            j.read_scanlines && j.abort_ && j.destroy;
@@ -352,6 +356,177 @@ int process(const Config& cfg, const uint8_t* rec, size_t len, uint64_t seed, in
 #endif
 }
 
+// ------------------------------------------------------------ coefficients
+// The GPU-reconstruction form of process(): the same crop / flip / colour
+// draws, but the host only entropy-decodes (jpeg_read_coefficients) and
+// copies the coefficient blocks that cover the crop (plus the one-sample
+// chroma margin the upsampling filter reads) into the batch arena;
+// csrc/jpeg.hip does the rest (jpeg_recon.h).  Layouts the reconstruction
+// does not cover (CMYK / RGB-coded / odd sampling / DCT-scaled files) and an
+// arena overflow take process() and are marked MODE_HOST.
+struct Arena {
+  int16_t* blocks = nullptr;  // [cap][64]
+  long cap = 0;
+  std::atomic<long> next{0};
+};
+
+#if defined(KFB_HAVE_JPEGLIB)
+// Block window of component `c` covering full-resolution rows [y, y+h) and
+// columns [x, x+w) (+ the upsampling margin).
+static void comp_window(const jpeg_decompress_struct& ci, int k, int y, int x, int h, int w,
+                        kfb::jpg::Comp& c) {
+  const jpeg_component_info& cp = ci.comp_info[k];
+  const int hmax = ci.max_h_samp_factor, vmax = ci.max_v_samp_factor;
+  c.h = cp.h_samp_factor;
+  c.v = cp.v_samp_factor;
+  c.dw = (int)(((long)ci.image_width * c.h + hmax - 1) / hmax);
+  c.dh = (int)(((long)ci.image_height * c.v + vmax - 1) / vmax);
+  const int hr = hmax / c.h, vr = vmax / c.v;
+  int r0 = y / vr, r1 = (y + h - 1) / vr, c0 = x / hr, c1 = (x + w - 1) / hr;
+  if (vr > 1) { r0 -= 1; r1 += 1; }
+  if (hr > 1) { c0 -= 1; c1 += 1; }
+  r0 = std::max(r0, 0);
+  c0 = std::max(c0, 0);
+  r1 = std::min(r1, c.dh - 1);
+  c1 = std::min(c1, c.dw - 1);
+  c.by0 = r0 / 8;
+  c.bx0 = c0 / 8;
+  c.bh = r1 / 8 - c.by0 + 1;
+  c.bw = c1 / 8 - c.bx0 + 1;
+  c.pad = 0;
+}
+
+static bool coef_layout_ok(const jpeg_decompress_struct& ci) {
+  if (ci.block_size != 8 || ci.image_width < 3 || ci.image_height < 1) return false;
+  if (ci.num_components == 1) return ci.jpeg_color_space == JCS_GRAYSCALE;
+  if (ci.num_components != 3 || ci.jpeg_color_space != JCS_YCbCr) return false;
+  const int hmax = ci.max_h_samp_factor, vmax = ci.max_v_samp_factor;
+  if (ci.comp_info[0].h_samp_factor != hmax || ci.comp_info[0].v_samp_factor != vmax) return false;
+  for (int k = 1; k < 3; ++k) {
+    const int h = ci.comp_info[k].h_samp_factor, v = ci.comp_info[k].v_samp_factor;
+    if (hmax % h || vmax % v) return false;
+    const int hr = hmax / h, vr = vmax / v;
+    // (libjpeg-turbo's fancy upsamplers: h1v1, h2v1, h2v2; h1v2 and wider
+    // ratios keep the host decode)
+    if (!((hr == 1 && vr == 1) || (hr == 2 && vr == 1) || (hr == 2 && vr == 2))) return false;
+    if (hr == 2 && (ci.image_width * h + hmax - 1) / hmax <= 2) return false;
+  }
+  return true;
+}
+#endif
+
+// 0: packed (MODE_COEF) or decoded on the host (MODE_HOST); 1: failure
+// (grey, MODE_HOST).  `host_img`: this image's slot of the host-decoded
+// buffer.
+int pack(const Config& cfg, const uint8_t* rec, size_t len, uint64_t seed, int position,
+         Arena& ar, kfb::jpg::Desc* d, float* prm, int32_t* label, uint8_t* host_img, int slot,
+         std::vector<uint8_t>& scratch, std::vector<uint8_t>& crop) {
+  std::memset(d, 0, sizeof(*d));
+  d->mode = kfb::jpg::MODE_HOST;
+  d->host_slot = slot;
+#if defined(KFB_HAVE_JPEGLIB)
+  Jpeg& J = jpeg();
+  if (J.ok && J.read_coefficients) {
+    scratch.resize(len + 4096);
+    long n = kfbrt_parse_example(rec, len, scratch.data(), scratch.size());
+    if (n == -2) {
+      scratch.resize(len * 2 + 65536);
+      n = kfbrt_parse_example(rec, len, scratch.data(), scratch.size());
+    }
+    Fields f;
+    if (n >= 0 && read_fields(scratch.data(), scratch.data() + n, f) && f.jpeg) {
+      struct jpeg_decompress_struct ci;
+      ErrMgr em;
+      ci.err = J.std_error(&em.pub);
+      em.pub.error_exit = on_error;
+      em.pub.output_message = on_message;
+      bool packed = false;
+      if (setjmp(em.jb)) {
+        J.destroy(&ci);
+        packed = false;
+      } else {
+        J.create(&ci, JPEG_LIB_VERSION, sizeof(ci));
+        J.mem_src(&ci, f.jpeg, (unsigned long)f.jpeg_len);
+        J.read_header(&ci, TRUE);
+        if (coef_layout_ok(ci)) {
+          Rng rng(seed);
+          const int H0 = (int)ci.image_height, W0 = (int)ci.image_width;
+          int y, x, h, w;
+          sample_box(H0, W0, f, rng, y, x, h, w);
+          const bool flip = rng.uniform() < 0.5;
+          kfb::jpg::Desc& D = *d;
+          D.ncomp = ci.num_components;
+          D.cy = y;
+          D.cx = x;
+          D.ch = h;
+          D.cw = w;
+          long need = 0;
+          for (int k = 0; k < D.ncomp; ++k) {
+            comp_window(ci, k, y, x, h, w, D.c[k]);
+            need += (long)D.c[k].bh * D.c[k].bw;
+          }
+          const long base = ar.next.fetch_add(need);
+          if (base + need <= ar.cap) {
+            jvirt_barray_ptr* coefs = J.read_coefficients(&ci);
+            long b = base;
+            for (int k = 0; k < D.ncomp; ++k) {
+              kfb::jpg::Comp& c = D.c[k];
+              c.blk = (int)b;
+              const JQUANT_TBL* qt = ci.comp_info[k].quant_table;
+              for (int i = 0; i < 64; ++i) D.q[k][i] = qt ? qt->quantval[i] : 1;
+              for (int r = 0; r < c.bh; ++r) {
+                JBLOCKARRAY rows = (*ci.mem->access_virt_barray)(
+                    (j_common_ptr)&ci, coefs[k], (JDIMENSION)(c.by0 + r), 1, FALSE);
+                std::memcpy(ar.blocks + 64 * b, rows[0][c.bx0], sizeof(JBLOCK) * c.bw);
+                b += c.bw;
+              }
+            }
+            static_assert(sizeof(JBLOCK) == 128, "16-bit coefficients");
+            D.mode = kfb::jpg::MODE_COEF;
+            *label = (int32_t)f.label;
+            prm[0] = flip ? 1.f : 0.f;
+            if (cfg.distortions) {
+              // (the same draws, in the same order, as process())
+              std::memset(prm + 1, 0, 7 * sizeof(float));
+              prm[1] = (float)rng.uniform(-32. / 255., 32. / 255.);
+              auto sat_hue = [&]() {
+                if (cfg.yiq) {
+                  prm[3] = (float)rng.uniform(-0.2, 0.2);
+                  prm[2] = (float)rng.uniform(0.5, 1.5);
+                } else {
+                  prm[2] = (float)rng.uniform(0.5, 1.5);
+                  prm[3] = (float)rng.uniform(-0.2, 0.2);
+                }
+              };
+              const int order = position % 2;
+              if (order == 0) {
+                sat_hue();
+                prm[4] = (float)rng.uniform(0.5, 1.5);
+              } else {
+                prm[4] = (float)rng.uniform(0.5, 1.5);
+                sat_hue();
+              }
+              prm[5] = (float)order;
+              prm[6] = 1.f;
+            } else {
+              std::memset(prm + 1, 0, 7 * sizeof(float));
+            }
+            packed = true;
+          }
+        }
+        J.abort_(&ci);
+        J.destroy(&ci);
+      }
+      if (packed) return 0;
+    }
+  }
+#endif
+  (void)ar;
+  d->mode = kfb::jpg::MODE_HOST;
+  d->host_slot = slot;
+  return process(cfg, rec, len, seed, position, host_img, prm, label, scratch, crop);
+}
+
 // ------------------------------------------------------------ worker pool
 struct Pipe {
   Config cfg;
@@ -367,7 +542,10 @@ struct Pipe {
   uint8_t* images = nullptr;
   float* params = nullptr;
   int32_t* labels = nullptr;
-  std::atomic<int> next{0}, failed{0};
+  // coefficient mode (kfbrt_imgpipe_run_coef): descriptors + block arena
+  kfb::jpg::Desc* descs = nullptr;
+  Arena* arena = nullptr;
+  std::atomic<int> next{0}, failed{0}, hosted{0};
   int active = 0;
   long gen = 0;
   bool stop = false;
@@ -375,9 +553,17 @@ struct Pipe {
   void work() {
     std::vector<uint8_t> scratch, crop;
     const size_t img_bytes = (size_t)cfg.height * cfg.width * 3;
-    for (int i; (i = next.fetch_add(1)) < n;)
-      failed += process(cfg, recs[i], lens[i], seeds[i], positions[i], images + i * img_bytes,
-                        params + (size_t)i * 8, labels + i, scratch, crop);
+    for (int i; (i = next.fetch_add(1)) < n;) {
+      if (descs) {
+        failed += pack(cfg, recs[i], lens[i], seeds[i], positions[i], *arena, descs + i,
+                       params + (size_t)i * 8, labels + i, images + i * img_bytes, i, scratch,
+                       crop);
+        hosted += descs[i].mode == kfb::jpg::MODE_HOST;
+      } else {
+        failed += process(cfg, recs[i], lens[i], seeds[i], positions[i], images + i * img_bytes,
+                          params + (size_t)i * 8, labels + i, scratch, crop);
+      }
+    }
   }
 
   void loop() {
@@ -444,6 +630,154 @@ API int kfbrt_imgpipe_run(void* h, int n, const uint8_t* const* recs, const size
   std::unique_lock<std::mutex> l(p->mu);
   p->done_cv.wait(l, [&] { return p->active == 0; });
   return p->failed.load();
+}
+
+// Coefficient mode: descs [n] (kfb::jpg::Desc), blocks [cap][64] int16 (the
+// batch arena), images [n][H][W][3] for the images decoded on the host
+// (MODE_HOST).  out3[0] = arena blocks used, out3[1] = images decoded on the
+// host; returns the failure count as kfbrt_imgpipe_run.
+API int kfbrt_imgpipe_run_coef(void* h, int n, const uint8_t* const* recs, const size_t* lens,
+                               const uint64_t* seeds, const int* positions, void* descs,
+                               int16_t* blocks, long cap, uint8_t* images, float* params,
+                               int32_t* labels, long* out2) {
+  Pipe* p = static_cast<Pipe*>(h);
+  Arena ar;
+  ar.blocks = blocks;
+  ar.cap = cap;
+  {
+    std::lock_guard<std::mutex> l(p->mu);
+    p->n = n;
+    p->recs = recs;
+    p->lens = lens;
+    p->seeds = seeds;
+    p->positions = positions;
+    p->images = images;
+    p->params = params;
+    p->labels = labels;
+    p->descs = static_cast<kfb::jpg::Desc*>(descs);
+    p->arena = &ar;
+    p->next = 0;
+    p->failed = 0;
+    p->hosted = 0;
+    p->active = (int)p->threads.size();
+    ++p->gen;
+  }
+  p->cv.notify_all();
+  p->work();
+  std::unique_lock<std::mutex> l(p->mu);
+  p->done_cv.wait(l, [&] { return p->active == 0; });
+  p->descs = nullptr;
+  p->arena = nullptr;
+  out2[0] = std::min(ar.next.load(), cap);
+  out2[1] = p->hosted.load();
+  return p->failed.load();
+}
+
+API int kfbrt_jpeg_desc_bytes() { return (int)sizeof(kfb::jpg::Desc); }
+
+// Host reference of csrc/jpeg.hip (tests; and the CPU form of the device
+// op): IDCT every arena block, then reconstruct + resize every image to
+// out [n][oh][ow][3] (MODE_HOST images are copied from `images`).
+API void kfbrt_jpeg_reconstruct(const void* descs, int n, const int16_t* blocks, long nblocks,
+                                const uint8_t* images, int oh, int ow, uint8_t* out) {
+  const kfb::jpg::Desc* D = static_cast<const kfb::jpg::Desc*>(descs);
+  std::vector<uint8_t> planes((size_t)nblocks * 64);
+  // block -> (image, component) for the dequantization table
+  for (int i = 0; i < n; ++i) {
+    if (D[i].mode != kfb::jpg::MODE_COEF) continue;
+    for (int k = 0; k < D[i].ncomp; ++k) {
+      const kfb::jpg::Comp& c = D[i].c[k];
+      for (long b = c.blk; b < c.blk + (long)c.bh * c.bw; ++b)
+        kfb::jpg::idct_islow(blocks + 64 * b, D[i].q[k], planes.data() + 64 * b);
+    }
+  }
+  const size_t img = (size_t)oh * ow * 3;
+  for (int i = 0; i < n; ++i) {
+    uint8_t* o = out + i * img;
+    if (D[i].mode != kfb::jpg::MODE_COEF) {
+      std::memcpy(o, images + (size_t)D[i].host_slot * img, img);
+      continue;
+    }
+    for (int r = 0; r < oh; ++r)
+      for (int c = 0; c < ow; ++c)
+        kfb::jpg::resized_pixel(planes.data(), D[i], oh, ow, r, c, o + ((size_t)r * ow + c) * 3);
+  }
+}
+
+// Test hook: the whole image through the coefficient path (crop = image,
+// no resize) into rgb [h][w][3] (cap bytes); returns 0, or -1 when the
+// layout is not covered / the buffer is too small / the decode fails.
+API int kfbrt_jpeg_decode_coef(const uint8_t* jpeg_bytes, size_t len, uint8_t* rgb, size_t cap,
+                               int* hw) {
+#if defined(KFB_HAVE_JPEGLIB)
+  Jpeg& J = jpeg();
+  if (!J.ok || !J.read_coefficients) return -1;
+  struct jpeg_decompress_struct ci;
+  ErrMgr em;
+  ci.err = J.std_error(&em.pub);
+  em.pub.error_exit = on_error;
+  em.pub.output_message = on_message;
+  kfb::jpg::Desc D;
+  std::memset(&D, 0, sizeof(D));
+  std::vector<int16_t> blocks;
+  if (setjmp(em.jb)) {
+    J.destroy(&ci);
+    return -1;
+  }
+  J.create(&ci, JPEG_LIB_VERSION, sizeof(ci));
+  J.mem_src(&ci, jpeg_bytes, (unsigned long)len);
+  J.read_header(&ci, TRUE);
+  const int H = (int)ci.image_height, W = (int)ci.image_width;
+  if (!coef_layout_ok(ci) || (size_t)H * W * 3 > cap) {
+    J.destroy(&ci);
+    return -1;
+  }
+  D.mode = kfb::jpg::MODE_COEF;
+  D.ncomp = ci.num_components;
+  D.ch = H;
+  D.cw = W;
+  long total = 0;
+  for (int k = 0; k < D.ncomp; ++k) {
+    comp_window(ci, k, 0, 0, H, W, D.c[k]);
+    D.c[k].blk = (int)total;
+    total += (long)D.c[k].bh * D.c[k].bw;
+  }
+  blocks.resize((size_t)total * 64);
+  jvirt_barray_ptr* coefs = J.read_coefficients(&ci);
+  for (int k = 0; k < D.ncomp; ++k) {
+    const kfb::jpg::Comp& c = D.c[k];
+    const JQUANT_TBL* qt = ci.comp_info[k].quant_table;
+    for (int i = 0; i < 64; ++i) D.q[k][i] = qt ? qt->quantval[i] : 1;
+    for (int r = 0; r < c.bh; ++r) {
+      JBLOCKARRAY rows = (*ci.mem->access_virt_barray)((j_common_ptr)&ci, coefs[k],
+                                                       (JDIMENSION)(c.by0 + r), 1, FALSE);
+      std::memcpy(blocks.data() + 64 * (c.blk + (long)r * c.bw), rows[0][c.bx0],
+                  sizeof(JBLOCK) * c.bw);
+    }
+  }
+  J.abort_(&ci);
+  J.destroy(&ci);
+  std::vector<uint8_t> planes((size_t)total * 64);
+  for (int k = 0; k < D.ncomp; ++k)
+    for (long b = D.c[k].blk; b < D.c[k].blk + (long)D.c[k].bh * D.c[k].bw; ++b)
+      kfb::jpg::idct_islow(blocks.data() + 64 * b, D.q[k], planes.data() + 64 * b);
+  for (int r = 0; r < H; ++r)
+    for (int c = 0; c < W; ++c) {
+      int px[3];
+      kfb::jpg::pixel_rgb(planes.data(), D, r, c, px);
+      for (int k = 0; k < 3; ++k) rgb[((size_t)r * W + c) * 3 + k] = (uint8_t)px[k];
+    }
+  hw[0] = H;
+  hw[1] = W;
+  return 0;
+#else
+  (void)jpeg_bytes;
+  (void)len;
+  (void)rgb;
+  (void)cap;
+  (void)hw;
+  return -1;
+#endif
 }
 
 API void kfbrt_imgpipe_destroy(void* h) {

@@ -116,6 +116,9 @@ class PrefetchInput:
             self._thread.start()
 
     def _host(self, batch):
+        from .preprocessing import JpegBatch
+        if isinstance(batch, JpegBatch):
+            return batch  # (already in pinned ring buffers)
         ts = [torch.from_numpy(np.ascontiguousarray(x)) for x in batch]
         if self.device.type == "cuda":
             ts = [t.pin_memory() for t in ts]
@@ -148,6 +151,23 @@ class PrefetchInput:
             self._q.put(None)
 
     def _to_device(self, ts):
+        from .preprocessing import JpegBatch
+        if isinstance(ts, JpegBatch):
+            # coefficient blocks -> JPEG reconstruction + resize on the device
+            # (csrc/jpeg.hip), then the flip / colour / scaling pass
+            from ..ops import jpeg as J
+            from ..ops import nn as F
+            s, dev = ts.slot, self.device
+            descs = s.descs.to(dev, non_blocking=True)
+            blocks = s.blocks[:ts.nblocks].to(dev, non_blocking=True)
+            hosted = s.images.to(dev, non_blocking=True) if ts.hosted else None
+            prm = s.params.to(dev, non_blocking=True)
+            lab = s.labels.to(dev, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            s.ev = ev  # the slot may be refilled once these copies are done
+            u8 = J.decode(descs, blocks, hosted, ts.n, ts.height, ts.width)
+            return [F.augment_u8(u8, prm, self.dtype), lab]
         img = ts[0].to(self.device, non_blocking=True)
         if len(ts) == 3 and img.dtype == torch.uint8:
             # (uint8 images, labels, augmentation params): flip, colour

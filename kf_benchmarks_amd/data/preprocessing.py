@@ -38,6 +38,7 @@ Semantics kept from the reference:
 from __future__ import annotations
 
 import glob
+import itertools
 import io
 import math
 import os
@@ -499,12 +500,73 @@ class BaseImagePreprocessor(InputPreprocessor):
         return _batched(self, src, threads)
 
 
+class JpegBatch:
+    """One train batch in GPU-reconstruction form (ops/jpeg.decode): the
+    packed coefficient blocks of every crop plus descriptors, the images the
+    host decoded itself, augmentation parameters and labels - views of one
+    pinned ring slot, which the consumer marks with ``slot.ev`` once its
+    device copies are enqueued (the producer waits for that before refilling
+    the slot)."""
+    __slots__ = ("slot", "n", "nblocks", "hosted", "height", "width")
+
+    def __init__(self, slot, n, nblocks, hosted, height, width):
+        self.slot, self.n, self.nblocks, self.hosted = slot, n, nblocks, hosted
+        self.height, self.width = height, width
+
+
+class _JpegSlot:
+    # arena blocks per image of the batch (shared: large crops borrow from
+    # small ones; an image that does not fit is decoded on the host)
+    BLOCKS_PER_IMAGE = 4096
+
+    def __init__(self, n, height, width):
+        import torch
+        from .. import runtime
+        pin = torch.cuda.is_available()
+
+        def buf(shape, dtype):
+            t = torch.empty(shape, dtype=dtype)
+            return t.pin_memory() if pin else t
+        self.descs = buf((n * runtime.jpeg_desc_bytes(),), torch.uint8)
+        self.blocks = buf((n * self.BLOCKS_PER_IMAGE, 64), torch.int16)
+        self.images = buf((n, height, width, 3), torch.uint8)
+        self.params = buf((n, 8), torch.float32)
+        self.labels = buf((n,), torch.int32)
+        self.ev = None
+
+    def wait_free(self):
+        if self.ev is not None:
+            self.ev.synchronize()
+            self.ev = None
+
+
+_JPEG_RING = 6  # slots: prefetch queue depth + the batch being copied + 1
+
+
 def _batched(pre, records: Iterator[bytes], threads: int):
     """Yields (images [bs,h,w,3] uint8|float32, labels int32 [bs]) using a
     thread pool; the per-image RNG depends only on (batch, position) so the
     output is deterministic regardless of thread scheduling."""
     bs = pre.batch_size
     base = np.random.SeedSequence(pre.seed)
+    if getattr(pre, "gpu_jpeg", False) and _NATIVE_PIPE and runtime.coef_pipeline_available():
+        # host threads entropy-decode only; reconstruction on the GPU
+        pipe = runtime.ImagePipe(threads, pre.height, pre.width, pre.distortions,
+                                 pre.distort_color_in_yiq)
+        ring = [_JpegSlot(bs, pre.height, pre.width) for _ in range(_JPEG_RING)]
+        try:
+            for k in itertools.count():
+                recs = [next(records) for _ in range(bs)]
+                seeds = base.spawn(1)[0].generate_state(bs, dtype=np.uint64)
+                slot = ring[k % len(ring)]
+                slot.wait_free()
+                nblocks, hosted, bad = pipe.run_coef(recs, seeds, slot)
+                if bad > 0:
+                    raise ValueError("%d of %d image records in this batch could not be "
+                                     "decoded (corrupt TFRecord / JPEG data)" % (bad, bs))
+                yield JpegBatch(slot, bs, nblocks, hosted, pre.height, pre.width)
+        finally:
+            pipe.close()
     if getattr(pre, "device_augment", False) and _NATIVE_PIPE and runtime.ImagePipe.available():
         # every per-image step in native threads (csrc/runtime/kfb_images.cpp)
         pipe = runtime.ImagePipe(threads, pre.height, pre.width, pre.distortions,
@@ -807,5 +869,7 @@ def make_batch_iterator(bench, subset="train"):
     if (type(pre) is RecordInputImagePreprocessor and pre.train and _DEVICE_AUGMENT
             and getattr(bench, "device", None) is not None and bench.device.type == "cuda"):
         pre.device_augment = True
+        # KFB_GPU_JPEG=0: the host threads decode the whole JPEG
+        pre.gpu_jpeg = os.environ.get("KFB_GPU_JPEG", "1") != "0"
     shift = bench.task_index / float(max(bench.num_replicas, 1))
     return pre.minibatch(bench.dataset, subset, bench.params, shift_ratio=shift)

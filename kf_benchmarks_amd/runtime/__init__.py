@@ -405,6 +405,34 @@ class ImagePipe:
                                           labels.ctypes.data)
         return images, params, labels, bad
 
+    def run_coef(self, records, seeds, slot, positions=None):
+        """GPU-reconstruction form of :meth:`run` into the (pinned) buffers of
+        ``slot`` (``descs`` uint8, ``blocks`` int16 [cap, 64], ``images``,
+        ``params``, ``labels``): the host entropy-decodes and packs each
+        crop's coefficient blocks (ops/jpeg.decode finishes on the GPU);
+        images whose layout the device path does not cover are decoded here
+        into ``images``.  -> (blocks used, images decoded on the host,
+        undecodable images)."""
+        import numpy as np
+        lib = self._lib
+        if not getattr(lib, "_coef_sigs", False):
+            lib.kfbrt_imgpipe_run_coef.argtypes = [ctypes.c_void_p, ctypes.c_int] + \
+                [ctypes.c_void_p] * 6 + [ctypes.c_long] + [ctypes.c_void_p] * 4
+            lib.kfbrt_imgpipe_run_coef.restype = ctypes.c_int
+            lib._coef_sigs = True
+        n = len(records)
+        bufs = (ctypes.c_char_p * n)(*records)
+        lens = np.asarray([len(r) for r in records], dtype=np.uint64)
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+        pos = np.ascontiguousarray(np.arange(n) if positions is None else positions, dtype=np.int32)
+        out2 = (ctypes.c_long * 2)()
+        bad = lib.kfbrt_imgpipe_run_coef(
+            self._h, n, ctypes.cast(bufs, ctypes.c_void_p), lens.ctypes.data, seeds.ctypes.data,
+            pos.ctypes.data, slot.descs.data_ptr(), slot.blocks.data_ptr(),
+            slot.blocks.shape[0], slot.images.data_ptr(), slot.params.data_ptr(),
+            slot.labels.data_ptr(), out2)
+        return int(out2[0]), int(out2[1]), bad
+
     def close(self):
         if getattr(self, "_h", None):
             self._lib.kfbrt_imgpipe_destroy(self._h)
@@ -415,3 +443,54 @@ class ImagePipe:
             self.close()
         except Exception:
             pass
+
+
+def jpeg_desc_bytes() -> int:
+    lib = _load()
+    lib.kfbrt_jpeg_desc_bytes.restype = ctypes.c_int
+    return int(lib.kfbrt_jpeg_desc_bytes())
+
+
+def coef_pipeline_available() -> bool:
+    """The host half of the GPU JPEG path (libjpeg with
+    jpeg_read_coefficients) is loadable."""
+    if not ImagePipe.available():
+        return False
+    try:
+        return jpeg_desc_bytes() > 0
+    except (OSError, AttributeError):
+        return False
+
+
+def jpeg_reconstruct(descs, n, blocks, images, height, width, out):
+    """Host reference of csrc/jpeg.hip (numpy arrays; ``out`` uint8
+    [n, height, width, 3] is filled)."""
+    import numpy as np
+    lib = _load()
+    lib.kfbrt_jpeg_reconstruct.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_long, ctypes.c_void_p, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_void_p]
+    lib.kfbrt_jpeg_reconstruct.restype = None
+    descs = np.ascontiguousarray(descs)
+    blocks = np.ascontiguousarray(blocks, dtype=np.int16)
+    img = None if images is None else np.ascontiguousarray(images)
+    lib.kfbrt_jpeg_reconstruct(descs.ctypes.data, int(n), blocks.ctypes.data, blocks.size // 64,
+                               None if img is None else img.ctypes.data, int(height), int(width),
+                               out.ctypes.data)
+    return out
+
+
+def jpeg_decode_coef(data: bytes):
+    """Test hook: the whole JPEG through the coefficient path (host form) ->
+    uint8 [h, w, 3], or None when its layout is not covered."""
+    import numpy as np
+    lib = _load()
+    lib.kfbrt_jpeg_decode_coef.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p,
+                                           ctypes.c_size_t, ctypes.c_void_p]
+    cap = 64 << 20
+    buf = np.empty((cap,), np.uint8)
+    hw = (ctypes.c_int * 2)()
+    if lib.kfbrt_jpeg_decode_coef(data, len(data), buf.ctypes.data, cap, hw) != 0:
+        return None
+    h, w = hw[0], hw[1]
+    return buf[:h * w * 3].reshape(h, w, 3).copy()
