@@ -115,7 +115,7 @@ def main(argv=None):
                       gradient_wire_dtype=a.wire_dtype, display_every=10**9,
                       all_reduce_spec=a.all_reduce_spec, hierarchical_copy=a.hierarchical_copy,
                       launch_tape=(bool(a.launch_tape) if a.launch_tape >= 0 else
-                                   (a.gpus == 1 and cuda and not a.data_dir)),
+                                   (a.gpus == 1 and cuda)),
                       data_dir=a.data_dir,
                       datasets_num_private_threads=a.input_threads or None,
                       datasets_repeat_cached_sample=bool(a.data_dir),

@@ -497,8 +497,12 @@ class BenchmarkCNN:
             why = self.strategy.tape_blocker()
             if why is not None:
                 return why
-        if not self.dataset.use_synthetic_gpu_inputs() or getattr(self, "fake_data", None):
+        if getattr(self, "fake_data", None):
             return "host-side input pipeline"
+        if not self.dataset.use_synthetic_gpu_inputs():
+            from .data.input_pipeline import PrefetchInput
+            if not (isinstance(self.input, PrefetchInput) and self.input.tape_capable()):
+                return "host-side input pipeline"
         if self.enable_auto_loss_scale:
             return "dynamic loss scaling reads the gradients on the host"
         if p.staged_vars or self.l2_mask is not None:
@@ -560,6 +564,7 @@ class BenchmarkCNN:
                 return e.outputs
             self._tape = t
             self._tape_loss = t.outputs[0]
+            self.input.tape_post()
             log_fn("launch tape: recorded %d native calls (per-step arguments: %s)"
                    % (len(t.recorder), ", ".join(t.recorder.keys()) or "none"))
             return loss, acc
@@ -573,6 +578,7 @@ class BenchmarkCNN:
         vals = self._tape_values(step)
         t.replay(vals)
         self.strategy.tape_post(step)
+        self.input.tape_post()
         self.global_step += 1
         loss = self._tape_loss
         if l2 is not None:

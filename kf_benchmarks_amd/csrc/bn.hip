@@ -1323,12 +1323,12 @@ static int flat_grid(long nvec) { return (int)((nvec + 256L * 4 - 1) / (256L * 4
 // The folded forms apply when the channels fit LDS and the tensor takes the
 // grid-stride pass (the flat pass of the >= 256 MB tensors keeps its
 // finalize launch): KFB_BN_FOLD=0 never.
-static int g_bn_fold = -1;  // -1: KFB_BN_FOLD (default on); kfb_bn_set_fold overrides
+static int g_bn_fold = -1;  // -1: KFB_BN_FOLD (default off); kfb_bn_set_fold overrides
 
 static bool fold_ok(long nvec, int C, int V) {
   if (g_bn_fold < 0) {
     const char* e = getenv("KFB_BN_FOLD");
-    g_bn_fold = (e && atoi(e) == 0) ? 0 : 1;
+    g_bn_fold = (e && atoi(e) != 0) ? 1 : 0;
   }
   const bool on = g_bn_fold != 0;
   const int cv = C / V;

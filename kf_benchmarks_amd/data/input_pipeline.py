@@ -50,6 +50,9 @@ class SyntheticInput:
         s = self.seed + self.step
         return {"input_seed": s & 0xFFFFFFFF, "input_seed_labels": (s + 1) & 0xFFFFFFFF}
 
+    def tape_post(self):
+        pass
+
     def close(self):
         pass
 
@@ -202,7 +205,59 @@ class PrefetchInput:
             return out, ev
         return self._to_device(item), None
 
+    # ---------------------------------------------------------- launch tape
+    # A taped step starts with native copies of the current batch (its device
+    # addresses per-step values) into buffers the tape owns, behind a
+    # recorded wait on the copy stream; the batch after it is fetched between
+    # replays (tape_post), so the recorded wait covers only this batch's
+    # copy / decode / augmentation work.
+    def tape_capable(self) -> bool:
+        return self._stream is not None
+
+    def _tape_next(self):
+        from ..ops import _native as N
+        if self._next is None:
+            self._next = self._fetch()
+        out, _ = self._next
+        self._next = None
+        cur = torch.cuda.current_stream(self.device)
+        for t in out:
+            t.record_stream(cur)
+        self._cur = out
+        N.stream_wait(cur.cuda_stream, self._stream.cuda_stream)
+        bufs = []
+        for i, t in enumerate(out):
+            b = torch.empty_like(t)
+            N.call("kfb_memcpy_d2d", b.data_ptr(), N.dyn("input_%d" % i, t.data_ptr()),
+                   t.numel() * t.element_size(), cur.cuda_stream)
+            bufs.append(b)
+        return tuple(bufs)
+
+    def tape_advance(self):
+        if self._next is None:
+            self._next = self._fetch()
+        out, _ = self._next
+        self._next = None
+        cur = torch.cuda.current_stream(self.device)
+        for t in out:
+            t.record_stream(cur)
+        self._cur = out
+
+    def tape_values(self):
+        return {"input_%d" % i: t.data_ptr() for i, t in enumerate(self._cur)}
+
+    def tape_post(self):
+        """Prefetch the next batch (after the taped step was enqueued)."""
+        if self._next is None:
+            try:
+                self._next = self._fetch()
+            except StopIteration:
+                self._exhausted = True
+
     def next(self):
+        from ..ops import _native as N
+        if N.recording() and self._stream is not None:
+            return self._tape_next()
         if self._next is None:
             self._next = self._fetch()
         out, ev = self._next

@@ -15,9 +15,9 @@ for mb in $MODELS; do
   extra="${extra//,/ }"
   echo "== $m bs $b $extra"
   timeout -k 10 300 python bench.py --model "$m" --batch_size "$b" --steps 10 --warmup 3 $extra \
-      > "$OUT/$m.log" 2>&1
+      > "$OUT/${m}_${b}.log" 2>&1
   rc=$?
-  tail -n 1 "$OUT/$m.log"
+  tail -n 1 "$OUT/${m}_${b}.log"
   case $rc in 0) ;; 124|134|137|139) echo "FATAL rc=$rc in $m"; exit $rc;; *) echo "rc=$rc";; esac
 done
 echo done

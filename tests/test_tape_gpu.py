@@ -212,7 +212,7 @@ def _replay_mode(request):
     from kf_benchmarks_amd.ops import _native as N
     N.load().kfb_tape_set_raw(1 if request.param == "raw" else 0)
     yield request.param
-    N.load().kfb_tape_set_raw(1)
+    N.load().kfb_tape_set_raw(0)
 
 
 def test_tape_bitwise_matches_eager(cuda, _deterministic, _replay_mode):
@@ -232,7 +232,9 @@ def test_tape_bitwise_matches_eager(cuda, _deterministic, _replay_mode):
 def test_raw_tape_records_launch_arguments(cuda):
     """The raw replay re-issues the kernel with the argument bytes captured
     at record time (pointers included): new input contents, same buffers."""
+    from kf_benchmarks_amd.ops import _native as N
     from kf_benchmarks_amd.ops import tape as T
+    N.load().kfb_tape_set_raw(1)
     a = torch.randn(1 << 16, device=cuda).to(torch.bfloat16)
     b = torch.randn(1 << 16, device=cuda).to(torch.bfloat16)
     t = T.StepTape(cuda)
@@ -245,6 +247,7 @@ def test_raw_tape_records_launch_arguments(cuda):
         torch.cuda.synchronize()
         assert y2.data_ptr() == y.data_ptr()
         assert torch.equal(y2, a + b)
+    N.load().kfb_tape_set_raw(0)
 
 
 def test_tape_oracle_catches_a_dropped_op(cuda, _deterministic, monkeypatch):
@@ -268,3 +271,37 @@ def test_tape_oracle_catches_a_dropped_op(cuda, _deterministic, monkeypatch):
     assert dropped and t["replays"] == 3
     bad = _same(e1, t)
     assert "weights" in bad and any("moving" in k for k in bad), bad
+
+
+def _real_records(d, n=48):
+    import os
+    import numpy as np
+    from kf_benchmarks_amd import runtime
+    from kf_benchmarks_amd.data.test_data import encode_jpeg, image_example
+    rng = np.random.default_rng(0)
+    os.makedirs(d, exist_ok=True)
+    with runtime.TFRecordWriter(os.path.join(d, "train-00000-of-00001")) as w:
+        for i in range(n):
+            h, wd = (int(v) for v in rng.integers(60, 200, 2))
+            img = rng.normal(128, 50, (h, wd, 3)).clip(0, 255).astype(np.uint8)
+            w.write(image_example("i%d" % i, encode_jpeg(img, 85), i % 10 + 1, "n%d" % i, "x",
+                                  [[0.1, 0.1, 0.9, 0.9]], h, wd))
+
+
+@pytest.mark.parametrize("gpu_jpeg", ["1", "0"], ids=["gpu_jpeg", "host_jpeg"])
+def test_real_data_step_tapes(cuda, tmp_path, monkeypatch, gpu_jpeg):
+    """Real TFRecord/JPEG input (host entropy decode, GPU reconstruction and
+    augmentation on the copy stream): the taped step starts with native
+    copies of the current batch into tape-owned buffers (per-step source
+    addresses) behind a recorded wait on the copy stream; the next batch is
+    fetched between replays.  Same images per step as eager, so the
+    trajectories agree."""
+    monkeypatch.setenv("KFB_GPU_JPEG", gpu_jpeg)
+    _real_records(str(tmp_path))
+    kw = dict(data_dir=str(tmp_path), data_name="imagenet")
+    le, we, _ = _run("resnet50", "momentum", False, **kw)
+    lt, wt, replays = _run("resnet50", "momentum", True, **kw)
+    assert replays == 3
+    for a, b in zip(le, lt):
+        assert abs(a - b) <= 2.5e-2 * max(1.0, abs(a)), (le, lt)
+    assert (wt - we).abs().max().item() <= 2e-2
