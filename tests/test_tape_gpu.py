@@ -300,8 +300,14 @@ def test_real_data_step_tapes(cuda, tmp_path, monkeypatch, gpu_jpeg):
     _real_records(str(tmp_path))
     kw = dict(data_dir=str(tmp_path), data_name="imagenet")
     le, we, _ = _run("resnet50", "momentum", False, **kw)
+    le2, we2, _ = _run("resnet50", "momentum", False, **kw)
     lt, wt, replays = _run("resnet50", "momentum", True, **kw)
     assert replays == 3
-    for a, b in zip(le, lt):
-        assert abs(a - b) <= 2.5e-2 * max(1.0, abs(a)), (le, lt)
-    assert (wt - we).abs().max().item() <= 2e-2
+    # (bound as test_tape_matches_eager: the eager run-to-run spread of the
+    # BN-statistics atomics, amplified by bf16 training at batch 8)
+    spread = 0.0
+    for a, a2, b in zip(le, le2, lt):
+        spread = max(spread, abs(a - a2))
+        assert abs(a2 - b) <= max(4 * spread, 2.5e-2 * max(1.0, abs(a2))), (le, le2, lt)
+    ref = (we - we2).abs().max().item()
+    assert (wt - we2).abs().max().item() <= max(4 * ref, 1e-3), ref

@@ -300,3 +300,19 @@ def test_hierarchical_copy_eight_workers(tmp_path):
     expected = tu.manually_compute_losses(tu.get_fake_var_update_inputs(), 8, params, "sum")
     for r in range(8):
         np.testing.assert_allclose(res[r]["losses"], expected[r], rtol=1e-5, atol=0)
+
+
+def test_strategy_tape_hooks():
+    """Launch-tape hooks of the KungFu strategies (the GPU tests replay
+    them): ada_sgd's three launch sequences re-record the tape at the
+    switch; the averaging strategies accept taping, per-step collectives
+    are declared."""
+    from kf_benchmarks_amd.parallel import variable_mgr as vm
+    from kf_benchmarks_amd.parallel.kungfu import PairAveraging
+    ada = vm.KungFuAdaSGD.__new__(vm.KungFuAdaSGD)
+    ada.switch_step = 4
+    phases = [ada.tape_phase(s) for s in range(7)]
+    assert phases == [(True, True)] * 3 + [(True, False)] + [(False, False)] * 3
+    assert ada.steps_use_collectives() and vm.KungFuSMA.steps_use_collectives(None)
+    assert not PairAveraging.steps_use_collectives(None)
+    assert vm.IndependentStrategy.tape_blocker(None) is None
