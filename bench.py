@@ -261,6 +261,9 @@ def main(argv=None):
         print(json.dumps(out))
         sys.stdout.flush()
     bench.strategy.close()  # collective: model stores / peers released on every rank
+    close_input = getattr(getattr(bench, "input", None), "close", None)
+    if close_input is not None:
+        close_input()  # input producer threads stopped before interpreter exit
     world.shutdown()
     return 0
 

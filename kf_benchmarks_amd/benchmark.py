@@ -889,6 +889,8 @@ class BenchmarkCNN:
             self.saver.save(p.train_dir, self.global_step)
         tracer.finish()
         self.strategy.close()
+        if getattr(self, "input", None) is not None:
+            self.input.close()
         if self.cluster_manager is not None:
             self.world.barrier(self.device if self.device_type == "cuda" else None)
             if self.world.is_chief:

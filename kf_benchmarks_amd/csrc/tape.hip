@@ -254,11 +254,11 @@ void raw_taint() {
 
 using namespace kfb::tape;
 
-// KFB_TAPE_RAW=1 (or kfb_tape_set_raw(1)): ops replay their recorded raw
-// launches; otherwise every op replays through its entry point
+// KFB_TAPE_RAW=0 (or kfb_tape_set_raw(0)): every op replays through its
+// entry point instead of its recorded raw launches
 static int g_raw_replay = [] {
   const char* e = getenv("KFB_TAPE_RAW");
-  return (e && atoi(e) != 0) ? 1 : 0;
+  return (e && atoi(e) == 0) ? 0 : 1;
 }();
 
 KFB_API void kfb_tape_set_raw(int on) { g_raw_replay = on ? 1 : 0; }

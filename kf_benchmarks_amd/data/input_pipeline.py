@@ -274,9 +274,31 @@ class PrefetchInput:
         return tuple(out)
 
     def close(self):
+        """Stops the producer and closes the batch generator (its native
+        worker pool) before the process exits: a producer thread left inside
+        a native call or a pinned-memory copy at interpreter shutdown can
+        abort the process."""
         self._stop.set()
         if self.producer is not None:
             self.producer.done()
+            return
+        t = getattr(self, "_thread", None)
+        for _ in range(100):  # unblock a put on a full queue until the producer sees _stop
+            if t is None or not t.is_alive():
+                break
+            try:
+                while True:
+                    self._q.get_nowait()
+            except queue.Empty:
+                pass
+            t.join(timeout=0.1)
+        if t is None or not t.is_alive():
+            close = getattr(self._it, "close", None)
+            if close is not None:
+                try:
+                    close()  # generator finally: the native pipe's threads are joined
+                except Exception:  # noqa: BLE001 - best effort at shutdown
+                    pass
 
 
 def make_input_source(bench, subset="train"):

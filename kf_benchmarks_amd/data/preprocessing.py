@@ -869,8 +869,8 @@ def make_batch_iterator(bench, subset="train"):
     if (type(pre) is RecordInputImagePreprocessor and pre.train and _DEVICE_AUGMENT
             and getattr(bench, "device", None) is not None and bench.device.type == "cuda"):
         pre.device_augment = True
-        # KFB_GPU_JPEG=1: host threads entropy-decode only, reconstruction on
-        # the GPU (csrc/jpeg.hip); otherwise they decode the whole JPEG
-        pre.gpu_jpeg = os.environ.get("KFB_GPU_JPEG", "0") == "1"
+        # host threads entropy-decode only, reconstruction on the GPU
+        # (csrc/jpeg.hip); KFB_GPU_JPEG=0: they decode the whole JPEG
+        pre.gpu_jpeg = os.environ.get("KFB_GPU_JPEG", "1") != "0"
     shift = bench.task_index / float(max(bench.num_replicas, 1))
     return pre.minibatch(bench.dataset, subset, bench.params, shift_ratio=shift)

@@ -87,7 +87,9 @@ _ig_tuned = {}
 _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
 _NO_S3 = os.environ.get("KFB_IGEMM_NOS3", "0") == "1"  # A/B knob: drop IG_S3
 _NO_S1 = os.environ.get("KFB_IGEMM_NOS1", "0") == "1"  # A/B knob: drop IG_S1
-_NO_S7 = os.environ.get("KFB_IGEMM_NOS7", "1") == "1"  # A/B knob: IG_S7 in the autotune (=0)
+# A/B knob: drop IG_S7 (in-network 18.87 / 18.87 vs 19.31 / 19.35 ms/step without it,
+# gpurun_out/r10o, profiles/r10_round4_ab.txt)
+_NO_S7 = os.environ.get("KFB_IGEMM_NOS7", "0") == "1"
 _NO_GSHORT = os.environ.get("KFB_IGEMM_NOGSHORT", "0") == "1"  # A/B knob: drop IG_GSHORT*
 _GSHORT3 = os.environ.get("KFB_IGEMM_GSHORT3", "1") != "0"  # A/B knob: the 3-stage forms
 _NO_MULTI = os.environ.get("KFB_IGEMM_NOMULTI", "0") == "1"  # A/B knob: drop IG_*MULTI*

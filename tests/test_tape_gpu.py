@@ -212,7 +212,7 @@ def _replay_mode(request):
     from kf_benchmarks_amd.ops import _native as N
     N.load().kfb_tape_set_raw(1 if request.param == "raw" else 0)
     yield request.param
-    N.load().kfb_tape_set_raw(0)
+    N.load().kfb_tape_set_raw(1)
 
 
 def test_tape_bitwise_matches_eager(cuda, _deterministic, _replay_mode):
@@ -247,7 +247,6 @@ def test_raw_tape_records_launch_arguments(cuda):
         torch.cuda.synchronize()
         assert y2.data_ptr() == y.data_ptr()
         assert torch.equal(y2, a + b)
-    N.load().kfb_tape_set_raw(0)
 
 
 def test_tape_oracle_catches_a_dropped_op(cuda, _deterministic, monkeypatch):
