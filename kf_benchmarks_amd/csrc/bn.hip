@@ -675,9 +675,28 @@ struct BnFoldB {
   int accumulate;
 };
 
-// sum over the nslab slots of channel c, 8 independent loads per array in flight
+// sum over the nslab slots of channel c: up to 32 slots with every load in
+// flight at once (one L2 round trip before the pass can start), beyond
+// that 8 independent loads per array per batch
 __device__ __forceinline__ void fold_ch(const float* __restrict__ pa, const float* __restrict__ pb,
                                         int nslab, int C, int c, double& sa, double& sb) {
+  if (nslab <= 32) {
+    float va[32], vb[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      va[u] = u < nslab ? pa[(long)u * C + c] : 0.f;
+      vb[u] = u < nslab ? pb[(long)u * C + c] : 0.f;
+    }
+    float a4[4] = {0.f, 0.f, 0.f, 0.f}, b4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      a4[u & 3] += va[u];
+      b4[u & 3] += vb[u];
+    }
+    sa = ((double)a4[0] + (double)a4[1]) + ((double)a4[2] + (double)a4[3]);
+    sb = ((double)b4[0] + (double)b4[1]) + ((double)b4[2] + (double)b4[3]);
+    return;
+  }
   float a[8], b[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) { a[u] = 0.f; b[u] = 0.f; }
