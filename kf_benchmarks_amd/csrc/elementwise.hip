@@ -555,6 +555,7 @@ KFB_API hipError_t kfb_wrelayout(int dtype, const void* src, void* dst, int cout
 // apool with a 1x1 window) and NASNet's one-pixel shift before its second
 // factorized-reduction path (tcb/models/nasnet_utils.py
 // _factorized_reduction: pad + slice).  V channels per thread.
+namespace kfb {
 template <typename T, int V>
 __global__ void __launch_bounds__(256)
 window_k(const T* __restrict__ src, T* __restrict__ dst, long total, int H, int W, int C,
@@ -593,6 +594,7 @@ window_k(const T* __restrict__ src, T* __restrict__ dst, long total, int H, int 
     *(Vec<T, V>*)(dst + i * V) = v;
   }
 }
+}  // namespace kfb
 
 KFB_API hipError_t kfb_window(int dtype, const void* src, void* dst, int N, int H, int W, int C,
                               int OH, int OW, int sh, int sw, int oh0, int ow0, int adjoint,
@@ -603,7 +605,7 @@ KFB_API hipError_t kfb_window(int dtype, const void* src, void* dst, int N, int 
   if (total == 0) return hipSuccess;
   KFB_DISPATCH_DTYPE(dtype, T, {
     KFB_DISPATCH_VEC(V, VV, {
-      hipLaunchKernelGGL((window_k<T, VV>), dim3(egrid(total)), dim3(256), 0, stream,
+      hipLaunchKernelGGL((kfb::window_k<T, VV>), dim3(egrid(total)), dim3(256), 0, stream,
                          (const T*)src, (T*)dst, total, H, W, C, OH, OW, sh, sw, oh0, ow0,
                          adjoint);
     });

@@ -292,10 +292,10 @@ class ModelStore:
         if self.device_check:
             N.call("kfb_seqlock_check", N.dyn("pa_word", vals["pa_word"]),
                    N.dyn("pa_seq", vals["pa_seq"]), self.ok.data_ptr(), self.torn.data_ptr(), ps)
-        ev = None
-        if not self.device_check:
-            ev = torch.cuda.Event()
-            ev.record(self.pull_stream)
+        # (finish_pull's host-side wait; the device-validated path orders the
+        # consumer with a native stream wait instead)
+        ev = torch.cuda.Event()
+        ev.record(self.pull_stream)
         peer, slot = vals["_pa"]
         self._inflight = (peer, slot, vals["pa_seq"], ev, out)
 

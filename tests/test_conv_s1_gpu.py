@@ -102,7 +102,10 @@ def test_s1_dgrad_fused_epilogue(s1, cuda, shape, mask_src, with_addend, grid, K
     torch.testing.assert_close(p[1], s2_, rtol=1e-2, atol=tol)
 
 
-def test_s1_finalizes_bn(s1, cuda):
+def test_s1_finalizes_bn(s1, cuda, monkeypatch):
+    # (forward finalize tails: KFB_BN_FIN=1; the default "grad" mode keeps
+    # them for the data-gradient kernels only)
+    monkeypatch.setattr(conv_hip, "_BN_FIN_MODE", "1")
     n, H, W = 8, 28, 28
     g = torch.Generator().manual_seed(9)
     x = torch.randn(n, H, W, 64, generator=g).to(torch.bfloat16).to(cuda)

@@ -16,11 +16,12 @@ def _strict(monkeypatch):
 
 def _run(model, optimizer, tape, steps=6, bs=8, **kw):
     steps = kw.pop("steps", steps)
+    lr = kw.pop("lr", 0.002)
     from kf_benchmarks_amd import params as P
     from kf_benchmarks_amd.benchmark import BenchmarkCNN
     p = P.make_params(model=model, batch_size=bs, num_gpus=1, use_bf16=True,
                       optimizer=optimizer, data_format="NHWC", variable_update="kungfu",
-                      launch_tape=tape, init_learning_rate=0.002, display_every=10 ** 9, **kw)
+                      launch_tape=tape, init_learning_rate=lr, display_every=10 ** 9, **kw)
     b = BenchmarkCNN(p)
     b.build()
     losses = []
@@ -297,16 +298,15 @@ def test_real_data_step_tapes(cuda, tmp_path, monkeypatch, gpu_jpeg):
     trajectories agree."""
     monkeypatch.setenv("KFB_GPU_JPEG", gpu_jpeg)
     _real_records(str(tmp_path))
-    kw = dict(data_dir=str(tmp_path), data_name="imagenet")
+    # a small learning rate keeps bf16 training at batch 8 from amplifying the
+    # run-to-run spread of the statistics atomics: each step's loss is then
+    # set by its batch, and a replay that fed another batch (or a stale one)
+    # is off by far more than the bound
+    kw = dict(data_dir=str(tmp_path), data_name="imagenet", lr=1e-5)
     le, we, _ = _run("resnet50", "momentum", False, **kw)
-    le2, we2, _ = _run("resnet50", "momentum", False, **kw)
     lt, wt, replays = _run("resnet50", "momentum", True, **kw)
     assert replays == 3
-    # (bound as test_tape_matches_eager: the eager run-to-run spread of the
-    # BN-statistics atomics, amplified by bf16 training at batch 8)
-    spread = 0.0
-    for a, a2, b in zip(le, le2, lt):
-        spread = max(spread, abs(a - a2))
-        assert abs(a2 - b) <= max(4 * spread, 2.5e-2 * max(1.0, abs(a2))), (le, le2, lt)
-    ref = (we - we2).abs().max().item()
-    assert (wt - we2).abs().max().item() <= max(4 * ref, 1e-3), ref
+    assert len(set(round(v, 3) for v in le)) == len(le)  # the batches differ
+    for a, b in zip(le, lt):
+        assert abs(a - b) <= 5e-3 * max(1.0, abs(a)), (le, lt)
+    assert (wt - we).abs().max().item() <= 1e-3
