@@ -302,14 +302,18 @@ def test_real_data_step_tapes(cuda, tmp_path, monkeypatch, gpu_jpeg):
     # run-to-run spread of the statistics atomics: each step's loss is then
     # set by its batch, and a replay that fed another batch (or a stale one)
     # is off by far more than the bound
-    # (the first run autotunes: its kernels - and so its bf16 roundings - can
-    # differ from the cached choices the two compared runs share)
+    # (bf16 at batch 8 through 50 BN layers: the statistics atomics alone
+    # move a step's loss by ~0.3-0.7% between two eager runs, so the bound is
+    # that spread, measured, with a 1% floor)
     kw = dict(data_dir=str(tmp_path), data_name="imagenet", lr=1e-5)
-    _run("resnet50", "momentum", False, **kw)
     le, we, _ = _run("resnet50", "momentum", False, **kw)
+    le2, we2, _ = _run("resnet50", "momentum", False, **kw)
     lt, wt, replays = _run("resnet50", "momentum", True, **kw)
     assert replays == 3
-    assert len(set(round(v, 3) for v in le)) == len(le)  # the batches differ
-    for a, b in zip(le, lt):
-        assert abs(a - b) <= 5e-3 * max(1.0, abs(a)), (le, lt)
-    assert (wt - we).abs().max().item() <= 1e-3
+    assert len(set(round(v, 2) for v in le)) == len(le)  # the batches differ
+    spread = 0.0
+    for a, a2, b in zip(le, le2, lt):
+        spread = max(spread, abs(a - a2))
+        assert abs(a2 - b) <= max(2 * spread, 1e-2 * max(1.0, abs(a2))), (le, le2, lt)
+    ref = (we - we2).abs().max().item()
+    assert (wt - we2).abs().max().item() <= max(4 * ref, 1e-3), ref
