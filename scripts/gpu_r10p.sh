@@ -21,6 +21,8 @@ run() {
   echo "$name rc=$rc $(grep -o '"value": [0-9.]*' "$OUT/$name.log") $(grep -o '"ms_per_step": [0-9.]*' "$OUT/$name.log") $(grep -o '"launch_tape": [a-z]*' "$OUT/$name.log")"
   case $rc in 0) ;; *) exit $rc;; esac
 }
+step probe 120 python -u scripts/tape_launch_probe.py
+step realtape 400 python -u -m pytest -x -q -p no:cacheprovider --timeout-method thread --timeout 300 tests/test_tape_gpu.py -k real_data
 step foldtest 400 python -u -m pytest -x -q -p no:cacheprovider --timeout-method thread --timeout 300 tests/test_bn_fin_gpu.py
 for r in 1 2; do
   run off_$r "" KFB_BN_FOLD=0

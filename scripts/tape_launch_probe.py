@@ -4,12 +4,15 @@ tensors, a chain on one stream) replayed raw (hipLaunchKernel from the
 recorded arguments) and through the entry points (libffi + host logic);
 host time per launch without waiting for the GPU, and GPU-inclusive time
 per launch with a synchronize after each replay."""
+import sys
 import time
 
-import torch
+sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
 
-from kf_benchmarks_amd.ops import _native as N
-from kf_benchmarks_amd.ops import tape as T
+import torch  # noqa: E402
+
+from kf_benchmarks_amd.ops import _native as N  # noqa: E402
+from kf_benchmarks_amd.ops import tape as T  # noqa: E402
 
 
 def main(n=1000, reps=20):
