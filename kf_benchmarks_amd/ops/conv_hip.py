@@ -552,6 +552,11 @@ def _wgrad_launch(dy, x, dw, geo, target):
 # KFB_CONV_AUTOTUNE=0 pins _WGRAD_TARGET_BLOCKS.
 _AUTOTUNE = os.environ.get("KFB_CONV_AUTOTUNE", "1") != "0" and "KFB_WGRAD_BLOCKS" not in os.environ
 _WGRAD_CANDIDATES = (384, 512, 768, 1024)
+# KFB_WGRAD_MAXBLOCKS: drop larger workgroup targets (fewer reduction splits,
+# less slab traffic beside the compute stream; in-network A/B knob)
+if os.environ.get("KFB_WGRAD_MAXBLOCKS"):
+    _WGRAD_CANDIDATES = tuple(t for t in _WGRAD_CANDIDATES
+                              if t <= int(os.environ["KFB_WGRAD_MAXBLOCKS"])) or (384,)
 # bit 16 of a candidate selects the LDS-DMA wgrad kernel (wgrad_glds_k: 128-wide
 # output-channel tiles, operands < 2 GiB); KFB_WGRAD_ALGO=classic|glds pins one
 _WGRAD_GLDS = 1 << 16
