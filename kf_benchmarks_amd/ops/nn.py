@@ -779,10 +779,12 @@ N.register_optional("kfb_bn_pool_num_slabs", [N.I] * 8, N.c_int)
 N.register_optional("kfb_bn_relu_maxpool_bwd", [N.I, N.P, N.P, N.P, N.P, N.P] + [N.I] * 12 +
                     [N.P] * 7 + [N.I] + [N.P] * 3 + [N.I, N.I, N.P])
 
-# KFB_POOL_LINK=1: the stem BN+ReLU+max-pool backward takes its BN partials
-# from its consumers' dgrad epilogue (sum dz', sum dz' (z - beta), rescaled by
-# 1 / (gamma * invstd)) instead of its own pass over x
-_POOL_LINK = os.environ.get("KFB_POOL_LINK", "0") == "1"
+# The stem BN+ReLU+max-pool backward takes its BN partials from its
+# consumers' dgrad epilogue (sum dz', sum dz' (z - beta), rescaled by
+# 1 / (gamma * invstd)) instead of its own pass over x.  Default since round
+# 4: 18.93 / 18.75 / 18.72 vs 19.09 / 19.06 / 18.82 ms/step interleaved
+# (gpurun_out/r10t, profiles/r10_round4_ab.txt); KFB_POOL_LINK=0 turns it off.
+_POOL_LINK = os.environ.get("KFB_POOL_LINK", "1") == "1"
 
 
 # Called once at the top of the stem BN+ReLU+max-pool backward (the point
