@@ -333,6 +333,16 @@ KFB_API int kfb_tape_end_op(void* h, int op, int allow_raw) {
   return o.raw_ok ? 1 : 0;
 }
 
+// Device operations (launches, memsets, waits, copies) the raw ops re-issue per replay.
+KFB_API long kfb_tape_raw_launches(void* h) {
+  Tape* t = (Tape*)h;
+  if (!t) return -1;
+  long n = 0;
+  for (const Op& o : t->ops)
+    if (o.raw_ok && !o.patched) n += (long)o.raw.size();
+  return n;
+}
+
 // Number of ops a replay re-issues raw (the rest call their entry point).
 KFB_API int kfb_tape_raw_ops(void* h) {
   Tape* t = (Tape*)h;

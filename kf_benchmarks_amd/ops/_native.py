@@ -58,6 +58,7 @@ _SIGS = {
     "kfb_tape_begin_op": [P, I],
     "kfb_tape_end_op": [P, I, I],
     "kfb_tape_raw_ops": [P],
+    "kfb_tape_raw_launches": [P],
     "kfb_tape_set_raw": [I],
     "kfb_host_register": [P, ctypes.c_size_t, P],
     "kfb_host_unregister": [P],
@@ -105,7 +106,8 @@ _SIGS = {
 }
 _RESTYPES = {"kfb_bn_num_slabs": c_int, "kfb_colsum_num_slabs": c_int,
              "kfb_gemm_splits": c_int, "kfb_ctc_max_states": c_int, "kfb_tape_new": c_void_p,
-             "kfb_tape_free": None, "kfb_tape_set_raw": None}
+             "kfb_tape_free": None, "kfb_tape_set_raw": None,
+             "kfb_tape_raw_launches": ctypes.c_long}
 # Optional symbols (added by later kernel files); bound if present.
 _OPTIONAL = {}
 

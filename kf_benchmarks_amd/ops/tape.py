@@ -179,8 +179,8 @@ class Recorder:
             by.setdefault(name, []).append(t)
         tot = sum(buf) / max(replays, 1)
         rows = sorted(by.items(), key=lambda kv: -sum(kv[1]))[:top]
-        out = ["tape host time per replayed step: %.3f ms over %d calls (%d raw)"
-               % (1e3 * tot, n, self.raw_ops())]
+        out = ["tape host time per replayed step: %.3f ms over %d calls (%d raw, %d device ops)"
+               % (1e3 * tot, n, self.raw_ops(), N.load().kfb_tape_raw_launches(self.h))]
         for name, ts in rows:
             out.append("  %-28s %5d calls %8.3f ms  %6.2f us/call" % (
                 name, len(ts), 1e3 * sum(ts) / max(replays, 1),

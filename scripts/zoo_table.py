@@ -24,7 +24,7 @@ def main():
             if not js:
                 continue
             r = json.loads(js[-1])
-            m = re.search(r"tape host time per replayed step: ([0-9.]+) ms over (\d+) calls \((\d+) raw\)",
+            m = re.search(r"tape host time per replayed step: ([0-9.]+) ms over (\d+) calls \((\d+) raw",
                           text)
             r["tape_host"] = (float(m.group(1)), int(m.group(2)), int(m.group(3))) if m else None
             name = os.path.basename(path)[:-4]
