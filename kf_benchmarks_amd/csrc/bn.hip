@@ -1354,12 +1354,18 @@ static bool fold_ok(long nvec, int C, int V) {
   const bool on = g_bn_fold != 0;
   const int cv = C / V;
   return on && V == 8 && C <= FOLD_CMAX && cv > 0 && (cv & (cv - 1)) == 0 && 256 % cv == 0 &&
-         !flat_ok(nvec, C, V) && nvec < (1L << 31) - 2L * FOLD_GRID * 256;
+         !flat_ok(nvec, C, V) && nvec < (1L << 31) - 2L * 4096 * 256;
 }
 
 static int fold_grid(long nvec) {
+  // KFB_BN_FOLD_GRID: workgroup cap of the folded passes (A/B knob, <= 4096)
+  static const long cap = [] {
+    const char* e = getenv("KFB_BN_FOLD_GRID");
+    const long v = e ? atol(e) : FOLD_GRID;
+    return v < 256 ? 256L : v > 4096 ? 4096L : v;
+  }();
   long b = (nvec + 255) / 256;
-  if (b > FOLD_GRID) b = FOLD_GRID;
+  if (b > cap) b = cap;
   return (int)(b < 1 ? 1 : b);
 }
 
