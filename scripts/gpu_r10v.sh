@@ -15,6 +15,6 @@ run() {
 }
 for r in 1 2; do
   run off_$r KFB_BN_FOLD=0
-  run f2048_$r KFB_BN_FOLD=1 KFB_BN_FOLD_GRID=2048
-  run f4096_$r KFB_BN_FOLD=1 KFB_BN_FOLD_GRID=4096
+  run f512_$r KFB_BN_FOLD=1 KFB_BN_FOLD_GRID=512
+  run f256_$r KFB_BN_FOLD=1 KFB_BN_FOLD_GRID=256
 done
