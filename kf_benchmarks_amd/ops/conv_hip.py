@@ -95,6 +95,8 @@ _GSHORT3 = os.environ.get("KFB_IGEMM_GSHORT3", "1") != "0"  # A/B knob: the 3-st
 _NO_MULTI = os.environ.get("KFB_IGEMM_NOMULTI", "0") == "1"  # A/B knob: drop IG_*MULTI*
 _NO_BIG = os.environ.get("KFB_IGEMM_NOBIG", "0") == "1"  # A/B knob: drop IG_GBIG*
 _SK = os.environ.get("KFB_IGEMM_SK", "0") == "1"  # offer IG_SK128 to the autotune
+# KFB_IGEMM_SK_SMALL=0: not even on the few-tile (small-batch) layers
+_SK_SMALL = os.environ.get("KFB_IGEMM_SK_SMALL", "1") != "0"
 # KFB_IGEMM_EARLY=1: offer the early-epilogue-operand kernels (IG_*_E) to the
 # autotune.  Off: at 3 workgroups per CU (their early operands stay live
 # through the K loop) they lost to the 4-workgroup one-stage kernel on every
@@ -395,11 +397,16 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
                 cands += (IG_GBIG256_32,)
         if 64 < ncol <= 256 and ((M + 511) // 512) * ((ncol + 127) // 128) >= 256:
             cands += (IG_GBIG512,)
-    if fast and _SK and C % 64 == 0 and ncol > 64:
+    M_ = geo[0] * geo[4] * geo[5]
+    few_tiles = ((M_ + 127) // 128) * ((ncol + 127) // 128) < 2 * 256
+    if fast and (_SK or (few_tiles and _SK_SMALL)) and C % 64 == 0 and ncol > 64:
         # stream-K: measured slower than the one-tile kernels on every
-        # ResNet-50 geometry (per-item setup, pipeline refill and the fix-up
-        # tail cost more than the partial round it removes at K <= 4608,
-        # profiles/r7_stream_k.txt); candidate only with KFB_IGEMM_SK=1
+        # ResNet-50 bs256 geometry (per-item setup, pipeline refill and the
+        # fix-up tail cost more than the partial round it removes at
+        # K <= 4608, profiles/r7_stream_k.txt); offered where a layer has
+        # fewer 128x128 tiles than two per CU (small batches: the one-tile
+        # kernels then leave CUs idle through a long K loop), and everywhere
+        # with KFB_IGEMM_SK=1
         cands += (IG_SK128,)
     if fast and C % 64 != 0:
         # 8-channel geometry: the generic loader competes with the FAST ones
