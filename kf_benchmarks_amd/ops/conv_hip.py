@@ -95,8 +95,10 @@ _GSHORT3 = os.environ.get("KFB_IGEMM_GSHORT3", "1") != "0"  # A/B knob: the 3-st
 _NO_MULTI = os.environ.get("KFB_IGEMM_NOMULTI", "0") == "1"  # A/B knob: drop IG_*MULTI*
 _NO_BIG = os.environ.get("KFB_IGEMM_NOBIG", "0") == "1"  # A/B knob: drop IG_GBIG*
 _SK = os.environ.get("KFB_IGEMM_SK", "0") == "1"  # offer IG_SK128 to the autotune
-# KFB_IGEMM_SK_SMALL=0: not even on the few-tile (small-batch) layers
-_SK_SMALL = os.environ.get("KFB_IGEMM_SK_SMALL", "1") != "0"
+# KFB_IGEMM_SK_SMALL=1: offer it on the few-tile (small-batch) layers
+# (neutral in the network: ResNet-152 bs32 14.02 / 14.06 vs 14.04 / 13.94 ms,
+# ResNet-50 bs64 7.09 / 7.04 vs 7.08 / 7.06; gpurun_out/r11a)
+_SK_SMALL = os.environ.get("KFB_IGEMM_SK_SMALL", "0") == "1"
 # KFB_IGEMM_EARLY=1: offer the early-epilogue-operand kernels (IG_*_E) to the
 # autotune.  Off: at 3 workgroups per CU (their early operands stay live
 # through the K loop) they lost to the 4-workgroup one-stage kernel on every
