@@ -1366,9 +1366,15 @@ static int g_bn_fold = -1;  // -1: KFB_BN_FOLD (default off); kfb_bn_set_fold ov
 static bool fold_ok(long nvec, int C, int V) {
   if (g_bn_fold < 0) {
     const char* e = getenv("KFB_BN_FOLD");
-    g_bn_fold = (e && atoi(e) != 0) ? 1 : 0;
+    g_bn_fold = e ? atoi(e) : 0;
   }
-  const bool on = g_bn_fold != 0;
+  // KFB_BN_FOLD=2: only tensors up to KFB_BN_FOLD_MAXMB (default 16) MB, where
+  // the removed launch boundary weighs most against the pass
+  static const long max_bytes = [] {
+    const char* e = getenv("KFB_BN_FOLD_MAXMB");
+    return (e ? atol(e) : 16L) << 20;
+  }();
+  const bool on = g_bn_fold == 1 || (g_bn_fold == 2 && nvec * 16 <= max_bytes);
   const int cv = C / V;
   return on && V == 8 && C <= FOLD_CMAX && C % FOLD_CB == 0 && cv > 0 &&
          !flat_ok(nvec, C, V) && nvec < (1L << 31) - 2L * 4096 * 256;
