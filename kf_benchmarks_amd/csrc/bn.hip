@@ -1361,18 +1361,21 @@ static int flat_grid(long nvec) { return (int)((nvec + 256L * 4 - 1) / (256L * 4
 // finalize launch): KFB_BN_FOLD=0 never.
 // default off: in-network +0.16..0.40 ms/step against the finalize launches
 // (gpurun_out/r10o: 19.27 / 19.03 with the fold vs 18.87 / 18.87 without)
-static int g_bn_fold = -1;  // -1: KFB_BN_FOLD (default off); kfb_bn_set_fold overrides
+static int g_bn_fold = -1;  // -1: KFB_BN_FOLD (0 never, 1 always, 2 small tensors: default)
 
 static bool fold_ok(long nvec, int C, int V) {
   if (g_bn_fold < 0) {
     const char* e = getenv("KFB_BN_FOLD");
-    g_bn_fold = e ? atoi(e) : 0;
+    g_bn_fold = e ? atoi(e) : 2;
   }
-  // KFB_BN_FOLD=2: only tensors up to KFB_BN_FOLD_MAXMB (default 16) MB, where
-  // the removed launch boundary weighs most against the pass
+  // mode 2 (the default): only tensors up to KFB_BN_FOLD_MAXMB (default 8) MB,
+  // where the removed launch boundary weighs most against the pass - the
+  // small-batch layers (ResNet-152 bs32 at 16 MB: 13.91 / 13.86 vs 13.99 /
+  // 14.02 ms); at batch 256 no BN tensor is that small (the folded passes
+  // lose there, profiles/r10_bn_fold_vs_launch.txt)
   static const long max_bytes = [] {
     const char* e = getenv("KFB_BN_FOLD_MAXMB");
-    return (e ? atol(e) : 16L) << 20;
+    return (e ? atol(e) : 8L) << 20;
   }();
   const bool on = g_bn_fold == 1 || (g_bn_fold == 2 && nvec * 16 <= max_bytes);
   const int cv = C / V;
@@ -1470,7 +1473,7 @@ hipError_t bn_finalize_grad_launch(const float* slots, int C, long rows, const f
 }  // namespace kfb
 
 // test / A/B hook: 0 turns the folded finalize-in-apply passes off, 1 on
-KFB_API void kfb_bn_set_fold(int on) { g_bn_fold = on ? 1 : 0; }
+KFB_API void kfb_bn_set_fold(int mode) { g_bn_fold = mode; }
 
 KFB_API int kfb_bn_num_slabs(long rows, int C) {
   const int V = vec_width(C);
