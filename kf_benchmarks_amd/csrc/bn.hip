@@ -721,25 +721,14 @@ __device__ __forceinline__ void fold_ch(const float* __restrict__ pa, const floa
   for (int u = 0; u < 8; ++u) { sa += a[u]; sb += b[u]; }
 }
 
-// Channel-block form: workgroup b owns the 64 channels of block b % (C/64)
-// (8 vectors of 8) over rows b / (C/64), + G, ...: it folds only those 64
-// channels' slots (64 threads, every slot load in flight), so the slot
-// traffic does not grow with C x the grid.  Its 256 threads cover 32 rows x
-// 8 vectors per pass.
-constexpr int FOLD_CB = 64;
-
 template <typename T, int V, bool RES, bool RELU>
 __global__ void __launch_bounds__(256)
 bn_apply_fold_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y, long nvec,
                 int C, BnFoldF f, uint8_t* __restrict__ mb) {
-  if constexpr (V * 8 != FOLD_CB) return;  // (instantiated for every vector width; used at 8)
-  __shared__ float lsc[FOLD_CB], lsf[FOLD_CB];
+  __shared__ float lsc[FOLD_CMAX], lsf[FOLD_CMAX], lmean[FOLD_CMAX];
   __shared__ int last;
-  const int ncb = C / FOLD_CB, cb = (int)blockIdx.x % ncb, g = (int)blockIdx.x / ncb;
-  const int G = (int)gridDim.x / ncb;
   const double n = (double)f.rows;
-  if (threadIdx.x < FOLD_CB) {
-    const int c = cb * FOLD_CB + (int)threadIdx.x;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
     double s, q;
     fold_ch(f.psum, f.psq, f.nslab, C, c, s, q);
     // (the math of bn_finalize_stats_k)
@@ -749,15 +738,16 @@ bn_apply_fold_k(const T* __restrict__ x, const T* __restrict__ res, T* __restric
     double var = q / n - dm * dm;
     if (var < 0.0) var = 0.0;
     const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
-    const float gm = f.gamma ? f.gamma[c] : 1.f;
+    const float g = f.gamma ? f.gamma[c] : 1.f;
     const float b = f.beta ? f.beta[c] : 0.f;
-    lsc[threadIdx.x] = gm * invstd;
-    lsf[threadIdx.x] = b - (float)mean * gm * invstd;
-    if (g == 0) {
+    lsc[c] = g * invstd;
+    lsf[c] = b - (float)mean * g * invstd;
+    lmean[c] = (float)mean;
+    if (blockIdx.x == 0) {
       f.save_mean[c] = (float)mean;
       f.save_invstd[c] = invstd;
-      f.scale[c] = gm * invstd;
-      f.shift[c] = b - (float)mean * gm * invstd;
+      f.scale[c] = g * invstd;
+      f.shift[c] = b - (float)mean * g * invstd;
       if (f.run_mean) {
         const double unbiased = f.rows > 1 ? var * n / (n - 1.0) : var;
         f.run_mean[c] = f.run_mean[c] * f.decay + (float)mean * (1.f - f.decay);
@@ -766,10 +756,13 @@ bn_apply_fold_k(const T* __restrict__ x, const T* __restrict__ res, T* __restric
     }
   }
   __syncthreads();
-  const int vl = (int)threadIdx.x & 7, r = (int)threadIdx.x >> 3;
+  const unsigned cv = (unsigned)(C / V);
+  const unsigned nn = (unsigned)nvec, stride = gridDim.x * blockDim.x;
+  const unsigned i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = (int)(i0 % cv) * V;  // fixed: the host makes stride a multiple of cv
   float sc[V], sf[V];
 #pragma unroll
-  for (int k = 0; k < V; ++k) { sc[k] = lsc[vl * V + k]; sf[k] = lsf[vl * V + k]; }
+  for (int k = 0; k < V; ++k) { sc[k] = lsc[c + k]; sf[k] = lsf[c + k]; }
   auto apply = [&](float (&v)[V], const float (&rr)[V]) {
 #pragma unroll
     for (int k = 0; k < V; ++k) {
@@ -779,59 +772,43 @@ bn_apply_fold_k(const T* __restrict__ x, const T* __restrict__ res, T* __restric
       v[k] = o;
     }
   };
-  const long cv = C / V, rows = nvec / cv, step = (long)G * 32;
-  const long col = (long)cb * (FOLD_CB / V) + vl;
-  long row = (long)g * 32 + r;
-  for (; row + step < rows; row += 2 * step) {
-    const long i0 = row * cv + col, i1 = (row + step) * cv + col;
+  unsigned i = i0;
+  for (; i + stride < nn; i += 2 * stride) {
     float v0[V], v1[V], r0[V], r1[V];
-    load_vec<T, V>(x + i0 * V, v0);
-    load_vec<T, V>(x + i1 * V, v1);
+    load_vec<T, V>(x + (long)i * V, v0);
+    load_vec<T, V>(x + (long)(i + stride) * V, v1);
     if (RES) {
-      load_vec<T, V>(res + i0 * V, r0);
-      load_vec<T, V>(res + i1 * V, r1);
+      load_vec<T, V>(res + (long)i * V, r0);
+      load_vec<T, V>(res + (long)(i + stride) * V, r1);
     }
     apply(v0, r0);
     apply(v1, r1);
-    store_vec<T, V>(y + i0 * V, v0);
-    store_vec<T, V>(y + i1 * V, v1);
+    store_vec<T, V>(y + (long)i * V, v0);
+    store_vec<T, V>(y + (long)(i + stride) * V, v1);
     if (RELU) {
-      relu_bits<T, V>(mb, i0, v0);
-      relu_bits<T, V>(mb, i1, v1);
+      relu_bits<T, V>(mb, i, v0);
+      relu_bits<T, V>(mb, i + stride, v1);
     }
   }
-  if (row < rows) {
-    const long i0 = row * cv + col;
+  if (i < nn) {
     float v0[V], r0[V];
-    load_vec<T, V>(x + i0 * V, v0);
-    if (RES) load_vec<T, V>(res + i0 * V, r0);
+    load_vec<T, V>(x + (long)i * V, v0);
+    if (RES) load_vec<T, V>(res + (long)i * V, r0);
     apply(v0, r0);
-    store_vec<T, V>(y + i0 * V, v0);
-    if (RELU) relu_bits<T, V>(mb, i0, v0);
+    store_vec<T, V>(y + (long)i * V, v0);
+    if (RELU) relu_bits<T, V>(mb, i, v0);
   }
-  // The new statistics shift, once every workgroup has read the old one:
-  // the last to arrive copies the means the row-group-0 workgroups published
-  // (agent release in those before their ticket, acquire in the last).
+  // the new statistics shift, once every workgroup has read the old one
   if (f.kshift && f.counter) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      if (g == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
       const int prev = __hip_atomic_fetch_add(f.counter, 1, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
       last = prev == (int)gridDim.x - 1;
     }
     __syncthreads();
     if (last) {
-      if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __syncthreads();
-      for (int cc = threadIdx.x; cc < C; cc += blockDim.x) f.kshift[cc] = f.save_mean[cc];
+      for (int cc = threadIdx.x; cc < C; cc += blockDim.x) f.kshift[cc] = lmean[cc];
       if (threadIdx.x == 0)
         __hip_atomic_store(f.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -842,74 +819,80 @@ template <typename T, int V, bool MASK, bool DRES>
 __global__ void __launch_bounds__(256)
 bn_bwd_apply_fold_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __restrict__ x,
                     T* __restrict__ dx, T* __restrict__ dres, long nvec, int C, BnFoldB f) {
-  if constexpr (V * 8 != FOLD_CB) return;  // (instantiated for every vector width; used at 8)
-  __shared__ float la[FOLD_CB], lb[FOLD_CB], lc[FOLD_CB];
-  const int ncb = C / FOLD_CB, cb = (int)blockIdx.x % ncb, g = (int)blockIdx.x / ncb;
-  const int G = (int)gridDim.x / ncb;
+  __shared__ float la[FOLD_CMAX], lb[FOLD_CMAX], lc[FOLD_CMAX];
   const double n = (double)f.rows;
-  if (threadIdx.x < FOLD_CB) {
-    const int c = cb * FOLD_CB + (int)threadIdx.x;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
     double s1, s2;
     fold_ch(f.pdy, f.pdyx, f.nslab, C, c, s1, s2);
     // (the math of bn_finalize_grad_k)
     const float is = f.invstd[c];
-    const float gm = f.gamma ? f.gamma[c] : 1.f;
-    const double A = (double)gm * is;
+    const float g = f.gamma ? f.gamma[c] : 1.f;
+    const double A = (double)g * is;
     const double B = -A * (double)is * (double)is * s2 / n;
-    la[threadIdx.x] = (float)A;
-    lb[threadIdx.x] = (float)B;
-    lc[threadIdx.x] = (float)(-A * s1 / n - (double)f.mean[c] * B);
-    if (g == 0) {
+    la[c] = (float)A;
+    lb[c] = (float)B;
+    lc[c] = (float)(-A * s1 / n - (double)f.mean[c] * B);
+    if (blockIdx.x == 0) {
       if (f.dgamma) f.dgamma[c] = (f.accumulate ? f.dgamma[c] : 0.f) + (float)(s2 * is);
       if (f.dbeta) f.dbeta[c] = (f.accumulate ? f.dbeta[c] : 0.f) + (float)s1;
     }
   }
   __syncthreads();
-  const int vl = (int)threadIdx.x & 7, r = (int)threadIdx.x >> 3;
+  const unsigned cv = (unsigned)(C / V);
+  const unsigned nn = (unsigned)nvec, stride = gridDim.x * blockDim.x;
+  const unsigned i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = (int)(i0 % cv) * V;
   float a[V], b[V], cc[V];
 #pragma unroll
-  for (int k = 0; k < V; ++k) {
-    a[k] = la[vl * V + k];
-    b[k] = lb[vl * V + k];
-    cc[k] = lc[vl * V + k];
-  }
-  const long cv = C / V, rows = nvec / cv, step = (long)G * 32;
-  const long col = (long)cb * (FOLD_CB / V) + vl;
-  auto fin = [&](long i, float (&g0)[V], const float (&x0)[V], const float (&y0)[V]) {
+  for (int k = 0; k < V; ++k) { a[k] = la[c + k]; b[k] = lb[c + k]; cc[k] = lc[c + k]; }
+  auto one = [&](unsigned i) {
+    float g0[V], x0[V];
+    load_vec<T, V>(dy + (long)i * V, g0);
+    load_vec<T, V>(x + (long)i * V, x0);
     if (MASK) {
+      float y0[V];
+      load_vec<T, V>(y + (long)i * V, y0);
 #pragma unroll
       for (int k = 0; k < V; ++k) g0[k] = y0[k] > 0.f ? g0[k] : 0.f;
     }
-    if (DRES) store_vec<T, V>(dres + i * V, g0);
+    if (DRES) store_vec<T, V>(dres + (long)i * V, g0);
     float o0[V];
 #pragma unroll
     for (int k = 0; k < V; ++k) o0[k] = g0[k] * a[k] + x0[k] * b[k] + cc[k];
-    store_vec<T, V>(dx + i * V, o0);
+    store_vec<T, V>(dx + (long)i * V, o0);
   };
-  long row = (long)g * 32 + r;
-  for (; row + step < rows; row += 2 * step) {
-    // both rows' loads issue before either is used
-    const long i0 = row * cv + col, i1 = (row + step) * cv + col;
-    float g0[V], g1[V], x0[V], x1[V], y0[V], y1[V];
-    load_vec<T, V>(dy + i0 * V, g0);
-    load_vec<T, V>(x + i0 * V, x0);
-    load_vec<T, V>(dy + i1 * V, g1);
-    load_vec<T, V>(x + i1 * V, x1);
+  unsigned i = i0;
+  for (; i + stride < nn; i += 2 * stride) {
+    // both vectors' loads issue before either is used (as step2 above)
+    float g0[V], g1[V], x0[V], x1[V];
+    load_vec<T, V>(dy + (long)i * V, g0);
+    load_vec<T, V>(x + (long)i * V, x0);
+    load_vec<T, V>(dy + (long)(i + stride) * V, g1);
+    load_vec<T, V>(x + (long)(i + stride) * V, x1);
     if (MASK) {
-      load_vec<T, V>(y + i0 * V, y0);
-      load_vec<T, V>(y + i1 * V, y1);
+      float y0[V], y1[V];
+      load_vec<T, V>(y + (long)i * V, y0);
+      load_vec<T, V>(y + (long)(i + stride) * V, y1);
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        g0[k] = y0[k] > 0.f ? g0[k] : 0.f;
+        g1[k] = y1[k] > 0.f ? g1[k] : 0.f;
+      }
     }
-    fin(i0, g0, x0, y0);
-    fin(i1, g1, x1, y1);
+    if (DRES) {
+      store_vec<T, V>(dres + (long)i * V, g0);
+      store_vec<T, V>(dres + (long)(i + stride) * V, g1);
+    }
+    float o0[V], o1[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      o0[k] = g0[k] * a[k] + x0[k] * b[k] + cc[k];
+      o1[k] = g1[k] * a[k] + x1[k] * b[k] + cc[k];
+    }
+    store_vec<T, V>(dx + (long)i * V, o0);
+    store_vec<T, V>(dx + (long)(i + stride) * V, o1);
   }
-  if (row < rows) {
-    const long i0 = row * cv + col;
-    float g0[V], x0[V], y0[V];
-    load_vec<T, V>(dy + i0 * V, g0);
-    load_vec<T, V>(x + i0 * V, x0);
-    if (MASK) load_vec<T, V>(y + i0 * V, y0);
-    fin(i0, g0, x0, y0);
-  }
+  if (i < nn) one(i);
 }
 
 // Backward apply of y = relu(bn(x) + bn_r(xr)) with a pre-masked dy: both
@@ -1361,41 +1344,29 @@ static int flat_grid(long nvec) { return (int)((nvec + 256L * 4 - 1) / (256L * 4
 // finalize launch): KFB_BN_FOLD=0 never.
 // default off: in-network +0.16..0.40 ms/step against the finalize launches
 // (gpurun_out/r10o: 19.27 / 19.03 with the fold vs 18.87 / 18.87 without)
-static int g_bn_fold = -1;  // -1: KFB_BN_FOLD (0 never, 1 always, 2 small tensors: default)
+static int g_bn_fold = -1;  // -1: KFB_BN_FOLD (default off); kfb_bn_set_fold overrides
 
 static bool fold_ok(long nvec, int C, int V) {
   if (g_bn_fold < 0) {
     const char* e = getenv("KFB_BN_FOLD");
-    g_bn_fold = e ? atoi(e) : 2;
+    g_bn_fold = (e && atoi(e) != 0) ? 1 : 0;
   }
-  // mode 2 (the default): only tensors up to KFB_BN_FOLD_MAXMB (default 8) MB,
-  // where the removed launch boundary weighs most against the pass - the
-  // small-batch layers (ResNet-152 bs32 at 16 MB: 13.91 / 13.86 vs 13.99 /
-  // 14.02 ms); at batch 256 no BN tensor is that small (the folded passes
-  // lose there, profiles/r10_bn_fold_vs_launch.txt)
-  static const long max_bytes = [] {
-    const char* e = getenv("KFB_BN_FOLD_MAXMB");
-    return (e ? atol(e) : 8L) << 20;
-  }();
-  const bool on = g_bn_fold == 1 || (g_bn_fold == 2 && nvec * 16 <= max_bytes);
+  const bool on = g_bn_fold != 0;
   const int cv = C / V;
-  return on && V == 8 && C <= FOLD_CMAX && C % FOLD_CB == 0 && cv > 0 &&
+  return on && V == 8 && C <= FOLD_CMAX && cv > 0 && (cv & (cv - 1)) == 0 && 256 % cv == 0 &&
          !flat_ok(nvec, C, V) && nvec < (1L << 31) - 2L * 4096 * 256;
 }
 
-// (C / FOLD_CB) channel blocks x G row groups of 32 rows
-static int fold_grid(long nvec, int C) {
+static int fold_grid(long nvec) {
   // KFB_BN_FOLD_GRID: workgroup cap of the folded passes (A/B knob, <= 4096)
   static const long cap = [] {
     const char* e = getenv("KFB_BN_FOLD_GRID");
     const long v = e ? atol(e) : FOLD_GRID;
     return v < 256 ? 256L : v > 4096 ? 4096L : v;
   }();
-  const long ncb = C / FOLD_CB, rows = nvec / (C / 8);
-  long G = (rows + 63) / 64;  // (at least two rows per thread)
-  if (G > cap / ncb) G = cap / ncb;
-  if (G < 1) G = 1;
-  return (int)(ncb * G);
+  long b = (nvec + 255) / 256;
+  if (b > cap) b = cap;
+  return (int)(b < 1 ? 1 : b);
 }
 
 
@@ -1473,7 +1444,7 @@ hipError_t bn_finalize_grad_launch(const float* slots, int C, long rows, const f
 }  // namespace kfb
 
 // test / A/B hook: 0 turns the folded finalize-in-apply passes off, 1 on
-KFB_API void kfb_bn_set_fold(int mode) { g_bn_fold = mode; }
+KFB_API void kfb_bn_set_fold(int on) { g_bn_fold = on ? 1 : 0; }
 
 KFB_API int kfb_bn_num_slabs(long rows, int C) {
   const int V = vec_width(C);
@@ -1509,7 +1480,7 @@ KFB_API hipError_t kfb_bn_fwd_train(int dtype, const void* x, const void* res, v
         const BnFoldF f{psum, psq, nslab, rows, gamma, beta, decay, eps, run_mean, run_var,
                         save_mean, save_invstd, scale, shift, kshift,
                         (int*)(psq + (long)nslab * C) + 8};
-        const int gb = fold_grid(nv, C);
+        const int gb = fold_grid(nv);
         if (res) {
           if (relu)
             hipLaunchKernelGGL((bn_apply_fold_k<T, VV, true, true>), dim3(gb), dim3(256), 0,
@@ -1647,7 +1618,7 @@ KFB_API hipError_t kfb_bn_bwd(int dtype, const void* dy, const void* y, const vo
         // the finalize folds into the apply pass (see bn_apply_fold_k)
         const BnFoldB f{pdy, pdyx, nslab, rows, gamma, save_mean, save_invstd, dgamma, dbeta,
                         accumulate};
-        const int gb = fold_grid(nvec, C);
+        const int gb = fold_grid(nvec);
         if (relu) {
           if (dres)
             hipLaunchKernelGGL((bn_bwd_apply_fold_k<T, VV, true, true>), dim3(gb), dim3(256), 0,

@@ -119,7 +119,7 @@ def test_resnet_trains_same_with_in_kernel_finalize(cuda, monkeypatch, force):
 def fold_toggle(cuda):
     from kf_benchmarks_amd.ops import _native as N
     yield lambda on: N.load().kfb_bn_set_fold(int(on))
-    N.load().kfb_bn_set_fold(2)  # (the default: small tensors only)
+    N.load().kfb_bn_set_fold(0)  # (the default)
 
 
 @pytest.mark.parametrize("C,relu,res", [(64, True, False), (256, True, True), (512, False, False)])
