@@ -44,9 +44,33 @@ __global__ void __launch_bounds__(256) idct_k(const int16_t* __restrict__ blocks
   }
 }
 
+// grid (CROP_GRID, n): the crop of image blockIdx.y reconstructed once, one
+// thread per crop pixel (fancy-upsampled chroma + YCbCr -> RGB), into the
+// batch's crop-RGB buffer - the resize then reads each source pixel instead
+// of rebuilding it for every output pixel that touches it.
+constexpr int CROP_GRID = 64;
+
+__global__ void __launch_bounds__(256) crop_rgb_k(const jpg::Desc* __restrict__ descs,
+                                                  const uint8_t* __restrict__ planes,
+                                                  uint8_t* __restrict__ rgb) {
+  const jpg::Desc& d = descs[blockIdx.y];
+  if (d.mode != jpg::MODE_COEF || d.rgb_off < 0) return;
+  const long area = (long)d.ch * d.cw;
+  for (long p = blockIdx.x * 256L + threadIdx.x; p < area; p += CROP_GRID * 256L) {
+    const int y = (int)(p / d.cw), x = (int)(p - (long)y * d.cw);
+    int px[3];
+    jpg::pixel_rgb(planes, d, d.cy + y, d.cx + x, px);
+    uint8_t* o = rgb + 3L * (d.rgb_off + p);
+    o[0] = (uint8_t)px[0];
+    o[1] = (uint8_t)px[1];
+    o[2] = (uint8_t)px[2];
+  }
+}
+
 // grid (ceil(oh * ow / 256), n): one thread per output pixel.
 __global__ void __launch_bounds__(256) rgb_k(const jpg::Desc* __restrict__ descs,
                                              const uint8_t* __restrict__ planes,
+                                             const uint8_t* __restrict__ crop_rgb,
                                              const uint8_t* __restrict__ host_imgs,
                                              uint8_t* __restrict__ out, int oh, int ow) {
   const int img = blockIdx.y;
@@ -62,7 +86,10 @@ __global__ void __launch_bounds__(256) rgb_k(const jpg::Desc* __restrict__ descs
     return;
   }
   uint8_t px[3];
-  jpg::resized_pixel(planes, d, oh, ow, p / ow, p % ow, px);
+  if (crop_rgb && d.rgb_off >= 0)
+    jpg::resized_from_rgb(crop_rgb, d, oh, ow, p / ow, p % ow, px);
+  else
+    jpg::resized_pixel(planes, d, oh, ow, p / ow, p % ow, px);
   o[0] = px[0];
   o[1] = px[1];
   o[2] = px[2];
@@ -78,15 +105,21 @@ KFB_API int kfb_jpeg_desc_bytes() { return (int)sizeof(jpg::Desc); }
 // descs [n] (device copy of the host descriptors), blocks [nblocks][64]
 // int16, planes [nblocks][64] uint8 scratch, host_imgs [n][oh][ow][3] (the
 // MODE_HOST images; nullable when there are none) -> out [n][oh][ow][3].
+// crop_rgb (nullable): scratch of 3 x the crops' pixel count (the host's
+// kfbrt_imgpipe_run_coef reports it); without it every output pixel
+// rebuilds its four source pixels.
 KFB_API hipError_t kfb_jpeg_decode(const void* descs, int n, const int16_t* blocks, long nblocks,
-                                   uint8_t* planes, const uint8_t* host_imgs, int oh, int ow,
-                                   uint8_t* out, hipStream_t stream) {
+                                   uint8_t* planes, uint8_t* crop_rgb, const uint8_t* host_imgs,
+                                   int oh, int ow, uint8_t* out, hipStream_t stream) {
   if (n <= 0 || oh <= 0 || ow <= 0 || (long)oh * ow >= (1L << 31) / 3) return hipErrorInvalidValue;
   const jpg::Desc* d = static_cast<const jpg::Desc*>(descs);
   if (nblocks > 0)
     hipLaunchKernelGGL(jpeg::idct_k, dim3((unsigned)n * 3, jpeg::SPLIT), dim3(256), 0, stream,
                        blocks, d, planes, nblocks);
+  if (nblocks > 0 && crop_rgb)
+    hipLaunchKernelGGL(jpeg::crop_rgb_k, dim3(jpeg::CROP_GRID, (unsigned)n), dim3(256), 0, stream,
+                       d, planes, crop_rgb);
   hipLaunchKernelGGL(jpeg::rgb_k, dim3((unsigned)((oh * ow + 255) / 256), (unsigned)n), dim3(256),
-                     0, stream, d, planes, host_imgs, out, oh, ow);
+                     0, stream, d, planes, (const uint8_t*)crop_rgb, host_imgs, out, oh, ow);
   return hipGetLastError();
 }

@@ -48,7 +48,7 @@ struct Desc {
   int ncomp;    // 1 (grayscale) or 3 (YCbCr)
   int cy, cx, ch, cw;  // training crop in full-resolution pixels
   int host_slot;       // MODE_HOST: index into the host-decoded image buffer
-  int pad;
+  int rgb_off;         // MODE_COEF: first pixel of this crop in the batch's crop-RGB buffer
   Comp c[3];
   uint16_t q[3][64];   // dequantization tables, natural order
 };
@@ -204,6 +204,37 @@ KFB_HD inline void resized_pixel(const uint8_t* planes, const Desc& d, int oh, i
   for (int k = 0; k < 3; ++k) {
     const float t = (float)p00[k] + ax * (float)(p01[k] - p00[k]);
     const float b = (float)p10[k] + ax * (float)(p11[k] - p10[k]);
+    float v = t + ay * (b - t) + 0.5f;
+    v = v < 0.f ? 0.f : v > 255.f ? 255.f : v;
+    out3[k] = (uint8_t)v;
+  }
+}
+
+// resized_pixel over a crop already reconstructed into rgb (the crop's
+// [ch][cw][3] pixels from pixel 3 * rgb_off): the same arithmetic, so the
+// same bytes.
+KFB_HD inline void resized_from_rgb(const uint8_t* rgb, const Desc& d, int oh, int ow, int i,
+                                    int j, uint8_t* out3) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+  const float fy = (float)d.ch / (float)oh, fx = (float)d.cw / (float)ow;
+  float sy = ((float)i + 0.5f) * fy - 0.5f;
+  sy = sy < 0.f ? 0.f : sy > (float)(d.ch - 1) ? (float)(d.ch - 1) : sy;
+  float sx = ((float)j + 0.5f) * fx - 0.5f;
+  sx = sx < 0.f ? 0.f : sx > (float)(d.cw - 1) ? (float)(d.cw - 1) : sx;
+  const int y0 = (int)sy, x0 = (int)sx;
+  const int y1 = y0 + 1 < d.ch ? y0 + 1 : d.ch - 1, x1 = x0 + 1 < d.cw ? x0 + 1 : d.cw - 1;
+  const float ay = sy - (float)y0, ax = sx - (float)x0;
+  const uint8_t* base = rgb + 3L * d.rgb_off;
+  const uint8_t* q00 = base + 3L * ((long)y0 * d.cw + x0);
+  const uint8_t* q01 = base + 3L * ((long)y0 * d.cw + x1);
+  const uint8_t* q10 = base + 3L * ((long)y1 * d.cw + x0);
+  const uint8_t* q11 = base + 3L * ((long)y1 * d.cw + x1);
+  for (int k = 0; k < 3; ++k) {
+    const int p00 = q00[k], p01 = q01[k], p10 = q10[k], p11 = q11[k];
+    const float t = (float)p00 + ax * (float)(p01 - p00);
+    const float b = (float)p10 + ax * (float)(p11 - p10);
     float v = t + ay * (b - t) + 0.5f;
     v = v < 0.f ? 0.f : v > 255.f ? 255.f : v;
     out3[k] = (uint8_t)v;

@@ -635,7 +635,8 @@ API int kfbrt_imgpipe_run(void* h, int n, const uint8_t* const* recs, const size
 // Coefficient mode: descs [n] (kfb::jpg::Desc), blocks [cap][64] int16 (the
 // batch arena), images [n][H][W][3] for the images decoded on the host
 // (MODE_HOST).  out3[0] = arena blocks used, out3[1] = images decoded on the
-// host; returns the failure count as kfbrt_imgpipe_run.
+// host, out2[2] = pixels of the reconstructed crops (the device's crop-RGB
+// buffer); returns the failure count as kfbrt_imgpipe_run.
 API int kfbrt_imgpipe_run_coef(void* h, int n, const uint8_t* const* recs, const size_t* lens,
                                const uint64_t* seeds, const int* positions, void* descs,
                                int16_t* blocks, long cap, uint8_t* images, float* params,
@@ -666,10 +667,22 @@ API int kfbrt_imgpipe_run_coef(void* h, int n, const uint8_t* const* recs, const
   p->work();
   std::unique_lock<std::mutex> l(p->mu);
   p->done_cv.wait(l, [&] { return p->active == 0; });
+  // each reconstructed crop's place in the device's crop-RGB buffer (batch
+  // order: deterministic), out2[2] = its size in pixels
+  long rgb = 0;
+  for (int i = 0; i < n; ++i) {
+    kfb::jpg::Desc& d = p->descs[i];
+    d.rgb_off = -1;  // (the device rebuilds such a crop per output pixel)
+    if (d.mode == kfb::jpg::MODE_COEF && rgb + (long)d.ch * d.cw < (1L << 31) / 3) {
+      d.rgb_off = (int)rgb;
+      rgb += (long)d.ch * d.cw;
+    }
+  }
   p->descs = nullptr;
   p->arena = nullptr;
   out2[0] = std::min(ar.next.load(), cap);
   out2[1] = p->hosted.load();
+  out2[2] = rgb;
   return p->failed.load();
 }
 

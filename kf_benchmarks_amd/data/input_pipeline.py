@@ -169,7 +169,7 @@ class PrefetchInput:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(dev))
             s.ev = ev  # the slot may be refilled once these copies are done
-            u8 = J.decode(descs, blocks, hosted, ts.n, ts.height, ts.width)
+            u8 = J.decode(descs, blocks, hosted, ts.n, ts.height, ts.width, ts.crop_pixels)
             return [F.augment_u8(u8, prm, self.dtype), lab]
         img = ts[0].to(self.device, non_blocking=True)
         if len(ts) == 3 and img.dtype == torch.uint8:

@@ -507,11 +507,11 @@ class JpegBatch:
     pinned ring slot, which the consumer marks with ``slot.ev`` once its
     device copies are enqueued (the producer waits for that before refilling
     the slot)."""
-    __slots__ = ("slot", "n", "nblocks", "hosted", "height", "width")
+    __slots__ = ("slot", "n", "nblocks", "hosted", "height", "width", "crop_pixels")
 
-    def __init__(self, slot, n, nblocks, hosted, height, width):
+    def __init__(self, slot, n, nblocks, hosted, height, width, crop_pixels=-1):
         self.slot, self.n, self.nblocks, self.hosted = slot, n, nblocks, hosted
-        self.height, self.width = height, width
+        self.height, self.width, self.crop_pixels = height, width, crop_pixels
 
 
 class _JpegSlot:
@@ -564,7 +564,8 @@ def _batched(pre, records: Iterator[bytes], threads: int):
                 if bad > 0:
                     raise ValueError("%d of %d image records in this batch could not be "
                                      "decoded (corrupt TFRecord / JPEG data)" % (bad, bs))
-                yield JpegBatch(slot, bs, nblocks, hosted, pre.height, pre.width)
+                yield JpegBatch(slot, bs, nblocks, hosted, pre.height, pre.width,
+                                pipe.crop_pixels)
         finally:
             pipe.close()
     if getattr(pre, "device_augment", False) and _NATIVE_PIPE and runtime.ImagePipe.available():

@@ -21,11 +21,11 @@ import torch
 from . import _native as N
 
 N.register_optional("kfb_jpeg_desc_bytes", [], N.c_int)
-N.register_optional("kfb_jpeg_decode", [N.P, N.I, N.P, N.L, N.P, N.P, N.I, N.I, N.P, N.P])
+N.register_optional("kfb_jpeg_decode", [N.P, N.I, N.P, N.L, N.P, N.P, N.P, N.I, N.I, N.P, N.P])
 
 
 def decode(descs: torch.Tensor, blocks: torch.Tensor, host_images, n: int, height: int,
-           width: int) -> torch.Tensor:
+           width: int, crop_pixels: int = -1) -> torch.Tensor:
     """descs: uint8 [n * desc_bytes]; blocks: int16 [nblocks, 64];
     host_images: uint8 [n, H, W, 3] or None (images the host decoded
     itself) -> uint8 [n, height, width, 3] on the tensors' device."""
@@ -43,8 +43,12 @@ def decode(descs: torch.Tensor, blocks: torch.Tensor, host_images, n: int, heigh
     nblocks = blocks.numel() // 64
     planes = torch.empty((max(nblocks, 1) * 64,), dtype=torch.uint8, device=descs.device)
     out = torch.empty((n, height, width, 3), dtype=torch.uint8, device=descs.device)
+    # crop_pixels (kfbrt_imgpipe_run_coef's third count): each crop is rebuilt
+    # once into this scratch, then resized; < 0: per output pixel
+    crop = (torch.empty((max(crop_pixels, 1) * 3,), dtype=torch.uint8, device=descs.device)
+            if crop_pixels >= 0 else None)
     N.call("kfb_jpeg_decode", descs.data_ptr(), n, blocks.data_ptr() if nblocks else None,
-           nblocks, planes.data_ptr(),
+           nblocks, planes.data_ptr(), None if crop is None else crop.data_ptr(),
            None if host_images is None else host_images.contiguous().data_ptr(),
            height, width, out.data_ptr(), N.stream(descs.device))
     return out

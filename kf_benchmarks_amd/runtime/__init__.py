@@ -425,12 +425,13 @@ class ImagePipe:
         lens = np.asarray([len(r) for r in records], dtype=np.uint64)
         seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
         pos = np.ascontiguousarray(np.arange(n) if positions is None else positions, dtype=np.int32)
-        out2 = (ctypes.c_long * 2)()
+        out2 = (ctypes.c_long * 3)()
         bad = lib.kfbrt_imgpipe_run_coef(
             self._h, n, ctypes.cast(bufs, ctypes.c_void_p), lens.ctypes.data, seeds.ctypes.data,
             pos.ctypes.data, slot.descs.data_ptr(), slot.blocks.data_ptr(),
             slot.blocks.shape[0], slot.images.data_ptr(), slot.params.data_ptr(),
             slot.labels.data_ptr(), out2)
+        self.crop_pixels = int(out2[2])
         return int(out2[0]), int(out2[1]), bad
 
     def close(self):

@@ -155,13 +155,16 @@ def test_gpu_reconstruction_matches_host_reference(cuda):
         pipe = runtime.ImagePipe(4, oh, ow, False, False)
         try:
             nblocks, hosted, bad = pipe.run_coef(recs, np.arange(n, dtype=np.uint64), slot)
+            crop_pixels = pipe.crop_pixels
         finally:
             pipe.close()
-        assert bad == 0
+        assert bad == 0 and crop_pixels > 0
         ref = np.empty((n, oh, ow, 3), np.uint8)
         runtime.jpeg_reconstruct(slot.descs.numpy(), n, slot.blocks[:nblocks].numpy(),
                                  slot.images.numpy(), oh, ow, ref)
-        got = J.decode(slot.descs.to(cuda), slot.blocks[:nblocks].to(cuda),
-                       slot.images.to(cuda) if hosted else None, n, oh, ow)
-        torch.cuda.synchronize()
-        np.testing.assert_array_equal(got.cpu().numpy(), ref)
+        # two-pass (each crop rebuilt once, then resized) and per-output-pixel
+        for cp in (crop_pixels, -1):
+            got = J.decode(slot.descs.to(cuda), slot.blocks[:nblocks].to(cuda),
+                           slot.images.to(cuda) if hosted else None, n, oh, ow, cp)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(got.cpu().numpy(), ref)
