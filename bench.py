@@ -66,9 +66,10 @@ def main(argv=None):
                     help="host preprocessing threads with --data_dir (0: the default)")
     ap.add_argument("--launch_tape", type=int, default=-1,
                     help="1: record one step's native launches after warmup and replay them "
-                         "from C++ (ops/tape.py); falls back to eager where not eligible.  "
-                         "-1 (default): on for one GPU with synthetic data, off otherwise "
-                         "(multi-rank taped replay is exercised only as a 1-rank RCCL group)")
+                         "from C++ (ops/tape.py); falls back to eager where not eligible (at "
+                         "N > 1 it needs the native RCCL communicator, which a startup "
+                         "self-test validates against torch's group; see comm.selftest in the "
+                         "JSON).  -1 (default): on for GPU runs")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
@@ -114,8 +115,7 @@ def main(argv=None):
                       kernel_impl=a.kernel_impl, bucket_size_mb=a.bucket_size_mb,
                       gradient_wire_dtype=a.wire_dtype, display_every=10**9,
                       all_reduce_spec=a.all_reduce_spec, hierarchical_copy=a.hierarchical_copy,
-                      launch_tape=(bool(a.launch_tape) if a.launch_tape >= 0 else
-                                   (a.gpus == 1 and cuda)),
+                      launch_tape=(bool(a.launch_tape) if a.launch_tape >= 0 else cuda),
                       data_dir=a.data_dir,
                       datasets_num_private_threads=a.input_threads or None,
                       datasets_repeat_cached_sample=bool(a.data_dir),
@@ -195,6 +195,8 @@ def main(argv=None):
     taped_steps = getattr(getattr(bench, "_tape", None), "replays", 0) > 0
     comm_info = {
         "backend": world.device_backend,
+        # native-communicator startup check (None: no native communicator)
+        "selftest": getattr(bench, "comm_selftest", None),
         "buckets": reducer.num_buckets if reducer is not None else 0,
         # replayed steps skip the reducer's Python bookkeeping: not measured
         "collectives_per_step": (None if taped_steps else
@@ -247,6 +249,8 @@ def main(argv=None):
                        "all_reduce_spec": a.all_reduce_spec,
                        "launch_tape": (getattr(bench, "_tape", None) is not None
                                        and bench._tape.replays > 0),
+                       "launch_tape_off_reason": (None if taped_steps else
+                                                  getattr(bench, "_tape_reason", None)),
                        "hierarchical_copy": a.hierarchical_copy,
                        "optimizer": a.optimizer,
                        "kernel_impl": a.kernel_impl, "loss_first": warm_loss,

@@ -418,6 +418,7 @@ class BenchmarkCNN:
                 if k:
                     mask[off:off + n] = 1.0
             self.l2_mask = mask
+        self.comm_selftest = self._validate_comm()
         self.input = self._make_input()
         self._tape = None
         self._tape_warm = 0
@@ -425,6 +426,28 @@ class BenchmarkCNN:
         if p.launch_tape and self._tape_reason is not None:
             log_fn("launch tape: not used (%s)" % self._tape_reason)
         self._built = True
+
+    def _validate_comm(self):
+        """Multi-rank runs on the native communicator: check it bitwise
+        against torch's host group on this job's collective buffer sizes and
+        dtypes (gradient buckets and their wire dtype, the whole model) before
+        any step runs; KFB_NATIVE_COMM=auto falls back to torch's
+        ProcessGroupNCCL (and so to eager steps) if it fails."""
+        if self.world.native is None or not self.world.communicates:
+            return None
+        sizes = {1, self.flat.numel}
+        dtypes = [torch.float32]
+        r = getattr(self.strategy, "reducer", None)
+        if r is not None:
+            sizes.update(e - s for s, e in r.buckets)
+            if r.wire_dtype is not None:
+                dtypes.append(r.wire_dtype)
+        st = comm.validate_native(sorted(sizes), tuple(dtypes))
+        if st is not None:
+            log_fn("Native RCCL self-test: %s (%d checks%s)"
+                   % ("passed" if st["ok"] else "FAILED", st["checked"],
+                      "" if st["ok"] else "; " + ", ".join(st["failed"])))
+        return st
 
     def _make_input(self):
         from .data.input_pipeline import make_input_source

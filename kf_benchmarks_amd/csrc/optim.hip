@@ -22,6 +22,8 @@
 // runs extra elementwise passes over the model.
 #include "common.h"
 
+#include <cstring>
+
 namespace kfb {
 
 enum OptKind : int { SGD = 0, MOMENTUM = 1, RMSPROP = 2, ADAM = 3 };
@@ -238,6 +240,74 @@ KFB_API hipError_t kfb_host_register(void* p, size_t bytes, void** dev) {
 }
 
 KFB_API hipError_t kfb_host_unregister(void* p) { return hipHostUnregister(p); }
+
+// ---------------------------------------------------------------------------
+// Peer model slots over HIP IPC (KungFu PairAveraging, parallel/kungfu.py).
+// The exporter publishes the IPC handle of the allocation that holds its
+// slots plus the slots' byte offset inside it (the caching allocator hands
+// out sub-ranges of larger blocks); the importer opens the handle on ITS OWN
+// device (the peer's memory mapped into this device's address space, peer
+// access enabled), so no rank ever creates a context on a peer's GPU.
+
+// handle (64 bytes) and the byte offset of p within its allocation
+KFB_API hipError_t kfb_ipc_export(void* p, void* handle, long long* offset) {
+  hipIpcMemHandle_t h;
+  hipError_t e = hipIpcGetMemHandle(&h, p);
+  if (e != hipSuccess) return e;
+  void* base = nullptr;
+  size_t size = 0;
+  e = hipMemGetAddressRange(&base, &size, p);
+  if (e != hipSuccess) return e;
+  memcpy(handle, &h, sizeof(h));
+  *offset = (long long)((char*)p - (char*)base);
+  return hipSuccess;
+}
+
+KFB_API int kfb_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
+
+// Opens a peer's handle on `device` (this rank's own GPU): *base receives the
+// mapped base address of the peer allocation.  The calling thread's current
+// device is restored.
+KFB_API hipError_t kfb_ipc_open(const void* handle, int device, void** base) {
+  int prev = -1;
+  hipError_t e = hipGetDevice(&prev);
+  if (e != hipSuccess) return e;
+  if (prev != device && (e = hipSetDevice(device)) != hipSuccess) return e;
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  e = hipIpcOpenMemHandle(base, h, hipIpcMemLazyEnablePeerAccess);
+  if (prev != device) {
+    const hipError_t e2 = hipSetDevice(prev);
+    if (e == hipSuccess) e = e2;
+  }
+  return e;
+}
+
+KFB_API hipError_t kfb_ipc_close(void* base) { return hipIpcCloseMemHandle(base); }
+
+// Peer access from `device` to `peer` (both physical indices as this process
+// sees them); already-enabled counts as success, an impossible pairing as
+// hipErrorPeerAccessUnsupported.
+KFB_API hipError_t kfb_enable_peer(int device, int peer) {
+  if (device == peer) return hipSuccess;
+  int can = 0;
+  hipError_t e = hipDeviceCanAccessPeer(&can, device, peer);
+  if (e != hipSuccess) return e;
+  if (!can) return hipErrorPeerAccessUnsupported;
+  int prev = -1;
+  if ((e = hipGetDevice(&prev)) != hipSuccess) return e;
+  if (prev != device && (e = hipSetDevice(device)) != hipSuccess) return e;
+  e = hipDeviceEnablePeerAccess(peer, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();
+    e = hipSuccess;
+  }
+  if (prev != device) {
+    const hipError_t e2 = hipSetDevice(prev);
+    if (e == hipSuccess) e = e2;
+  }
+  return e;
+}
 
 // y (fp32) = x (bf16 / fp16): a low-precision gradient wire buffer back into
 // the flat fp32 gradient.

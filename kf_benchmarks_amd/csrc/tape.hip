@@ -174,15 +174,15 @@ static const Sig* get_sig(Tape* t, const char* types) {
 static_assert(std::is_nothrow_move_constructible<Raw>::value, "Raw moves must not copy");
 static_assert(std::is_nothrow_move_constructible<Op>::value, "Op moves must not copy");
 
-// the op being recorded (one at a time, by the thread that added it)
-static Tape* g_rt = nullptr;
-static int g_rop = -1;
-static std::thread::id g_rtid;
+// the op being recorded (one at a time, by the thread that added it).
+// thread_local: another thread launching while an op records (the input
+// producer's JPEG / augment kernels) sees no tape and never touches the
+// recording thread's ops vector
+static thread_local Tape* g_rt = nullptr;
+static thread_local int g_rop = -1;
 
 static Op* cur_op() {
-  if (!g_rt || g_rop < 0 || g_rop >= (int)g_rt->ops.size() ||
-      std::this_thread::get_id() != g_rtid)
-    return nullptr;
+  if (!g_rt || g_rop < 0 || g_rop >= (int)g_rt->ops.size()) return nullptr;
   return &g_rt->ops[g_rop];
 }
 
@@ -317,7 +317,6 @@ KFB_API int kfb_tape_begin_op(void* h, int op) {
   if (!t || op < 0 || op >= (int)t->ops.size()) return -1;
   g_rt = t;
   g_rop = op;
-  g_rtid = std::this_thread::get_id();
   kfb::g_raw_rec.store(1);
   return 0;
 }

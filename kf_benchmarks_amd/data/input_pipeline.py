@@ -106,6 +106,7 @@ class PrefetchInput:
         self._err: Optional[BaseException] = None
         self._stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         self._next = None
+        self._last = self._tape_bufs = None
         self.producer = None
         if batch_group_size > 1:
             from ..cnn_util import ImageProducer
@@ -168,7 +169,7 @@ class PrefetchInput:
             lab = s.labels.to(dev, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(dev))
-            s.ev = ev  # the slot may be refilled once these copies are done
+            s.release(ev)  # the slot may be refilled once these copies are done
             u8 = J.decode(descs, blocks, hosted, ts.n, ts.height, ts.width, ts.crop_pixels)
             return [F.augment_u8(u8, prm, self.dtype), lab]
         img = ts[0].to(self.device, non_blocking=True)
@@ -231,7 +232,14 @@ class PrefetchInput:
             N.call("kfb_memcpy_d2d", b.data_ptr(), N.dyn("input_%d" % i, t.data_ptr()),
                    t.numel() * t.element_size(), cur.cuda_stream)
             bufs.append(b)
+        self._tape_bufs = self._last = tuple(bufs)
         return tuple(bufs)
+
+    def consumed(self):
+        """The device tensors the last step's forward read: the tape-owned
+        copies (which every replay refills) once a tape was recorded, the
+        fetched batch in an eager step (tests compare their contents)."""
+        return self._last
 
     def tape_advance(self):
         if self._next is None:
@@ -242,6 +250,7 @@ class PrefetchInput:
         for t in out:
             t.record_stream(cur)
         self._cur = out
+        self._last = self._tape_bufs
 
     def tape_values(self):
         return {"input_%d" % i: t.data_ptr() for i, t in enumerate(self._cur)}
@@ -266,6 +275,7 @@ class PrefetchInput:
             cur.wait_event(ev)
             for t in out:
                 t.record_stream(cur)
+        self._last = tuple(out)
         try:
             self._next = self._fetch()
         except StopIteration:
@@ -281,6 +291,11 @@ class PrefetchInput:
         self._stop.set()
         if self.producer is not None:
             self.producer.done()
+            try:
+                while True:
+                    _drop(self._q.get_nowait())
+            except queue.Empty:
+                pass
             return
         t = getattr(self, "_thread", None)
         for _ in range(100):  # unblock a put on a full queue until the producer sees _stop
@@ -288,7 +303,7 @@ class PrefetchInput:
                 break
             try:
                 while True:
-                    self._q.get_nowait()
+                    _drop(self._q.get_nowait())
             except queue.Empty:
                 pass
             t.join(timeout=0.1)
@@ -299,6 +314,14 @@ class PrefetchInput:
                     close()  # generator finally: the native pipe's threads are joined
                 except Exception:  # noqa: BLE001 - best effort at shutdown
                     pass
+
+
+def _drop(item):
+    """A queued batch that will never be copied: its pinned ring slot (GPU
+    JPEG path) goes back to the producer."""
+    slot = getattr(item, "slot", None)
+    if slot is not None:
+        slot.release()
 
 
 def make_input_source(bench, subset="train"):

@@ -520,6 +520,7 @@ class _JpegSlot:
     BLOCKS_PER_IMAGE = 4096
 
     def __init__(self, n, height, width):
+        import threading
         import torch
         from .. import runtime
         pin = torch.cuda.is_available()
@@ -533,14 +534,40 @@ class _JpegSlot:
         self.params = buf((n, 8), torch.float32)
         self.labels = buf((n,), torch.int32)
         self.ev = None
+        # set while no yielded batch lives in the slot: a batch waiting in a
+        # prefetch queue (no copy enqueued yet) keeps it cleared, so the
+        # producer can never refill a slot whose batch is still queued
+        self._free = threading.Event()
+        self._free.set()
+
+    def claim(self):
+        self._free.clear()
+
+    def release(self, ev=None):
+        """The consumer enqueued its device copies of this slot (``ev`` fires
+        when they are done), or dropped the batch (ev None)."""
+        self.ev = ev
+        self._free.set()
 
     def wait_free(self):
+        self._free.wait()
         if self.ev is not None:
             self.ev.synchronize()
             self.ev = None
 
 
-_JPEG_RING = 6  # slots: prefetch queue depth + the batch being copied + 1
+# pinned ring slots by default; make_batch_iterator sizes the ring from the
+# consumer's real lookahead (prefetch queue + ImageProducer groups)
+_JPEG_RING = 6
+
+
+def jpeg_ring_slots(prefetch_depth: int, batch_group_size: int) -> int:
+    """Slots so the producer is never blocked by the ring before it is by the
+    queue: every batch the queue (depth) or an ImageProducer (up to 3G-1
+    ahead) can hold, plus the one being copied and the one being filled."""
+    g = max(int(batch_group_size or 1), 1)
+    ahead = max(int(prefetch_depth), 1) + (3 * g if g > 1 else 0)
+    return max(_JPEG_RING, ahead + 2)
 
 
 def _batched(pre, records: Iterator[bytes], threads: int):
@@ -553,13 +580,15 @@ def _batched(pre, records: Iterator[bytes], threads: int):
         # host threads entropy-decode only; reconstruction on the GPU
         pipe = runtime.ImagePipe(threads, pre.height, pre.width, pre.distortions,
                                  pre.distort_color_in_yiq)
-        ring = [_JpegSlot(bs, pre.height, pre.width) for _ in range(_JPEG_RING)]
+        ring = [_JpegSlot(bs, pre.height, pre.width)
+                for _ in range(getattr(pre, "jpeg_ring", _JPEG_RING))]
         try:
             for k in itertools.count():
                 recs = [next(records) for _ in range(bs)]
                 seeds = base.spawn(1)[0].generate_state(bs, dtype=np.uint64)
                 slot = ring[k % len(ring)]
                 slot.wait_free()
+                slot.claim()
                 nblocks, hosted, bad = pipe.run_coef(recs, seeds, slot)
                 if bad > 0:
                     raise ValueError("%d of %d image records in this batch could not be "
@@ -873,5 +902,7 @@ def make_batch_iterator(bench, subset="train"):
         # host threads entropy-decode only, reconstruction on the GPU
         # (csrc/jpeg.hip); KFB_GPU_JPEG=0: they decode the whole JPEG
         pre.gpu_jpeg = os.environ.get("KFB_GPU_JPEG", "1") != "0"
+        pre.jpeg_ring = jpeg_ring_slots(max(bench.params.datasets_prefetch_buffer_size, 1) + 1,
+                                        bench.params.batch_group_size)
     shift = bench.task_index / float(max(bench.num_replicas, 1))
     return pre.minibatch(bench.dataset, subset, bench.params, shift_ratio=shift)

@@ -62,6 +62,11 @@ _SIGS = {
     "kfb_tape_set_raw": [I],
     "kfb_host_register": [P, ctypes.c_size_t, P],
     "kfb_host_unregister": [P],
+    "kfb_ipc_export": [P, P, P],
+    "kfb_ipc_handle_bytes": [],
+    "kfb_ipc_open": [P, I, P],
+    "kfb_ipc_close": [P],
+    "kfb_enable_peer": [I, I],
     "kfb_nonfinite": [P, L, P, P],
     "kfb_half_sumsq": [P, L, P, P],
     "kfb_cast_f32": [P, P, I, L, P],
@@ -104,7 +109,7 @@ _SIGS = {
     "kfb_ssd_heads": [I, P, P, I, I, I, I, L, I, L, I, I, P],
     "kfb_slab_colsum": [P, I, I, P, I, P],
 }
-_RESTYPES = {"kfb_bn_num_slabs": c_int, "kfb_colsum_num_slabs": c_int,
+_RESTYPES = {"kfb_ipc_handle_bytes": c_int, "kfb_bn_num_slabs": c_int, "kfb_colsum_num_slabs": c_int,
              "kfb_gemm_splits": c_int, "kfb_ctc_max_states": c_int, "kfb_tape_new": c_void_p,
              "kfb_tape_free": None, "kfb_tape_set_raw": None,
              "kfb_tape_raw_launches": ctypes.c_long}

@@ -187,6 +187,7 @@ class Hierarchical:
         self.leader = self.members[0]
         leaders = [g[0] for g in groups]
         self.is_leader = rank == self.leader
+        self.closed = False
         from . import comm as _comm
         world = _comm.get_world()
         self.native = None
@@ -213,7 +214,18 @@ class Hierarchical:
                 lead.all_reduce(buf, op=op).wait()
             return [g.broadcast(buf, src=0)]
 
+    def close(self):
+        """Destroys the native subgroup communicators (the world's own is
+        destroyed by comm.World.shutdown).  Idempotent."""
+        if self.native and not self.closed:
+            for c in self.native:
+                if c is not None:
+                    c.close()
+        self.closed = True
+
     def launch(self, buf, op: str = "sum"):
+        if self.closed:
+            raise RuntimeError("Hierarchical all-reduce used after close()")
         if self.native is not None:
             return self._launch_native(buf, op)
         import torch.distributed as dist

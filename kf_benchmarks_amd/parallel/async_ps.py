@@ -49,16 +49,27 @@ class _SharedState:
                 f.write(b"\0" * 64)
             open(self.lock_path, "wb").close()
         cuda = tensors[0].is_cuda
+        self._opened = []
         if cuda:
+            # rank 0's buffers mapped into every other rank's OWN device
+            # (parallel/ipc.py: no context on rank 0's GPU)
+            from . import ipc
+            dev = tensors[0].device
             if world.rank == 0:
                 self.shared = [t.detach().clone() for t in tensors]
-                from torch.multiprocessing.reductions import reduce_tensor
-                handles = [reduce_tensor(t) for t in self.shared]
+                torch.cuda.synchronize(dev)
+                infos = [ipc.export_slots(t) for t in self.shared]
             else:
-                handles = None
-            handles = comm.all_gather_object(handles)[0]
+                infos = None
+            infos = comm.all_gather_object(infos)[0]
             if world.rank != 0:
-                self.shared = [fn(*args) for fn, args in handles]
+                mine = ipc.export_view(dev)
+                self.shared = []
+                for t, info in zip(tensors, infos):
+                    base = ipc.open_peer_slots(info, mine)
+                    self._opened.append(base)
+                    self.shared.append(ipc.wrap(base + info["offset"], t.numel(), t.dtype, dev)
+                                       .view(t.shape))
         else:
             paths = ["/dev/shm/kfb_ps_var_%s_%d" % (job, i) for i in range(len(tensors))]
             if world.rank == 0:
@@ -99,7 +110,14 @@ class _SharedState:
         self._step_m.close()
         self._step_f.close()
         self._lock_f.close()
-        comm.all_gather_object(True)  # nobody maps the files any more
+        if self._opened:
+            from . import ipc
+            torch.cuda.synchronize(self.shared[0].device)
+            self.shared = []
+            for base in self._opened:
+                ipc.close_mapping(base)
+            self._opened = []
+        comm.all_gather_object(True)  # nobody maps the files / buffers any more
         if self.world.rank == 0:
             for p in [self.lock_path, self.step_path] + list(getattr(self, "_paths", [])):
                 try:

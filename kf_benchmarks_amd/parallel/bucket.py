@@ -239,6 +239,11 @@ class BucketReducer:
         self._relaxed_step += 1
         self._active = False
 
+    def close(self):
+        """Releases the reducer's own communicators (hierarchical subgroups)."""
+        if self.hierarchical is not None:
+            self.hierarchical.close()
+
     def finish(self):
         """Launch whatever did not fire (unused params, overlap off) and make
         the current stream wait for every bucket."""

@@ -75,6 +75,18 @@ class World:
             return "nccl"
         return self.backend or "none"
 
+    def fall_back_to_torch(self, reason: str):
+        """Collective: drop the native communicator and carry the device
+        collectives on a torch ProcessGroupNCCL (created here, every rank)."""
+        import warnings
+        warnings.warn("native RCCL communicator disabled (%s); device collectives on torch's "
+                      "ProcessGroupNCCL" % reason)
+        if self.native is not None:
+            self.native.close(abort=True)
+            self.native = None
+        if self.device_group is None and self.backend != "nccl" and torch.cuda.is_available():
+            self.device_group = dist.new_group(list(range(self.size)), backend="nccl")
+
     def shutdown(self):
         if self.native is not None:
             self.native.close()
@@ -299,6 +311,68 @@ def reset_world():
     """Test helper: forget the cached world (does not destroy the group)."""
     global _WORLD
     _WORLD = None
+
+
+def selftest_device_collectives(cand, sizes, dtypes=(torch.float32,), device=None,
+                                 seed: int = 0) -> dict:
+    """Checks a candidate device communicator ``cand`` (all_reduce /
+    broadcast returning works whose wait() orders the current stream, and
+    barrier) against torch's host-side group on the same buffers, bitwise:
+    for every buffer size and dtype a broadcast from rank 0 and a sum / max
+    all-reduce of small integer-valued data (exact in every dtype and any
+    summation order, so a correct collective matches bit for bit), then a
+    barrier.  Collective over all ranks; every rank returns the same verdict
+    {"ok", "checked", "failed"} (any rank's mismatch fails all)."""
+    w = get_world()
+    dev = device if device is not None else getattr(cand, "device", None)
+    failed = []
+    checked = 0
+    for n in sizes:
+        n = int(n)
+        for dt in dtypes:
+            lim = 16 if dt in (torch.bfloat16, torch.float16) else 1024
+            g = torch.Generator().manual_seed((seed * 1000003 + w.rank * 7919 + n) & 0x7FFFFFFF)
+            host = torch.randint(-lim, lim + 1, (n,), generator=g).to(dt)
+            for kind in ("broadcast", "sum", "max"):
+                ref = host.clone().float()
+                if kind == "broadcast":
+                    dist.broadcast(ref, 0)
+                else:
+                    dist.all_reduce(ref, op=_ROP[kind])
+                buf = host.to(dev) if dev is not None else host.clone()
+                work = cand.broadcast(buf, 0) if kind == "broadcast" else \
+                    cand.all_reduce(buf, kind)
+                if work is not None:
+                    work.wait()
+                got = buf.float().cpu()
+                checked += 1
+                if not torch.equal(got, ref.to(dt).float()):
+                    failed.append("%s n=%d %s" % (kind, n, str(dt).replace("torch.", "")))
+    cand.barrier()
+    verdicts = all_gather_object(failed)
+    bad = sorted({f for fl in verdicts for f in fl})
+    return {"ok": not bad, "checked": checked, "failed": bad[:8]}
+
+
+def validate_native(sizes, dtypes=(torch.float32,)) -> Optional[dict]:
+    """KFB_NATIVE_COMM=auto: self-test the native communicator on the job's
+    buffer sizes and fall back to torch's ProcessGroupNCCL if it fails.
+    Returns the self-test record (None: no native communicator)."""
+    w = get_world()
+    if w.native is None or not w.has_pg:
+        return None
+    from . import rccl as _rccl
+    try:
+        st = selftest_device_collectives(w.native, sizes, dtypes)
+    except Exception as e:  # noqa: BLE001 - a raising collective is a failed test
+        st = {"ok": False, "checked": 0, "failed": ["raised: %s" % e]}
+        # (the other ranks' verdicts are unknown: agree on failure)
+        all_gather_object(["raised"])
+    st["mode"] = _rccl.mode()
+    if not st["ok"] and _rccl.mode() == "auto":
+        w.fall_back_to_torch("self-test failed: %s" % ", ".join(st["failed"]))
+        st["fallback"] = "torch ProcessGroupNCCL"
+    return st
 
 
 _ROP = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}

@@ -60,6 +60,7 @@ import numpy as np
 import torch
 
 from . import comm
+from .ipc import close_mapping, export_slots, open_peer_slots
 from .variable_mgr import Strategy
 
 
@@ -149,13 +150,19 @@ class ModelStore:
             self.slots[0].copy_(flat)
             self.slots[1].copy_(flat)
             torch.cuda.synchronize(flat.device)
-            from torch.multiprocessing.reductions import reduce_tensor
-            handle = reduce_tensor(self.slots)
-            handles = comm.all_gather_object(handle)
+            # the slots' IPC handle, opened by every peer on ITS OWN device
+            # (native hipIpcOpenMemHandle; torch's tensor rebuild would open it
+            # on this rank's device index and create a context there)
+            info = export_slots(self.slots)
+            infos = comm.all_gather_object(info)
             self.peer_slots = {}
-            for r, (fn, args) in enumerate(handles):
+            self._opened = []
+            for r, pinfo in enumerate(infos):
                 if r != self.rank:
-                    self.peer_slots[r] = fn(*args)
+                    base = open_peer_slots(pinfo, info)
+                    self._opened.append(base)
+                    nb = self.slots[0].numel() * self.slots.element_size()
+                    self.peer_slots[r] = (base + pinfo["offset"], base + pinfo["offset"] + nb)
             self.pull_stream = torch.cuda.Stream(flat.device)
             # device-side seqlock validation (flag read by the fused
             # optimizer) when every peer header can be mapped for the GPU
@@ -269,7 +276,7 @@ class ModelStore:
         """The per-step values of a pull of ``peer``'s latest committed model
         (launch tape: the recorded copy and seqlock check read them)."""
         slot, v = self._snapshot_header(peer)
-        return {"pa_src": self.peer_slots[peer][slot].data_ptr(),
+        return {"pa_src": self.peer_slots[peer][slot],
                 "pa_word": self.hdr.device_word(peer, slot) or 0, "pa_seq": v,
                 "_pa": (peer, slot)}
 
@@ -348,6 +355,11 @@ class ModelStore:
             self.abort_publish()
         self.flush()
         self.hdr.close()
+        if self.cuda and self._opened:
+            torch.cuda.synchronize(self.device)
+            for base in self._opened:
+                close_mapping(base)
+            self._opened = []
         if not self.cuda:
             try:
                 os.remove(self.path)

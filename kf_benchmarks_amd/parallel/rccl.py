@@ -58,14 +58,20 @@ def available() -> bool:
         return False
 
 
+def mode() -> str:
+    """KFB_NATIVE_COMM: ``auto`` (default) - device collectives of a
+    multi-process run on this communicator, validated at startup against
+    torch's gloo group (:func:`comm.selftest_device_collectives`), falling
+    back to torch's ProcessGroupNCCL if the check fails; ``1`` - this
+    communicator, no fallback; ``0`` - torch's ProcessGroupNCCL only.  With
+    the native communicator no ProcessGroupNCCL exists unless the fallback
+    creates one: subgroups are native communicators too (:func:`subgroup`)."""
+    v = os.environ.get("KFB_NATIVE_COMM", "auto").strip().lower()
+    return v if v in ("0", "1", "auto") else "auto"
+
+
 def enabled() -> bool:
-    """KFB_NATIVE_COMM=1 selects this communicator for the device
-    collectives of a multi-process run; the default is torch's
-    ProcessGroupNCCL (the path every multi-GPU run takes until the native one
-    has a recorded multi-GPU run with matching losses).  With it on, no
-    ProcessGroupNCCL is created at all: subgroups are native communicators
-    too (:func:`subgroup`)."""
-    return os.environ.get("KFB_NATIVE_COMM", "0") == "1"
+    return mode() != "0"
 
 
 def subgroup(world_native: "NativeComm", ranks, store, tag: str):

@@ -144,7 +144,8 @@ class Strategy:
         return self.name
 
     def close(self):
-        pass
+        if self.reducer is not None:
+            self.reducer.close()
 
 
 class IndependentStrategy(Strategy):
@@ -242,6 +243,7 @@ class KungFuSMA(Strategy):
         if self._work is not None:
             self._work.wait()
             self._work = None
+        super().close()
 
 
 class KungFuAdaSGD(Strategy):
@@ -308,6 +310,7 @@ class KungFuAdaSGD(Strategy):
 
     def close(self):
         self.sma.close()
+        super().close()
 
 
 MEAN_OVER_TOWERS = ("parameter_server", "distributed_replicated")

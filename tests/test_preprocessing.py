@@ -316,3 +316,28 @@ def test_device_augment_batches_on_host(tmp_path):
     assert prm.shape == (8, 8) and labels.dtype == np.int32
     out = F.augment_u8(torch.from_numpy(imgs), torch.from_numpy(prm), torch.float32)
     assert out.shape == (8, 227, 227, 3) and out.min() >= -1.0 and out.max() <= 1.0
+
+
+def test_jpeg_ring_slot_is_held_while_its_batch_is_queued():
+    """A yielded GPU-JPEG batch keeps its pinned ring slot until the consumer
+    enqueued its copies (or dropped it): the producer cannot refill a slot
+    whose batch still waits in a prefetch queue, however deep the queue."""
+    import threading
+    import time
+    slot = pre._JpegSlot(2, 8, 8)
+    slot.wait_free()  # a fresh slot is free
+    slot.claim()
+    done = threading.Event()
+    th = threading.Thread(target=lambda: (slot.wait_free(), done.set()), daemon=True)
+    th.start()
+    time.sleep(0.2)
+    assert not done.is_set()  # queued, not yet copied: refilling must wait
+    slot.release(None)
+    assert done.wait(5)
+    th.join(5)
+
+
+def test_jpeg_ring_follows_the_lookahead():
+    assert pre.jpeg_ring_slots(2, 1) == pre._JPEG_RING
+    assert pre.jpeg_ring_slots(9, 1) == 11  # queue of 9 + copying + filling
+    assert pre.jpeg_ring_slots(3, 3) == 3 + 9 + 2  # ImageProducer keeps <= 3G-1 ahead
