@@ -629,274 +629,6 @@ bn_bwd_apply_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __res
   }
 }
 
-// ---- finalize folded into the apply pass ---------------------------------
-// A BN whose statistics (or backward partials) come from a conv epilogue's
-// [2][nslab][C] slots needs a finalize before its apply; as its own launch
-// that is a 5-7 us kernel on the critical path per BN.  In these forms every
-// workgroup of the (grid-stride, <= FOLD_GRID workgroups) apply pass folds
-// the slots of all C channels itself into LDS at its start - 2 x nslab
-// independent loads per channel, one channel (or two) per thread, served by
-// L2 - and workgroup 0 writes the per-channel results the rest of the step
-// reads (saved mean / invstd, scale / shift, running statistics; dgamma /
-// dbeta).  The statistics shift K the forward partials are centered on is
-// read by every workgroup's fold, so the new K is written by the last
-// workgroup to finish (arrival counter in the slot buffer's zeroed tail).
-constexpr int FOLD_GRID = 1024;
-constexpr int FOLD_CMAX = 512;
-
-struct BnFoldF {
-  const float* psum;
-  const float* psq;
-  int nslab;
-  long rows;
-  const float* gamma;
-  const float* beta;
-  float decay, eps;
-  float* run_mean;
-  float* run_var;
-  float* save_mean;
-  float* save_invstd;
-  float* scale;
-  float* shift;
-  float* kshift;
-  int* counter;
-};
-
-struct BnFoldB {
-  const float* pdy;
-  const float* pdyx;
-  int nslab;
-  long rows;
-  const float* gamma;
-  const float* mean;
-  const float* invstd;
-  float* dgamma;
-  float* dbeta;
-  int accumulate;
-};
-
-// sum over the nslab slots of channel c: up to 32 slots with every load in
-// flight at once (one L2 round trip before the pass can start), beyond
-// that 8 independent loads per array per batch
-__device__ __forceinline__ void fold_ch(const float* __restrict__ pa, const float* __restrict__ pb,
-                                        int nslab, int C, int c, double& sa, double& sb) {
-  if (nslab <= 32) {
-    float va[32], vb[32];
-#pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      va[u] = u < nslab ? pa[(long)u * C + c] : 0.f;
-      vb[u] = u < nslab ? pb[(long)u * C + c] : 0.f;
-    }
-    float a4[4] = {0.f, 0.f, 0.f, 0.f}, b4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      a4[u & 3] += va[u];
-      b4[u & 3] += vb[u];
-    }
-    sa = ((double)a4[0] + (double)a4[1]) + ((double)a4[2] + (double)a4[3]);
-    sb = ((double)b4[0] + (double)b4[1]) + ((double)b4[2] + (double)b4[3]);
-    return;
-  }
-  float a[8], b[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) { a[u] = 0.f; b[u] = 0.f; }
-  int k = 0;
-  for (; k + 8 <= nslab; k += 8) {
-    float va[8], vb[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      va[u] = pa[(long)(k + u) * C + c];
-      vb[u] = pb[(long)(k + u) * C + c];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) { a[u] += va[u]; b[u] += vb[u]; }
-  }
-  for (; k < nslab; ++k) {
-    a[0] += pa[(long)k * C + c];
-    b[0] += pb[(long)k * C + c];
-  }
-  sa = 0.0;
-  sb = 0.0;
-#pragma unroll
-  for (int u = 0; u < 8; ++u) { sa += a[u]; sb += b[u]; }
-}
-
-template <typename T, int V, bool RES, bool RELU>
-__global__ void __launch_bounds__(256)
-bn_apply_fold_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y, long nvec,
-                int C, BnFoldF f, uint8_t* __restrict__ mb) {
-  __shared__ float lsc[FOLD_CMAX], lsf[FOLD_CMAX], lmean[FOLD_CMAX];
-  __shared__ int last;
-  const double n = (double)f.rows;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    double s, q;
-    fold_ch(f.psum, f.psq, f.nslab, C, c, s, q);
-    // (the math of bn_finalize_stats_k)
-    const double k = f.kshift ? (double)f.kshift[c] : 0.0;
-    const double dm = s / n;
-    const double mean = k + dm;
-    double var = q / n - dm * dm;
-    if (var < 0.0) var = 0.0;
-    const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
-    const float g = f.gamma ? f.gamma[c] : 1.f;
-    const float b = f.beta ? f.beta[c] : 0.f;
-    lsc[c] = g * invstd;
-    lsf[c] = b - (float)mean * g * invstd;
-    lmean[c] = (float)mean;
-    if (blockIdx.x == 0) {
-      f.save_mean[c] = (float)mean;
-      f.save_invstd[c] = invstd;
-      f.scale[c] = g * invstd;
-      f.shift[c] = b - (float)mean * g * invstd;
-      if (f.run_mean) {
-        const double unbiased = f.rows > 1 ? var * n / (n - 1.0) : var;
-        f.run_mean[c] = f.run_mean[c] * f.decay + (float)mean * (1.f - f.decay);
-        f.run_var[c] = f.run_var[c] * f.decay + (float)unbiased * (1.f - f.decay);
-      }
-    }
-  }
-  __syncthreads();
-  const unsigned cv = (unsigned)(C / V);
-  const unsigned nn = (unsigned)nvec, stride = gridDim.x * blockDim.x;
-  const unsigned i0 = blockIdx.x * blockDim.x + threadIdx.x;
-  const int c = (int)(i0 % cv) * V;  // fixed: the host makes stride a multiple of cv
-  float sc[V], sf[V];
-#pragma unroll
-  for (int k = 0; k < V; ++k) { sc[k] = lsc[c + k]; sf[k] = lsf[c + k]; }
-  auto apply = [&](float (&v)[V], const float (&rr)[V]) {
-#pragma unroll
-    for (int k = 0; k < V; ++k) {
-      float o = v[k] * sc[k] + sf[k];
-      if (RES) o += rr[k];
-      if (RELU) o = fmaxf(o, 0.f);
-      v[k] = o;
-    }
-  };
-  unsigned i = i0;
-  for (; i + stride < nn; i += 2 * stride) {
-    float v0[V], v1[V], r0[V], r1[V];
-    load_vec<T, V>(x + (long)i * V, v0);
-    load_vec<T, V>(x + (long)(i + stride) * V, v1);
-    if (RES) {
-      load_vec<T, V>(res + (long)i * V, r0);
-      load_vec<T, V>(res + (long)(i + stride) * V, r1);
-    }
-    apply(v0, r0);
-    apply(v1, r1);
-    store_vec<T, V>(y + (long)i * V, v0);
-    store_vec<T, V>(y + (long)(i + stride) * V, v1);
-    if (RELU) {
-      relu_bits<T, V>(mb, i, v0);
-      relu_bits<T, V>(mb, i + stride, v1);
-    }
-  }
-  if (i < nn) {
-    float v0[V], r0[V];
-    load_vec<T, V>(x + (long)i * V, v0);
-    if (RES) load_vec<T, V>(res + (long)i * V, r0);
-    apply(v0, r0);
-    store_vec<T, V>(y + (long)i * V, v0);
-    if (RELU) relu_bits<T, V>(mb, i, v0);
-  }
-  // the new statistics shift, once every workgroup has read the old one
-  if (f.kshift && f.counter) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const int prev = __hip_atomic_fetch_add(f.counter, 1, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-      last = prev == (int)gridDim.x - 1;
-    }
-    __syncthreads();
-    if (last) {
-      for (int cc = threadIdx.x; cc < C; cc += blockDim.x) f.kshift[cc] = lmean[cc];
-      if (threadIdx.x == 0)
-        __hip_atomic_store(f.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-template <typename T, int V, bool MASK, bool DRES>
-__global__ void __launch_bounds__(256)
-bn_bwd_apply_fold_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __restrict__ x,
-                    T* __restrict__ dx, T* __restrict__ dres, long nvec, int C, BnFoldB f) {
-  __shared__ float la[FOLD_CMAX], lb[FOLD_CMAX], lc[FOLD_CMAX];
-  const double n = (double)f.rows;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    double s1, s2;
-    fold_ch(f.pdy, f.pdyx, f.nslab, C, c, s1, s2);
-    // (the math of bn_finalize_grad_k)
-    const float is = f.invstd[c];
-    const float g = f.gamma ? f.gamma[c] : 1.f;
-    const double A = (double)g * is;
-    const double B = -A * (double)is * (double)is * s2 / n;
-    la[c] = (float)A;
-    lb[c] = (float)B;
-    lc[c] = (float)(-A * s1 / n - (double)f.mean[c] * B);
-    if (blockIdx.x == 0) {
-      if (f.dgamma) f.dgamma[c] = (f.accumulate ? f.dgamma[c] : 0.f) + (float)(s2 * is);
-      if (f.dbeta) f.dbeta[c] = (f.accumulate ? f.dbeta[c] : 0.f) + (float)s1;
-    }
-  }
-  __syncthreads();
-  const unsigned cv = (unsigned)(C / V);
-  const unsigned nn = (unsigned)nvec, stride = gridDim.x * blockDim.x;
-  const unsigned i0 = blockIdx.x * blockDim.x + threadIdx.x;
-  const int c = (int)(i0 % cv) * V;
-  float a[V], b[V], cc[V];
-#pragma unroll
-  for (int k = 0; k < V; ++k) { a[k] = la[c + k]; b[k] = lb[c + k]; cc[k] = lc[c + k]; }
-  auto one = [&](unsigned i) {
-    float g0[V], x0[V];
-    load_vec<T, V>(dy + (long)i * V, g0);
-    load_vec<T, V>(x + (long)i * V, x0);
-    if (MASK) {
-      float y0[V];
-      load_vec<T, V>(y + (long)i * V, y0);
-#pragma unroll
-      for (int k = 0; k < V; ++k) g0[k] = y0[k] > 0.f ? g0[k] : 0.f;
-    }
-    if (DRES) store_vec<T, V>(dres + (long)i * V, g0);
-    float o0[V];
-#pragma unroll
-    for (int k = 0; k < V; ++k) o0[k] = g0[k] * a[k] + x0[k] * b[k] + cc[k];
-    store_vec<T, V>(dx + (long)i * V, o0);
-  };
-  unsigned i = i0;
-  for (; i + stride < nn; i += 2 * stride) {
-    // both vectors' loads issue before either is used (as step2 above)
-    float g0[V], g1[V], x0[V], x1[V];
-    load_vec<T, V>(dy + (long)i * V, g0);
-    load_vec<T, V>(x + (long)i * V, x0);
-    load_vec<T, V>(dy + (long)(i + stride) * V, g1);
-    load_vec<T, V>(x + (long)(i + stride) * V, x1);
-    if (MASK) {
-      float y0[V], y1[V];
-      load_vec<T, V>(y + (long)i * V, y0);
-      load_vec<T, V>(y + (long)(i + stride) * V, y1);
-#pragma unroll
-      for (int k = 0; k < V; ++k) {
-        g0[k] = y0[k] > 0.f ? g0[k] : 0.f;
-        g1[k] = y1[k] > 0.f ? g1[k] : 0.f;
-      }
-    }
-    if (DRES) {
-      store_vec<T, V>(dres + (long)i * V, g0);
-      store_vec<T, V>(dres + (long)(i + stride) * V, g1);
-    }
-    float o0[V], o1[V];
-#pragma unroll
-    for (int k = 0; k < V; ++k) {
-      o0[k] = g0[k] * a[k] + x0[k] * b[k] + cc[k];
-      o1[k] = g1[k] * a[k] + x1[k] * b[k] + cc[k];
-    }
-    store_vec<T, V>(dx + (long)i * V, o0);
-    store_vec<T, V>(dx + (long)(i + stride) * V, o1);
-  }
-  if (i < nn) one(i);
-}
-
-// Backward apply of y = relu(bn(x) + bn_r(xr)) with a pre-masked dy: both
-// input gradients from one read of dy (dx = dy*A + x*B + Cc, dxr likewise).
 template <typename T, int V, int U = 0>
 __global__ void __launch_bounds__(256)
 bn_bwd_apply2_k(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ xr,
@@ -1339,37 +1071,6 @@ static bool flat_ok(long nvec, int C, int V) {
 
 static int flat_grid(long nvec) { return (int)((nvec + 256L * 4 - 1) / (256L * 4)); }
 
-// The folded forms apply when the channels fit LDS and the tensor takes the
-// grid-stride pass (the flat pass of the >= 256 MB tensors keeps its
-// finalize launch): KFB_BN_FOLD=0 never.
-// default off: in-network +0.16..0.40 ms/step against the finalize launches
-// (gpurun_out/r10o: 19.27 / 19.03 with the fold vs 18.87 / 18.87 without)
-static int g_bn_fold = -1;  // -1: KFB_BN_FOLD (default off); kfb_bn_set_fold overrides
-
-static bool fold_ok(long nvec, int C, int V) {
-  if (g_bn_fold < 0) {
-    const char* e = getenv("KFB_BN_FOLD");
-    g_bn_fold = (e && atoi(e) != 0) ? 1 : 0;
-  }
-  const bool on = g_bn_fold != 0;
-  const int cv = C / V;
-  return on && V == 8 && C <= FOLD_CMAX && cv > 0 && (cv & (cv - 1)) == 0 && 256 % cv == 0 &&
-         !flat_ok(nvec, C, V) && nvec < (1L << 31) - 2L * 4096 * 256;
-}
-
-static int fold_grid(long nvec) {
-  // KFB_BN_FOLD_GRID: workgroup cap of the folded passes (A/B knob, <= 4096)
-  static const long cap = [] {
-    const char* e = getenv("KFB_BN_FOLD_GRID");
-    const long v = e ? atol(e) : FOLD_GRID;
-    return v < 256 ? 256L : v > 4096 ? 4096L : v;
-  }();
-  long b = (nvec + 255) / 256;
-  if (b > cap) b = cap;
-  return (int)(b < 1 ? 1 : b);
-}
-
-
 static int stream_grid(long nvec) {
   long b = (nvec + 255) / 256;
   if (b > 256L * 16) b = 256L * 16;  // grid-stride beyond 16 blocks per CU
@@ -1443,8 +1144,6 @@ hipError_t bn_finalize_grad_launch(const float* slots, int C, long rows, const f
 }
 }  // namespace kfb
 
-// test / A/B hook: 0 turns the folded finalize-in-apply passes off, 1 on
-KFB_API void kfb_bn_set_fold(int on) { g_bn_fold = on ? 1 : 0; }
 
 KFB_API int kfb_bn_num_slabs(long rows, int C) {
   const int V = vec_width(C);
@@ -1473,31 +1172,6 @@ KFB_API hipError_t kfb_bn_fwd_train(int dtype, const void* x, const void* res, v
         hipLaunchKernelGGL((bn_partial_stats_k<T, VV>), grid, dim3(BN_THREADS), lds, stream,
                            (const T*)x, rows, C, g.cw, g.tpr, g.rpi, slab_rows, psum, psq,
                            kshift);
-      const long nv = rows * C / VV;
-      // 3: a conv epilogue's stats_buffer (with its zeroed counter tail after
-      // psq): the finalize folds into the apply pass where fold_ok
-      if (have_partials == 3 && fold_ok(nv, C, VV)) {
-        const BnFoldF f{psum, psq, nslab, rows, gamma, beta, decay, eps, run_mean, run_var,
-                        save_mean, save_invstd, scale, shift, kshift,
-                        (int*)(psq + (long)nslab * C) + 8};
-        const int gb = fold_grid(nv);
-        if (res) {
-          if (relu)
-            hipLaunchKernelGGL((bn_apply_fold_k<T, VV, true, true>), dim3(gb), dim3(256), 0,
-                               stream, (const T*)x, (const T*)res, (T*)y, nv, C, f, mbits);
-          else
-            hipLaunchKernelGGL((bn_apply_fold_k<T, VV, true, false>), dim3(gb), dim3(256), 0,
-                               stream, (const T*)x, (const T*)res, (T*)y, nv, C, f, mbits);
-        } else {
-          if (relu)
-            hipLaunchKernelGGL((bn_apply_fold_k<T, VV, false, true>), dim3(gb), dim3(256), 0,
-                               stream, (const T*)x, (const T*)nullptr, (T*)y, nv, C, f, mbits);
-          else
-            hipLaunchKernelGGL((bn_apply_fold_k<T, VV, false, false>), dim3(gb), dim3(256), 0,
-                               stream, (const T*)x, (const T*)nullptr, (T*)y, nv, C, f, mbits);
-        }
-        return hipGetLastError();  // (the dispatch macros are plain switches)
-      }
       if (have_partials != 2)  // 2: the producing conv's last workgroup finalized (BnFin)
         hipLaunchKernelGGL(bn_finalize_stats_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,
                            psum, psq, nslab, C, rows, gamma, beta, decay, eps, run_mean, run_var,
@@ -1614,32 +1288,6 @@ KFB_API hipError_t kfb_bn_bwd(int dtype, const void* dy, const void* y, const vo
                            stream, (const T*)dy, (const T*)y, (const T*)x, save_mean, rows, C,
                            g.cw, g.tpr, g.rpi, slab_rows, pdy, pdyx);
       const long nvec = rows * C / VV;
-      if (have_partials == 1 && fold_ok(nvec, C, VV)) {
-        // the finalize folds into the apply pass (see bn_apply_fold_k)
-        const BnFoldB f{pdy, pdyx, nslab, rows, gamma, save_mean, save_invstd, dgamma, dbeta,
-                        accumulate};
-        const int gb = fold_grid(nvec);
-        if (relu) {
-          if (dres)
-            hipLaunchKernelGGL((bn_bwd_apply_fold_k<T, VV, true, true>), dim3(gb), dim3(256), 0,
-                               stream, (const T*)dy, (const T*)y, (const T*)x, (T*)dx, (T*)dres,
-                               nvec, C, f);
-          else
-            hipLaunchKernelGGL((bn_bwd_apply_fold_k<T, VV, true, false>), dim3(gb), dim3(256), 0,
-                               stream, (const T*)dy, (const T*)y, (const T*)x, (T*)dx, (T*)dres,
-                               nvec, C, f);
-        } else {
-          if (dres)
-            hipLaunchKernelGGL((bn_bwd_apply_fold_k<T, VV, false, true>), dim3(gb), dim3(256), 0,
-                               stream, (const T*)dy, (const T*)y, (const T*)x, (T*)dx, (T*)dres,
-                               nvec, C, f);
-          else
-            hipLaunchKernelGGL((bn_bwd_apply_fold_k<T, VV, false, false>), dim3(gb), dim3(256),
-                               0, stream, (const T*)dy, (const T*)y, (const T*)x, (T*)dx,
-                               (T*)dres, nvec, C, f);
-        }
-        return hipGetLastError();
-      }
       if (have_partials != 2)  // 2: the producing dgrad's last workgroup finalized (BnGFin)
         hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,
                            pdy, pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta,

@@ -2539,7 +2539,10 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
   // skips its finalize launch
   // flags: bit 0 = ReLU after the bias (forward epilogue), bit 1 = zero-fill
   // the unsampled pixels of a stride-2 scatter (see IgArgs::zfill), bit 2 =
-  // `mask` is a ReLU bit mask (see IgArgs::maskbits)
+  // `mask` is a ReLU bit mask (see IgArgs::maskbits), bit 3 = statistics
+  // only: the streaming 1x1 kernel (IG_ALGO_S1) sums the output's BN
+  // statistics without storing it (its consumer recomputes it,
+  // kfb_bn_fwd_train_recompute)
   if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
   const int relu = flags & 1, zfill = (flags >> 1) & 1;
   if (zfill && !(ys == 2 && YH == 2 * OH && YW == 2 * OW)) return hipErrorInvalidValue;
@@ -2591,6 +2594,12 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
   // its geometry the default kernel below runs
   if (algo == IG_ALGO_S3 && fast && !c8 && conv_s3_fits(a)) return launch_conv_s3(dtype, a, stream);
   // IG_ALGO_S1: the streaming 1x1 K -> 4K-channel kernel (conv_s1.hip)
+  if ((flags >> 3) & 1) {  // statistics only: S1 with its stores dropped
+    if (algo != IG_ALGO_S1 || !stats || xbn || addend || !fast || c8) return hipErrorInvalidValue;
+    a.ybytes = 0;
+    if (!conv_s1_fits(a)) return hipErrorInvalidValue;
+    return launch_conv_s1(dtype, a, stream);
+  }
   if (algo == IG_ALGO_S1 && fast && !c8 && conv_s1_fits(a)) return launch_conv_s1(dtype, a, stream);
   // IG_ALGO_S7: the streaming stem conv over the pixel-pair view (conv_s7.hip)
   if (algo == IG_ALGO_S7 && !t && conv_s7_fits(a)) return launch_conv_s7(dtype, a, stream);

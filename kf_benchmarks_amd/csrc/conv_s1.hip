@@ -21,6 +21,13 @@
 //    a tile's stores may stay in flight for D tiles (the counted wait covers
 //    only the DMAs of the next tile and what came before them); one barrier
 //    per tile;
+//  * apply form (EPI_APPLY): the conv whose output only a residual BN + ReLU
+//    consumes is computed twice - once for the BN statistics with its stores
+//    dropped (IgArgs::ybytes 0), once here with the BN apply, residual add and
+//    ReLU in the epilogue (the residual streams through the ring like the
+//    data gradient's addend); y itself is stored from this pass.  At 56x56
+//    64 -> 256 that replaces writing y (411 MB) in one pass and reading it
+//    back (411 MB) in the next by a second read of x (103 MB);
 //  * the waves finish their WCH x 32 accumulators from registers:
 //    v_permlane32_swap pairs give each lane 8 consecutive channels of one
 //    pixel, whose epilogue operands it reads from the ring (chunk-swizzled
@@ -42,7 +49,7 @@ typedef __attribute__((ext_vector_type(4))) unsigned int v4u_t;
 constexpr int BMP = 32;              // pixels per tile
 constexpr int LDS_CAP = 160 * 1024;  // per CU
 
-enum { EPI_STATS = 0, EPI_DGRAD = 2 };
+enum { EPI_STATS = 0, EPI_APPLY = 1, EPI_DGRAD = 2 };
 
 // per input-channel count K: WCH channels per wave (4 waves along channels);
 // WPC workgroups per CU share its LDS
@@ -64,14 +71,20 @@ struct Cfg {
   static constexpr int XD = XB / 4096;          // x DMAs per wave (1 KB each)
   static constexpr int YD = YB / 4096;          // per epilogue operand per wave
   static constexpr bool DG = EPI == EPI_DGRAD;
-  static constexpr int STB = XB + (DG ? 2 * YB + MBA : 0);  // ring stage
+  static constexpr bool AP = EPI == EPI_APPLY;
+  static constexpr int STB = XB + (DG ? 2 * YB + MBA : AP ? YB : 0);  // ring stage
+  static constexpr int DMAS = XD + (DG ? 2 * YD + 1 : AP ? YD : 0);  // DMAs per wave per tile
+  // stores per lane per tile (16-byte y / out stores, out's ReLU-bit bytes;
+  // the apply form issues all three even when y / the bits are not kept)
+  static constexpr int ST = (AP ? 3 : 1) * 2 * CT;
+  // ring stages: what LDS holds, at most 7, and few enough that the counted
+  // wait below fits vmcnt (< 64)
   static constexpr int NST0 = LDS_CAP / WPC / STB;
-  static constexpr int NST = NST0 > 7 ? 7 : NST0;
+  static constexpr int NSTV = (63 + DMAS) / (ST + DMAS) + 1;
+  static constexpr int NST = NST0 < NSTV ? (NST0 > 7 ? 7 : NST0) : (NSTV > 7 ? 7 : NSTV);
   static constexpr int D = NST - 1;             // prefetch distance (tiles)
-  static constexpr int DMAS = XD + (DG ? 2 * YD + 1 : 0);  // DMAs per wave per tile
-  static constexpr int ST = 2 * CT;             // 16-byte stores per lane per tile
   static constexpr int WAIT = ST * D + (D - 1) * DMAS;
-  static_assert(XD >= 1 && (!DG || YD >= 1), "tile split");
+  static_assert(XD >= 1 && (!(DG || AP) || YD >= 1), "tile split");
   static_assert(MB <= MBA, "bits area");
   static_assert(D >= 1 && WAIT < 64, "pipeline depth");
 };
@@ -144,7 +157,8 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
   const __amdgpu_buffer_rsrc_t yrs =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, a.ybytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.addend ? a.addend : a.y), (short)0, a.addend ? a.ybytes : 0, 0x00020000);
+      (void*)(a.addend ? a.addend : a.y), (short)0,
+      a.addend ? (a.out ? a.outbytes : a.ybytes) : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t xbrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.xbn ? a.xbn : a.y), (short)0, a.xbn ? a.ybytes : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
@@ -152,6 +166,12 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
       0x00020000);
   const unsigned xbn_mask = a.xbn != nullptr ? ~0u : 0u;
   const int ldy2 = a.Ncol * 2;
+  // apply form: out (same layout as y) and its ReLU bits ([M * Ncol / 8])
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.out ? a.out : a.y), (short)0, a.out ? a.outbytes : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t obrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.out_bits ? (void*)a.out_bits : a.y), (short)0,
+      a.out_bits ? a.outbytes / 16 : 0, 0x00020000);
 
   // this wave's weight slice as MFMA A fragments (rows = output channels
   // ns0 + WCH wid + 32 i + l32, k = 16 ks + 8 hh .. +7), resident in VGPRs
@@ -163,7 +183,8 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
     for (int ks = 0; ks < KS; ++ks) af[i][ks] = *(const v8s*)(wr + 16 * ks);
   }
   // channel parameters of this lane's chunks cc = (WCH/8) w + 4 i + 2 p + hh
-  float pa[CT][2][8];
+  // (the apply form: BN scale in pa, shift in pb)
+  float pa[CT][2][8], pb[CT][2][8];
 #pragma unroll
   for (int i = 0; i < CT; ++i)
 #pragma unroll
@@ -172,7 +193,10 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
       for (int k = 0; k < 8; ++k) {
         const int ch = ns0 + 8 * ((C::WCH / 8) * wid + 4 * i + 2 * p + hh) + k;
         if constexpr (EPI == EPI_STATS) pa[i][p][k] = a.kshift ? a.kshift[ch] : 0.f;
-        else pa[i][p][k] = a.mean ? a.mean[ch] : 0.f;
+        else if constexpr (EPI == EPI_APPLY) {
+          pa[i][p][k] = a.bn_scale[ch];
+          pb[i][p][k] = a.bn_shift[ch];
+        } else pa[i][p][k] = a.mean ? a.mean[ch] : 0.f;
       }
   // (retire those register loads here, not at their first use inside the
   // tile loop, where the compiler's wait would also drain the ring)
@@ -185,7 +209,10 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(pa[i][p][k]));
+      for (int k = 0; k < 8; ++k) {
+        asm volatile("" ::"v"(pa[i][p][k]));
+        if constexpr (EPI == EPI_APPLY) asm volatile("" ::"v"(pb[i][p][k]));
+      }
 
   // one tile's operands into ring stage st; the same DMA count in every
   // wave and every iteration (tiles past the end load nothing: offset -1),
@@ -204,6 +231,19 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
         const int off =
             p < pend ? p * C::XROW + (((lane % LPR) ^ xsw<K>(pl)) << 4) : -1;
         dma16(xrs, sb + j * 1024, off);
+      }
+    }
+    if constexpr (EPI == EPI_APPLY) {
+      // residual slice rows (2 NS bytes): chunk c at c ^ (p & 15)
+      constexpr int LPR = NS / 8;
+#pragma unroll
+      for (int q = 0; q < C::YD; ++q) {
+        const int j = wid * C::YD + q;
+        const int pl = j * (64 / LPR) + lane / LPR;
+        const int p = p0 + pl;
+        const int off =
+            p < pend ? p * ldy2 + ns0 * 2 + (((lane % LPR) ^ (pl & 15)) << 4) : -1;
+        dma16(ars, sb + C::XB + j * 1024, off);
       }
     }
     if constexpr (EPI == EPI_DGRAD) {
@@ -269,6 +309,21 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
     // prefetch pipeline each tile
     v8s ea[CT][2], ex[CT][2];
     unsigned em[CT][2];
+    if constexpr (EPI == EPI_APPLY) {
+#pragma unroll
+      for (int i = 0; i < CT; ++i)
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          const int cc = (C::WCH / 8) * wid + 4 * i + 2 * pp + hh;
+          const unsigned so = lds_addr(sb + C::XB) + l32 * C::YROW + ((cc ^ (l32 & 15)) << 4);
+          asm volatile("ds_read_b128 %0, %1" : "=v"(ea[i][pp]) : "v"(so));
+        }
+      if constexpr (CT == 1)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ea[0][0]), "+v"(ea[0][1]));
+      else
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(ea[0][0]), "+v"(ea[0][1]), "+v"(ea[CT - 1][0]), "+v"(ea[CT - 1][1]));
+    }
     if constexpr (EPI == EPI_DGRAD) {
 #pragma unroll
       for (int i = 0; i < CT; ++i)
@@ -323,6 +378,25 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
             s1[i][pp][k] += d;
             s2[i][pp][k] = fmaf(d, d, s2[i][pp][k]);
           }
+        } else if constexpr (EPI == EPI_APPLY) {
+          // the BN apply of bn.hip bn_apply_k on the stored (rounded) y
+          const Vec<T, 8> rv = __builtin_bit_cast(Vec<T, 8>, ea[i][pp]);
+          const float floor_ = a.relu ? 0.f : -INFINITY;
+          Vec<T, 8> outv;
+          unsigned bits = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            ov.v[k] = (T)v[k];
+            float o = (float)ov.v[k] * pa[i][pp][k] + pb[i][pp][k];
+            o = fmaxf(o + (float)rv.v[k], floor_);
+            outv.v[k] = (T)o;
+            bits |= ((float)outv.v[k] > 0.f ? 1u : 0u) << k;
+          }
+          const int ooff = valid ? p * ldy2 + (ns0 + 8 * cc) * 2 : -1;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u_t, outv), ors, ooff, 0,
+                                                 0);
+          __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bits, obrs,
+                                               valid ? (p * a.Ncol + ns0 + 8 * cc) / 8 : -1, 0, 0);
         } else {
           const Vec<T, 8> av = __builtin_bit_cast(Vec<T, 8>, ea[i][pp]);
           const Vec<T, 8> xv = __builtin_bit_cast(Vec<T, 8>, ex[i][pp]);
@@ -387,14 +461,20 @@ static int slice_width(int K) { return K <= 128 ? 256 : 128; }
 }  // namespace s1
 
 bool conv_s1_fits(const IgArgs& a) {
-  const bool dg = a.addend || a.xbn;
   const int K = a.C;
-  return !(dg && a.kshift) && !(!dg && a.mask) &&
-         (K == 64 || K == 128 || K == 256 || K == 512) && a.Ncol % s1::slice_width(K) == 0 &&
-         a.KH == 1 && a.KW == 1 && a.sh == 1 && a.sw == 1 && a.pt == 0 && a.pl == 0 &&
-         a.OH == a.H && a.OW == a.W && a.YH == a.OH && a.YW == a.OW && a.ys == 1 &&
-         a.ldy == a.Ncol && !a.zfill && !a.c8 && a.xbytes > 0 && a.wbytes > 0 && a.ybytes > 0 &&
-         !a.bias && !a.relu &&
+  const bool geo = (K == 64 || K == 128 || K == 256 || K == 512) &&
+                   a.Ncol % s1::slice_width(K) == 0 && a.KH == 1 && a.KW == 1 && a.sh == 1 &&
+                   a.sw == 1 && a.pt == 0 && a.pl == 0 && a.OH == a.H && a.OW == a.W &&
+                   a.YH == a.OH && a.YW == a.OW && a.ys == 1 && a.ldy == a.Ncol && !a.zfill &&
+                   !a.c8 && a.xbytes > 0 && a.wbytes > 0 && !a.bias;
+  if (a.out) {  // apply form: BN apply (+ residual, ReLU) of the recomputed output
+    return geo && a.bn_scale && a.bn_shift && a.outbytes > 0 && !a.stats && !a.xbn &&
+           !a.mask && !a.mcoef && (a.ybytes == 0 || a.ybytes == a.outbytes);
+  }
+  const bool dg = a.addend || a.xbn;
+  return geo && !(dg && a.kshift) && !(!dg && a.mask) && !a.relu &&
+         // statistics-only forward (ybytes 0: stores dropped)
+         (a.ybytes > 0 || (a.stats && !dg)) &&
          // producer-BN ReLU mask: none or the bit mask
          !(dg && a.xbn && ((a.mask && !a.maskbits) || (!a.mask && a.mcoef))) &&
          !(dg && !a.xbn && a.mask);
@@ -427,14 +507,7 @@ static int s1_grid(int tiles, int nsl, int wpc) {
         cus = n;
     }
   });
-  // KFB_S1_OVERSUB=k: k workgroups per slot, the hardware dispatcher then
-  // balances the runs over CUs a concurrent kernel holds (A/B knob)
-  static const int over = [] {
-    const char* e = getenv("KFB_S1_OVERSUB");
-    const int v = e ? atoi(e) : 1;
-    return v > 0 ? v : 1;
-  }();
-  int g = g_s1_grid_force > 0 ? g_s1_grid_force : cus * wpc * over;
+  int g = g_s1_grid_force > 0 ? g_s1_grid_force : cus * wpc;
   // whole pixel groups (one workgroup per slice each), at most one tile each
   int groups = g / nsl;
   if (groups > tiles) groups = tiles;
@@ -442,52 +515,42 @@ static int s1_grid(int tiles, int nsl, int wpc) {
   return groups * nsl;
 }
 
-template <typename T, int K, int WPC>
-static void launch_s1_w(const IgArgs& a, int tiles, int nsl, bool dg, int mask, hipStream_t s) {
-  const int grid = s1_grid(tiles, nsl, WPC);
-  if (!dg)
-    hipLaunchKernelGGL((s1::conv_s1_k<T, K, s1::EPI_STATS, 0, WPC>), dim3(grid), dim3(256), 0, s,
-                       a, tiles, nsl);
-  else if (mask)
-    hipLaunchKernelGGL((s1::conv_s1_k<T, K, s1::EPI_DGRAD, 1, WPC>), dim3(grid), dim3(256), 0, s,
-                       a, tiles, nsl);
-  else
-    hipLaunchKernelGGL((s1::conv_s1_k<T, K, s1::EPI_DGRAD, 0, WPC>), dim3(grid), dim3(256), 0, s,
-                       a, tiles, nsl);
+template <typename T, int K, int EPI, int MASK, int WPC>
+static void launch_s1_k(const IgArgs& a, int tiles, int nsl, hipStream_t s) {
+  hipLaunchKernelGGL((s1::conv_s1_k<T, K, EPI, MASK, WPC>), dim3(s1_grid(tiles, nsl, WPC)),
+                     dim3(256), 0, s, a, tiles, nsl);
 }
 
 template <typename T, int K>
-static void launch_s1(const IgArgs& a, int tiles, int nsl, bool dg, int mask, hipStream_t s) {
-  if (s1_wpc(K, dg) == 2) {
+static void launch_s1(const IgArgs& a, int tiles, int nsl, int epi, int mask, hipStream_t s) {
+  if (s1_wpc(K, epi == s1::EPI_DGRAD) == 2) {
     if constexpr (K <= 256) {
-      if (!dg)
-        hipLaunchKernelGGL((s1::conv_s1_k<T, K, s1::EPI_STATS, 0, 2>),
-                           dim3(s1_grid(tiles, nsl, 2)), dim3(256), 0, s, a, tiles, nsl);
+      if (epi == s1::EPI_STATS) launch_s1_k<T, K, s1::EPI_STATS, 0, 2>(a, tiles, nsl, s);
+      else if (epi == s1::EPI_APPLY) launch_s1_k<T, K, s1::EPI_APPLY, 0, 2>(a, tiles, nsl, s);
       else if constexpr (K != 128) {
-        if (mask)
-          hipLaunchKernelGGL((s1::conv_s1_k<T, K, s1::EPI_DGRAD, 1, 2>),
-                             dim3(s1_grid(tiles, nsl, 2)), dim3(256), 0, s, a, tiles, nsl);
-        else
-          hipLaunchKernelGGL((s1::conv_s1_k<T, K, s1::EPI_DGRAD, 0, 2>),
-                             dim3(s1_grid(tiles, nsl, 2)), dim3(256), 0, s, a, tiles, nsl);
+        if (mask) launch_s1_k<T, K, s1::EPI_DGRAD, 1, 2>(a, tiles, nsl, s);
+        else launch_s1_k<T, K, s1::EPI_DGRAD, 0, 2>(a, tiles, nsl, s);
       }
       return;
     }
   }
-  launch_s1_w<T, K, 1>(a, tiles, nsl, dg, mask, s);
+  if (epi == s1::EPI_STATS) launch_s1_k<T, K, s1::EPI_STATS, 0, 1>(a, tiles, nsl, s);
+  else if (epi == s1::EPI_APPLY) launch_s1_k<T, K, s1::EPI_APPLY, 0, 1>(a, tiles, nsl, s);
+  else if (mask) launch_s1_k<T, K, s1::EPI_DGRAD, 1, 1>(a, tiles, nsl, s);
+  else launch_s1_k<T, K, s1::EPI_DGRAD, 0, 1>(a, tiles, nsl, s);
 }
 
 template <typename T>
 static hipError_t launch_s1_t(const IgArgs& a, hipStream_t s) {
   const int tiles = (a.M + s1::BMP - 1) / s1::BMP;
   const int nsl = a.Ncol / s1::slice_width(a.C);
-  const bool dg = a.addend || a.xbn;
-  const int mask = (dg && a.xbn && a.mask) ? 1 : 0;
+  const int epi = a.out ? s1::EPI_APPLY : (a.addend || a.xbn) ? s1::EPI_DGRAD : s1::EPI_STATS;
+  const int mask = (epi == s1::EPI_DGRAD && a.xbn && a.mask) ? 1 : 0;
   switch (a.C) {
-    case 64: launch_s1<T, 64>(a, tiles, nsl, dg, mask, s); break;
-    case 128: launch_s1<T, 128>(a, tiles, nsl, dg, mask, s); break;
-    case 256: launch_s1<T, 256>(a, tiles, nsl, dg, mask, s); break;
-    case 512: launch_s1<T, 512>(a, tiles, nsl, dg, mask, s); break;
+    case 64: launch_s1<T, 64>(a, tiles, nsl, epi, mask, s); break;
+    case 128: launch_s1<T, 128>(a, tiles, nsl, epi, mask, s); break;
+    case 256: launch_s1<T, 256>(a, tiles, nsl, epi, mask, s); break;
+    case 512: launch_s1<T, 512>(a, tiles, nsl, epi, mask, s); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -503,6 +566,79 @@ hipError_t launch_conv_s1(int dtype, const IgArgs& a, hipStream_t stream) {
 }  // namespace kfb
 
 KFB_API void kfb_conv_s1_set_grid(int g) { kfb::g_s1_grid_force = g; }
+
+// The apply form (EPI_APPLY): y = conv1x1(x, w) recomputed (NHWC [N,H,W,C] ->
+// [N,H,W,Ncol]), stored to y when y != null, and out = relu?(bf16(y) * scale
+// + shift + res) (res nullable) with out's ReLU bit mask (bits nullable).
+KFB_API hipError_t kfb_conv_s1_apply(int dtype, const void* x, const void* w, void* y, void* out,
+                                     const void* res, int N, int H, int W, int C, int Ncol,
+                                     const float* scale, const float* shift, int relu,
+                                     uint8_t* bits, hipStream_t stream);
+
+// The BN forward (training) of a conv whose output was never stored: the
+// statistics were summed by the conv's statistics-only pass (psum / psq
+// slots, finalized here unless `finalized`), then one apply-form pass
+// recomputes y, stores it (the BN backward reads it) and writes
+// out = relu?(bn(y) + res) with its ReLU bit mask.  The two launches of
+// kfb_bn_fwd_train's finalize + apply, with y's write moved from the
+// conv's first pass into the apply pass and the apply's read of y replaced
+// by the conv's 4x smaller input.
+KFB_API hipError_t kfb_bn_fwd_train_recompute(
+    int dtype, const void* x, const void* w, void* y, void* out, const void* res, int N, int H,
+    int W, int C, int Ncol, const float* gamma, const float* beta, float decay, float eps,
+    float* run_mean, float* run_var, float* save_mean, float* save_invstd, float* scale,
+    float* shift, const float* psum, const float* psq, int nslab, int finalized, float* kshift,
+    int relu, uint8_t* bits, hipStream_t stream) {
+  if (!finalized) {
+    const hipError_t e =
+        kfb::bn_finalize_stats_launch(psum, psq, nslab, Ncol, (long)N * H * W, gamma, beta, decay,
+                                      eps, run_mean, run_var, save_mean, save_invstd, scale, shift,
+                                      kshift, stream);
+    if (e != hipSuccess) return e;
+  }
+  return kfb_conv_s1_apply(dtype, x, w, y, out, res, N, H, W, C, Ncol, scale, shift, relu, bits,
+                           stream);
+}
+
+KFB_API hipError_t kfb_conv_s1_apply(int dtype, const void* x, const void* w, void* y, void* out,
+                                     const void* res, int N, int H, int W, int C, int Ncol,
+                                     const float* scale, const float* shift, int relu,
+                                     uint8_t* bits, hipStream_t stream) {
+  if (C % 8 || Ncol % 8) return hipErrorInvalidValue;
+  const long xbytes = (long)N * H * W * C * 2, wbytes = (long)Ncol * C * 2;
+  const long obytes = (long)N * H * W * Ncol * 2;
+  if (xbytes >= (1L << 31) || obytes >= (1L << 31)) return hipErrorInvalidValue;
+  kfb::IgArgs a{};
+  a.x = x;
+  a.w = w;
+  a.y = y ? y : out;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.C = C;
+  a.OH = H;
+  a.OW = W;
+  a.KH = a.KW = a.sh = a.sw = 1;
+  a.Ncol = Ncol;
+  a.Ktot = C;
+  a.M = N * H * W;
+  a.YH = H;
+  a.YW = W;
+  a.ys = 1;
+  a.ldy = Ncol;
+  a.addend = res;
+  a.relu = relu ? 1 : 0;
+  a.xbytes = (int)xbytes;
+  a.wbytes = (int)wbytes;
+  a.ybytes = y ? (int)obytes : 0;
+  a.out = out;
+  a.bn_scale = scale;
+  a.bn_shift = shift;
+  a.out_bits = bits;
+  a.outbytes = (int)obytes;
+  if (!out || !kfb::conv_s1_fits(a)) return hipErrorInvalidValue;
+  return kfb::launch_conv_s1(dtype, a, stream);
+}
 
 KFB_API int kfb_conv_s1_applicable(int C, int Ncol, int KH, int KW, int sh, int sw, int pt, int pl,
                                    int H, int W, int OH, int OW) {

@@ -109,6 +109,16 @@ struct IgArgs {
   int maskbits;
   BnFin fin;
   BnGFin gfin;
+  // Streaming 1x1 apply form (conv_s1.hip EPI_APPLY, out != null): the conv
+  // output y is recomputed from x and w instead of read back, and the BN
+  // apply of its consumer runs in the epilogue:
+  //   out = relu?(bf16(y) * bn_scale[n] + bn_shift[n] + addend), y stored too
+  //   (ybytes 0: not stored), out_bits = out's ReLU bit mask (nullable)
+  void* out;
+  const float* bn_scale;
+  const float* bn_shift;
+  uint8_t* out_bits;
+  int outbytes;  // byte size of out (< 2 GiB)
 };
 
 constexpr int IG_BK = 64;
@@ -255,6 +265,7 @@ hipError_t bn_finalize_stats_launch(const float* psum, const float* psq, int nsl
 bool conv_s3_fits(const IgArgs& a);
 hipError_t launch_conv_s3(int dtype, const IgArgs& a, hipStream_t stream);
 // conv_s1.hip: the streaming 1x1 64 -> 256-channel kernel (IG_ALGO_S1)
+// (ybytes 0 in a statistics-only launch: the output is not stored)
 bool conv_s1_fits(const IgArgs& a);
 hipError_t launch_conv_s1(int dtype, const IgArgs& a, hipStream_t stream);
 // conv_s7.hip: the streaming stem conv (IG_ALGO_S7)

@@ -191,6 +191,11 @@ class ConvNetBuilder:
             # conv feeds is created under the same scope right below)
             bnl = self._peek_bn_layer(name, num_out_channels)
             stats = conv_hip.stats_buffer(num_out_channels, x.device, shift=bnl.stat_shift)
+            # a conv whose output only this residual BN reads (ResNet block
+            # output): the conv may leave it unstored and the BN's apply pass
+            # recompute it (conv_hip.conv_fwd / nn._BatchNormTrain)
+            stats._kfb_defer = (residual is not None and pool is None
+                                and not isinstance(residual, F.DeferredBN))
             # the plain BN forward (not the dual / fused-pool forms, which
             # finalize on their own) takes the conv's in-kernel finalize
             if not (defer_bn and activation is None and residual is None and pool is None) \

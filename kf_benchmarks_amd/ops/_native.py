@@ -38,6 +38,9 @@ _SIGS = {
                               P, P, F, F, P, P, P, P, P, P, P, P, I, I, P, P, P, P],
     "kfb_bn_bwd_dual": [I, P, P, P, P, P, L, I, P, P, P, P, P, P, P, I, P, P, P, I,
                         P, P, P, P, P, P, P, I, P, P, P, I, P],
+    "kfb_bn_fwd_train_recompute": [I, P, P, P, P, P, I, I, I, I, I, P, P, F, F, P, P, P, P, P, P,
+                                   P, P, I, I, P, I, P, P],
+    "kfb_conv_s1_apply": [I, P, P, P, P, P, I, I, I, I, I, P, P, I, P, P],
     "kfb_bn_fwd_infer": [I, P, P, P, L, I, P, P, P, P, F, P, P, I, P],
     "kfb_bn_bwd": [I, P, P, P, P, P, L, I, P, P, P, P, P, P, P, I, P, P, P, I, I, I, P],
     "kfb_opt_step": [I, P, P, P, P, P, I, P, L, F, F, F, F, F, F, F, F, F, I, P, F, F, P, P, P],

@@ -95,10 +95,6 @@ _GSHORT3 = os.environ.get("KFB_IGEMM_GSHORT3", "1") != "0"  # A/B knob: the 3-st
 _NO_MULTI = os.environ.get("KFB_IGEMM_NOMULTI", "0") == "1"  # A/B knob: drop IG_*MULTI*
 _NO_BIG = os.environ.get("KFB_IGEMM_NOBIG", "0") == "1"  # A/B knob: drop IG_GBIG*
 _SK = os.environ.get("KFB_IGEMM_SK", "0") == "1"  # offer IG_SK128 to the autotune
-# KFB_IGEMM_SK_SMALL=1: offer it on the few-tile (small-batch) layers
-# (neutral in the network: ResNet-152 bs32 14.02 / 14.06 vs 14.04 / 13.94 ms,
-# ResNet-50 bs64 7.09 / 7.04 vs 7.08 / 7.06; gpurun_out/r11a)
-_SK_SMALL = os.environ.get("KFB_IGEMM_SK_SMALL", "0") == "1"
 # KFB_IGEMM_EARLY=1: offer the early-epilogue-operand kernels (IG_*_E) to the
 # autotune.  Off: at 3 workgroups per CU (their early operands stay live
 # through the K loop) they lost to the 4-workgroup one-stage kernel on every
@@ -241,10 +237,6 @@ def stats_buffer(channels, device, shift=None):
 # dgrad tails about break even and remove ~17 launches per step.
 _BN_FIN_MODE = os.environ.get("KFB_BN_FIN", "grad")
 _BN_FIN = _BN_FIN_MODE != "0"
-# KFB_S3_DGRAD=0: the streaming 3x3 kernel for forward convs only (its dgrad
-# form runs beside the weight-gradient side stream, which can hold CUs its
-# one-workgroup-per-CU grid waits for)
-_S3_DGRAD = os.environ.get("KFB_S3_DGRAD", "1") != "0"
 
 
 def attach_bn_finalize(stats, gamma, beta, rm, rv, decay, eps, st, coef):
@@ -346,7 +338,8 @@ def _time_candidates(cands, run, rounds=2, reps=3, label=None):
             _ALGO_NAMES.update({v: k for k, v in IG_ALGOS.items()})
         ranked = sorted(best_t.items(), key=lambda kv: kv[1])
         print("[autotune] %s: %s" % (label, "  ".join(
-            "%s %.1f" % (("s3w" if c >> 16 == 2 else "glds/%d" % (c & 0xFFFF)) if c >= (1 << 16)
+            "%s %.1f" % (("s3w" if c >> 16 == 2 else "%s/%d" % (_WGRAD_NAMES[c >> 16], c & 0xFFFF))
+                         if c >= (1 << 16)
                          else _ALGO_NAMES.get(c, c),
                          1e3 * t / reps) for c, t in ranked)),
             file=sys.stderr, flush=True)
@@ -399,15 +392,12 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
                 cands += (IG_GBIG256_32,)
         if 64 < ncol <= 256 and ((M + 511) // 512) * ((ncol + 127) // 128) >= 256:
             cands += (IG_GBIG512,)
-    M_ = geo[0] * geo[4] * geo[5]
-    few_tiles = ((M_ + 127) // 128) * ((ncol + 127) // 128) < 2 * 256
-    if fast and (_SK or (few_tiles and _SK_SMALL)) and C % 64 == 0 and ncol > 64:
+    if fast and _SK and C % 64 == 0 and ncol > 64:
         # stream-K: measured slower than the one-tile kernels on every
         # ResNet-50 bs256 geometry (per-item setup, pipeline refill and the
         # fix-up tail cost more than the partial round it removes at
-        # K <= 4608, profiles/r7_stream_k.txt); offered where a layer has
-        # fewer 128x128 tiles than two per CU (small batches: the one-tile
-        # kernels then leave CUs idle through a long K loop), and everywhere
+        # K <= 4608, profiles/r7_stream_k.txt) and neutral on the few-tile
+        # small-batch layers (ResNet-152 bs32, ResNet-50 bs64); offered only
         # with KFB_IGEMM_SK=1
         cands += (IG_SK128,)
     if fast and C % 64 != 0:
@@ -417,8 +407,7 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
         cands += (IG_DB,)
     if fast and _EARLY_EPI and (xbn is not None or addend is not None):
         cands += (IG_ONEBUF_N64_E, IG_CLASSIC_N64_E)
-    if fast and not _NO_S3 and (_S3_DGRAD or (xbn is None and addend is None)) \
-            and N.load().kfb_conv_s3_applicable(
+    if fast and not _NO_S3 and N.load().kfb_conv_s3_applicable(
             C, ncol, KH, KW, geo[8], geo[9], geo[10], geo[11], geo[1], geo[2], geo[4], geo[5]) \
             and geo[13] == geo[4] and geo[14] == geo[5] and geo[15] == 1 and geo[16] == ncol:
         cands += (IG_S3,)
@@ -453,15 +442,28 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
 
 def _igemm(x, wmat, y, N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy,
            trans, stats=None, mask=None, xbn=None, mean=None, addend=None, mcoef=None,
-           bias=None, relu=False, zfill=False):
+           bias=None, relu=False, zfill=False, defer=False):
     """``zfill``: stride-2 scatter whose epilogue also zeroes the unsampled
-    pixels of each 2x2 block (the output needs no separate zero fill)."""
+    pixels of each 2x2 block (the output needs no separate zero fill).
+    ``defer`` (forward statistics): where the tuned kernel is the streaming
+    1x1 one, sum the statistics without storing the output (its consumer
+    recomputes it); returns True then."""
     geo = (N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy, int(trans))
     # a uint8 mask is the producer BN's ReLU bit mask (IgArgs::maskbits)
     mbits = mask is not None and mask.dtype == torch.uint8
     flags = int(bool(relu)) | (2 if zfill else 0) | (4 if mbits else 0)
     algo = _igemm_algo(x, wmat, y, geo, (stats, mask, xbn, mean, addend, mcoef), (bias, flags))
+    deferred = (defer and algo == IG_S1 and stats is not None and xbn is None
+                and addend is None and bias is None)
+    if deferred:
+        flags |= 8
     _igemm_call(algo, x, wmat, y, geo, stats, mask, xbn, mean, addend, mcoef, bias, flags)
+    return deferred
+
+
+# KFB_BN_RECOMPUTE=0: a residual BN's producing streaming 1x1 conv stores its
+# output (the BN apply reads it back) instead of recomputing it in the apply
+_RECOMPUTE = os.environ.get("KFB_BN_RECOMPUTE", "0") == "1"
 
 
 def conv_fwd(x, wl, stride, pads, stats=None, bias=None, relu=False):
@@ -476,8 +478,13 @@ def conv_fwd(x, wl, stride, pads, stats=None, bias=None, relu=False):
     OH = (H + pt + pb - KH) // sh + 1
     OW = (W + pl + pr - KW) // sw + 1
     y = torch.empty((n, OH, OW, cout), dtype=x.dtype, device=x.device)
-    _igemm(x, wl, y, n, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, cout, OH, OW, 1, cout, False,
-           stats, bias=bias, relu=relu)
+    # a stats buffer marked by its consuming residual BN (models/builder.py):
+    # the streaming 1x1 kernel leaves y unwritten; the BN's apply pass
+    # recomputes it from (x, wl) and stores it (nn._BatchNormTrain)
+    defer = _RECOMPUTE and stats is not None and getattr(stats, "_kfb_defer", False)
+    if _igemm(x, wl, y, n, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, cout, OH, OW, 1, cout, False,
+              stats, bias=bias, relu=relu, defer=defer):
+        y._kfb_recompute = (x, wl)
     return y
 
 
@@ -561,14 +568,13 @@ def _wgrad_launch(dy, x, dw, geo, target):
 # KFB_CONV_AUTOTUNE=0 pins _WGRAD_TARGET_BLOCKS.
 _AUTOTUNE = os.environ.get("KFB_CONV_AUTOTUNE", "1") != "0" and "KFB_WGRAD_BLOCKS" not in os.environ
 _WGRAD_CANDIDATES = (384, 512, 768, 1024)
-# KFB_WGRAD_MAXBLOCKS: drop larger workgroup targets (fewer reduction splits,
-# less slab traffic beside the compute stream; in-network A/B knob)
-if os.environ.get("KFB_WGRAD_MAXBLOCKS"):
-    _WGRAD_CANDIDATES = tuple(t for t in _WGRAD_CANDIDATES
-                              if t <= int(os.environ["KFB_WGRAD_MAXBLOCKS"])) or (384,)
 # bit 16 of a candidate selects the LDS-DMA wgrad kernel (wgrad_glds_k: 128-wide
-# output-channel tiles, operands < 2 GiB); KFB_WGRAD_ALGO=classic|glds pins one
+# output-channel tiles, operands < 2 GiB); KFB_WGRAD_ALGO=classic|glds pins one.
+# (Its 2-stage ring of 64-row steps was measured against a 4-stage ring of
+# 32-row steps and a 3-stage ring of 64-row steps at one workgroup per CU:
+# neither won a single ResNet-50 geometry, profiles/r12_wgrad_rings.txt.)
 _WGRAD_GLDS = 1 << 16
+_WGRAD_NAMES = {1: "glds", 2: "s3w"}
 _WGRAD_ALGO = os.environ.get("KFB_WGRAD_ALGO", "")
 _wgrad_tuned = {}
 

@@ -230,12 +230,7 @@ def _relu_bits_buffer(x, rows, C):
     return torch.empty((rows * C // 8,), dtype=torch.uint8, device=x.device)
 
 
-def _foldable(stats):
-    """A conv epilogue's stats_buffer (its zeroed counter tail follows the
-    slots): the BN forward may fold its finalize into the apply pass
-    (csrc/bn.hip bn_apply_fold_k; have_partials = 3)."""
-    return (stats is not None and getattr(stats, "_kfb_counter", None) is not None
-            and stats.is_cuda)
+RECOMPUTED = 0  # BN forwards that recomputed their input (tests)
 
 
 class _BatchNormTrain(torch.autograd.Function):
@@ -268,12 +263,30 @@ class _BatchNormTrain(torch.autograd.Function):
         res = residual.contiguous() if residual is not None else None
         rec = relu and residual is None and _MASK_RECOMPUTE
         mbits = _relu_bits_buffer(x, rows, C) if relu and not rec else None
-        N.call("kfb_bn_fwd_train", N.dt(x), x.data_ptr(), N.ptr(res), y.data_ptr(), rows, C,
-               N.ptr(gamma), N.ptr(beta), float(decay), float(eps), N.ptr(rm), N.ptr(rv),
-               st[0].data_ptr(), st[1].data_ptr(), coef[:C].data_ptr(),
-               coef[C:].data_ptr(), psum.data_ptr(), psq.data_ptr(), nslab, int(relu),
-               2 if fin is not None else (3 if _foldable(stats) else int(stats is not None)),
-               N.ptr(_conv_hip().stats_shift(stats)), N.ptr(mbits), N.stream(dev))
+        # x never stored by its producing conv (conv_hip.conv_fwd, statistics
+        # only): the apply pass recomputes it from the conv's input and
+        # weights and stores it on the way (csrc/conv_s1.hip EPI_APPLY)
+        rc = getattr(x, "_kfb_recompute", None) if stats is not None else None
+        if rc is not None:
+            global RECOMPUTED
+            RECOMPUTED += 1
+            xin, wl = rc
+            x._kfb_recompute = None
+            n_, h_, w_, cin = xin.shape
+            N.call("kfb_bn_fwd_train_recompute", N.dt(x), xin.data_ptr(), wl.data_ptr(),
+                   x.data_ptr(), y.data_ptr(), N.ptr(res), n_, h_, w_, cin, C, N.ptr(gamma),
+                   N.ptr(beta), float(decay), float(eps), N.ptr(rm), N.ptr(rv),
+                   st[0].data_ptr(), st[1].data_ptr(), coef[:C].data_ptr(),
+                   coef[C:].data_ptr(), psum.data_ptr(), psq.data_ptr(), nslab,
+                   int(fin is not None), N.ptr(_conv_hip().stats_shift(stats)), int(relu),
+                   N.ptr(mbits), N.stream(dev))
+        else:
+            N.call("kfb_bn_fwd_train", N.dt(x), x.data_ptr(), N.ptr(res), y.data_ptr(), rows, C,
+                   N.ptr(gamma), N.ptr(beta), float(decay), float(eps), N.ptr(rm), N.ptr(rv),
+                   st[0].data_ptr(), st[1].data_ptr(), coef[:C].data_ptr(),
+                   coef[C:].data_ptr(), psum.data_ptr(), psq.data_ptr(), nslab, int(relu),
+                   2 if fin is not None else int(stats is not None),
+                   N.ptr(_conv_hip().stats_shift(stats)), N.ptr(mbits), N.stream(dev))
         ctx.save_for_backward(x, y if relu else None, gamma, st)
         ctx.relu = relu
         ctx.has_res = residual is not None
@@ -772,7 +785,6 @@ class _AvgPool(torch.autograd.Function):
         return _pool_link_grad(ctx.link, dx), None, None, None, None, None, None, None
 
 
-N.register_optional("kfb_bn_set_fold", [N.I], None)
 N.register_optional("kfb_bn_relu_maxpool_fwd", [N.I, N.P, N.P, N.P] + [N.I] * 12 +
                     [N.P, N.P, N.F, N.F] + [N.P] * 8 + [N.I, N.P, N.P])
 N.register_optional("kfb_bn_pool_num_slabs", [N.I] * 8, N.c_int)

@@ -313,6 +313,11 @@ def reset_world():
     _WORLD = None
 
 
+# KFB_SELFTEST_INJECT=1 (tests): rank 0's check sees a wrong sum, so the
+# fallback branch runs on a real communicator
+_SELFTEST_INJECT = os.environ.get("KFB_SELFTEST_INJECT") == "1"
+
+
 def selftest_device_collectives(cand, sizes, dtypes=(torch.float32,), device=None,
                                  seed: int = 0) -> dict:
     """Checks a candidate device communicator ``cand`` (all_reduce /
@@ -345,6 +350,8 @@ def selftest_device_collectives(cand, sizes, dtypes=(torch.float32,), device=Non
                 if work is not None:
                     work.wait()
                 got = buf.float().cpu()
+                if _SELFTEST_INJECT and kind == "sum" and n > 1 and w.rank == 0:
+                    got[0] += 1  # (test hook: a wrong sum on rank 0)
                 checked += 1
                 if not torch.equal(got, ref.to(dt).float()):
                     failed.append("%s n=%d %s" % (kind, n, str(dt).replace("torch.", "")))

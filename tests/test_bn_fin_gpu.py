@@ -113,77 +113,3 @@ def test_resnet_trains_same_with_in_kernel_finalize(cuda, monkeypatch, force):
         ref = (bb[k] - bb2[k]).abs().max().item()
         assert (ba[k] - bb[k]).abs().max().item() <= max(8 * ref, 2e-2 * bb[k].abs().max().item()
                                                          + 2e-3), k
-
-
-@pytest.fixture
-def fold_toggle(cuda):
-    from kf_benchmarks_amd.ops import _native as N
-    yield lambda on: N.load().kfb_bn_set_fold(int(on))
-    N.load().kfb_bn_set_fold(0)  # (the default)
-
-
-@pytest.mark.parametrize("C,relu,res", [(64, True, False), (256, True, True), (512, False, False)])
-def test_bn_forward_fold_matches_finalize_launch(cuda, fold_toggle, C, relu, res):
-    """The BN forward with its finalize folded into the apply pass (every
-    workgroup folds the conv epilogue's slots; workgroup 0 writes the saved
-    and running statistics; the last one updates the statistics shift)
-    equals the separate finalize launch + apply."""
-    from kf_benchmarks_amd.ops import nn as Fn
-    n, H, W = 8, 14, 14
-    g = torch.Generator().manual_seed(21)
-    x = (torch.randn(n, H, W, C, generator=g) * 2 + 0.5).to(torch.bfloat16).to(cuda)
-    r = torch.randn(n, H, W, C, generator=g).to(torch.bfloat16).to(cuda) if res else None
-    gamma = (torch.rand(C, generator=g) + 0.5).to(cuda)
-    beta = torch.randn(C, generator=g).to(cuda)
-    shift0 = (torch.randn(C, generator=g) * 0.3).to(cuda)
-    out = {}
-    for on in (False, True):
-        fold_toggle(on)
-        shift = shift0.clone()
-        st = conv_hip.stats_buffer(C, cuda, shift=shift)
-        full = st._kfb_counter
-        st.zero_()
-        full.zero_()
-        # the slots a conv epilogue would have filled: sums of (x - K), (x - K)^2
-        xd = x.float().reshape(-1, C) - shift
-        st.view(2, conv_hip.STATS_SPREAD, C)[0, 0] = xd.sum(0)
-        st.view(2, conv_hip.STATS_SPREAD, C)[1, 0] = (xd * xd).sum(0)
-        rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
-        y = Fn.batch_norm(x, gamma, beta, rm, rv, 0.9, 1e-3, True, relu=relu, residual=r,
-                          stats=st)
-        torch.cuda.synchronize()
-        out[on] = (y.float(), rm.clone(), rv.clone(), shift.clone())
-    for a, b in zip(out[False], out[True]):
-        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
-    # the shift moved to this batch's mean
-    torch.testing.assert_close(out[True][3], x.float().reshape(-1, C).mean(0), rtol=1e-3,
-                               atol=1e-3)
-
-
-def test_resnet_trains_same_with_folded_bn_finalize(cuda, fold_toggle, monkeypatch):
-    """ResNet-50 at batch 8: BN finalizes folded into the apply passes
-    (forward and backward) train like the separate finalize launches, up to
-    the run-to-run spread of the statistics atomics."""
-    from kf_benchmarks_amd import params as P
-    from kf_benchmarks_amd.benchmark import BenchmarkCNN
-
-    def run(on):
-        fold_toggle(on)
-        p = P.make_params(model="resnet50", batch_size=8, num_gpus=1, use_bf16=True,
-                          optimizer="momentum", data_format="NHWC", variable_update="kungfu",
-                          init_learning_rate=0.002, display_every=10 ** 9)
-        b = BenchmarkCNN(p)
-        b.build()
-        losses = [float(b.train_step(need_loss=True)[0]) for _ in range(4)]
-        torch.cuda.synchronize()
-        return losses, b.flat.flat.detach().float().cpu().clone()
-
-    lb, wb = run(False)
-    lb2, wb2 = run(False)
-    la, wa = run(True)
-    spread = 0.0
-    for x, y, y2 in zip(la, lb, lb2):
-        spread = max(spread, abs(y - y2))
-        assert abs(x - y) <= max(4 * spread, 2.5e-2 * max(1.0, abs(y))), (la, lb, lb2)
-    ref = (wb - wb2).abs().max().item()
-    assert (wa - wb).abs().max().item() <= max(4 * ref, 1e-3), ref

@@ -1,0 +1,78 @@
+"""Residual-BN input recompute (ResNet block output): the conv that feeds a
+residual BN + ReLU sums the BN statistics without storing its output
+(streaming 1x1 kernel, statistics only), and the BN's apply pass recomputes
+the conv output from the conv's input and weights, stores it for the
+backward, and applies BN + residual + ReLU in the same epilogue
+(csrc/conv_s1.hip EPI_APPLY, nn._BatchNormTrain).  Exact oracle: in a
+bitwise-repeatable configuration (CIFAR-sized ResNet-50 at batch 4; the
+streaming 1x1 kernel on at most 32 workgroups, so every statistics slot
+takes one atomic add) the recompute path trains bit for bit like the
+stored-output path, eager and taped."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def _exact(monkeypatch, cuda):
+    from kf_benchmarks_amd.ops import _native as N
+    from kf_benchmarks_amd.ops import conv_hip
+    monkeypatch.setattr(conv_hip, "_NO_S3", True)
+    monkeypatch.setattr(conv_hip, "_NO_S7", True)
+    monkeypatch.setenv("KFB_TAPE_STRICT", "1")
+    N.load().kfb_set_deterministic(1)
+    N.load().kfb_conv_s1_set_grid(32)
+    yield
+    N.load().kfb_conv_s1_set_grid(0)
+    N.load().kfb_set_deterministic(0)
+
+
+def _run(recompute, tape, monkeypatch, steps=5):
+    from kf_benchmarks_amd import params as P
+    from kf_benchmarks_amd.benchmark import BenchmarkCNN
+    from kf_benchmarks_amd.ops import conv_hip
+    from kf_benchmarks_amd.ops import nn as F
+    # (the kernel choices tuned by the first run are reused by the others)
+    monkeypatch.setattr(conv_hip, "_RECOMPUTE", recompute)
+    p = P.make_params(model="resnet50", batch_size=4, num_gpus=1, use_bf16=True,
+                      optimizer="momentum", data_format="NHWC", variable_update="kungfu",
+                      launch_tape=tape, init_learning_rate=1e-3, loss_type_to_report="base_loss",
+                      display_every=10 ** 9)
+    b = BenchmarkCNN(p)
+    b.model.image_size = 32
+    b.build()
+    n0 = F.RECOMPUTED
+    losses = [float(b.train_step(need_loss=True)[0]) for _ in range(steps)]
+    torch.cuda.synchronize()
+    w = b.flat.flat.detach().float().cpu().clone()
+    bufs = {k: t.detach().float().cpu().clone() for k, t in b.net.named_buffers()}
+    tp = getattr(b, "_tape", None)
+    return dict(losses=losses, w=w, bufs=bufs, used=F.RECOMPUTED - n0,
+                replays=tp.replays if tp is not None else 0)
+
+
+def _diff(a, b):
+    bad = []
+    if a["losses"] != b["losses"]:
+        bad.append("losses %s vs %s" % (a["losses"], b["losses"]))
+    if not torch.equal(a["w"], b["w"]):
+        bad.append("weights (max %g)" % (a["w"] - b["w"]).abs().max().item())
+    bad += [k for k in a["bufs"] if not torch.equal(a["bufs"][k], b["bufs"][k])]
+    return bad
+
+
+def test_recompute_trains_bitwise_like_stored(_exact, monkeypatch):
+    stored = _run(False, False, monkeypatch)
+    stored2 = _run(False, False, monkeypatch)
+    assert not _diff(stored, stored2), "not repeatable: %s" % _diff(stored, stored2)[:6]
+    assert stored["used"] == 0
+    rec = _run(True, False, monkeypatch)
+    # every identity block of the 4 stages (2 + 3 + 5 + 2) where the conv
+    # feeding the block-output BN runs on the streaming 1x1 kernel
+    assert rec["used"] > 0 and rec["used"] % 5 == 0, rec["used"]
+    assert not _diff(stored, rec), _diff(stored, rec)[:6]
+    taped = _run(True, True, monkeypatch)
+    assert taped["replays"] == 2
+    assert not _diff(stored, taped), _diff(stored, taped)[:6]

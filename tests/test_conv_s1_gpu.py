@@ -194,3 +194,48 @@ def test_dgrad_finalizes_bn_backward(cuda, monkeypatch, K, algo):
     assert not direct
     torch.testing.assert_close(dparams[0].double(), s2 * invstd.double(), rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dparams[1].double(), s1, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+@pytest.mark.parametrize("grid", GRIDS)
+@pytest.mark.parametrize("K", KS)
+@pytest.mark.parametrize("res,relu", [(True, True), (False, True), (True, False)])
+def test_s1_apply_form(cuda, shape, grid, K, res, relu):
+    """The apply form (EPI_APPLY, kfb_conv_s1_apply): y = conv1x1(x, w)
+    recomputed and stored, out = relu?(bf16(y) * scale + shift + res) and
+    out's ReLU bit mask - vs the fp32 reference of the same math, y bitwise
+    equal to the forward kernel's stored output."""
+    N.load().kfb_conv_s1_set_grid(grid)
+    n, H, W = shape
+    C = 4 * K
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(n, H, W, K, generator=g).to(torch.bfloat16).to(cuda)
+    w = (torch.randn(C, 1, 1, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(cuda)
+    scale = (torch.rand(C, generator=g) + 0.5).to(cuda)
+    shift = torch.randn(C, generator=g).to(cuda)
+    r = torch.randn(n, H, W, C, generator=g).to(torch.bfloat16).to(cuda) if res else None
+    y = torch.empty(n, H, W, C, dtype=torch.bfloat16, device=cuda)
+    out = torch.empty_like(y)
+    bits = torch.empty(n * H * W * C // 8, dtype=torch.uint8, device=cuda)
+    N.call("kfb_conv_s1_apply", N.dt(x), x.data_ptr(), w.data_ptr(), y.data_ptr(),
+           out.data_ptr(), N.ptr(r), n, H, W, K, C, scale.data_ptr(), shift.data_ptr(),
+           int(relu), bits.data_ptr(), N.stream(cuda))
+    # the forward kernel's own output of the same conv (statistics epilogue)
+    st = conv_hip.stats_buffer(C, cuda).zero_()
+    conv_hip._IG_FORCE, saved = conv_hip.IG_S1, conv_hip._IG_FORCE
+    try:
+        y_fwd = conv_hip.conv_fwd(x, w, (1, 1), (0, 0, 0, 0), st)
+    finally:
+        conv_hip._IG_FORCE = saved
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_fwd)
+    yb = y.float().reshape(-1, C)
+    ref = yb * scale + shift
+    if res:
+        ref = ref + r.float().reshape(-1, C)
+    if relu:
+        ref = torch.relu(ref)
+    torch.testing.assert_close(out.float().reshape(-1, C), ref, rtol=1e-2, atol=1e-2)
+    assert torch.equal(bits.cpu(), _bits(out.cpu()))
+    ref_y = x.float().reshape(-1, K) @ w.float().reshape(C, K).t()
+    torch.testing.assert_close(yb.cpu(), ref_y.cpu(), rtol=2e-2, atol=2e-2)

@@ -227,3 +227,33 @@ def test_two_ranks_pair_averaging_taped(cuda, tmp_path):
         assert r["pa_publishes"] == 6
         assert r["wsum"] != r["w0"] and r["wsum"] == r["wsum"]
         assert all(l == l and abs(l) < 1e3 for l in r["losses"])
+
+
+@pytest.mark.parametrize("inject", [False, True], ids=["selftest_passes", "selftest_fails"])
+def test_bench_native_selftest_and_fallback(cuda, inject):
+    """bench.py through a real 1-rank RCCL group (KFB_FORCE_PG=1) with the
+    default KFB_NATIVE_COMM=auto: the native communicator's startup self-test
+    (every bucket size, broadcast / sum / max, bitwise against the gloo
+    group) passes and the step is taped with its collectives; with a wrong
+    sum injected into the check, the run falls back in-process to torch's
+    ProcessGroupNCCL and stays eager - the JSON says which path ran."""
+    env = dict(os.environ, PYTHONPATH=ROOT, KFB_FORCE_PG="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "KFB_DIST_BACKEND", "KFB_NATIVE_COMM"):
+        env.pop(k, None)
+    if inject:
+        env["KFB_SELFTEST_INJECT"] = "1"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "4",
+           "--batch_size", "32"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    st = out["comm"]["selftest"]
+    assert st is not None and st["checked"] > 0 and st["mode"] == "auto"
+    if inject:
+        assert not st["ok"] and st["fallback"] and st["failed"]
+        assert out["backend"] == "nccl" and out["config"]["launch_tape"] is False
+        assert "torch.distributed" in out["config"]["launch_tape_off_reason"]
+    else:
+        assert st["ok"] and "fallback" not in st
+        assert out["backend"] == "rccl" and out["config"]["launch_tape"] is True
+    assert out["weights_in_sync"] is True and out["value"] > 0
