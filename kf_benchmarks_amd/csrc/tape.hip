@@ -25,6 +25,7 @@
 // Calls are made through libffi (the library ctypes itself uses, loaded at
 // run time): argument type codes come from the Python-side signature table.
 #include "common.h"
+#include <hip/hip_ext.h>
 
 #include <dlfcn.h>
 
@@ -112,6 +113,11 @@ struct Raw {
   const void* q = nullptr;
   int value = 0;
   size_t bytes = 0;
+  // replay plan (plan_binds): a launch that carries the completion event of
+  // the cross-stream wait right after it on its stream, and that wait, which
+  // then only enqueues the wait (no event-record marker on the source stream)
+  hipEvent_t bind_ev = nullptr;
+  bool bound = false;
 };
 
 struct Op {
@@ -189,14 +195,76 @@ static Op* cur_op() {
 static hipError_t replay_raw(const Raw& r) {
   switch (r.kind) {
     case 0:
+      if (r.bind_ev)
+        return hipExtLaunchKernel(r.fn, r.grid, r.block, const_cast<void**>(r.argv.data()), r.shm,
+                                  r.s, nullptr, r.bind_ev, 0);
       return hipLaunchKernel(r.fn, r.grid, r.block, const_cast<void**>(r.argv.data()), r.shm,
                              r.s);
     case 1: return hipMemsetAsync(r.p, r.value, r.bytes, r.s);
     case 2: {
-      const hipError_t e = hipEventRecord(r.ev, r.s2);
+      const hipError_t e = r.bound ? hipSuccess : hipEventRecord(r.ev, r.s2);
       return e != hipSuccess ? e : hipStreamWaitEvent(r.s, r.ev, 0);
     }
     default: return hipMemcpyAsync(r.p, r.q, r.bytes, hipMemcpyDeviceToDevice, r.s);
+  }
+}
+
+// KFB_TAPE_BIND=0: replay every cross-stream wait as record + wait
+static const bool g_bind = [] {
+  const char* e = getenv("KFB_TAPE_BIND");
+  return !(e && atoi(e) == 0);
+}();
+
+// A cross-stream wait recorded right after a kernel launch on its source
+// stream (nothing else issued on that stream in between) is replayed by
+// launching that kernel with the wait's event as its completion event
+// (hipExtLaunchKernel stopEvent) and enqueueing only the wait: the source
+// stream then carries no separate event-record marker, which costs the
+// producing stream ~2-3 us per wait (scripts/probes/evgap.hip).  Same
+// ordering: the source stream is in order, so the kernel's completion is
+// the completion of everything enqueued on it before the wait.  Anything
+// else issued on a stream (memset, copy, its own wait, an op replayed
+// through its entry point) ends the candidate launch for that stream.
+static void plan_binds(Tape* t, bool raw_replay) {
+  struct Last {
+    hipStream_t s;
+    Raw* r;
+  };
+  std::vector<Last> last;
+  auto find = [&](hipStream_t s) -> Raw** {
+    for (Last& l : last)
+      if (l.s == s) return &l.r;
+    return nullptr;
+  };
+  auto set = [&](hipStream_t s, Raw* r) {
+    if (Raw** p = find(s)) *p = r;
+    else last.push_back({s, r});
+  };
+  for (Op& op : t->ops) {
+    const bool raw = raw_replay && op.raw_ok && !op.patched;
+    for (Raw& r : op.raw) {
+      r.bind_ev = nullptr;
+      r.bound = false;
+    }
+    if (!raw) {
+      last.clear();  // the entry point may issue anything on any stream
+      continue;
+    }
+    for (Raw& r : op.raw) {
+      if (r.kind == 0) {
+        set(r.s, &r);
+      } else if (r.kind == 2) {
+        Raw** p = find(r.s2);
+        if (g_bind && p && *p && !(*p)->bind_ev && r.s2 != r.s) {
+          (*p)->bind_ev = r.ev;
+          r.bound = true;
+        }
+        if (p) *p = nullptr;  // (one wait per bound launch)
+        set(r.s, nullptr);    // a later wait on r.s must also cover this wait
+      } else {
+        set(r.s, nullptr);
+      }
+    }
   }
 }
 
@@ -360,6 +428,7 @@ KFB_API int kfb_tape_replay(void* h, const int* pop, const int* parg, const uint
   if (!t) return -1;
   for (int k = 0; k < npatch; ++k)
     if (kfb_tape_patch(h, pop[k], parg[k], pval[k]) != 0) return -2;
+  plan_binds(t, g_raw_replay != 0);
   call_fn call = ffi().call;
   static const bool prof = getenv("KFB_TAPE_PROFILE") != nullptr;
   if (prof && t->host_s.size() != t->ops.size()) t->host_s.assign(t->ops.size(), 0.0);
