@@ -718,7 +718,7 @@ class BenchmarkCNN:
             return
         # gradients of the range written on the compute stream are enqueued
         # before this point; the side stream's own wgrads precede it in order
-        _native.stream_wait(side.cuda_stream, _native.stream(self.device))
+        _native.stream_wait(side.cuda_stream, _native.stream(self.device), device_only=True)
         conv_hip._queue_join(self.device)
         with torch.cuda.stream(side):
             self.optimizer.step(args["lr"], grad_scale=args["grad_scale"],

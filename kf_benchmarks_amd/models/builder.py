@@ -122,7 +122,7 @@ class ConvNetBuilder:
             return
         main = torch.cuda.current_stream(x.device)
         side = _branch_stream(x.device)
-        N.stream_wait(side.cuda_stream, main.cuda_stream)  # recordable (launch tape)
+        N.stream_wait(side.cuda_stream, main.cuda_stream, device_only=True)  # recordable
         with torch.cuda.stream(side):
             yield
 
@@ -136,7 +136,7 @@ class ConvNetBuilder:
         side = _BRANCH_STREAMS.get(x.device.index)
         cur = torch.cuda.current_stream(x.device)
         if side is not None and side != cur:
-            N.stream_wait(cur.cuda_stream, side.cuda_stream)
+            N.stream_wait(cur.cuda_stream, side.cuda_stream, device_only=True)
             x.record_stream(cur)
         return t
 

@@ -46,6 +46,7 @@ _SIGS = {
     "kfb_opt_step": [I, P, P, P, P, P, I, P, L, F, F, F, F, F, F, F, F, F, I, P, F, F, P, P, P],
     "kfb_seqlock_check": [P, ctypes.c_longlong, P, P, P],
     "kfb_event_create": [P],
+    "kfb_event_create_device": [P],
     "kfb_event_destroy": [P],
     "kfb_stream_wait": [P, P, P],
     "kfb_memset": [P, I, ctypes.c_size_t, P],
@@ -250,24 +251,34 @@ def loaded_path():
 _EVENTS = {}
 
 
-def _pair_event(dst, src):
-    key = (dst, src)
+def _pair_event(dst, src, device_only=False):
+    key = (dst, src, device_only)
     ev = _EVENTS.get(key)
     if ev is None:
         h = ctypes.c_void_p()
-        err = load().kfb_event_create(ctypes.byref(h))
+        lib = load()
+        err = (lib.kfb_event_create_device if device_only and _DEVICE_EVENTS
+               else lib.kfb_event_create)(ctypes.byref(h))
         if err != 0:
             raise NativeError("kfb_event_create failed with hipError %d" % err)
         ev = _EVENTS[key] = h.value
     return ev
 
 
-def stream_wait(dst_stream: int, src_stream: int):
+# KFB_DEVICE_EVENTS=0: every cross-stream wait records with the system-scope fence
+_DEVICE_EVENTS = os.environ.get("KFB_DEVICE_EVENTS", "1") != "0"
+
+
+def stream_wait(dst_stream: int, src_stream: int, device_only: bool = False):
     """``dst`` waits for the work enqueued on ``src`` so far (raw hipStream_t
-    handles) - the recordable form of torch's Stream.wait_stream."""
+    handles) - the recordable form of torch's Stream.wait_stream.
+    ``device_only``: both streams run kernels of this device and nothing on
+    the host or another device reads what ``src`` wrote through this
+    ordering, so the event skips the system-scope release fence."""
     if dst_stream == src_stream:
         return
-    call("kfb_stream_wait", dst_stream, src_stream, _pair_event(dst_stream, src_stream))
+    call("kfb_stream_wait", dst_stream, src_stream,
+         _pair_event(dst_stream, src_stream, device_only))
 
 
 def zero_(t: torch.Tensor):

@@ -753,7 +753,7 @@ def join_wgrad_stream(device=None):
     cur = torch.cuda.current_stream(device)
     st = _SIDE_STREAMS.get(cur.device.index)
     if st is not None and st != cur:
-        N.stream_wait(cur.cuda_stream, st.cuda_stream)
+        N.stream_wait(cur.cuda_stream, st.cuda_stream, device_only=True)
 
 
 N.register_optional("kfb_s2d_stem", [N.I, N.P, N.P] + [N.I] * 9 + [N.P])
@@ -936,7 +936,7 @@ class _Conv2d(torch.autograd.Function):
         side = wgrad_stream(dy.device)
         if side is None:
             return False
-        N.stream_wait(side.cuda_stream, N.stream(dy.device))
+        N.stream_wait(side.cuda_stream, N.stream(dy.device), device_only=True)
         _queue_join(dy.device)
         with torch.cuda.stream(side):
             conv_wgrad(dy, xp, wp.shape, stride, pads, out=sink)

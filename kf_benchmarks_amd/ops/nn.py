@@ -200,7 +200,7 @@ class BNLink:
         if self.pending is not None and self.pending_event is not None:
             cur = N.stream(self.pending.device)
             if cur != self.pending_event:
-                N.stream_wait(cur, self.pending_event)
+                N.stream_wait(cur, self.pending_event, device_only=True)
                 self.pending.record_stream(torch.cuda.current_stream(self.pending.device))
             self.pending_event = None
 
@@ -1107,7 +1107,7 @@ class _Linear(torch.autograd.Function):
                 # like the conv weight gradients: off the dgrad chain, on the
                 # side stream (the classifier's wgrad is a small latency-bound
                 # GEMM at the head of the backward critical path)
-                N.stream_wait(side.cuda_stream, N.stream(dev))
+                N.stream_wait(side.cuda_stream, N.stream(dev), device_only=True)
                 ch._queue_join(dev)
                 with torch.cuda.stream(side):
                     _gemm(_GEMM_WGRAD, x, K, dy, Nout, K, Nout, M, wsink, Nout, accumulate=True)

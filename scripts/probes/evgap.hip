@@ -5,6 +5,8 @@
 //   record  hipEventRecord(ev, A) after K1 + hipStreamWaitEvent(B, ev)
 //   ext     K1 launched with hipExtLaunchKernel(..., stopEvent = ev) (the
 //           event bound to the kernel, no separate marker) + hipStreamWaitEvent
+//   *-nsf   the same with events created hipEventDisableSystemFence
+//   *-dev   the same with events created hipEventReleaseToDevice
 // Printed: us per A-pair (K1 + K2) over REPS pairs, min of 5 rounds.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
@@ -37,13 +39,19 @@ int main() {
   hipStream_t A, Bs;
   CK(hipStreamCreateWithFlags(&A, hipStreamNonBlocking));
   CK(hipStreamCreateWithFlags(&Bs, hipStreamNonBlocking));
-  hipEvent_t ev[REPS];
-  for (int i = 0; i < REPS; ++i) CK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+  hipEvent_t evs[3][REPS];
+  const unsigned fl[3] = {0u, (unsigned)hipEventDisableSystemFence, (unsigned)hipEventReleaseToDevice};
+  for (int f = 0; f < 3; ++f)
+    for (int i = 0; i < REPS; ++i)
+      CK(hipEventCreateWithFlags(&evs[f][i], hipEventDisableTiming | fl[f]));
+  const char* names[7] = {"none", "record", "ext", "record-nsf", "ext-nsf", "record-dev", "ext-dev"};
   hipEvent_t t0, t1;
   CK(hipEventCreate(&t0));
   CK(hipEventCreate(&t1));
   for (int iters : {200, 2000}) {
-    for (int variant = 0; variant < 3; ++variant) {
+    for (int v = 0; v < 7; ++v) {
+      const int variant = v == 0 ? 0 : (v % 2 ? 1 : 2);
+      hipEvent_t* ev = evs[(v - 1) / 2 < 0 ? 0 : (v - 1) / 2];
       float best = 1e9;
       for (int round = 0; round < 6; ++round) {
         CK(hipDeviceSynchronize());
@@ -73,8 +81,7 @@ int main() {
         CK(hipEventElapsedTime(&ms, t0, t1));
         if (round > 0 && ms < best) best = ms;
       }
-      printf("iters %5d  %-6s  %7.2f us per K1+K2 pair\n", iters,
-             variant == 0 ? "none" : variant == 1 ? "record" : "ext", best * 1e3 / REPS);
+      printf("iters %5d  %-10s  %7.2f us per K1+K2 pair\n", iters, names[v], best * 1e3 / REPS);
     }
   }
   return 0;

@@ -81,27 +81,6 @@ def test_tape_records_gradient_sums_natively(cuda):
     assert torch.equal(T._native_add(torch.ops.aten.add.Tensor, (x, x), {}), x + x)
 
 
-def test_nasnet_tapes_and_tracks_eager(cuda, monkeypatch):
-    """NASNet (CIFAR form, drop path on): its cells read every hidden state
-    several times, so the autograd engine sums gradients between our native
-    backward ops; recorded as native adds the step tapes, and the replayed
-    steps track eager (drop-path keep probability and seeds as per-step
-    values)."""
-    from kf_benchmarks_amd.ops import conv_hip
-    monkeypatch.setattr(conv_hip, "_AUTOTUNE", False)  # (hundreds of geometries)
-    kw = dict(data_name="cifar10", steps=5)
-    le, we, _ = _run("nasnet", "momentum", False, **kw)
-    le2, we2, _ = _run("nasnet", "momentum", False, **kw)
-    lt, wt, replays = _run("nasnet", "momentum", True, **kw)
-    assert replays == 2
-    spread = 0.0
-    for a, a2, b in zip(le, le2, lt):
-        spread = max(spread, abs(a - a2))
-        assert abs(a2 - b) <= max(4 * spread, 2.5e-2 * max(1.0, abs(a2))), (le, le2, lt)
-    ref = (we - we2).abs().max().item()
-    assert (wt - we2).abs().max().item() <= max(4 * ref, 1e-3), ref
-
-
 def test_tape_refuses_torch_ops_in_step(cuda):
     """A step that launches a torch kernel cannot be taped: recording raises
     instead of producing a tape that silently skips it."""
@@ -228,6 +207,57 @@ def test_tape_bitwise_matches_eager(cuda, _deterministic, _replay_mode):
     # everything but the ops with per-step arguments (optimizer step, seeds)
     # replays raw
     assert raw >= 0.8 * ops, (raw, ops)
+
+
+def _run_exact_nasnet(tape, steps=5, bs=2):
+    from kf_benchmarks_amd import params as P
+    from kf_benchmarks_amd.benchmark import BenchmarkCNN
+    p = P.make_params(model="nasnet", data_name="cifar10", batch_size=bs, num_gpus=1,
+                      use_bf16=True, optimizer="momentum", data_format="NHWC",
+                      variable_update="kungfu", launch_tape=tape, init_learning_rate=0.002,
+                      display_every=10 ** 9, loss_type_to_report="base_loss")
+    b = BenchmarkCNN(p)
+    b.build()
+    losses = []
+    for _ in range(steps):
+        loss, _ = b.train_step(need_loss=True)
+        losses.append(float(loss))
+    torch.cuda.synchronize()
+    w = b.flat.flat.detach().float().cpu().clone()
+    bufs, slots = _state(b)
+    tp = getattr(b, "_tape", None)
+    layout = [(n, o, p.numel()) for n, p, o in zip(b.flat.names, b.flat.params, b.flat.offsets)]
+    return dict(losses=losses, w=w, bufs=bufs, slots=slots, layout=layout,
+                replays=tp.replays if tp is not None else 0)
+
+
+def _differing_params(a, b):
+    return [n for n, o, k in a["layout"] if not torch.equal(a["w"][o:o + k], b["w"][o:o + k])]
+
+
+def test_nasnet_tape_bitwise_matches_eager(cuda, _deterministic, monkeypatch):
+    """The exact oracle on NASNet (CIFAR form, drop path on, batch 2): two
+    streams (separable-branch side stream + weight-gradient stream), native
+    gradient sums between the backward ops and per-step drop-path seeds.
+    Every statistics slot takes one atomic at this batch (at batch 4 some
+    already take two, and eager differs from itself in the last bits from
+    the first step on), so eager is bitwise repeatable and the replayed
+    steps must reproduce it exactly; a cross-stream ordering race in the
+    replay (the waits the tape re-issues, bound to launches or not) shows
+    up as a mismatch here.  The reported loss is the base loss: the total
+    adds the L2 term, an atomic sum over NASNet's many weight tensors that
+    is not repeatable in the last bits.  (Replaces a batch-8 comparison within the
+    eager-vs-eager spread, which bf16 chaos made flaky: 3.3% apart at step
+    5 with a 2.5% floor, gpurun_out/devev.)"""
+    from kf_benchmarks_amd.ops import conv_hip
+    monkeypatch.setattr(conv_hip, "_AUTOTUNE", False)  # (hundreds of geometries)
+    e1 = _run_exact_nasnet(False)
+    e2 = _run_exact_nasnet(False)
+    assert not _same(e1, e2), "eager run is not bitwise repeatable: %s %s" % (
+        _same(e1, e2)[:8], _differing_params(e1, e2)[:12])
+    t = _run_exact_nasnet(True)
+    assert t["replays"] == 2
+    assert not _same(e1, t), (_same(e1, t)[:8], _differing_params(e1, t)[:12])
 
 
 def test_raw_tape_records_launch_arguments(cuda):
