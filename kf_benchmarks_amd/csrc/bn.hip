@@ -629,6 +629,164 @@ bn_bwd_apply_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __res
   }
 }
 
+// ---- backward apply with the gradient finalize folded in ------------------
+// In the backward pass a finalize launch sits between the dgrad that summed
+// a BN's backward partials and the apply pass that needs its coefficients;
+// beside the weight-gradient stream such a 5 us kernel waits for a dispatch
+// slot and took 19 us on average in the ResNet-50 bs256 step (38 launches,
+// 0.73 ms of the compute stream, profiles/r12_step_timeline.txt).  Here
+// each workgroup owns one 64-channel slice and a set of rows: it folds the
+// 32 conv-epilogue slots of its 64 channels (2 x 32 x 64 floats, one L2
+// round trip) with the arithmetic of fold_slabs + bn_finalize_grad_k, so
+// the coefficients are bitwise the finalize launch's, then streams its rows.
+// Workgroups of row block 0 write dgamma / dbeta and the coefficient arrays.
+// DUAL: the apply of kfb_bn_bwd_dual (the residual branch's coefficients
+// come from its own finalize launch: its partials are bn_partial_grad_k's).
+constexpr int FS_C = 64;      // channels per slice (8 lanes x 8 channels)
+constexpr int FS_SLOTS = 32;  // conv-epilogue slots (IG_SPREAD)
+
+struct BnFoldArgs {
+  const float* pdy;
+  const float* pdyx;
+  const float* gamma;
+  const float* mean;
+  const float* invstd;
+  float* dgamma;
+  float* dbeta;
+  float* coefA;
+  float* coefB;
+  float* coefC;
+  int accumulate;
+};
+
+template <typename T, bool DRES, bool DUAL>
+__global__ void __launch_bounds__(256)
+bn_bwd_apply_fold_k(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ xr,
+                    T* __restrict__ dx, T* __restrict__ dres, long rows, int C, BnFoldArgs f,
+                    const float* __restrict__ Ar, const float* __restrict__ Br,
+                    const float* __restrict__ Cr) {
+  static_assert(FOLD_Y == 16 && FS_SLOTS == 2 * FOLD_Y, "fold order of fold_slabs");
+  __shared__ double red[2][FOLD_Y][FS_C];
+  __shared__ double tot[2][FS_C];
+  __shared__ float cf[3][FS_C];
+  const int t = threadIdx.x;
+  const int ns = C / FS_C;
+  const int slice = blockIdx.x % ns, rb = blockIdx.x / ns, nrb = gridDim.x / ns;
+  const int c0 = slice * FS_C;
+  {
+    // fold_slabs' order for 32 slots: lane l holds float(p[l] + p[l + 16]),
+    // the 16 lanes are summed in double in lane order
+    const int arr = t >> 7, l = (t >> 3) & 15, q = t & 7;
+    const float* p = (arr ? f.pdyx : f.pdy) + c0 + 8 * q;
+    const float4* lo = (const float4*)(p + (long)l * C);
+    const float4* hi = (const float4*)(p + (long)(l + FOLD_Y) * C);
+    const float4 a0 = lo[0], a1 = lo[1], b0 = hi[0], b1 = hi[1];
+    const float s[8] = {a0.x + b0.x, a0.y + b0.y, a0.z + b0.z, a0.w + b0.w,
+                        a1.x + b1.x, a1.y + b1.y, a1.z + b1.z, a1.w + b1.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[arr][l][8 * q + k] = (double)s[k];
+  }
+  __syncthreads();
+  if (t < 2 * FS_C) {
+    const int arr = t >> 6, c = t & 63;
+    double s = 0.0;
+#pragma unroll
+    for (int l = 0; l < FOLD_Y; ++l) s += red[arr][l][c];
+    tot[arr][c] = s;
+  }
+  __syncthreads();
+  if (t < FS_C) {
+    const int c = c0 + t;
+    const double s1 = tot[0][t], s2 = tot[1][t];
+    // (the math of bn_finalize_grad_k)
+    const float is = f.invstd[c];
+    const float g = f.gamma ? f.gamma[c] : 1.f;
+    const double n = (double)rows;
+    const double A = (double)g * is;
+    const double B = -A * (double)is * (double)is * s2 / n;
+    const float a = (float)A, b = (float)B, cc = (float)(-A * s1 / n - (double)f.mean[c] * B);
+    cf[0][t] = a;
+    cf[1][t] = b;
+    cf[2][t] = cc;
+    if (rb == 0) {
+      if (f.dgamma) f.dgamma[c] = (f.accumulate ? f.dgamma[c] : 0.f) + (float)(s2 * is);
+      if (f.dbeta) f.dbeta[c] = (f.accumulate ? f.dbeta[c] : 0.f) + (float)s1;
+      f.coefA[c] = a;
+      f.coefB[c] = b;
+      f.coefC[c] = cc;
+    }
+  }
+  __syncthreads();
+  const int q = t & 7;
+  const int c = c0 + 8 * q;
+  float a[8], b[8], cc[8], ar[8], br[8], crr[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    a[k] = cf[0][8 * q + k];
+    b[k] = cf[1][8 * q + k];
+    cc[k] = cf[2][8 * q + k];
+  }
+  if constexpr (DUAL) {
+    coef_load<8>(Ar, c, ar);
+    coef_load<8>(Br, c, br);
+    coef_load<8>(Cr, c, crr);
+  }
+  const long step = (long)nrb * 32;
+  long r = (long)rb * 32 + (t >> 3);
+  auto one = [&](long e) {
+    float g0[8], x0[8], o[8];
+    load_vec<T, 8>(dy + e, g0);
+    load_vec<T, 8>(x + e, x0);
+    if constexpr (DUAL) {
+      float r0[8], o2[8];
+      load_vec<T, 8>(xr + e, r0);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o2[k] = g0[k] * ar[k] + r0[k] * br[k] + crr[k];
+      store_vec<T, 8>(dres + e, o2);
+    } else if constexpr (DRES) {
+      store_vec<T, 8>(dres + e, g0);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = g0[k] * a[k] + x0[k] * b[k] + cc[k];
+    store_vec<T, 8>(dx + e, o);
+  };
+  for (; r + step < rows; r += 2 * step) {
+    // both rows' loads issue before either is used
+    const long e0 = r * C + c, e1 = (r + step) * C + c;
+    float g0[8], g1[8], x0[8], x1[8], r0[8], r1[8];
+    load_vec<T, 8>(dy + e0, g0);
+    load_vec<T, 8>(x + e0, x0);
+    load_vec<T, 8>(dy + e1, g1);
+    load_vec<T, 8>(x + e1, x1);
+    if constexpr (DUAL) {
+      load_vec<T, 8>(xr + e0, r0);
+      load_vec<T, 8>(xr + e1, r1);
+    }
+    float o0[8], o1[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      o0[k] = g0[k] * a[k] + x0[k] * b[k] + cc[k];
+      o1[k] = g1[k] * a[k] + x1[k] * b[k] + cc[k];
+    }
+    if constexpr (DUAL) {
+      float q0[8], q1[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        q0[k] = g0[k] * ar[k] + r0[k] * br[k] + crr[k];
+        q1[k] = g1[k] * ar[k] + r1[k] * br[k] + crr[k];
+      }
+      store_vec<T, 8>(dres + e0, q0);
+      store_vec<T, 8>(dres + e1, q1);
+    } else if constexpr (DRES) {
+      store_vec<T, 8>(dres + e0, g0);
+      store_vec<T, 8>(dres + e1, g1);
+    }
+    store_vec<T, 8>(dx + e0, o0);
+    store_vec<T, 8>(dx + e1, o1);
+  }
+  if (r < rows) one(r * C + c);
+}
+
 template <typename T, int V, int U = 0>
 __global__ void __launch_bounds__(256)
 bn_bwd_apply2_k(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ xr,
@@ -1104,6 +1262,32 @@ static void launch_bwd_apply(int gb, hipStream_t stream, const void* dy, const v
                        Cc);
 }
 
+// KFB_BN_FOLD_BWD=1 (or kfb_bn_set_fold_bwd): the backward apply passes fold
+// their conv-epilogue partials (bn_bwd_apply_fold_k) instead of a finalize launch
+static int g_fold_bwd = -1;
+
+static bool fold_bwd_ok(int V, int nslab, int C, long rows) {
+  if (g_fold_bwd < 0) {
+    const char* e = getenv("KFB_BN_FOLD_BWD");
+    g_fold_bwd = (e && atoi(e) != 0) ? 1 : 0;
+  }
+  return g_fold_bwd && V == 8 && nslab == FS_SLOTS && C % FS_C == 0 && rows > 0;
+}
+
+static int fold_bwd_grid(long rows, int C) {
+  static const long target = [] {
+    const char* e = getenv("KFB_BN_FOLD_WGS");
+    const long v = e ? atol(e) : 1024;
+    return v < 64 ? 64L : v > 8192 ? 8192L : v;
+  }();
+  const int ns = C / FS_C;
+  long nrb = target / ns;
+  const long need = (rows + 63) / 64;  // two 32-row groups per iteration
+  if (nrb > need) nrb = need;
+  if (nrb < 1) nrb = 1;
+  return (int)(nrb * ns);
+}
+
 template <typename T, int V, bool RES, bool RELU>
 static void launch_apply(hipStream_t stream, const void* x, const void* res, void* y, long nvec,
                          int C, const float* scale, const float* shift, uint8_t* mb = nullptr) {
@@ -1144,6 +1328,9 @@ hipError_t bn_finalize_grad_launch(const float* slots, int C, long rows, const f
 }
 }  // namespace kfb
 
+
+// test / A/B hook: 1 folds the backward gradient finalize into the apply pass
+KFB_API void kfb_bn_set_fold_bwd(int on) { g_fold_bwd = on ? 1 : 0; }
 
 KFB_API int kfb_bn_num_slabs(long rows, int C) {
   const int V = vec_width(C);
@@ -1288,6 +1475,22 @@ KFB_API hipError_t kfb_bn_bwd(int dtype, const void* dy, const void* y, const vo
                            stream, (const T*)dy, (const T*)y, (const T*)x, save_mean, rows, C,
                            g.cw, g.tpr, g.rpi, slab_rows, pdy, pdyx);
       const long nvec = rows * C / VV;
+      if (have_partials == 1 && fold_bwd_ok(VV, nslab, C, rows)) {
+        const BnFoldArgs f{pdy, pdyx, gamma, save_mean, save_invstd, dgamma, dbeta,
+                           coefA, coefB, coefC, accumulate};
+        const dim3 gf(fold_bwd_grid(rows, C));
+        if (dres)
+          hipLaunchKernelGGL((bn_bwd_apply_fold_k<T, true, false>), gf, dim3(256), 0, stream,
+                             (const T*)dy, (const T*)x, (const T*)nullptr, (T*)dx, (T*)dres, rows,
+                             C, f, (const float*)nullptr, (const float*)nullptr,
+                             (const float*)nullptr);
+        else
+          hipLaunchKernelGGL((bn_bwd_apply_fold_k<T, false, false>), gf, dim3(256), 0, stream,
+                             (const T*)dy, (const T*)x, (const T*)nullptr, (T*)dx, (T*)nullptr,
+                             rows, C, f, (const float*)nullptr, (const float*)nullptr,
+                             (const float*)nullptr);
+        return hipGetLastError();
+      }
       if (have_partials != 2)  // 2: the producing dgrad's last workgroup finalized (BnGFin)
         hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,
                            pdy, pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta,
@@ -1327,12 +1530,22 @@ KFB_API hipError_t kfb_bn_bwd_dual(
                          dim3(BN_THREADS), lds, stream, (const T*)dy, (const T*)nullptr,
                          (const T*)xr, save_mean_r, rows, C, g.cw, g.tpr, g.rpi, slab_rows,
                          pdy_r, pdyx_r);
-      hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,
-                         pdy, pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta,
-                         coefA, coefB, coefC, accumulate, 0);
+      const bool fold = fold_bwd_ok(VV, nslab, C, rows);
+      if (!fold)
+        hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,
+                           pdy, pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta,
+                           coefA, coefB, coefC, accumulate, 0);
       hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,
                          pdy_r, pdyx_r, nslab_r, C, rows, gamma_r, save_mean_r, save_invstd_r,
                          dgamma_r, dbeta_r, coefA_r, coefB_r, coefC_r, accumulate_r, 0);
+      if (fold) {
+        const BnFoldArgs f{pdy, pdyx, gamma, save_mean, save_invstd, dgamma, dbeta,
+                           coefA, coefB, coefC, accumulate};
+        hipLaunchKernelGGL((bn_bwd_apply_fold_k<T, true, true>), dim3(fold_bwd_grid(rows, C)),
+                           dim3(256), 0, stream, (const T*)dy, (const T*)x, (const T*)xr, (T*)dx,
+                           (T*)dxr, rows, C, f, coefA_r, coefB_r, coefC_r);
+        return hipGetLastError();
+      }
       const long nvec = rows * C / VV;
       if (flat_ok(nvec, C, VV))
         hipLaunchKernelGGL((bn_bwd_apply2_k<T, VV, 4>), dim3(flat_grid(nvec)), dim3(256), 0,

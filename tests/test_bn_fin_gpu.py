@@ -113,3 +113,97 @@ def test_resnet_trains_same_with_in_kernel_finalize(cuda, monkeypatch, force):
         ref = (bb[k] - bb2[k]).abs().max().item()
         assert (ba[k] - bb[k]).abs().max().item() <= max(8 * ref, 2e-2 * bb[k].abs().max().item()
                                                          + 2e-3), k
+
+
+@pytest.fixture
+def fold_bwd(cuda):
+    from kf_benchmarks_amd.ops import _native as N
+    yield lambda on: N.load().kfb_bn_set_fold_bwd(int(on))
+    N.load().kfb_bn_set_fold_bwd(0)
+
+
+def _bwd_case(cuda, rows, C, seed):
+    g = torch.Generator().manual_seed(seed)
+    t = dict(
+        dy=torch.randn(rows, C, generator=g).to(torch.bfloat16).to(cuda),
+        x=(torch.randn(rows, C, generator=g) * 2 + 0.3).to(torch.bfloat16).to(cuda),
+        xr=torch.randn(rows, C, generator=g).to(torch.bfloat16).to(cuda),
+        gamma=(torch.rand(C, generator=g) + 0.5).to(cuda),
+        mean=(torch.randn(C, generator=g) * 0.1).to(cuda),
+        invstd=(torch.rand(C, generator=g) + 0.5).to(cuda),
+        # the 32 conv-epilogue slots of sum(dy') and sum(dy' (x - mean))
+        parts=(torch.randn(2, 32, C, generator=g) * 50).to(cuda),
+        gamma_r=(torch.rand(C, generator=g) + 0.5).to(cuda),
+        mean_r=(torch.randn(C, generator=g) * 0.1).to(cuda),
+        invstd_r=(torch.rand(C, generator=g) + 0.5).to(cuda))
+    return t
+
+
+@pytest.mark.parametrize("rows,C,dres", [(1000, 64, False), (12544, 2048, True),
+                                         (6272, 256, False), (3136, 512, True)])
+def test_bn_bwd_fold_matches_finalize_launch(cuda, fold_bwd, rows, C, dres):
+    """The backward apply pass with the gradient finalize folded in (every
+    workgroup folds its 64-channel slice of the conv-epilogue slots,
+    bn_bwd_apply_fold_k) gives exactly the finalize launch + apply pass:
+    coefficients, dgamma / dbeta (accumulated), dx and the residual
+    gradient, bitwise."""
+    from kf_benchmarks_amd.ops import _native as N
+    t = _bwd_case(cuda, rows, C, 7 + C)
+    out = {}
+    for on in (False, True):
+        fold_bwd(on)
+        dx = torch.empty_like(t["dy"])
+        dr = torch.empty_like(t["dy"]) if dres else None
+        coef = torch.full((3, C), float("nan"), device=cuda)
+        dgamma = torch.ones(C, device=cuda)
+        dbeta = torch.ones(C, device=cuda)
+        parts = t["parts"].clone()
+        N.call("kfb_bn_bwd", N.dt(t["dy"]), t["dy"].data_ptr(), None, t["x"].data_ptr(),
+               dx.data_ptr(), N.ptr(dr), rows, C, t["gamma"].data_ptr(), t["mean"].data_ptr(),
+               t["invstd"].data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), parts[0].data_ptr(),
+               parts[1].data_ptr(), 32, coef[0].data_ptr(), coef[1].data_ptr(),
+               coef[2].data_ptr(), 0, 1, 1, N.stream(cuda))
+        torch.cuda.synchronize()
+        out[on] = (dx, dr, coef, dgamma, dbeta)
+    for k, (a, b) in enumerate(zip(out[False], out[True])):
+        if a is not None:
+            assert torch.equal(a, b), k
+    # against the formula on the host
+    s1, s2 = t["parts"][0].double().sum(0), t["parts"][1].double().sum(0)
+    A = t["gamma"].double() * t["invstd"].double()
+    B = -A * t["invstd"].double() ** 2 * s2 / rows
+    Cc = -A * s1 / rows - t["mean"].double() * B
+    ref = t["dy"].double() * A + t["x"].double() * B + Cc
+    torch.testing.assert_close(out[True][0].double(), ref, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(out[True][3].double(), 1 + s2 * t["invstd"].double(), rtol=1e-5,
+                               atol=1e-3)
+
+
+@pytest.mark.parametrize("rows,C", [(3136, 256), (12544, 2048)])
+def test_bn_bwd_dual_fold_matches_finalize_launch(cuda, fold_bwd, rows, C):
+    """kfb_bn_bwd_dual (y = relu(bn(x) + bn_r(xr)) backward) with the main
+    BN's finalize folded into the apply pass equals the two finalize
+    launches + apply, bitwise (the residual branch keeps its launch)."""
+    from kf_benchmarks_amd.ops import _native as N
+    t = _bwd_case(cuda, rows, C, 11 + C)
+    out = {}
+    for on in (False, True):
+        fold_bwd(on)
+        dx, dxr = torch.empty_like(t["dy"]), torch.empty_like(t["dy"])
+        coef = torch.full((6, C), float("nan"), device=cuda)
+        dg = torch.zeros(4, C, device=cuda)
+        parts = t["parts"].clone()
+        nr = 64
+        pr = torch.zeros(2, nr, C, device=cuda)
+        N.call("kfb_bn_bwd_dual", N.dt(t["dy"]), t["dy"].data_ptr(), t["x"].data_ptr(),
+               t["xr"].data_ptr(), dx.data_ptr(), dxr.data_ptr(), rows, C,
+               t["gamma"].data_ptr(), t["mean"].data_ptr(), t["invstd"].data_ptr(),
+               dg[0].data_ptr(), dg[1].data_ptr(), parts[0].data_ptr(), parts[1].data_ptr(), 32,
+               coef[0].data_ptr(), coef[1].data_ptr(), coef[2].data_ptr(), 0,
+               t["gamma_r"].data_ptr(), t["mean_r"].data_ptr(), t["invstd_r"].data_ptr(),
+               dg[2].data_ptr(), dg[3].data_ptr(), pr[0].data_ptr(), pr[1].data_ptr(), nr,
+               coef[3].data_ptr(), coef[4].data_ptr(), coef[5].data_ptr(), 0, N.stream(cuda))
+        torch.cuda.synchronize()
+        out[on] = (dx, dxr, coef, dg)
+    for k, (a, b) in enumerate(zip(out[False], out[True])):
+        assert torch.equal(a, b), k

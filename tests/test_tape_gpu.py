@@ -209,6 +209,24 @@ def test_tape_bitwise_matches_eager(cuda, _deterministic, _replay_mode):
     assert raw >= 0.8 * ops, (raw, ops)
 
 
+def test_bn_fold_bwd_bitwise(cuda, _deterministic):
+    """Backward BN finalize folded into the apply passes (KFB_BN_FOLD_BWD):
+    the folded coefficients are bitwise the finalize launch's, so the exact
+    oracle's eager step is unchanged by the mode, and its taped replay
+    reproduces it bit for bit."""
+    from kf_benchmarks_amd.ops import _native as N
+    e1 = _run_exact(False)
+    N.load().kfb_bn_set_fold_bwd(1)
+    try:
+        e2 = _run_exact(False)
+        t = _run_exact(True)
+    finally:
+        N.load().kfb_bn_set_fold_bwd(0)
+    assert not _same(e1, e2), _same(e1, e2)[:8]
+    assert t["replays"] == 3
+    assert not _same(e1, t), _same(e1, t)[:8]
+
+
 def _run_exact_nasnet(tape, steps=5, bs=2):
     from kf_benchmarks_amd import params as P
     from kf_benchmarks_amd.benchmark import BenchmarkCNN
