@@ -236,6 +236,12 @@ __device__ __forceinline__ void coef_load(const float* __restrict__ p, int c, fl
   for (int k = 0; k < V; ++k) o[k] = p[c + k];
 }
 
+// dx = g*A + x*B + C with one fixed FMA order, so every backward apply kernel
+// (launch-finalized or folded) rounds the same way
+__device__ __forceinline__ float bwd_fma(float g, float a, float x, float b, float c) {
+  return __builtin_fmaf(g, a, __builtin_fmaf(x, b, c));
+}
+
 // ReLU bit mask of one 8-channel vector of a 2-byte output: bit k of byte
 // mb[i] = (stored y[8i + k] > 0), from the value as rounded to T, so it equals
 // the test a consumer would make on y itself.  A conv dgrad epilogue reads
@@ -264,7 +270,7 @@ bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y
                    const float (&sf)[V]) {
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      float o = v[k] * sc[k] + sf[k];
+      float o = __builtin_fmaf(v[k], sc[k], sf[k]);
       if (RES) o += rr[k];
       if (RELU) o = fmaxf(o, 0.f);
       v[k] = o;
@@ -568,7 +574,7 @@ bn_bwd_apply_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __res
         if (DRES) store_vec<T, V>(dres + (long)i * V, g[u]);
         float o[V];
 #pragma unroll
-        for (int k = 0; k < V; ++k) o[k] = g[u][k] * a[k] + xv[u][k] * b[k] + cc[k];
+        for (int k = 0; k < V; ++k) o[k] = bwd_fma(g[u][k], a[k], xv[u][k], b[k], cc[k]);
         store_vec<T, V>(dx + (long)i * V, o);
       }
     }
@@ -602,8 +608,8 @@ bn_bwd_apply_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __res
     float o0[V], o1[V];
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      o0[k] = g0[k] * a[k] + x0[k] * b[k] + cc[k];
-      o1[k] = g1[k] * a[k] + x1[k] * b[k] + cc[k];
+      o0[k] = bwd_fma(g0[k], a[k], x0[k], b[k], cc[k]);
+      o1[k] = bwd_fma(g1[k], a[k], x1[k], b[k], cc[k]);
     }
     store_vec<T, V>(dx + (long)ia * V, o0);
     if (two) store_vec<T, V>(dx + (long)ib * V, o1);
@@ -673,52 +679,68 @@ bn_bwd_apply_fold_k(const T* __restrict__ dy, const T* __restrict__ x, const T* 
   const int ns = C / FS_C;
   const int slice = blockIdx.x % ns, rb = blockIdx.x / ns, nrb = gridDim.x / ns;
   const int c0 = slice * FS_C;
+  const int q = t & 7;
+  const int c = c0 + 8 * q;
+  const long step = (long)nrb * 32;
+  long r = (long)rb * 32 + (t >> 3);
+  // the first two rows' operands are issued before the fold, so their
+  // latency overlaps its L2 round trip and LDS reduction
+  float g0[8], g1[8], x0[8], x1[8], r0[8], r1[8];
+  const bool has0 = r < rows, has1 = r + step < rows;
+  if (has0) {
+    load_vec<T, 8>(dy + r * C + c, g0);
+    load_vec<T, 8>(x + r * C + c, x0);
+    if constexpr (DUAL) load_vec<T, 8>(xr + r * C + c, r0);
+  }
+  if (has1) {
+    load_vec<T, 8>(dy + (r + step) * C + c, g1);
+    load_vec<T, 8>(x + (r + step) * C + c, x1);
+    if constexpr (DUAL) load_vec<T, 8>(xr + (r + step) * C + c, r1);
+  }
   {
     // fold_slabs' order for 32 slots: lane l holds float(p[l] + p[l + 16]),
     // the 16 lanes are summed in double in lane order
-    const int arr = t >> 7, l = (t >> 3) & 15, q = t & 7;
+    const int arr = t >> 7, l = (t >> 3) & 15;
     const float* p = (arr ? f.pdyx : f.pdy) + c0 + 8 * q;
     const float4* lo = (const float4*)(p + (long)l * C);
     const float4* hi = (const float4*)(p + (long)(l + FOLD_Y) * C);
     const float4 a0 = lo[0], a1 = lo[1], b0 = hi[0], b1 = hi[1];
-    const float s[8] = {a0.x + b0.x, a0.y + b0.y, a0.z + b0.z, a0.w + b0.w,
-                        a1.x + b1.x, a1.y + b1.y, a1.z + b1.z, a1.w + b1.w};
+    const float sv[8] = {a0.x + b0.x, a0.y + b0.y, a0.z + b0.z, a0.w + b0.w,
+                         a1.x + b1.x, a1.y + b1.y, a1.z + b1.z, a1.w + b1.w};
 #pragma unroll
-    for (int k = 0; k < 8; ++k) red[arr][l][8 * q + k] = (double)s[k];
+    for (int k = 0; k < 8; ++k) red[arr][l][8 * q + k] = (double)sv[k];
   }
   __syncthreads();
   if (t < 2 * FS_C) {
-    const int arr = t >> 6, c = t & 63;
-    double s = 0.0;
+    const int arr = t >> 6, cc = t & 63;
+    double sum = 0.0;
 #pragma unroll
-    for (int l = 0; l < FOLD_Y; ++l) s += red[arr][l][c];
-    tot[arr][c] = s;
+    for (int l = 0; l < FOLD_Y; ++l) sum += red[arr][l][cc];
+    tot[arr][cc] = sum;
   }
   __syncthreads();
   if (t < FS_C) {
-    const int c = c0 + t;
+    const int ch = c0 + t;
     const double s1 = tot[0][t], s2 = tot[1][t];
     // (the math of bn_finalize_grad_k)
-    const float is = f.invstd[c];
-    const float g = f.gamma ? f.gamma[c] : 1.f;
+    const float is = f.invstd[ch];
+    const float g = f.gamma ? f.gamma[ch] : 1.f;
     const double n = (double)rows;
     const double A = (double)g * is;
     const double B = -A * (double)is * (double)is * s2 / n;
-    const float a = (float)A, b = (float)B, cc = (float)(-A * s1 / n - (double)f.mean[c] * B);
-    cf[0][t] = a;
-    cf[1][t] = b;
-    cf[2][t] = cc;
+    const float av = (float)A, bv = (float)B, cv = (float)(-A * s1 / n - (double)f.mean[ch] * B);
+    cf[0][t] = av;
+    cf[1][t] = bv;
+    cf[2][t] = cv;
     if (rb == 0) {
-      if (f.dgamma) f.dgamma[c] = (f.accumulate ? f.dgamma[c] : 0.f) + (float)(s2 * is);
-      if (f.dbeta) f.dbeta[c] = (f.accumulate ? f.dbeta[c] : 0.f) + (float)s1;
-      f.coefA[c] = a;
-      f.coefB[c] = b;
-      f.coefC[c] = cc;
+      if (f.dgamma) f.dgamma[ch] = (f.accumulate ? f.dgamma[ch] : 0.f) + (float)(s2 * is);
+      if (f.dbeta) f.dbeta[ch] = (f.accumulate ? f.dbeta[ch] : 0.f) + (float)s1;
+      f.coefA[ch] = av;
+      f.coefB[ch] = bv;
+      f.coefC[ch] = cv;
     }
   }
   __syncthreads();
-  const int q = t & 7;
-  const int c = c0 + 8 * q;
   float a[8], b[8], cc[8], ar[8], br[8], crr[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -731,60 +753,40 @@ bn_bwd_apply_fold_k(const T* __restrict__ dy, const T* __restrict__ x, const T* 
     coef_load<8>(Br, c, br);
     coef_load<8>(Cr, c, crr);
   }
-  const long step = (long)nrb * 32;
-  long r = (long)rb * 32 + (t >> 3);
-  auto one = [&](long e) {
-    float g0[8], x0[8], o[8];
-    load_vec<T, 8>(dy + e, g0);
-    load_vec<T, 8>(x + e, x0);
+  // one row's outputs from its loaded operands
+  auto emit = [&](long e, const float (&gv)[8], const float (&xv)[8], const float (&rv)[8]) {
+    float o[8];
     if constexpr (DUAL) {
-      float r0[8], o2[8];
-      load_vec<T, 8>(xr + e, r0);
+      float o2[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o2[k] = g0[k] * ar[k] + r0[k] * br[k] + crr[k];
+      for (int k = 0; k < 8; ++k) o2[k] = bwd_fma(gv[k], ar[k], rv[k], br[k], crr[k]);
       store_vec<T, 8>(dres + e, o2);
     } else if constexpr (DRES) {
-      store_vec<T, 8>(dres + e, g0);
+      store_vec<T, 8>(dres + e, gv);
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = g0[k] * a[k] + x0[k] * b[k] + cc[k];
+    for (int k = 0; k < 8; ++k) o[k] = bwd_fma(gv[k], a[k], xv[k], b[k], cc[k]);
     store_vec<T, 8>(dx + e, o);
   };
-  for (; r + step < rows; r += 2 * step) {
+  if (!has0) return;
+  emit(r * C + c, g0, x0, r0);
+  if (!has1) return;
+  emit((r + step) * C + c, g1, x1, r1);
+  for (r += 2 * step; r < rows; r += 2 * step) {
     // both rows' loads issue before either is used
+    const bool two = r + step < rows;
     const long e0 = r * C + c, e1 = (r + step) * C + c;
-    float g0[8], g1[8], x0[8], x1[8], r0[8], r1[8];
     load_vec<T, 8>(dy + e0, g0);
     load_vec<T, 8>(x + e0, x0);
-    load_vec<T, 8>(dy + e1, g1);
-    load_vec<T, 8>(x + e1, x1);
-    if constexpr (DUAL) {
-      load_vec<T, 8>(xr + e0, r0);
-      load_vec<T, 8>(xr + e1, r1);
+    if constexpr (DUAL) load_vec<T, 8>(xr + e0, r0);
+    if (two) {
+      load_vec<T, 8>(dy + e1, g1);
+      load_vec<T, 8>(x + e1, x1);
+      if constexpr (DUAL) load_vec<T, 8>(xr + e1, r1);
     }
-    float o0[8], o1[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      o0[k] = g0[k] * a[k] + x0[k] * b[k] + cc[k];
-      o1[k] = g1[k] * a[k] + x1[k] * b[k] + cc[k];
-    }
-    if constexpr (DUAL) {
-      float q0[8], q1[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        q0[k] = g0[k] * ar[k] + r0[k] * br[k] + crr[k];
-        q1[k] = g1[k] * ar[k] + r1[k] * br[k] + crr[k];
-      }
-      store_vec<T, 8>(dres + e0, q0);
-      store_vec<T, 8>(dres + e1, q1);
-    } else if constexpr (DRES) {
-      store_vec<T, 8>(dres + e0, g0);
-      store_vec<T, 8>(dres + e1, g1);
-    }
-    store_vec<T, 8>(dx + e0, o0);
-    store_vec<T, 8>(dx + e1, o1);
+    emit(e0, g0, x0, r0);
+    if (two) emit(e1, g1, x1, r1);
   }
-  if (r < rows) one(r * C + c);
 }
 
 template <typename T, int V, int U = 0>
@@ -827,8 +829,8 @@ bn_bwd_apply2_k(const T* __restrict__ dy, const T* __restrict__ x, const T* __re
         float o[V], q[V];
 #pragma unroll
         for (int j = 0; j < V; ++j) {
-          o[j] = g[u][j] * k.a[j] + xv[u][j] * k.b[j] + k.c[j];
-          q[j] = g[u][j] * k.ar[j] + rv[u][j] * k.br[j] + k.cr[j];
+          o[j] = bwd_fma(g[u][j], k.a[j], xv[u][j], k.b[j], k.c[j]);
+          q[j] = bwd_fma(g[u][j], k.ar[j], rv[u][j], k.br[j], k.cr[j]);
         }
         store_vec<T, V>(dx + (long)i * V, o);
         store_vec<T, V>(dxr + (long)i * V, q);
@@ -843,8 +845,8 @@ bn_bwd_apply2_k(const T* __restrict__ dy, const T* __restrict__ x, const T* __re
     load_vec<T, V>(xr + (long)i * V, rv);
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      o[j] = g[j] * k.a[j] + xv[j] * k.b[j] + k.c[j];
-      orr[j] = g[j] * k.ar[j] + rv[j] * k.br[j] + k.cr[j];
+      o[j] = bwd_fma(g[j], k.a[j], xv[j], k.b[j], k.c[j]);
+      orr[j] = bwd_fma(g[j], k.ar[j], rv[j], k.br[j], k.cr[j]);
     }
     store_vec<T, V>(dx + (long)i * V, o);
     store_vec<T, V>(dxr + (long)i * V, orr);
@@ -864,10 +866,10 @@ bn_bwd_apply2_k(const T* __restrict__ dy, const T* __restrict__ x, const T* __re
       float o0[V], q0[V], o1[V], q1[V];
 #pragma unroll
       for (int j = 0; j < V; ++j) {
-        o0[j] = g0[j] * k.a[j] + x0[j] * k.b[j] + k.c[j];
-        q0[j] = g0[j] * k.ar[j] + r0[j] * k.br[j] + k.cr[j];
-        o1[j] = g1[j] * k.a[j] + x1[j] * k.b[j] + k.c[j];
-        q1[j] = g1[j] * k.ar[j] + r1[j] * k.br[j] + k.cr[j];
+        o0[j] = bwd_fma(g0[j], k.a[j], x0[j], k.b[j], k.c[j]);
+        q0[j] = bwd_fma(g0[j], k.ar[j], r0[j], k.br[j], k.cr[j]);
+        o1[j] = bwd_fma(g1[j], k.a[j], x1[j], k.b[j], k.c[j]);
+        q1[j] = bwd_fma(g1[j], k.ar[j], r1[j], k.br[j], k.cr[j]);
       }
       store_vec<T, V>(dx + (long)i * V, o0);
       store_vec<T, V>(dxr + (long)i * V, q0);
@@ -1179,7 +1181,7 @@ bn_pool3s2_k(const T* __restrict__ dz, const T* __restrict__ z, const uint8_t* _
         } else {
           float o[8];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) o[k] = gr[a][b][k] * cA[k] + xv[k] * cB[k] + cC[k];
+          for (int k = 0; k < 8; ++k) o[k] = bwd_fma(gr[a][b][k], cA[k], xv[k], cB[k], cC[k]);
           store_vec<T, 8>(dx + e, o);
         }
       }
@@ -1262,16 +1264,27 @@ static void launch_bwd_apply(int gb, hipStream_t stream, const void* dy, const v
                        Cc);
 }
 
-// KFB_BN_FOLD_BWD=1 (or kfb_bn_set_fold_bwd): the backward apply passes fold
-// their conv-epilogue partials (bn_bwd_apply_fold_k) instead of a finalize launch
+// KFB_BN_FOLD_BWD (or kfb_bn_set_fold_bwd): the backward apply passes fold
+// their conv-epilogue partials (bn_bwd_apply_fold_k) instead of a finalize
+// launch - 1 (default): tensors up to KFB_BN_FOLD_MAXMB (32 MB), 2: every
+// size, 0: never.  At 50+ MB the slice layout streams slower than the
+// grid-stride / flat passes by more than the launch it saves (ResNet-50
+// bs256: 14x14x256 30 vs 18 us, profiles/r12_bn_fold_bwd.txt); below, the
+// launch it removes waits for a dispatch slot beside the weight-gradient
+// stream (ResNet-152 bs32 2,515 -> 2,581-2,606 img/s).
 static int g_fold_bwd = -1;
 
 static bool fold_bwd_ok(int V, int nslab, int C, long rows) {
   if (g_fold_bwd < 0) {
     const char* e = getenv("KFB_BN_FOLD_BWD");
-    g_fold_bwd = (e && atoi(e) != 0) ? 1 : 0;
+    g_fold_bwd = e ? atoi(e) : 1;
   }
-  return g_fold_bwd && V == 8 && nslab == FS_SLOTS && C % FS_C == 0 && rows > 0;
+  static const long max_bytes = [] {
+    const char* e = getenv("KFB_BN_FOLD_MAXMB");
+    return (long)((e ? atof(e) : 32.0) * (1 << 20));
+  }();
+  return g_fold_bwd && V == 8 && nslab == FS_SLOTS && C % FS_C == 0 && rows > 0 &&
+         (g_fold_bwd == 2 || rows * C * 2 <= max_bytes);
 }
 
 static int fold_bwd_grid(long rows, int C) {
@@ -1330,7 +1343,11 @@ hipError_t bn_finalize_grad_launch(const float* slots, int C, long rows, const f
 
 
 // test / A/B hook: 1 folds the backward gradient finalize into the apply pass
-KFB_API void kfb_bn_set_fold_bwd(int on) { g_fold_bwd = on ? 1 : 0; }
+KFB_API void kfb_bn_set_fold_bwd(int mode) { g_fold_bwd = mode; }
+KFB_API int kfb_bn_get_fold_bwd() {
+  fold_bwd_ok(0, 0, 0, 0);  // (resolves the environment default)
+  return g_fold_bwd;
+}
 
 KFB_API int kfb_bn_num_slabs(long rows, int C) {
   const int V = vec_width(C);

@@ -118,8 +118,9 @@ def test_resnet_trains_same_with_in_kernel_finalize(cuda, monkeypatch, force):
 @pytest.fixture
 def fold_bwd(cuda):
     from kf_benchmarks_amd.ops import _native as N
-    yield lambda on: N.load().kfb_bn_set_fold_bwd(int(on))
-    N.load().kfb_bn_set_fold_bwd(0)
+    prev = N.load().kfb_bn_get_fold_bwd()
+    yield lambda on: N.load().kfb_bn_set_fold_bwd(2 if on else 0)  # (2: at every size)
+    N.load().kfb_bn_set_fold_bwd(prev)
 
 
 def _bwd_case(cuda, rows, C, seed):

@@ -215,13 +215,15 @@ def test_bn_fold_bwd_bitwise(cuda, _deterministic):
     oracle's eager step is unchanged by the mode, and its taped replay
     reproduces it bit for bit."""
     from kf_benchmarks_amd.ops import _native as N
-    e1 = _run_exact(False)
-    N.load().kfb_bn_set_fold_bwd(1)
+    prev = N.load().kfb_bn_get_fold_bwd()
+    N.load().kfb_bn_set_fold_bwd(0)
     try:
+        e1 = _run_exact(False)
+        N.load().kfb_bn_set_fold_bwd(2)
         e2 = _run_exact(False)
         t = _run_exact(True)
     finally:
-        N.load().kfb_bn_set_fold_bwd(0)
+        N.load().kfb_bn_set_fold_bwd(prev)
     assert not _same(e1, e2), _same(e1, e2)[:8]
     assert t["replays"] == 3
     assert not _same(e1, t), _same(e1, t)[:8]
