@@ -1267,11 +1267,11 @@ static void launch_bwd_apply(int gb, hipStream_t stream, const void* dy, const v
 // KFB_BN_FOLD_BWD (or kfb_bn_set_fold_bwd): the backward apply passes fold
 // their conv-epilogue partials (bn_bwd_apply_fold_k) instead of a finalize
 // launch - 1 (default): tensors up to KFB_BN_FOLD_MAXMB (32 MB), 2: every
-// size, 0: never.  At 50+ MB the slice layout streams slower than the
-// grid-stride / flat passes by more than the launch it saves (ResNet-50
-// bs256: 14x14x256 30 vs 18 us, profiles/r12_bn_fold_bwd.txt); below, the
-// launch it removes waits for a dispatch slot beside the weight-gradient
-// stream (ResNet-152 bs32 2,515 -> 2,581-2,606 img/s).
+// size, 0: never.  On the large tensors the slice layout streams slower
+// than the grid-stride / flat passes (every size: ResNet-50 bs256 +0.1
+// ms/step; up to 16 or 32 MB: -0.09 ms, profiles/r12_bn_fold_bwd.txt); on
+// the small ones the launch it removes waits for a dispatch slot beside the
+// weight-gradient stream (ResNet-152 bs32 2,515 -> 2,581-2,606 img/s).
 static int g_fold_bwd = -1;
 
 static bool fold_bwd_ok(int V, int nslab, int C, long rows) {
