@@ -172,7 +172,9 @@ __device__ __forceinline__ void epi_load(const IgArgs& a, const EpiRsrc& r, int 
 // Pass-group size of the dgrad-style epilogue of a BM x BN tile on NT threads.
 template <int BM, int BN, int NT>
 constexpr int epi_group() {
-  return BM * (BN / 8) / NT > 4 ? 4 : BM * (BN / 8) / NT;
+  // the largest of 4 .. 1 passes that divides the tile's pass count
+  constexpr int np = BM * (BN / 8) / NT;
+  return np % 4 == 0 ? (np > 4 ? 4 : np) : np % 3 == 0 && np > 3 ? 3 : np % 2 == 0 ? 2 : 1;
 }
 
 // EARLY: the first pass group's operands were loaded by the kernel before
@@ -896,11 +898,14 @@ __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * 
     igemm_glds_k(IgArgs a) {
   constexpr int NT = WGM * WGN * 64;
   constexpr int SLAB = NT / 8;  // rows one DMA instruction of every wave covers
+  // pixel rows of the LDS tile: BM rounded up to whole DMA slabs (BM = 224:
+  // 7 MFMA rows per wave, the slab rows past BM load nothing)
+  constexpr int BMA = (BM + SLAB - 1) / SLAB * SLAB;
   static_assert(STAGES == 2 || STAGES == 3, "ring depth");
-  static_assert(BM % SLAB == 0 && BN % SLAB == 0 && SLAB % 16 == 0, "DMA slabs");
+  static_assert(BN % SLAB == 0 && SLAB % 16 == 0 && BM % (16 * WGM) == 0, "DMA slabs");
   constexpr int TM = BM / WGM / 16, TN = BN / WGN / 16;
-  constexpr int XI = BM / SLAB, WI = BN / SLAB;  // DMA instructions per thread per K step
-  constexpr int STAGE = (BM + BN) * IG_BK;       // elements per ring stage
+  constexpr int XI = BMA / SLAB, WI = BN / SLAB;  // DMA instructions per thread per K step
+  constexpr int STAGE = (BMA + BN) * IG_BK;       // elements per ring stage
   static_assert(BM * BN <= STAGES * STAGE, "epilogue staging exceeds the ring");
   __shared__ __attribute__((aligned(16))) T smem[STAGES * STAGE];
 
@@ -922,7 +927,7 @@ __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * 
 #pragma unroll
   for (int i = 0; i < XI; ++i) {
     const int m = m0 + i * SLAB + rr;
-    const bool ok = m < a.M;
+    const bool ok = m < a.M && (BMA == BM || i * SLAB + rr < BM);
     const int mm = ok ? m : 0;
     const int img = mm / OHW, rem = mm - img * OHW;
     const int oh = rem / a.OW, ow = rem - oh * a.OW;
@@ -942,7 +947,7 @@ __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * 
   int s_cc = 0, s_kh = 0, s_kw = 0, s_tap = 0, s_tapi = 0, s_k = 0;
   auto issue = [&](int stage) {
     T* xs = smem + stage * STAGE;
-    T* ws = xs + BM * IG_BK;
+    T* ws = xs + BMA * IG_BK;
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
       const bool ok = (tapmask[i] >> s_tapi) & 1ull;
@@ -984,7 +989,7 @@ __global__ void __launch_bounds__(WGM * WGN * 64, (glds_occupancy<BM, BN, WGM * 
   const int wm = wid % WGM, wn = wid / WGM;
   auto compute = [&](int stage) {
     const T* xs = smem + stage * STAGE;
-    const T* ws = xs + BM * IG_BK;
+    const T* ws = xs + BMA * IG_BK;
     if constexpr (MF32) {
       // four 16-deep sub-steps; lane l reads chunk 2ks + l/32 of row l % 32
 #pragma unroll
@@ -2340,6 +2345,15 @@ static void launch_glds_big(const IgArgs& a, bool wide, hipStream_t s, bool mf32
                        dim3(((a.M + 511) / 512) * ((a.Ncol + 127) / 128)), dim3(512), 0, s, a);
 }
 
+// 224 x 256 tiles on the same 8 waves (7 x 4 MFMA tiles per wave): where M
+// is 196 pixels per image (14x14), 224-row tiles give 224 tiles instead of
+// 196 256-row ones on 256 CUs - 7/8 of the work per tile with every CU used
+template <typename T>
+static void launch_glds_224(const IgArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((igemm_glds_k<T, 224, 256, 2, 4, 2>),
+                     dim3(((a.M + 223) / 224) * ((a.Ncol + 255) / 256)), dim3(512), 0, s, a);
+}
+
 template <typename T>
 static void launch_8p(const IgArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((igemm_8p_k<T>), dim3(((a.M + 255) / 256) * ((a.Ncol + 255) / 256)),
@@ -2510,7 +2524,7 @@ enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_G
        IG_ALGO_GENERIC = 21, IG_ALGO_SK128 = 22, IG_ALGO_G8P = 23, IG_ALGO_ONEBUF_E = 24,
        IG_ALGO_ONEBUF_N64_E = 25, IG_ALGO_CLASSIC_N64_E = 26, IG_ALGO_DB = 27,
        IG_ALGO_GBIG256_32 = 28, IG_ALGO_GSHORT128_32 = 29, IG_ALGO_GSHORT64_32 = 30,
-       IG_ALGO_S3 = 31, IG_ALGO_S1 = 32, IG_ALGO_S7 = 33 };
+       IG_ALGO_S3 = 31, IG_ALGO_S1 = 32, IG_ALGO_S7 = 33, IG_ALGO_GBIG224 = 34 };
 
 static bool c8_geometry(int C, int KH, int KW) {
   return C == 8 && (KW == 1 || KW == 2 || KW == 4 || KW == 8) && (KH * KW) % 8 == 0;
@@ -2628,6 +2642,12 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
     const bool three = algo >= IG_ALGO_GSHORT64_3;
     if (dtype == BF16) launch_glds_short<bf16>(a, wide, three, stream);
     else if (dtype == F16) launch_glds_short<f16>(a, wide, three, stream);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
+  if (algo == IG_ALGO_GBIG224 && fast) {
+    if (dtype == BF16) launch_glds_224<bf16>(a, stream);
+    else if (dtype == F16) launch_glds_224<f16>(a, stream);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }

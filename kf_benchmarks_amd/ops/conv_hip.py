@@ -70,6 +70,9 @@ IG_S1 = 32
 # streaming stem conv over the pixel-pair view (csrc/conv_s7.hip): one image
 # band per CU, input rows through an LDS ring, weights in VGPRs
 IG_S7 = 33
+# 224 x 256 tiles on the 8-wave LDS-DMA kernel (7 MFMA rows per wave): 224
+# tiles instead of 196 for the 14x14 layers at batch 256 (M = 196 per image)
+IG_GBIG224 = 34
 IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N64,
             "glds_n64": IG_GLDS_N64, "onebuf": IG_ONEBUF, "onebuf_n64": IG_ONEBUF_N64,
             "tall512": IG_TALL512, "tall256": IG_TALL256, "small": IG_SMALL,
@@ -81,7 +84,7 @@ IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N6
             "onebuf_n64_e": IG_ONEBUF_N64_E, "classic_n64_e": IG_CLASSIC_N64_E, "db": IG_DB,
             "gbig256_32": IG_GBIG256_32, "gshort128_32": IG_GSHORT128_32,
             "gshort64_32": IG_GSHORT64_32, "s3": IG_S3, "s1": IG_S1,
-            "s7": IG_S7}
+            "s7": IG_S7, "gbig224": IG_GBIG224}
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
@@ -94,6 +97,7 @@ _NO_GSHORT = os.environ.get("KFB_IGEMM_NOGSHORT", "0") == "1"  # A/B knob: drop 
 _GSHORT3 = os.environ.get("KFB_IGEMM_GSHORT3", "1") != "0"  # A/B knob: the 3-stage forms
 _NO_MULTI = os.environ.get("KFB_IGEMM_NOMULTI", "0") == "1"  # A/B knob: drop IG_*MULTI*
 _NO_BIG = os.environ.get("KFB_IGEMM_NOBIG", "0") == "1"  # A/B knob: drop IG_GBIG*
+_NO_224 = os.environ.get("KFB_IGEMM_NO224", "0") == "1"  # A/B knob: drop IG_GBIG224
 _SK = os.environ.get("KFB_IGEMM_SK", "0") == "1"  # offer IG_SK128 to the autotune
 # KFB_IGEMM_EARLY=1: offer the early-epilogue-operand kernels (IG_*_E) to the
 # autotune.  Off: at 3 workgroups per CU (their early operands stay live
@@ -388,6 +392,9 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
         M = geo[0] * geo[4] * geo[5]
         if ncol >= 256 and ((M + 255) // 256) * ((ncol + 255) // 256) >= 192:
             cands += (IG_GBIG256,) + ((IG_G8P,) if C % 64 == 0 else ())
+            if not _NO_224 and ((M + 223) // 224) * ((ncol + 255) // 256) > \
+                    ((M + 255) // 256) * ((ncol + 255) // 256):
+                cands += (IG_GBIG224,)
             if _MF32:
                 cands += (IG_GBIG256_32,)
         if 64 < ncol <= 256 and ((M + 511) // 512) * ((ncol + 127) // 128) >= 256:
