@@ -2354,6 +2354,14 @@ static void launch_glds_224(const IgArgs& a, hipStream_t s) {
                      dim3(((a.M + 223) / 224) * ((a.Ncol + 255) / 256)), dim3(512), 0, s, a);
 }
 
+// 448 x 128 (waves 4 x 2 of 112 x 64): for the 128-channel layers, 448 tiles
+// at 28x28 batch 256 (1.75 rounds on 256 CUs) where 512 x 128 has 392 (1.53)
+template <typename T>
+static void launch_glds_448(const IgArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((igemm_glds_k<T, 448, 128, 4, 2, 2>),
+                     dim3(((a.M + 447) / 448) * ((a.Ncol + 127) / 128)), dim3(512), 0, s, a);
+}
+
 template <typename T>
 static void launch_8p(const IgArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((igemm_8p_k<T>), dim3(((a.M + 255) / 256) * ((a.Ncol + 255) / 256)),
@@ -2524,7 +2532,8 @@ enum { IG_ALGO_CLASSIC = 1, IG_ALGO_GLDS = 2, IG_ALGO_CLASSIC_N64 = 3, IG_ALGO_G
        IG_ALGO_GENERIC = 21, IG_ALGO_SK128 = 22, IG_ALGO_G8P = 23, IG_ALGO_ONEBUF_E = 24,
        IG_ALGO_ONEBUF_N64_E = 25, IG_ALGO_CLASSIC_N64_E = 26, IG_ALGO_DB = 27,
        IG_ALGO_GBIG256_32 = 28, IG_ALGO_GSHORT128_32 = 29, IG_ALGO_GSHORT64_32 = 30,
-       IG_ALGO_S3 = 31, IG_ALGO_S1 = 32, IG_ALGO_S7 = 33, IG_ALGO_GBIG224 = 34 };
+       IG_ALGO_S3 = 31, IG_ALGO_S1 = 32, IG_ALGO_S7 = 33, IG_ALGO_GBIG224 = 34,
+       IG_ALGO_GBIG448 = 35 };
 
 static bool c8_geometry(int C, int KH, int KW) {
   return C == 8 && (KW == 1 || KW == 2 || KW == 4 || KW == 8) && (KH * KW) % 8 == 0;
@@ -2642,6 +2651,12 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
     const bool three = algo >= IG_ALGO_GSHORT64_3;
     if (dtype == BF16) launch_glds_short<bf16>(a, wide, three, stream);
     else if (dtype == F16) launch_glds_short<f16>(a, wide, three, stream);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
+  if (algo == IG_ALGO_GBIG448 && fast) {
+    if (dtype == BF16) launch_glds_448<bf16>(a, stream);
+    else if (dtype == F16) launch_glds_448<f16>(a, stream);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }

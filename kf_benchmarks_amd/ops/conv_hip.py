@@ -73,6 +73,8 @@ IG_S7 = 33
 # 224 x 256 tiles on the 8-wave LDS-DMA kernel (7 MFMA rows per wave): 224
 # tiles instead of 196 for the 14x14 layers at batch 256 (M = 196 per image)
 IG_GBIG224 = 34
+# 448 x 128 tiles (waves 4 x 2 of 112 x 64) for the 128-channel layers
+IG_GBIG448 = 35
 IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N64,
             "glds_n64": IG_GLDS_N64, "onebuf": IG_ONEBUF, "onebuf_n64": IG_ONEBUF_N64,
             "tall512": IG_TALL512, "tall256": IG_TALL256, "small": IG_SMALL,
@@ -84,7 +86,8 @@ IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N6
             "onebuf_n64_e": IG_ONEBUF_N64_E, "classic_n64_e": IG_CLASSIC_N64_E, "db": IG_DB,
             "gbig256_32": IG_GBIG256_32, "gshort128_32": IG_GSHORT128_32,
             "gshort64_32": IG_GSHORT64_32, "s3": IG_S3, "s1": IG_S1,
-            "s7": IG_S7, "gbig224": IG_GBIG224}
+            "s7": IG_S7, "gbig224": IG_GBIG224,
+            "gbig448": IG_GBIG448}
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
 _NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
@@ -399,6 +402,8 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
                 cands += (IG_GBIG256_32,)
         if 64 < ncol <= 256 and ((M + 511) // 512) * ((ncol + 127) // 128) >= 256:
             cands += (IG_GBIG512,)
+        if 64 < ncol <= 256 and not _NO_224 and ((M + 447) // 448) * ((ncol + 127) // 128) >= 256:
+            cands += (IG_GBIG448,)
     if fast and _SK and C % 64 == 0 and ncol > 64:
         # stream-K: measured slower than the one-tile kernels on every
         # ResNet-50 bs256 geometry (per-item setup, pipeline refill and the

@@ -34,7 +34,7 @@ SHAPES = [
                         "gshort64_3", "gshort128_3", "multi2", "multi4", "small_multi4",
                         "gmulti64", "gmulti128", "gbig256", "gbig512", "generic",
                         "sk128", "g8p", "onebuf_n64_e", "classic_n64_e", "db",
-                        "gbig256_32", "gshort128_32", "gshort64_32", "gbig224"])
+                        "gbig256_32", "gshort128_32", "gshort64_32", "gbig224", "gbig448"])
 def ig_algo(request, monkeypatch):
     """Runs a test once per igemm kernel (register-staged / LDS-DMA ring /
     single LDS stage, 128- or 64-channel-wide tiles)."""
