@@ -18,8 +18,6 @@ from kf_benchmarks_amd.ops import conv_hip  # noqa: E402
 def parse_target(t):
     if t.startswith("glds/"):
         return int(t.split("/")[1]) | conv_hip._WGRAD_GLDS
-    if t.startswith("big8/"):
-        return int(t.split("/")[1]) | conv_hip._WGRAD_BIG8
     if t == "s3w":
         return conv_hip._WGRAD_S3
     return int(t)
@@ -56,8 +54,7 @@ def main():
         e.record()
         e.synchronize()
         us = s.elapsed_time(e) * 1e3 / a.iters
-        name = ("%s/%d" % (conv_hip._WGRAD_NAMES[t >> 16], t & 0xFFFF)) if t >> 16 in (1, 3) \
-            else "s3w" if t >> 16 == 2 else str(t)
+        name = ("glds/%d" % (t & 0xFFFF)) if t >> 16 == 1 else "s3w" if t >> 16 == 2 else str(t)
         print("%dx%d %d->%d k%d  %-10s %8.1f us  %6.0f TF/s" % (H, H, C, a.cout, K, name, us,
                                                                flops / us / 1e6), flush=True)
 
