@@ -131,8 +131,11 @@ __device__ __forceinline__ int xsw(int p) {
   return K == 64 ? (p >> 1) & 7 : p & 15;
 }
 
-// MASK (EPI_DGRAD): 0 none, 1 the producer BN's ReLU bit mask
-template <typename T, int K, int EPI, int MASK, int WPC>
+// MASK (EPI_DGRAD): 0 none, 1 the producer BN's ReLU bit mask.  FULL: every
+// 32-pixel tile is whole (M % 32 == 0, every ResNet batch size that is a
+// multiple of 32 / 8 / 2 at 56 / 28 / 14), so the per-element pixel masks of
+// the statistics fold away
+template <typename T, int K, int EPI, int MASK, int WPC, bool FULL = false>
 __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int nsl) {
   using C = Cfg<K, EPI, WPC>;
   constexpr int NS = C::NS, CT = C::CT, KS = C::KS, D = C::D, NST = C::NST;
@@ -164,7 +167,8 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
   const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.mask ? a.mask : a.y), (short)0, (a.mask && MASK == 1) ? a.ybytes / 16 : 0,
       0x00020000);
-  const unsigned xbn_mask = a.xbn != nullptr ? ~0u : 0u;
+  // (the bit mask always comes with the BN input: MASK 1 selects x - mean)
+  const unsigned xbn_mask = (MASK == 1 || a.xbn != nullptr) ? ~0u : 0u;
   const int ldy2 = a.Ncol * 2;
   // apply form: out (same layout as y) and its ReLU bits ([M * Ncol / 8])
   const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
@@ -354,7 +358,7 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
     }
     const int p = (t0 + t) * BMP + l32;
     const bool valid = p < a.M;
-    const unsigned vmask = valid ? ~0u : 0u;
+    const unsigned vmask = (FULL || valid) ? ~0u : 0u;
 #pragma unroll
     for (int i = 0; i < CT; ++i)
 #pragma unroll
@@ -517,8 +521,12 @@ static int s1_grid(int tiles, int nsl, int wpc) {
 
 template <typename T, int K, int EPI, int MASK, int WPC>
 static void launch_s1_k(const IgArgs& a, int tiles, int nsl, hipStream_t s) {
-  hipLaunchKernelGGL((s1::conv_s1_k<T, K, EPI, MASK, WPC>), dim3(s1_grid(tiles, nsl, WPC)),
-                     dim3(256), 0, s, a, tiles, nsl);
+  if (a.M % s1::BMP == 0)
+    hipLaunchKernelGGL((s1::conv_s1_k<T, K, EPI, MASK, WPC, true>), dim3(s1_grid(tiles, nsl, WPC)),
+                       dim3(256), 0, s, a, tiles, nsl);
+  else
+    hipLaunchKernelGGL((s1::conv_s1_k<T, K, EPI, MASK, WPC>), dim3(s1_grid(tiles, nsl, WPC)),
+                       dim3(256), 0, s, a, tiles, nsl);
 }
 
 template <typename T, int K>
