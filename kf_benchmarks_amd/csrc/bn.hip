@@ -1527,8 +1527,10 @@ KFB_API hipError_t kfb_bn_bwd(int dtype, const void* dy, const void* y, const vo
 
 // Backward of y = relu(bn(x) + bn_r(xr)) (kfb_bn_fwd_train_dual) when dy
 // arrives ReLU-masked with bn's partial sums [nslab][C] already produced by
-// the consuming conv's dgrad epilogue: bn_r's partials (one pass over dy, xr),
-// both finalizes, and ONE apply pass writing dx and dxr.
+// the consuming conv's dgrad epilogue: bn_r's partials (one pass over dy, xr,
+// unless `partials_r_ready`: the dgrad epilogue summed them too,
+// kfb_conv_s1_dgrad_dual, into pdy_r / pdyx_r), both finalizes, and ONE apply
+// pass writing dx and dxr.
 KFB_API hipError_t kfb_bn_bwd_dual(
     int dtype, const void* dy, const void* x, const void* xr, void* dx, void* dxr, long rows,
     int C, const float* gamma, const float* save_mean, const float* save_invstd, float* dgamma,
@@ -1536,17 +1538,19 @@ KFB_API hipError_t kfb_bn_bwd_dual(
     float* coefC, int accumulate, const float* gamma_r, const float* save_mean_r,
     const float* save_invstd_r, float* dgamma_r, float* dbeta_r, float* pdy_r, float* pdyx_r,
     int nslab_r, float* coefA_r, float* coefB_r, float* coefC_r, int accumulate_r,
-    hipStream_t stream) {
+    int partials_r_ready, hipStream_t stream) {
   const int V = vec_width(C);
   KFB_DISPATCH_DTYPE(dtype, T, {
     KFB_DISPATCH_VEC(V, VV, {
-      Geo g = make_geo<VV>(C);
-      const long slab_rows = (rows + nslab_r - 1) / nslab_r;
-      const size_t lds = 2 * (size_t)g.rpi * g.tpr * VV * sizeof(float);
-      hipLaunchKernelGGL((bn_partial_grad_k<T, VV, false>), dim3(nslab_r, g.nchunk),
-                         dim3(BN_THREADS), lds, stream, (const T*)dy, (const T*)nullptr,
-                         (const T*)xr, save_mean_r, rows, C, g.cw, g.tpr, g.rpi, slab_rows,
-                         pdy_r, pdyx_r);
+      if (!partials_r_ready) {
+        Geo g = make_geo<VV>(C);
+        const long slab_rows = (rows + nslab_r - 1) / nslab_r;
+        const size_t lds = 2 * (size_t)g.rpi * g.tpr * VV * sizeof(float);
+        hipLaunchKernelGGL((bn_partial_grad_k<T, VV, false>), dim3(nslab_r, g.nchunk),
+                           dim3(BN_THREADS), lds, stream, (const T*)dy, (const T*)nullptr,
+                           (const T*)xr, save_mean_r, rows, C, g.cw, g.tpr, g.rpi, slab_rows,
+                           pdy_r, pdyx_r);
+      }
       const bool fold = fold_bwd_ok(VV, nslab, C, rows);
       if (!fold)
         hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,

@@ -52,8 +52,9 @@ constexpr int LDS_CAP = 160 * 1024;  // per CU
 enum { EPI_STATS = 0, EPI_APPLY = 1, EPI_DGRAD = 2 };
 
 // per input-channel count K: WCH channels per wave (4 waves along channels);
-// WPC workgroups per CU share its LDS
-template <int K, int EPI, int WPC>
+// WPC workgroups per CU share its LDS; DU: the dual-BN data gradient (a third
+// epilogue operand, the second BN's input)
+template <int K, int EPI, int WPC, bool DU = false>
 struct Cfg {
   static constexpr int WCH = K <= 128 ? 64 : 32;
   static constexpr int NS = 4 * WCH;            // channels per workgroup
@@ -72,8 +73,10 @@ struct Cfg {
   static constexpr int YD = YB / 4096;          // per epilogue operand per wave
   static constexpr bool DG = EPI == EPI_DGRAD;
   static constexpr bool AP = EPI == EPI_APPLY;
-  static constexpr int STB = XB + (DG ? 2 * YB + MBA : AP ? YB : 0);  // ring stage
-  static constexpr int DMAS = XD + (DG ? 2 * YD + 1 : AP ? YD : 0);  // DMAs per wave per tile
+  static constexpr int NY = DU ? 3 : 2;         // dgrad operand tiles (addend, x_bn[, x_bn2])
+  static constexpr int MOFF = XB + NY * YB;      // the ReLU bits' offset in a dgrad stage
+  static constexpr int STB = XB + (DG ? NY * YB + MBA : AP ? YB : 0);  // ring stage
+  static constexpr int DMAS = XD + (DG ? NY * YD + 1 : AP ? YD : 0);  // DMAs per wave per tile
   // stores per lane per tile (16-byte y / out stores, out's ReLU-bit bytes;
   // the apply form issues all three even when y / the bits are not kept)
   static constexpr int ST = (AP ? 3 : 1) * 2 * CT;
@@ -131,13 +134,16 @@ __device__ __forceinline__ int xsw(int p) {
   return K == 64 ? (p >> 1) & 7 : p & 15;
 }
 
-// MASK (EPI_DGRAD): 0 none, 1 the producer BN's ReLU bit mask.  FULL: every
+// MASK (EPI_DGRAD): 0 none, 1 the producer BN's ReLU bit mask, 2 the bit mask
+// of a dual-BN output y = relu(bn(x) + bn2(x2)): also bn2's backward partial
+// sum y'(x2 - mean2) into IgArgs::stats2 (kfb_conv_s1_dgrad_dual).  FULL: every
 // 32-pixel tile is whole (M % 32 == 0, every ResNet batch size that is a
 // multiple of 32 / 8 / 2 at 56 / 28 / 14), so the per-element pixel masks of
 // the statistics fold away
 template <typename T, int K, int EPI, int MASK, int WPC, bool FULL = false>
 __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int nsl) {
-  using C = Cfg<K, EPI, WPC>;
+  constexpr bool DU = MASK == 2;
+  using C = Cfg<K, EPI, WPC, DU>;
   constexpr int NS = C::NS, CT = C::CT, KS = C::KS, D = C::D, NST = C::NST;
   constexpr int STB = C::STB;
   __shared__ __attribute__((aligned(16))) char ring[NST * STB];
@@ -165,10 +171,12 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
   const __amdgpu_buffer_rsrc_t xbrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.xbn ? a.xbn : a.y), (short)0, a.xbn ? a.ybytes : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.mask ? a.mask : a.y), (short)0, (a.mask && MASK == 1) ? a.ybytes / 16 : 0,
+      (void*)(a.mask ? a.mask : a.y), (short)0, (a.mask && MASK >= 1) ? a.ybytes / 16 : 0,
       0x00020000);
-  // (the bit mask always comes with the BN input: MASK 1 selects x - mean)
-  const unsigned xbn_mask = (MASK == 1 || a.xbn != nullptr) ? ~0u : 0u;
+  const __amdgpu_buffer_rsrc_t x2rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.xbn2 ? a.xbn2 : a.y), (short)0, (DU && a.xbn2) ? a.ybytes : 0, 0x00020000);
+  // (the bit mask always comes with the BN input: MASK >= 1 selects x - mean)
+  const unsigned xbn_mask = (MASK >= 1 || a.xbn != nullptr) ? ~0u : 0u;
   const int ldy2 = a.Ncol * 2;
   // apply form: out (same layout as y) and its ReLU bits ([M * Ncol / 8])
   const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
@@ -188,7 +196,7 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
   }
   // channel parameters of this lane's chunks cc = (WCH/8) w + 4 i + 2 p + hh
   // (the apply form: BN scale in pa, shift in pb)
-  float pa[CT][2][8], pb[CT][2][8];
+  float pa[CT][2][8], pb[CT][2][8], pm2[CT][2][8];
 #pragma unroll
   for (int i = 0; i < CT; ++i)
 #pragma unroll
@@ -201,6 +209,7 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
           pa[i][p][k] = a.bn_scale[ch];
           pb[i][p][k] = a.bn_shift[ch];
         } else pa[i][p][k] = a.mean ? a.mean[ch] : 0.f;
+        if constexpr (DU) pm2[i][p][k] = a.mean2[ch];
       }
   // (retire those register loads here, not at their first use inside the
   // tile loop, where the compiler's wait would also drain the ring)
@@ -216,6 +225,7 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
       for (int k = 0; k < 8; ++k) {
         asm volatile("" ::"v"(pa[i][p][k]));
         if constexpr (EPI == EPI_APPLY) asm volatile("" ::"v"(pb[i][p][k]));
+        if constexpr (DU) asm volatile("" ::"v"(pm2[i][p][k]));
       }
 
   // one tile's operands into ring stage st; the same DMA count in every
@@ -262,24 +272,25 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
             p < pend ? p * ldy2 + ns0 * 2 + (((lane % LPR) ^ (pl & 15)) << 4) : -1;
         dma16(ars, sb + C::XB + j * 1024, off);
         dma16(xbrs, sb + C::XB + C::YB + j * 1024, off);
+        if constexpr (DU) dma16(x2rs, sb + C::XB + 2 * C::YB + j * 1024, off);
       }
       // ReLU bits: NS / 8 bytes per pixel, this wave's quarter of the tile
       const int byte = 256 * wid + 4 * lane;
       const int pl = byte / (NS / 8);
       const int p = p0 + pl;
-      const int off = (MASK == 1 && byte < C::MB && p < pend)
+      const int off = (MASK >= 1 && byte < C::MB && p < pend)
                           ? p * (a.Ncol / 8) + ns0 / 8 + byte % (NS / 8) : -1;
-      dma4(mrs, sb + C::XB + 2 * C::YB + 256 * wid, off);
+      dma4(mrs, sb + C::MOFF + 256 * wid, off);
     }
   };
 
-  float s1[CT][2][8], s2[CT][2][8];
+  float s1[CT][2][8], s2[CT][2][8], s3[CT][2][8];
 #pragma unroll
   for (int i = 0; i < CT; ++i)
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { s1[i][p][k] = 0.f; s2[i][p][k] = 0.f; }
+      for (int k = 0; k < 8; ++k) { s1[i][p][k] = 0.f; s2[i][p][k] = 0.f; s3[i][p][k] = 0.f; }
   const int fx = xsw<K>(l32);
   auto keep_if = [](float x, unsigned m) { return u2f(f2u(x) & m); };
 
@@ -311,7 +322,7 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
     // asm: a plain LDS read here makes hipcc wait for every LDS-DMA in
     // flight (it cannot tell the ring stages apart), which would drain the
     // prefetch pipeline each tile
-    v8s ea[CT][2], ex[CT][2];
+    v8s ea[CT][2], ex[CT][2], ex2[CT][2];
     unsigned em[CT][2];
     if constexpr (EPI == EPI_APPLY) {
 #pragma unroll
@@ -337,14 +348,23 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
           const unsigned so = lds_addr(sb + C::XB) + l32 * C::YROW + ((cc ^ (l32 & 15)) << 4);
           asm volatile("ds_read_b128 %0, %1" : "=v"(ea[i][pp]) : "v"(so));
           asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ex[i][pp]) : "v"(so), "i"(C::YB));
-          if constexpr (MASK == 1) {
-            const unsigned mo = lds_addr(sb + C::XB + 2 * C::YB) + ((l32 * (NS / 8) + cc) & ~1);
+          if constexpr (DU)
+            asm volatile("ds_read_b128 %0, %1 offset:%2"
+                         : "=v"(ex2[i][pp]) : "v"(so), "i"(2 * C::YB));
+          if constexpr (MASK >= 1) {
+            const unsigned mo = lds_addr(sb + C::MOFF) + ((l32 * (NS / 8) + cc) & ~1);
             asm volatile("ds_read_u16 %0, %1" : "=v"(em[i][pp]) : "v"(mo));
           } else {
             em[i][pp] = 0xFFu;
           }
         }
       // (the registers pass through the wait: their uses stay behind it)
+      if constexpr (DU && CT == 1)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ex2[0][0]), "+v"(ex2[0][1]));
+      else if constexpr (DU)
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(ex2[0][0]), "+v"(ex2[0][1]), "+v"(ex2[CT - 1][0]),
+                       "+v"(ex2[CT - 1][1]));
       if constexpr (CT == 1)
         asm volatile("s_waitcnt lgkmcnt(0)"
                      : "+v"(ea[0][0]), "+v"(ea[0][1]), "+v"(ex[0][0]), "+v"(ex[0][1]),
@@ -404,7 +424,8 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
         } else {
           const Vec<T, 8> av = __builtin_bit_cast(Vec<T, 8>, ea[i][pp]);
           const Vec<T, 8> xv = __builtin_bit_cast(Vec<T, 8>, ex[i][pp]);
-          const unsigned mk = MASK == 1 ? (em[i][pp] >> (8 * (cc & 1))) & 0xFFu : 0xFFu;
+          const unsigned mk = MASK >= 1 ? (em[i][pp] >> (8 * (cc & 1))) & 0xFFu : 0xFFu;
+          const Vec<T, 8> x2v = __builtin_bit_cast(Vec<T, 8>, DU ? ex2[i][pp] : ex[i][pp]);
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             float x = v[k] + (float)av.v[k];
@@ -414,6 +435,8 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
             const float dx = (float)xv.v[k] - pa[i][pp][k];
             s2[i][pp][k] =
                 fmaf(xd, u2f((f2u(dx) & xbn_mask) | (f2u(x) & ~xbn_mask)), s2[i][pp][k]);
+            if constexpr (DU)
+              s3[i][pp][k] = fmaf(xd, (float)x2v.v[k] - pm2[i][pp][k], s3[i][pp][k]);
             ov.v[k] = (T)x;
           }
         }
@@ -442,6 +465,7 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
           for (int o = 1; o < 32; o <<= 1) {
             s1[i][pp][k] += __shfl_xor(s1[i][pp][k], o, 64);
             s2[i][pp][k] += __shfl_xor(s2[i][pp][k], o, 64);
+            if constexpr (DU) s3[i][pp][k] += __shfl_xor(s3[i][pp][k], o, 64);
           }
         }
     if (l32 == 0) {
@@ -454,6 +478,7 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
             const int ch = ns0 + 8 * ((C::WCH / 8) * wid + 4 * i + 2 * pp + hh) + k;
             atomicAdd(a.stats + (long)(b % IG_SPREAD) * a.Ncol + ch, s1[i][pp][k]);
             atomicAdd(a.stats + (long)(IG_SPREAD + b % IG_SPREAD) * a.Ncol + ch, s2[i][pp][k]);
+            if constexpr (DU) atomicAdd(a.stats2 + (long)(b % IG_SPREAD) * a.Ncol + ch, s3[i][pp][k]);
           }
     }
   }
@@ -476,6 +501,9 @@ bool conv_s1_fits(const IgArgs& a) {
            !a.mask && !a.mcoef && (a.ybytes == 0 || a.ybytes == a.outbytes);
   }
   const bool dg = a.addend || a.xbn;
+  // dual-BN partials: the bit-mask data gradient only
+  if (a.xbn2 && !(dg && a.xbn && a.mask && a.maskbits && a.stats && a.stats2 && a.mean2))
+    return false;
   return geo && !(dg && a.kshift) && !(!dg && a.mask) && !a.relu &&
          // statistics-only forward (ybytes 0: stores dropped)
          (a.ybytes > 0 || (a.stats && !dg)) &&
@@ -531,6 +559,10 @@ static void launch_s1_k(const IgArgs& a, int tiles, int nsl, hipStream_t s) {
 
 template <typename T, int K>
 static void launch_s1(const IgArgs& a, int tiles, int nsl, int epi, int mask, hipStream_t s) {
+  if (mask == 2) {  // dual-BN partials: three operand tiles per stage, one workgroup per CU
+    launch_s1_k<T, K, s1::EPI_DGRAD, 2, 1>(a, tiles, nsl, s);
+    return;
+  }
   if (s1_wpc(K, epi == s1::EPI_DGRAD) == 2) {
     if constexpr (K <= 256) {
       if (epi == s1::EPI_STATS) launch_s1_k<T, K, s1::EPI_STATS, 0, 2>(a, tiles, nsl, s);
@@ -553,7 +585,7 @@ static hipError_t launch_s1_t(const IgArgs& a, hipStream_t s) {
   const int tiles = (a.M + s1::BMP - 1) / s1::BMP;
   const int nsl = a.Ncol / s1::slice_width(a.C);
   const int epi = a.out ? s1::EPI_APPLY : (a.addend || a.xbn) ? s1::EPI_DGRAD : s1::EPI_STATS;
-  const int mask = (epi == s1::EPI_DGRAD && a.xbn && a.mask) ? 1 : 0;
+  const int mask = (epi == s1::EPI_DGRAD && a.xbn && a.mask) ? (a.xbn2 ? 2 : 1) : 0;
   switch (a.C) {
     case 64: launch_s1<T, 64>(a, tiles, nsl, epi, mask, s); break;
     case 128: launch_s1<T, 128>(a, tiles, nsl, epi, mask, s); break;
@@ -645,6 +677,52 @@ KFB_API hipError_t kfb_conv_s1_apply(int dtype, const void* x, const void* w, vo
   a.out_bits = bits;
   a.outbytes = (int)obytes;
   if (!out || !kfb::conv_s1_fits(a)) return hipErrorInvalidValue;
+  return kfb::launch_conv_s1(dtype, a, stream);
+}
+
+// Data gradient of a 1x1 stride-1 conv (dX [N,H,W,Ncol] = dY [N,H,W,K] W,
+// w = [Ncol][K]) whose input is a dual-BN block output y = relu(bn(x) +
+// bn2(x2)) (kfb_bn_fwd_train_dual): the epilogue adds `addend` (nullable),
+// applies y's ReLU bit mask and accumulates both BNs' backward partials -
+// stats [2][IG_SPREAD][Ncol] (sum y', sum y'(x - mean)) and stats2
+// [IG_SPREAD][Ncol] (sum y'(x2 - mean2)), so the dual backward
+// (kfb_bn_bwd_dual) needs no partial pass over y' and x2.  Streaming kernel
+// geometries only (kfb_conv_s1_applicable); 16-byte aligned pointers.
+KFB_API hipError_t kfb_conv_s1_dgrad_dual(int dtype, const void* dy, const void* w, void* dx,
+                                          int N, int H, int W, int K, int Ncol, float* stats,
+                                          const uint8_t* bits, const void* xbn, const float* mean,
+                                          const void* addend, const void* xbn2,
+                                          const float* mean2, float* stats2,
+                                          hipStream_t stream) {
+  if (K % 8 || Ncol % 8 || !stats || !bits || !xbn || !mean || !xbn2 || !mean2 || !stats2)
+    return hipErrorInvalidValue;
+  const long xbytes = (long)N * H * W * K * 2, wbytes = (long)Ncol * K * 2;
+  const long ybytes = (long)N * H * W * Ncol * 2;
+  if (xbytes >= (1L << 31) || ybytes >= (1L << 31)) return hipErrorInvalidValue;
+  kfb::IgArgs a{};
+  a.x = dy;
+  a.w = w;
+  a.y = dx;
+  a.N = N;
+  a.H = a.OH = a.YH = H;
+  a.W = a.OW = a.YW = W;
+  a.C = a.Ktot = K;
+  a.KH = a.KW = a.sh = a.sw = a.ys = 1;
+  a.Ncol = a.ldy = Ncol;
+  a.M = N * H * W;
+  a.stats = stats;
+  a.mask = bits;
+  a.maskbits = 1;
+  a.xbn = xbn;
+  a.mean = mean;
+  a.addend = addend;
+  a.xbytes = (int)xbytes;
+  a.wbytes = (int)wbytes;
+  a.ybytes = (int)ybytes;
+  a.xbn2 = xbn2;
+  a.mean2 = mean2;
+  a.stats2 = stats2;
+  if (!kfb::conv_s1_fits(a)) return hipErrorInvalidValue;
   return kfb::launch_conv_s1(dtype, a, stream);
 }
 

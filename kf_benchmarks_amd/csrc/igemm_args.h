@@ -119,6 +119,15 @@ struct IgArgs {
   const float* bn_shift;
   uint8_t* out_bits;
   int outbytes;  // byte size of out (< 2 GiB)
+  // Second BN of a dual-BN block output y = relu(bn(x) + bn2(x2))
+  // (kfb_bn_fwd_train_dual; conv_s1.hip EPI_DGRAD with the bit mask only):
+  // the masked y' is also the output gradient of bn2, whose backward
+  // partial stats2[slot][n] += sum y'(xbn2 - mean2) ([IG_SPREAD][Ncol]) the
+  // epilogue accumulates beside the first BN's; bn2's sum y' is the first
+  // half of `stats`.  xbn2 == null: off.
+  const void* xbn2;
+  const float* mean2;
+  float* stats2;
 };
 
 constexpr int IG_BK = 64;

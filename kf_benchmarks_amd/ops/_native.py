@@ -37,7 +37,7 @@ _SIGS = {
     "kfb_bn_fwd_train_dual": [I, P, P, P, L, I, P, P, F, F, P, P, P, P, P, P, P, P, I,
                               P, P, F, F, P, P, P, P, P, P, P, P, I, I, P, P, P, P],
     "kfb_bn_bwd_dual": [I, P, P, P, P, P, L, I, P, P, P, P, P, P, P, I, P, P, P, I,
-                        P, P, P, P, P, P, P, I, P, P, P, I, P],
+                        P, P, P, P, P, P, P, I, P, P, P, I, I, P],
     "kfb_bn_fwd_train_recompute": [I, P, P, P, P, P, I, I, I, I, I, P, P, F, F, P, P, P, P, P, P,
                                    P, P, I, I, P, I, P, P],
     "kfb_conv_s1_apply": [I, P, P, P, P, P, I, I, I, I, I, P, P, I, P, P],

@@ -30,6 +30,7 @@ N.register_optional("kfb_conv_s3_applicable", [N.I] * 12, N.c_int)
 N.register_optional("kfb_conv_s3_set_grid", [N.I], None)
 N.register_optional("kfb_conv_s1_applicable", [N.I] * 12, N.c_int)
 N.register_optional("kfb_conv_s1_set_grid", [N.I], None)
+N.register_optional("kfb_conv_s1_dgrad_dual", [N.I, N.P, N.P, N.P] + [N.I] * 5 + [N.P] * 9)
 N.register_optional("kfb_conv_s7_applicable", [N.I] * 12, N.c_int)
 N.register_optional("kfb_set_deterministic", [N.I], None)
 
@@ -454,7 +455,7 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
 
 def _igemm(x, wmat, y, N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW, ys, ldy,
            trans, stats=None, mask=None, xbn=None, mean=None, addend=None, mcoef=None,
-           bias=None, relu=False, zfill=False, defer=False):
+           bias=None, relu=False, zfill=False, defer=False, dual=None):
     """``zfill``: stride-2 scatter whose epilogue also zeroes the unsampled
     pixels of each 2x2 block (the output needs no separate zero fill).
     ``defer`` (forward statistics): where the tuned kernel is the streaming
@@ -465,6 +466,17 @@ def _igemm(x, wmat, y, N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW
     mbits = mask is not None and mask.dtype == torch.uint8
     flags = int(bool(relu)) | (2 if zfill else 0) | (4 if mbits else 0)
     algo = _igemm_algo(x, wmat, y, geo, (stats, mask, xbn, mean, addend, mcoef), (bias, flags))
+    if (dual is not None and algo == IG_S1 and mbits and xbn is not None and stats is not None
+            and mcoef is None and bias is None and not trans and ys == 1 and YH == OH
+            and getattr(stats, "_kfb_gfin", None) is None):
+        # dual-BN data gradient: both BNs' backward partials in one pass
+        xr, mean_r, parts_r = dual
+        N.call("kfb_conv_s1_dgrad_dual", N.dt(x), x.data_ptr(), wmat.data_ptr(), y.data_ptr(),
+               N_, H, W, C, ncol, stats.data_ptr(), mask.data_ptr(), xbn.data_ptr(),
+               mean.data_ptr(), N.ptr(addend), xr.data_ptr(), mean_r.data_ptr(),
+               parts_r.data_ptr(), N.stream(x.device))
+        parts_r._kfb_dual_done = True
+        return False
     deferred = (defer and algo == IG_S1 and stats is not None and xbn is None
                 and addend is None and bias is None)
     if deferred:
@@ -506,14 +518,18 @@ def is_scatter_dgrad(w_shape, stride, pads):
 
 
 def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None, addend=None, wt=None,
-               addend_inplace=False):
+               addend_inplace=False, dual=None):
     """``fuse`` = (stats, mask, xbn, mean[, mcoef]): also apply the producer
     BN's ReLU mask (read from ``mask``, or recomputed from ``xbn`` with the BN's
     [scale | shift] ``mcoef``) to dX and accumulate its backward partial sums
     (see BNLink).
     ``addend``: gradient already produced by other consumers, added to dX
     (not combined with ``fuse`` on the strided-1x1 scatter path, where
-    ``addend_inplace`` lets dX accumulate into the addend's own buffer)."""
+    ``addend_inplace`` lets dX accumulate into the addend's own buffer).
+    ``dual`` = (x_r, mean_r, parts_r): the producer is a dual-BN output
+    relu(bn(x) + bn_r(x_r)) with the ReLU bit mask; where the streaming 1x1
+    kernel runs it also sums bn_r's partial into the zeroed [32][C] parts_r
+    and marks it ``_kfb_dual_done``."""
     n, H, W, C = x_shape
     # _igemm's fused operands: stats, mask, xbn, mean, addend, mcoef
     f5 = tuple(fuse) + (None,) * (5 - len(fuse)) if fuse is not None else (None,) * 5
@@ -544,7 +560,7 @@ def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None, addend=None, wt=None,
             dx = (torch.empty if zfill else torch.zeros)((n, H, W, C), dtype=dy.dtype,
                                                          device=dy.device)
         _igemm(dy, wt, dx, n, OH, OW, cout, OH, OW, 1, 1, 1, 1, 0, 0, C, H, W, ys, C, False, *fz,
-               zfill=zfill)
+               zfill=zfill, dual=dual if ys == 1 and OH == H and OW == W else None)
         return dx
     if sh == 1 and sw == 1 and KH - 1 - pt >= 0 and KH - 1 - pb >= 0 \
             and KW - 1 - pl >= 0 and KW - 1 - pr >= 0:
@@ -1025,10 +1041,16 @@ class _Conv2d(torch.autograd.Function):
                                 mk = link.mbits if link.mbits is not None else xp
                             fuse = (parts, mk, xbn, link.mean, link.mcoef if rec else None)
                             attach_bn_grad_finalize(parts, link, cin, dy.device)
+                        dual = None
+                        if fuse is not None and link.dual is not None and not scatter \
+                                and mk is not None and mk is link.mbits:
+                            dual = link.dual + (STATS_ARENA.take(STATS_SPREAD * cin, dy.device),)
                         dx = conv_dgrad(dy, wp, xp.shape, stride, pads, fuse, addend=pend,
-                                        wt=ctx.wt, addend_inplace=owned)
+                                        wt=ctx.wt, addend_inplace=owned, dual=dual)
                         if fuse is not None:
                             link.partials = fuse[0]
+                            if dual is not None and getattr(dual[2], "_kfb_dual_done", False):
+                                link.partials_r = dual[2]
                 else:
                     sparse = (stride[0] if not padded and stride[0] == stride[1]
                               and is_scatter_dgrad(wp.shape, stride, pads) else None)

@@ -119,7 +119,7 @@ class BNLink:
     __slots__ = ("x_bn", "mean", "relu", "convs", "resid", "pools", "other", "accum", "partials",
                  "pending",
                  "pending_owned", "arrived", "mcoef", "pending_sparse", "pending_event", "mbits",
-                 "gfin")
+                 "gfin", "dual", "partials_r")
 
     def __init__(self, x_bn, mean, relu, mcoef=None):
         self.x_bn, self.mean, self.relu = x_bn, mean, relu
@@ -147,6 +147,12 @@ class BNLink:
         # last consumer's dgrad may run the BN's backward finalize in its
         # last workgroup (conv_hip.attach_bn_grad_finalize)
         self.gfin = None
+        # (x_r, mean_r) of the second BN of a dual-BN output relu(bn(x) +
+        # bn_r(x_r)): a streaming 1x1 last consumer also sums bn_r's backward
+        # partial into ``partials_r`` ([STATS_SPREAD][C], with the first half
+        # of ``partials`` as its sum of dy'); None: the dual backward's pass
+        self.dual = None
+        self.partials_r = None
 
     @property
     def fusable(self):
@@ -404,6 +410,10 @@ class DeferredBN:
 
 # the dual BN backward hands a pre-masked dy to bn_r as is (no copy)
 _DUAL_ALIAS_RES = True
+# ... and takes bn_r's backward partials from its last consumer's streaming
+# 1x1 dgrad epilogue (kfb_conv_s1_dgrad_dual) instead of a pass over dy and
+# xr (KFB_S1_DUAL=0: that pass)
+_S1_DUAL = os.environ.get("KFB_S1_DUAL", "1") != "0"
 # ... and with a pre-masked dy runs both BN backwards with one apply pass
 # (kfb_bn_bwd_dual; KFB_DUAL_BN_BWD=0: two separate BN backwards)
 _DUAL_BWD_FUSE = os.environ.get("KFB_DUAL_BN_BWD", "1") != "0"
@@ -443,6 +453,8 @@ class _BatchNormTrainDual(torch.autograd.Function):
         ctx.params = (gamma, beta, gamma_r, beta_r)
         link = BNLink(x, st[0], relu)
         link.mbits = mbits
+        if _S1_DUAL and _DUAL_BWD_FUSE and relu and mbits is not None:
+            link.dual = (xr, st_r[0])
         y._kfb_bn_link = link
         ctx.link = link
         return y
@@ -460,10 +472,19 @@ class _BatchNormTrainDual(torch.autograd.Function):
             parts = link.partials
             link.partials = None
             nslab = parts.numel() // (2 * C)
-            nslab_r = N.query("kfb_bn_num_slabs", rows, C)
-            ws = torch.empty((2 * nslab_r * C + 6 * C,), dtype=torch.float32, device=dev)
-            pr = ws[:2 * nslab_r * C]
-            coef = ws[2 * nslab_r * C:].view(6, C)
+            pr_ready = link.partials_r is not None
+            if pr_ready:
+                # bn_r's partials from the dgrad epilogue: sum dy' (shared) | sum dy'(xr - mean_r)
+                nslab_r = nslab
+                pdy_r, pdyx_r = parts[:nslab * C].data_ptr(), link.partials_r.data_ptr()
+                link.partials_r = None
+                coef = torch.empty((6, C), dtype=torch.float32, device=dev)
+            else:
+                nslab_r = N.query("kfb_bn_num_slabs", rows, C)
+                ws = torch.empty((2 * nslab_r * C + 6 * C,), dtype=torch.float32, device=dev)
+                pr = ws[:2 * nslab_r * C]
+                pdy_r, pdyx_r = pr[:nslab_r * C].data_ptr(), pr[nslab_r * C:].data_ptr()
+                coef = ws[2 * nslab_r * C:].view(6, C)
             t, tr = _bn_grad_targets(gp, bp, C, dev), _bn_grad_targets(gp_r, bp_r, C, dev)
             dx, dxr = torch.empty_like(x), torch.empty_like(xr)
             N.call("kfb_bn_bwd_dual", N.dt(x), dy.data_ptr(), x.data_ptr(), xr.data_ptr(),
@@ -471,10 +492,9 @@ class _BatchNormTrainDual(torch.autograd.Function):
                    st[1].data_ptr(), t[1], t[2], parts[:nslab * C].data_ptr(),
                    parts[nslab * C:].data_ptr(), nslab, coef[0].data_ptr(),
                    coef[1].data_ptr(), coef[2].data_ptr(), int(t[0]), N.ptr(gamma_r),
-                   st_r[0].data_ptr(), st_r[1].data_ptr(), tr[1], tr[2],
-                   pr[:nslab_r * C].data_ptr(), pr[nslab_r * C:].data_ptr(), nslab_r,
+                   st_r[0].data_ptr(), st_r[1].data_ptr(), tr[1], tr[2], pdy_r, pdyx_r, nslab_r,
                    coef[3].data_ptr(), coef[4].data_ptr(), coef[5].data_ptr(), int(tr[0]),
-                   N.stream(dev))
+                   int(pr_ready), N.stream(dev))
             dg, db = _bn_grad_result(t[0], t[3], gp, bp)
             dg_r, db_r = _bn_grad_result(tr[0], tr[3], gp_r, bp_r)
             return (dx, dg, db, dxr, dg_r, db_r) + (None,) * 11

@@ -203,7 +203,7 @@ def test_bn_bwd_dual_fold_matches_finalize_launch(cuda, fold_bwd, rows, C):
                coef[0].data_ptr(), coef[1].data_ptr(), coef[2].data_ptr(), 0,
                t["gamma_r"].data_ptr(), t["mean_r"].data_ptr(), t["invstd_r"].data_ptr(),
                dg[2].data_ptr(), dg[3].data_ptr(), pr[0].data_ptr(), pr[1].data_ptr(), nr,
-               coef[3].data_ptr(), coef[4].data_ptr(), coef[5].data_ptr(), 0, N.stream(cuda))
+               coef[3].data_ptr(), coef[4].data_ptr(), coef[5].data_ptr(), 0, 0, N.stream(cuda))
         torch.cuda.synchronize()
         out[on] = (dx, dxr, coef, dg)
     for k, (a, b) in enumerate(zip(out[False], out[True])):

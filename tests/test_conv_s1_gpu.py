@@ -102,6 +102,47 @@ def test_s1_dgrad_fused_epilogue(s1, cuda, shape, mask_src, with_addend, grid, K
     torch.testing.assert_close(p[1], s2_, rtol=1e-2, atol=tol)
 
 
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+@pytest.mark.parametrize("with_addend", [False, True])
+@pytest.mark.parametrize("grid", [0, 5])
+@pytest.mark.parametrize("K", KS)
+def test_s1_dgrad_dual_partials(s1, cuda, shape, with_addend, grid, K):
+    """The dual-BN form (kfb_conv_s1_dgrad_dual): dX bitwise the single-BN
+    kernel's, the first BN's partials equal in total, and the second BN's
+    sum dy'(x2 - mean2) against an fp32 reference."""
+    N.load().kfb_conv_s1_set_grid(grid)
+    n, H, W = shape
+    C = 4 * K
+    g = torch.Generator().manual_seed(9)
+    dt = torch.bfloat16
+    w = (torch.randn(K, 1, 1, C, generator=g) / K ** 0.5).to(dt).to(cuda)
+    dy = torch.randn(n, H, W, K, generator=g).to(dt).to(cuda)
+    xb = torch.randn(n, H, W, C, generator=g).to(dt).to(cuda)
+    x2 = (torch.randn(n, H, W, C, generator=g) * 2 + 0.5).to(dt).to(cuda)
+    mean = torch.randn(C, generator=g).to(cuda)
+    mean2 = torch.randn(C, generator=g).to(cuda)
+    bits = _bits(torch.randn(n, H, W, C, generator=g)).to(cuda)
+    add = torch.randn(n, H, W, C, generator=g).to(dt).to(cuda) if with_addend else None
+    parts = conv_hip.stats_buffer(C, cuda).zero_()
+    ref = conv_hip.conv_dgrad(dy, w, xb.shape, (1, 1), (0, 0, 0, 0), (parts, bits, xb, mean),
+                              addend=add)
+    parts_d = conv_hip.stats_buffer(C, cuda).zero_()
+    parts_r = torch.zeros(conv_hip.STATS_SPREAD * C, device=cuda)
+    dx = conv_hip.conv_dgrad(dy, w, xb.shape, (1, 1), (0, 0, 0, 0), (parts_d, bits, xb, mean),
+                             addend=add, dual=(x2, mean2, parts_r))
+    assert getattr(parts_r, "_kfb_dual_done", False)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, ref)
+    p = parts.view(2, conv_hip.STATS_SPREAD, C).sum(1).cpu()
+    pd = parts_d.view(2, conv_hip.STATS_SPREAD, C).sum(1).cpu()
+    o = dx.float().cpu()
+    d2 = x2.float().cpu() - mean2.cpu()
+    tol = 4e-3 * (o.abs() * (1 + d2.abs())).sum((0, 1, 2)).max().item()
+    torch.testing.assert_close(pd, p, rtol=1e-3, atol=tol)
+    pr = parts_r.view(conv_hip.STATS_SPREAD, C).sum(0).cpu()
+    torch.testing.assert_close(pr, (o * d2).sum((0, 1, 2)), rtol=1e-2, atol=tol)
+
+
 def test_s1_finalizes_bn(s1, cuda, monkeypatch):
     # (forward finalize tails: KFB_BN_FIN=1; the default "grad" mode keeps
     # them for the data-gradient kernels only)

@@ -165,6 +165,31 @@ def test_deferred_shortcut_bn_network(cuda, monkeypatch):
     assert cos[len(cos) // 2] > 0.99 and cos[0] > 0.9, (cos[0], cos[len(cos) // 2])
 
 
+def test_s1_dual_partials_network(cuda, monkeypatch):
+    """ResNet-50's four projection-block outputs relu(bn(x) + bn_r(x_r)):
+    with the streaming 1x1 kernel forced, the next block's conv-a data
+    gradient sums bn_r's backward partials too (kfb_conv_s1_dgrad_dual, so
+    the dual backward skips its partial pass); the gradients agree with the
+    partial-pass path (forward identical; bf16 backward by cosine, as above)."""
+    from kf_benchmarks_amd.models import builder
+    from kf_benchmarks_amd.ops import _native as N, conv_hip, nn as F
+    monkeypatch.setattr(builder, "_DEFER_BN", True)
+    monkeypatch.setattr(conv_hip, "_IG_FORCE", conv_hip.IG_S1)
+    names = []
+    orig = N.call
+    monkeypatch.setattr(N, "call", lambda name, *a: names.append(name) or orig(name, *a))
+    loss_d, dual = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
+    assert names.count("kfb_conv_s1_dgrad_dual") == 4, names.count("kfb_conv_s1_dgrad_dual")
+    monkeypatch.setattr(F, "_S1_DUAL", False)
+    names.clear()
+    loss_p, sep = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
+    assert "kfb_conv_s1_dgrad_dual" not in names
+    assert loss_d == loss_p
+    cos = sorted(_cos(dual[k], ref) for k, ref in sep.items() if ref.norm() > 0)
+    print("dual-partial vs partial-pass cosines: min %.4f median %.4f" % (cos[0], cos[len(cos) // 2]))
+    assert cos[len(cos) // 2] > 0.99 and cos[0] > 0.9, (cos[0], cos[len(cos) // 2])
+
+
 def _kernel_names(fn):
     from torch.profiler import ProfilerActivity, profile
     with profile(activities=[ProfilerActivity.CUDA]) as prof:
