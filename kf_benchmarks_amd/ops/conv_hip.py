@@ -485,9 +485,12 @@ def _igemm(x, wmat, y, N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW
     return deferred
 
 
-# KFB_BN_RECOMPUTE=0: a residual BN's producing streaming 1x1 conv stores its
-# output (the BN apply reads it back) instead of recomputing it in the apply
-_RECOMPUTE = os.environ.get("KFB_BN_RECOMPUTE", "0") == "1"
+# KFB_BN_RECOMPUTE=1: a residual BN's producing streaming 1x1 conv sums the
+# statistics without storing its output; the BN's apply pass recomputes it
+# (profiles/r12_bn_recompute.txt).  =<K> (K > 1): only for convs with at most
+# K input channels; 0: off (the conv stores y, the BN apply reads it back).
+_RC = os.environ.get("KFB_BN_RECOMPUTE", "0")
+_RECOMPUTE = True if _RC == "1" else (int(_RC) if _RC.isdigit() and int(_RC) > 1 else False)
 
 
 def conv_fwd(x, wl, stride, pads, stats=None, bias=None, relu=False):
@@ -505,7 +508,8 @@ def conv_fwd(x, wl, stride, pads, stats=None, bias=None, relu=False):
     # a stats buffer marked by its consuming residual BN (models/builder.py):
     # the streaming 1x1 kernel leaves y unwritten; the BN's apply pass
     # recomputes it from (x, wl) and stores it (nn._BatchNormTrain)
-    defer = _RECOMPUTE and stats is not None and getattr(stats, "_kfb_defer", False)
+    defer = (bool(_RECOMPUTE) and stats is not None and getattr(stats, "_kfb_defer", False)
+             and (_RECOMPUTE is True or C <= _RECOMPUTE))
     if _igemm(x, wl, y, n, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, cout, OH, OW, 1, cout, False,
               stats, bias=bias, relu=relu, defer=defer):
         y._kfb_recompute = (x, wl)
