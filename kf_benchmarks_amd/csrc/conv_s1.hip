@@ -82,7 +82,16 @@ struct Cfg {
   static constexpr int ST = (AP ? 3 : 1) * 2 * CT;
   // ring stages: what LDS holds, at most 7, and few enough that the counted
   // wait below fits vmcnt (< 64)
-  static constexpr int NST0 = LDS_CAP / WPC / STB;
+  // y staged through LDS (STAGED): each wave writes its 32-pixel x WCH-channel
+  // tile into a private region, reads it back as whole 128-byte (WCH 64) /
+  // 64-byte (WCH 32) row pieces and stores those: the per-lane 16-byte pieces
+  // of 32 pixel rows per store instruction cap the write stream at ~3.1 TB/s,
+  // full-line pieces reach ~5.5 (scripts/probes/s1store.hip); where the
+  // staging area leaves at least two ring stages (not the apply form)
+  static constexpr int STG = 4 * BMP * WCH * 2;
+  static constexpr int NSTS = (LDS_CAP / WPC - STG) / STB;
+  static constexpr bool STAGED = !AP && NSTS >= 2;
+  static constexpr int NST0 = STAGED ? NSTS : LDS_CAP / WPC / STB;
   static constexpr int NSTV = (63 + DMAS) / (ST + DMAS) + 1;
   static constexpr int NST = NST0 < NSTV ? (NST0 > 7 ? 7 : NST0) : (NSTV > 7 ? 7 : NSTV);
   static constexpr int D = NST - 1;             // prefetch distance (tiles)
@@ -146,11 +155,17 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
   using C = Cfg<K, EPI, WPC, DU>;
   constexpr int NS = C::NS, CT = C::CT, KS = C::KS, D = C::D, NST = C::NST;
   constexpr int STB = C::STB;
-  __shared__ __attribute__((aligned(16))) char ring[NST * STB];
+  __shared__ __attribute__((aligned(16))) char ring[NST * STB + (C::STAGED ? C::STG : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hh = lane >> 5, l32 = lane & 31;
+  // this wave's staging rows (STAGED): WCH * 2 bytes per pixel, 16-byte chunk
+  // j of row r at j ^ sgz(r) (8 lanes of one ds_write / ds_read phase hit 8
+  // distinct 16-byte bank groups)
+  constexpr int SROW = C::WCH * 2;
+  const unsigned stg = lds_addr(ring + NST * STB) + (unsigned)(wid * BMP * SROW);
+  auto sgz = [](int r) { return SROW == 128 ? (r & 7) : ((r >> 1) & 3); };
   // XCD-aware placement: r runs over the workgroups of one XCD first
   // (dispatch round-robins blockIdx over the 8 XCDs); the nsl slices of a
   // pixel group are consecutive r
@@ -440,9 +455,42 @@ __global__ void __launch_bounds__(256, WPC) conv_s1_k(IgArgs a, int tiles, int n
             ov.v[k] = (T)x;
           }
         }
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u_t, ov), yrs,
-                                               valid ? p * ldy2 + (ns0 + 8 * cc) * 2 : -1, 0, 0);
+        if constexpr (C::STAGED) {
+          const int j = 4 * i + 2 * pp + hh;  // chunk within the wave's columns
+          const unsigned sa = stg + l32 * SROW + ((j ^ sgz(l32)) << 4);
+          asm volatile("ds_write_b128 %0, %1" ::"v"(sa), "v"(__builtin_bit_cast(v4u_t, ov)));
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u_t, ov), yrs,
+                                                 valid ? p * ldy2 + (ns0 + 8 * cc) * 2 : -1, 0,
+                                                 0);
+        }
       }
+    if constexpr (C::STAGED) {
+      // whole row pieces back out: WCH / 16 stores per lane, as many as the
+      // per-lane pieces they replace (the counted ring wait is unchanged)
+      constexpr int LPR = SROW / 16;  // lanes per row piece
+      constexpr int NQ = C::WCH / 16;
+      v4u_t sv[NQ];
+      asm volatile("s_waitcnt lgkmcnt(0)");
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int r = q * (64 / LPR) + lane / LPR, c = lane % LPR;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(sv[q]) : "v"(stg + r * SROW + ((c ^ sgz(r)) << 4)));
+      }
+      if constexpr (NQ == 2)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(sv[0]), "+v"(sv[NQ - 1]));
+      else
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(sv[0]), "+v"(sv[1]), "+v"(sv[2]), "+v"(sv[NQ - 1]));
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int r = q * (64 / LPR) + lane / LPR, c = lane % LPR;
+        const int pr = (t0 + t) * BMP + r;
+        __builtin_amdgcn_raw_buffer_store_b128(
+            sv[q], yrs, (FULL || pr < a.M) ? pr * ldy2 + (ns0 + C::WCH * wid + 8 * c) * 2 : -1, 0,
+            0);
+      }
+    }
     // tile t+1's operands landed for every wave (issued in iteration t+1-D;
     // after them: the stores of tiles t+1-D .. t and the DMAs of tiles
     // t+2 .. t+D) and every wave is done reading stage st
