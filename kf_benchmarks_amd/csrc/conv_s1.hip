@@ -565,13 +565,16 @@ static int g_s1_grid_force = 0;  // test hook: workgroups per launch (0 = one pe
 // workgroups per CU: 2 where two fit (LDS ring and registers: the variants
 // below 256 VGPR + AGPR at one workgroup per CU) - the second workgroup's
 // waves hide the first's MFMA / LDS / epilogue latencies, which one wave per
-// SIMD leaves exposed; KFB_S1_WPC=1 forces one
+// SIMD leaves exposed - except the K = 64 data gradient: at one workgroup
+// its output stores go through the LDS staging (no room beside two rings),
+// 291 -> 279 us at 56x56, ResNet-50 -0.06 ms/step on 4 interleaved pairs
+// (profiles/r12_s1_staged_stores.txt); KFB_S1_WPC=1 forces one
 static int s1_wpc(int K, bool dg) {
   static const int force = [] {
     const char* e = getenv("KFB_S1_WPC");
     return e ? atoi(e) : 0;
   }();
-  const bool two = dg ? (K == 64 || K == 256) : (K <= 256);
+  const bool two = dg ? K == 256 : K <= 256;
   return (force == 1 || !two) ? 1 : 2;
 }
 
