@@ -665,16 +665,22 @@ struct BnFoldArgs {
   int accumulate;
 };
 
-template <typename T, bool DRES, bool DUAL>
+// FR (with DUAL): the second BN's finalize is folded too, from fr.pdyx and
+// the first BN's sum dy' (the dual dgrad epilogue's partials,
+// kfb_conv_s1_dgrad_dual); else its coefficients Ar / Br / Cr come from a
+// finalize launch.
+template <typename T, bool DRES, bool DUAL, bool FR = false>
 __global__ void __launch_bounds__(256)
 bn_bwd_apply_fold_k(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ xr,
                     T* __restrict__ dx, T* __restrict__ dres, long rows, int C, BnFoldArgs f,
                     const float* __restrict__ Ar, const float* __restrict__ Br,
-                    const float* __restrict__ Cr) {
+                    const float* __restrict__ Cr, BnFoldArgs fr) {
   static_assert(FOLD_Y == 16 && FS_SLOTS == 2 * FOLD_Y, "fold order of fold_slabs");
-  __shared__ double red[2][FOLD_Y][FS_C];
-  __shared__ double tot[2][FS_C];
-  __shared__ float cf[3][FS_C];
+  static_assert(!FR || DUAL, "second-BN fold needs the dual form");
+  constexpr int NA = FR ? 3 : 2;  // slot arrays: sum dy', sum dy'(x - mean)[, sum dy'(xr - mean_r)]
+  __shared__ double red[NA][FOLD_Y][FS_C];
+  __shared__ double tot[NA][FS_C];
+  __shared__ float cf[FR ? 6 : 3][FS_C];
   const int t = threadIdx.x;
   const int ns = C / FS_C;
   const int slice = blockIdx.x % ns, rb = blockIdx.x / ns, nrb = gridDim.x / ns;
@@ -710,8 +716,21 @@ bn_bwd_apply_fold_k(const T* __restrict__ dy, const T* __restrict__ x, const T* 
 #pragma unroll
     for (int k = 0; k < 8; ++k) red[arr][l][8 * q + k] = (double)sv[k];
   }
+  if constexpr (FR) {
+    if (t < 128) {  // the second BN's sum dy'(xr - mean_r) slots, same order
+      const int l = (t >> 3) & 15;
+      const float* p = fr.pdyx + c0 + 8 * q;
+      const float4* lo = (const float4*)(p + (long)l * C);
+      const float4* hi = (const float4*)(p + (long)(l + FOLD_Y) * C);
+      const float4 a0 = lo[0], a1 = lo[1], b0 = hi[0], b1 = hi[1];
+      const float sv[8] = {a0.x + b0.x, a0.y + b0.y, a0.z + b0.z, a0.w + b0.w,
+                           a1.x + b1.x, a1.y + b1.y, a1.z + b1.z, a1.w + b1.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[NA - 1][l][8 * q + k] = (double)sv[k];
+    }
+  }
   __syncthreads();
-  if (t < 2 * FS_C) {
+  if (t < NA * FS_C) {
     const int arr = t >> 6, cc = t & 63;
     double sum = 0.0;
 #pragma unroll
@@ -739,6 +758,26 @@ bn_bwd_apply_fold_k(const T* __restrict__ dy, const T* __restrict__ x, const T* 
       f.coefB[ch] = bv;
       f.coefC[ch] = cv;
     }
+  } else if (FR && t < 2 * FS_C) {
+    // the second BN: its sum dy' is the first's (one ReLU-masked dy')
+    const int u = t - FS_C, ch = c0 + u;
+    const double s1 = tot[0][u], s2 = tot[NA - 1][u];
+    const float is = fr.invstd[ch];
+    const float g = fr.gamma ? fr.gamma[ch] : 1.f;
+    const double n = (double)rows;
+    const double A = (double)g * is;
+    const double B = -A * (double)is * (double)is * s2 / n;
+    const float av = (float)A, bv = (float)B, cv = (float)(-A * s1 / n - (double)fr.mean[ch] * B);
+    cf[FR ? 3 : 0][u] = av;
+    cf[FR ? 4 : 0][u] = bv;
+    cf[FR ? 5 : 0][u] = cv;
+    if (rb == 0) {
+      if (fr.dgamma) fr.dgamma[ch] = (fr.accumulate ? fr.dgamma[ch] : 0.f) + (float)(s2 * is);
+      if (fr.dbeta) fr.dbeta[ch] = (fr.accumulate ? fr.dbeta[ch] : 0.f) + (float)s1;
+      fr.coefA[ch] = av;
+      fr.coefB[ch] = bv;
+      fr.coefC[ch] = cv;
+    }
   }
   __syncthreads();
   float a[8], b[8], cc[8], ar[8], br[8], crr[8];
@@ -748,7 +787,14 @@ bn_bwd_apply_fold_k(const T* __restrict__ dy, const T* __restrict__ x, const T* 
     b[k] = cf[1][8 * q + k];
     cc[k] = cf[2][8 * q + k];
   }
-  if constexpr (DUAL) {
+  if constexpr (FR) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      ar[k] = cf[FR ? 3 : 0][8 * q + k];
+      br[k] = cf[FR ? 4 : 0][8 * q + k];
+      crr[k] = cf[FR ? 5 : 0][8 * q + k];
+    }
+  } else if constexpr (DUAL) {
     coef_load<8>(Ar, c, ar);
     coef_load<8>(Br, c, br);
     coef_load<8>(Cr, c, crr);
@@ -1287,6 +1333,17 @@ static bool fold_bwd_ok(int V, int nslab, int C, long rows) {
          (g_fold_bwd == 2 || rows * C * 2 <= max_bytes);
 }
 
+// KFB_BN_FOLD_R=0: the dual backward's second BN keeps its finalize launch
+// even when its partials could be folded (A/B switch)
+static int g_fold_r = -1;  // -1: from the environment
+static bool fold_r_on() {
+  if (g_fold_r < 0) {
+    const char* e = getenv("KFB_BN_FOLD_R");
+    g_fold_r = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return g_fold_r != 0;
+}
+
 static int fold_bwd_grid(long rows, int C) {
   static const long target = [] {
     const char* e = getenv("KFB_BN_FOLD_WGS");
@@ -1341,6 +1398,11 @@ hipError_t bn_finalize_grad_launch(const float* slots, int C, long rows, const f
 }
 }  // namespace kfb
 
+
+// test / A/B hook: 1 folds the dual backward's second-BN finalize into the
+// apply pass when its partials allow it (KFB_BN_FOLD_R)
+KFB_API void kfb_bn_set_fold_r(int on) { kfb::g_fold_r = on ? 1 : 0; }
+KFB_API int kfb_bn_get_fold_r() { return kfb::fold_r_on() ? 1 : 0; }
 
 // test / A/B hook: 1 folds the backward gradient finalize into the apply pass
 KFB_API void kfb_bn_set_fold_bwd(int mode) { g_fold_bwd = mode; }
@@ -1500,12 +1562,12 @@ KFB_API hipError_t kfb_bn_bwd(int dtype, const void* dy, const void* y, const vo
           hipLaunchKernelGGL((bn_bwd_apply_fold_k<T, true, false>), gf, dim3(256), 0, stream,
                              (const T*)dy, (const T*)x, (const T*)nullptr, (T*)dx, (T*)dres, rows,
                              C, f, (const float*)nullptr, (const float*)nullptr,
-                             (const float*)nullptr);
+                             (const float*)nullptr, BnFoldArgs{});
         else
           hipLaunchKernelGGL((bn_bwd_apply_fold_k<T, false, false>), gf, dim3(256), 0, stream,
                              (const T*)dy, (const T*)x, (const T*)nullptr, (T*)dx, (T*)nullptr,
                              rows, C, f, (const float*)nullptr, (const float*)nullptr,
-                             (const float*)nullptr);
+                             (const float*)nullptr, BnFoldArgs{});
         return hipGetLastError();
       }
       if (have_partials != 2)  // 2: the producing dgrad's last workgroup finalized (BnGFin)
@@ -1556,15 +1618,31 @@ KFB_API hipError_t kfb_bn_bwd_dual(
         hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,
                            pdy, pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta,
                            coefA, coefB, coefC, accumulate, 0);
-      hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,
-                         pdy_r, pdyx_r, nslab_r, C, rows, gamma_r, save_mean_r, save_invstd_r,
-                         dgamma_r, dbeta_r, coefA_r, coefB_r, coefC_r, accumulate_r, 0);
+      // both finalizes folded into the apply when the second BN's partials
+      // came from the dgrad epilogue in the first BN's slot layout
+      const bool fold_r = fold && partials_r_ready && nslab_r == FS_SLOTS && pdy_r == pdy &&
+                          fold_r_on();
+      if (!fold_r)
+        hipLaunchKernelGGL(bn_finalize_grad_k, dim3(ceil_div(C, 64)), dim3(64, FOLD_Y), 0, stream,
+                           pdy_r, pdyx_r, nslab_r, C, rows, gamma_r, save_mean_r, save_invstd_r,
+                           dgamma_r, dbeta_r, coefA_r, coefB_r, coefC_r, accumulate_r, 0);
       if (fold) {
         const BnFoldArgs f{pdy, pdyx, gamma, save_mean, save_invstd, dgamma, dbeta,
                            coefA, coefB, coefC, accumulate};
-        hipLaunchKernelGGL((bn_bwd_apply_fold_k<T, true, true>), dim3(fold_bwd_grid(rows, C)),
-                           dim3(256), 0, stream, (const T*)dy, (const T*)x, (const T*)xr, (T*)dx,
-                           (T*)dxr, rows, C, f, coefA_r, coefB_r, coefC_r);
+        if (fold_r) {
+          const BnFoldArgs fr{pdy_r, pdyx_r, gamma_r, save_mean_r, save_invstd_r, dgamma_r,
+                              dbeta_r, coefA_r, coefB_r, coefC_r, accumulate_r};
+          hipLaunchKernelGGL((bn_bwd_apply_fold_k<T, true, true, true>),
+                             dim3(fold_bwd_grid(rows, C)), dim3(256), 0, stream, (const T*)dy,
+                             (const T*)x, (const T*)xr, (T*)dx, (T*)dxr, rows, C, f,
+                             (const float*)nullptr, (const float*)nullptr,
+                             (const float*)nullptr, fr);
+        } else {
+          hipLaunchKernelGGL((bn_bwd_apply_fold_k<T, true, true>), dim3(fold_bwd_grid(rows, C)),
+                             dim3(256), 0, stream, (const T*)dy, (const T*)x, (const T*)xr,
+                             (T*)dx, (T*)dxr, rows, C, f, coefA_r, coefB_r, coefC_r,
+                             BnFoldArgs{});
+        }
         return hipGetLastError();
       }
       const long nvec = rows * C / VV;

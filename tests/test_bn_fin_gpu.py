@@ -208,3 +208,47 @@ def test_bn_bwd_dual_fold_matches_finalize_launch(cuda, fold_bwd, rows, C):
         out[on] = (dx, dxr, coef, dg)
     for k, (a, b) in enumerate(zip(out[False], out[True])):
         assert torch.equal(a, b), k
+
+
+@pytest.mark.parametrize("rows,C", [(3136, 256), (12544, 2048), (50176, 64)])
+def test_bn_bwd_dual_fold_r_matches_finalize_launch(cuda, fold_bwd, rows, C):
+    """kfb_bn_bwd_dual with the second BN's partials from the dual dgrad
+    epilogue (partials_r_ready: its sum dy' is the first BN's slot array):
+    folding that BN's finalize into the apply pass as well equals its
+    finalize launch, bitwise (coefficients, dgamma / dbeta, dx, dxr)."""
+    from kf_benchmarks_amd.ops import _native as N
+    lib = N.load()
+    t = _bwd_case(cuda, rows, C, 23 + C)
+    pr = (torch.randn(32, C, generator=torch.Generator().manual_seed(C)) * 50).to(cuda)
+    prev = lib.kfb_bn_get_fold_r()
+    fold_bwd(True)
+    out = {}
+    try:
+        for on in (False, True):
+            lib.kfb_bn_set_fold_r(1 if on else 0)
+            dx, dxr = torch.empty_like(t["dy"]), torch.empty_like(t["dy"])
+            coef = torch.full((6, C), float("nan"), device=cuda)
+            dg = torch.zeros(4, C, device=cuda)
+            parts = t["parts"].clone()
+            N.call("kfb_bn_bwd_dual", N.dt(t["dy"]), t["dy"].data_ptr(), t["x"].data_ptr(),
+                   t["xr"].data_ptr(), dx.data_ptr(), dxr.data_ptr(), rows, C,
+                   t["gamma"].data_ptr(), t["mean"].data_ptr(), t["invstd"].data_ptr(),
+                   dg[0].data_ptr(), dg[1].data_ptr(), parts[0].data_ptr(), parts[1].data_ptr(),
+                   32, coef[0].data_ptr(), coef[1].data_ptr(), coef[2].data_ptr(), 0,
+                   t["gamma_r"].data_ptr(), t["mean_r"].data_ptr(), t["invstd_r"].data_ptr(),
+                   dg[2].data_ptr(), dg[3].data_ptr(), parts[0].data_ptr(), pr.data_ptr(), 32,
+                   coef[3].data_ptr(), coef[4].data_ptr(), coef[5].data_ptr(), 0, 1,
+                   N.stream(cuda))
+            torch.cuda.synchronize()
+            out[on] = (dx, dxr, coef, dg)
+    finally:
+        lib.kfb_bn_set_fold_r(prev)
+    for k, (a, b) in enumerate(zip(out[False], out[True])):
+        assert torch.equal(a, b), k
+    # the second BN against the formula on the host
+    s1, s2 = t["parts"][0].double().sum(0), pr.double().sum(0)
+    A = t["gamma_r"].double() * t["invstd_r"].double()
+    B = -A * t["invstd_r"].double() ** 2 * s2 / rows
+    Cc = -A * s1 / rows - t["mean_r"].double() * B
+    ref = t["dy"].double() * A + t["xr"].double() * B + Cc
+    torch.testing.assert_close(out[True][1].double(), ref, rtol=2e-2, atol=2e-2)
