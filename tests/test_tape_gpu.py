@@ -443,3 +443,45 @@ def test_real_data_tape_oracle_catches_a_stale_batch(cuda, tmp_path, monkeypatch
     assert t["digests"][3:] == e1["digests"][2:5], (t["digests"], e1["digests"])
     bad = _same(e1, t)
     assert "weights" in bad and any("moving" in k for k in bad), bad
+
+
+def _run_exact_r50_s1(tape, steps=6, bs=2):
+    """ResNet-50 at 64x64 with the streaming 1x1 kernel forced wherever it
+    applies: its staged output stores, the dual-BN partials of the
+    projection-block outputs and the folded dual backward all run; at batch 2
+    every statistics slot takes one atomic add (bitwise repeatable)."""
+    from kf_benchmarks_amd import params as P
+    from kf_benchmarks_amd.benchmark import BenchmarkCNN
+    p = P.make_params(model="resnet50", batch_size=bs, num_gpus=1, use_bf16=True,
+                      optimizer="momentum", data_format="NHWC", variable_update="kungfu",
+                      launch_tape=tape, init_learning_rate=0.01, display_every=10 ** 9,
+                      loss_type_to_report="base_loss")
+    b = BenchmarkCNN(p)
+    b.model.image_size = 64
+    b.build()
+    losses = []
+    for _ in range(steps):
+        loss, _ = b.train_step(need_loss=True)
+        losses.append(float(loss))
+    torch.cuda.synchronize()
+    w = b.flat.flat.detach().float().cpu().clone()
+    bufs, slots = _state(b)
+    tp = getattr(b, "_tape", None)
+    return dict(losses=losses, w=w, bufs=bufs, slots=slots,
+                replays=tp.replays if tp is not None else 0)
+
+
+def test_resnet50_s1_dual_tape_bitwise(cuda, _deterministic, monkeypatch):
+    from kf_benchmarks_amd.ops import _native as N
+    from kf_benchmarks_amd.ops import conv_hip
+    monkeypatch.setattr(conv_hip, "_IG_FORCE", conv_hip.IG_S1)
+    names = []
+    orig = N.call
+    monkeypatch.setattr(N, "call", lambda name, *a: names.append(name) or orig(name, *a))
+    e1 = _run_exact_r50_s1(False)
+    assert names.count("kfb_conv_s1_dgrad_dual") >= 4
+    e2 = _run_exact_r50_s1(False)
+    assert not _same(e1, e2), "eager run is not bitwise repeatable: %s" % _same(e1, e2)[:8]
+    t = _run_exact_r50_s1(True)
+    assert t["replays"] == 3
+    assert not _same(e1, t), _same(e1, t)[:8]
