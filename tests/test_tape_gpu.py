@@ -34,29 +34,23 @@ def _run(model, optimizer, tape, steps=6, bs=8, **kw):
     return losses, w, replays
 
 
-@pytest.mark.parametrize("model,optimizer", [("resnet50", "momentum"), ("alexnet", "adam"),
-                                             ("googlenet", "sgd")])
-def test_tape_matches_eager(cuda, model, optimizer):
-    le, we, _ = _run(model, optimizer, False)
-    le2, we2, _ = _run(model, optimizer, False)
-    lt, wt, replays = _run(model, optimizer, True)
-    assert replays == 3  # 2 warm eager steps, 1 recorded, 3 replayed
-    # BN statistics use float atomics, so two eager runs already differ in
-    # the last bits; the taped run must stay as close to eager as eager is
-    # to itself (plus a small floor)
-    # (run 1 also autotunes; runs 2 and 3 reuse its kernel choices)
-    # (bf16 training is chaotic: the eager-vs-eager spread can be small at one
-    # step and large at the next, so the bound uses the largest spread seen so
-    # far and a 2.5% floor; a replay bug shows up as a systematic, not a
-    # rounding-sized, departure)
-    spread = 0.0
-    for a, a2, b in zip(le, le2, lt):
-        spread = max(spread, abs(a - a2))
-        assert abs(a2 - b) <= max(4 * spread, 2.5e-2 * max(1.0, abs(a2))), (le, le2, lt)
-    ref = (we - we2).abs().max().item()
-    assert (wt - we2).abs().max().item() <= max(4 * ref, 1e-3), ref
+@pytest.mark.parametrize("model,optimizer,size,bs", [("resnet50", "momentum", 64, 2),
+                                                     ("alexnet", "adam", None, 4),
+                                                     ("googlenet", "sgd", None, 2)])
+def test_tape_matches_eager(cuda, _deterministic, model, optimizer, size, bs):
+    """A recorded-and-replayed step trains bit for bit like the eager step in
+    a repeatable configuration (one atomic add per statistics slot, the
+    fixed-order weight-gradient folds): losses, fp32 weights, buffers and
+    optimizer slots (Adam's step-dependent rate and dropout's per-step seeds
+    are per-step tape arguments)."""
+    e1 = _run_exact_model(model, optimizer, False, size, bs)
+    e2 = _run_exact_model(model, optimizer, False, size, bs)
+    assert not _same(e1, e2), "eager run is not bitwise repeatable: %s" % _same(e1, e2)[:8]
+    t = _run_exact_model(model, optimizer, True, size, bs)
+    assert t["replays"] == 3  # 2 warm eager steps, 1 recorded, 3 replayed
+    assert not _same(e1, t), _same(e1, t)[:8]
     # the replayed steps changed the weights (they ran at all)
-    assert lt[-1] != lt[2]
+    assert t["losses"][-1] != t["losses"][2]
 
 
 def test_tape_records_gradient_sums_natively(cuda):
@@ -92,32 +86,28 @@ def test_tape_refuses_torch_ops_in_step(cuda):
 
 
 @pytest.mark.parametrize("optimizer", ["momentum", "adam"])
-def test_early_update_matches_late(cuda, optimizer, monkeypatch):
+def test_early_update_matches_late(cuda, _deterministic, optimizer, monkeypatch):
     """The update of every variable but the stem's runs on the weight-gradient
-    stream at the top of the stem's backward (BenchmarkCNN._early_update);
-    the trajectory must match the all-after-backward update up to the
-    run-to-run spread of the BN-statistics atomics, eager and taped."""
+    stream at the top of the stem's backward (BenchmarkCNN._early_update,
+    opt-in); in the bitwise-repeatable ResNet-50 configuration (64x64, batch
+    2) the trajectory equals the all-after-backward update bit for bit, eager
+    and taped (losses, fp32 weights, BN buffers, optimizer slots)."""
     from kf_benchmarks_amd.benchmark import BenchmarkCNN
     monkeypatch.setattr(BenchmarkCNN, "_EARLY_UPDATE", False)
-    le, we, _ = _run("resnet50", optimizer, False)
-    le2, we2, _ = _run("resnet50", optimizer, False)
+    late = _run_exact_r50(False, optimizer)
+    late2 = _run_exact_r50(False, optimizer)
+    assert not _same(late, late2), "eager run is not bitwise repeatable: %s" % _same(late, late2)[:8]
     monkeypatch.setattr(BenchmarkCNN, "_EARLY_UPDATE", True)
     calls = []
     orig = BenchmarkCNN._early_update
     monkeypatch.setattr(BenchmarkCNN, "_early_update",
                         lambda self, *a: calls.append(1) or orig(self, *a))
-    lx, wx, _ = _run("resnet50", optimizer, False)
+    early = _run_exact_r50(False, optimizer)
     assert len(calls) == 6
-    lt, wt, replays = _run("resnet50", optimizer, True)
-    assert replays == 3
-    spread = 0.0
-    for a, a2, b, c in zip(le, le2, lx, lt):
-        spread = max(spread, abs(a - a2))
-        bound = max(4 * spread, 2.5e-2 * max(1.0, abs(a2)))
-        assert abs(a2 - b) <= bound and abs(a2 - c) <= bound, (le, le2, lx, lt)
-    ref = (we - we2).abs().max().item()
-    assert (wx - we2).abs().max().item() <= max(4 * ref, 1e-3), ref
-    assert (wt - we2).abs().max().item() <= max(4 * ref, 1e-3), ref
+    assert not _same(late, early), _same(late, early)[:8]
+    taped = _run_exact_r50(True, optimizer)
+    assert taped["replays"] == 3
+    assert not _same(late, taped), _same(late, taped)[:8]
 
 
 # ---------------------------------------------------------------------------
@@ -445,15 +435,38 @@ def test_real_data_tape_oracle_catches_a_stale_batch(cuda, tmp_path, monkeypatch
     assert "weights" in bad and any("moving" in k for k in bad), bad
 
 
-def _run_exact_r50_s1(tape, steps=6, bs=2):
-    """ResNet-50 at 64x64 with the streaming 1x1 kernel forced wherever it
-    applies: its staged output stores, the dual-BN partials of the
-    projection-block outputs and the folded dual backward all run; at batch 2
-    every statistics slot takes one atomic add (bitwise repeatable)."""
+def _run_exact_model(model, optimizer, tape, size, bs, steps=6):
+    from kf_benchmarks_amd import params as P
+    from kf_benchmarks_amd.benchmark import BenchmarkCNN
+    p = P.make_params(model=model, batch_size=bs, num_gpus=1, use_bf16=True,
+                      optimizer=optimizer, data_format="NHWC", variable_update="kungfu",
+                      launch_tape=tape, init_learning_rate=0.002, display_every=10 ** 9,
+                      loss_type_to_report="base_loss")
+    b = BenchmarkCNN(p)
+    if size:
+        b.model.image_size = size
+    b.build()
+    losses = []
+    for _ in range(steps):
+        loss, _ = b.train_step(need_loss=True)
+        losses.append(float(loss))
+    torch.cuda.synchronize()
+    w = b.flat.flat.detach().float().cpu().clone()
+    bufs, slots = _state(b)
+    tp = getattr(b, "_tape", None)
+    return dict(losses=losses, w=w, bufs=bufs, slots=slots,
+                replays=tp.replays if tp is not None else 0)
+
+
+def _run_exact_r50(tape, optimizer="momentum", steps=6, bs=2):
+    """ResNet-50 at 64x64, batch 2: every statistics slot takes one atomic add,
+    so with the fixed-order weight-gradient folds (_deterministic) an eager
+    step is bitwise repeatable (the kernel choices are the process's first
+    autotune's)."""
     from kf_benchmarks_amd import params as P
     from kf_benchmarks_amd.benchmark import BenchmarkCNN
     p = P.make_params(model="resnet50", batch_size=bs, num_gpus=1, use_bf16=True,
-                      optimizer="momentum", data_format="NHWC", variable_update="kungfu",
+                      optimizer=optimizer, data_format="NHWC", variable_update="kungfu",
                       launch_tape=tape, init_learning_rate=0.01, display_every=10 ** 9,
                       loss_type_to_report="base_loss")
     b = BenchmarkCNN(p)
@@ -472,16 +485,19 @@ def _run_exact_r50_s1(tape, steps=6, bs=2):
 
 
 def test_resnet50_s1_dual_tape_bitwise(cuda, _deterministic, monkeypatch):
+    """ResNet-50 with the streaming 1x1 kernel forced wherever it applies: its
+    staged output stores, the dual-BN partials of the projection-block outputs
+    and the folded dual backward all run; taped == eager, bitwise."""
     from kf_benchmarks_amd.ops import _native as N
     from kf_benchmarks_amd.ops import conv_hip
     monkeypatch.setattr(conv_hip, "_IG_FORCE", conv_hip.IG_S1)
     names = []
     orig = N.call
     monkeypatch.setattr(N, "call", lambda name, *a: names.append(name) or orig(name, *a))
-    e1 = _run_exact_r50_s1(False)
+    e1 = _run_exact_r50(False)
     assert names.count("kfb_conv_s1_dgrad_dual") >= 4
-    e2 = _run_exact_r50_s1(False)
+    e2 = _run_exact_r50(False)
     assert not _same(e1, e2), "eager run is not bitwise repeatable: %s" % _same(e1, e2)[:8]
-    t = _run_exact_r50_s1(True)
+    t = _run_exact_r50(True)
     assert t["replays"] == 3
     assert not _same(e1, t), _same(e1, t)[:8]
