@@ -468,7 +468,8 @@ def _igemm(x, wmat, y, N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW
     algo = _igemm_algo(x, wmat, y, geo, (stats, mask, xbn, mean, addend, mcoef), (bias, flags))
     if (dual is not None and algo == IG_S1 and mbits and xbn is not None and stats is not None
             and mcoef is None and bias is None and not trans and ys == 1 and YH == OH
-            and getattr(stats, "_kfb_gfin", None) is None):
+            and getattr(stats, "_kfb_gfin", None) is None
+            and 2 * max(x.numel(), y.numel()) < (1 << 31)):  # (the kernel's buffer ranges)
         # dual-BN data gradient: both BNs' backward partials in one pass
         xr, mean_r, parts_r = dual
         N.call("kfb_conv_s1_dgrad_dual", N.dt(x), x.data_ptr(), wmat.data_ptr(), y.data_ptr(),
