@@ -370,6 +370,18 @@ class ModuleNetwork(nn.Module):
     def forward(self, inputs, phase_train=True):
         return self.body(inputs, phase_train)
 
+    # launch-tape hooks (Network's): the module models (DeepSpeech2, NCF)
+    # draw no per-step dropout / drop-path values, so a replayed step has no
+    # per-step network arguments
+    def tape_begin_recording(self):
+        pass
+
+    def tape_end_recording(self):
+        pass
+
+    def tape_dropout_values(self):
+        return {}
+
     def ordered_layers(self):
         return [m for m in self.body.modules()
                 if any(True for _ in m.parameters(recurse=False))

@@ -501,3 +501,29 @@ def test_resnet50_s1_dual_tape_bitwise(cuda, _deterministic, monkeypatch):
     t = _run_exact_r50(True)
     assert t["replays"] == 3
     assert not _same(e1, t), _same(e1, t)[:8]
+
+
+@pytest.mark.parametrize("model,data_name,bs,kw", [
+    ("deepspeech2", "librispeech", 2, {}),
+    ("ncf", None, 256, dict(optimizer="adam", use_bf16=False))])
+def test_module_models_with_launch_tape(cuda, monkeypatch, model, data_name, bs, kw):
+    """The module models (DeepSpeech2, NCF: ModuleNetwork) accept the launch
+    tape's network hooks; their steps hold torch device ops (the per-step
+    synthetic inputs), so the recording is refused and the run stays eager
+    with the reason recorded (it used to raise AttributeError)."""
+    from kf_benchmarks_amd import params as P
+    from kf_benchmarks_amd.benchmark import BenchmarkCNN
+    monkeypatch.delenv("KFB_TAPE_STRICT", raising=False)
+    args = dict(model=model, batch_size=bs, num_gpus=1, use_bf16=True, optimizer="momentum",
+                data_format="NHWC", variable_update="kungfu", launch_tape=True,
+                display_every=10 ** 9)
+    if data_name:
+        args["data_name"] = data_name
+    args.update(kw)
+    b = BenchmarkCNN(P.make_params(**args))
+    b.build()
+    losses = [float(b.train_step(need_loss=True)[0]) for _ in range(4)]
+    torch.cuda.synchronize()
+    assert all(l == l for l in losses), losses  # finite
+    assert getattr(b, "_tape", None) is None
+    assert "recording failed" in (getattr(b, "_tape_reason", "") or "")
