@@ -418,6 +418,10 @@ class BenchmarkCNN:
                 if k:
                     mask[off:off + n] = 1.0
             self.l2_mask = mask
+            if self.device_type == "cuda" and self.flat.master is None:
+                # the update kernel applies the decay on the masked elements
+                # itself (no torch op in the step: the launch tape can record it)
+                self.optimizer.decay_mask = mask.to(torch.uint8)
         self.comm_selftest = self._validate_comm()
         self.input = self._make_input()
         self._tape = None
@@ -528,7 +532,7 @@ class BenchmarkCNN:
                 return "host-side input pipeline"
         if self.enable_auto_loss_scale:
             return "dynamic loss scaling reads the gradients on the host"
-        if p.staged_vars or self.l2_mask is not None:
+        if p.staged_vars or (self.l2_mask is not None and self.optimizer.decay_mask is None):
             return "staged variables / masked L2 use torch ops in the update"
         return None
 
@@ -653,7 +657,7 @@ class BenchmarkCNN:
                 wd = (p.weight_decay or 0.0) * self._l2_multiplier()
                 if self.strategy.update_is_empty:
                     wd = 0.0
-                if wd and self.l2_mask is not None:
+                if wd and self.l2_mask is not None and self.optimizer.decay_mask is None:
                     # model-specific L2 subset (custom_l2_loss, e.g. SSD without
                     # batch-norm variables): add wd * w on the masked elements
                     # before the gradient scale the optimizer applies

@@ -202,6 +202,17 @@ synthetic_labels_k(int* __restrict__ y, long n, int maxval, uint32_t seed) {
   }
 }
 
+// Uniform [lo, lo + scale) (SSD's synthetic images, boxes, classes and box
+// counts); ``salt`` separates the tensors drawn with one per-step seed.
+template <typename T>
+__global__ void __launch_bounds__(256)
+synthetic_uniform_k(T* __restrict__ x, long n, float lo, float scale, uint32_t seed,
+                    uint32_t salt) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    x[i] = from_f32<T>(lo + scale * u01(seed, (uint64_t)i, salt));
+}
+
 template <typename T, int V, bool RELU>
 __global__ void __launch_bounds__(256)
 add_k(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ y, long nvec) {
@@ -423,6 +434,15 @@ KFB_API hipError_t kfb_synthetic_images(int dtype, void* x, long n, float mean, 
 KFB_API hipError_t kfb_synthetic_labels(int* y, long n, int maxval, uint32_t seed,
                                         hipStream_t stream) {
   hipLaunchKernelGGL(synthetic_labels_k, dim3(egrid(n)), dim3(256), 0, stream, y, n, maxval, seed);
+  return hipGetLastError();
+}
+
+KFB_API hipError_t kfb_synthetic_uniform(int dtype, void* x, long n, float lo, float scale,
+                                         uint32_t seed, uint32_t salt, hipStream_t stream) {
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((synthetic_uniform_k<T>), dim3(egrid(n)), dim3(256), 0, stream, (T*)x, n,
+                       lo, scale, seed, salt);
+  });
   return hipGetLastError();
 }
 

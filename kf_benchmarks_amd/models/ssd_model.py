@@ -115,12 +115,14 @@ class SSD300Model(model_lib.CNNModel):
                 [bs]]
 
     def get_synthetic_inputs(self, input_name, nclass, device="cpu", seed=0):
-        g = torch.Generator(device="cpu").manual_seed(seed)
+        """Uniform images, boxes and class ids, 1..10 boxes per image, drawn on
+        the device (one launch each, re-sampled per step inside a launch tape)."""
         shapes = self.get_input_shapes("train")
-        images = torch.rand(shapes[0], generator=g).to(device, self.data_type)
-        boxes = torch.rand(shapes[1], generator=g).to(device)
-        classes = torch.rand(shapes[2], generator=g).to(device)
-        nboxes = (torch.rand(shapes[3], generator=g) * 9 + 1).to(device)
+        u = F_ops.synthetic_uniform
+        images = u(shapes[0], self.data_type, device, seed, 11)
+        boxes = u(shapes[1], torch.float32, device, seed, 12)
+        classes = u(shapes[2], torch.float32, device, seed, 13)
+        nboxes = u(shapes[3], torch.float32, device, seed, 14, 1.0, 10.0)
         return images, boxes, classes, nboxes
 
     # -------------------------------------------------------------- loss

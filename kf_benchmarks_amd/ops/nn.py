@@ -1475,6 +1475,20 @@ def augment_u8(images, params, dtype):
     return out
 
 
+def synthetic_uniform(shape, dtype, device, seed: int, salt: int, lo=0.0, hi=1.0):
+    """U[lo, hi) of ``shape`` made on the device (csrc/elementwise.hip): one
+    launch, the per-step seed a launch-tape argument, ``salt`` a per-tensor
+    constant.  CPU: torch's generator seeded with seed + salt."""
+    if torch.device(device).type != "cuda":
+        g = torch.Generator().manual_seed(seed + salt)
+        return (torch.rand(shape, generator=g) * (hi - lo) + lo).to(dtype)
+    x = torch.empty(shape, dtype=dtype, device=device)
+    N.call("kfb_synthetic_uniform", N.dt(x), x.data_ptr(), x.numel(), float(lo),
+           float(hi - lo), N.dyn("input_seed", seed & 0xFFFFFFFF), int(salt) & 0xFFFFFFFF,
+           N.stream(x.device))
+    return x
+
+
 def synthetic_labels(n, nclass, device, seed: int):
     # Reference: uniform in [0, nclass-1) (tcb/models/model.py:232-236).
     maxval = max(nclass - 1, 1)

@@ -151,6 +151,9 @@ class FusedOptimizer:
         self.adam = (adam_beta1, adam_beta2, adam_epsilon)
         self.nesterov = nesterov
         self.t = 0
+        # uint8 per flat element: weight decay applies only where it is
+        # nonzero (a model's L2 subset, e.g. SSD without batch-norm variables)
+        self.decay_mask = None
         dev, n = flat.device, flat.numel
         self.s1 = torch.zeros(n, dtype=torch.float32, device=dev) if kind != "sgd" else None
         self.s2 = None
@@ -223,7 +226,7 @@ class FusedOptimizer:
             if hi_ > lo:
                 N.call("kfb_opt_step", _KINDS[self.kind], at(w), at(g),
                        at(self.s1), at(self.s2), at(lp),
-                       N.dt(lp) if lp is not None else 0, None, hi_ - lo, N.dyn("lr", float(lr)),
+                       N.dt(lp) if lp is not None else 0, at(self.decay_mask), hi_ - lo, N.dyn("lr", float(lr)),
                        float(grad_scale), float(weight_decay), clipv, float(mom), float(b1),
                        float(b2), float(eps), N.dyn("lr_t", float(lr_t)), int(self.nesterov),
                        N.ptr(msrc),
@@ -257,7 +260,8 @@ class FusedOptimizer:
         w = self.flat.update_target
         gk = g * grad_scale
         if wd:
-            gk = gk + wd * w
+            dm = self.decay_mask
+            gk = gk + (wd * w if dm is None else wd * w * dm.to(w.device, w.dtype))
         if clip > 0:
             gk = gk.clamp(-clip, clip)
         if self.kind == "sgd":

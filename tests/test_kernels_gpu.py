@@ -197,6 +197,40 @@ def test_fused_optimizer(cuda, kind):
     torch.testing.assert_close(b[1], a[1], rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("kind", ["momentum", "adam"])
+def test_fused_optimizer_decay_mask(cuda, kind):
+    """Weight decay on a subset of the variables (a model's L2 filter, e.g.
+    SSD without batch-norm variables) applied inside the update kernel from a
+    uint8 per-element mask vs the CPU formula; masked-off elements get none."""
+    from kf_benchmarks_amd import optim
+    from kf_benchmarks_amd.models.model import Network
+    from kf_benchmarks_amd.models.resnet_model import create_resnet20_cifar_model
+
+    res = {}
+    for dev in ("cpu", cuda):
+        model = create_resnet20_cifar_model(None)
+        net = Network(model, 11, dev, torch.float32, seed=5)
+        flat = optim.FlatParams(net, torch.bfloat16)
+        opt = optim.FusedOptimizer(flat, kind)
+        mask = torch.zeros(flat.numel, dtype=torch.uint8)
+        for n, _, o, k in flat.segments():
+            if "batchnorm" not in n:
+                mask[o:o + k] = 1
+        assert 0 < int(mask.sum()) < flat.numel
+        opt.decay_mask = mask.to(flat.flat.device)
+        for i in range(3):
+            flat.grad.zero_()
+            opt.step(0.01, grad_scale=0.5, weight_decay=0.3)
+        res[str(dev)] = (flat.flat.cpu().clone(), mask)
+    (a, mask), (b, _) = res["cpu"], res[str(cuda)]
+    torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)
+    net = Network(create_resnet20_cifar_model(None), 11, "cpu", torch.float32, seed=5)
+    w0 = optim.FlatParams(net, torch.bfloat16).flat
+    off = mask == 0
+    assert torch.equal(b[off], w0[off])  # zero gradient, no decay: unchanged
+    assert not torch.equal(b[~off], w0[~off])
+
+
 @pytest.mark.parametrize("ok", [None, 1, 0])
 def test_fused_optimizer_model_averaging(cuda, ok):
     """The averaging folded into the optimizer pass (PairAveraging / SMA):
