@@ -194,10 +194,11 @@ synthetic_images8_k(T* __restrict__ x, unsigned n8, float mean, float std, uint3
 }
 
 __global__ void __launch_bounds__(256)
-synthetic_labels_k(int* __restrict__ y, long n, int maxval, uint32_t seed) {
+synthetic_labels_k(int* __restrict__ y, long n, int maxval, uint32_t seed, uint32_t salt) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long)gridDim.x * blockDim.x) {
-    int v = (int)(u01(seed, (uint64_t)i, 99u) * (float)maxval);
+    // (24-bit uniforms: maxval above 2^24 leaves some values unreachable)
+    int v = (int)(u01(seed, (uint64_t)i, salt) * (float)maxval);
     y[i] = v >= maxval ? maxval - 1 : v;
   }
 }
@@ -211,6 +212,28 @@ synthetic_uniform_k(T* __restrict__ x, long n, float lo, float scale, uint32_t s
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long)gridDim.x * blockDim.x)
     x[i] = from_f32<T>(lo + scale * u01(seed, (uint64_t)i, salt));
+}
+
+// y = a * b and its backward (da = dy * b, db = dy * a) in one pass: NCF's
+// GMF product of the user and item embeddings.
+template <typename T>
+__global__ void __launch_bounds__(256)
+mul_k(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ y, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    y[i] = from_f32<T>(to_f32(a[i]) * to_f32(b[i]));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+mul_bwd_k(const T* __restrict__ a, const T* __restrict__ b, const T* __restrict__ dy,
+          T* __restrict__ da, T* __restrict__ db, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    const float g = to_f32(dy[i]);
+    da[i] = from_f32<T>(g * to_f32(b[i]));
+    db[i] = from_f32<T>(g * to_f32(a[i]));
+  }
 }
 
 template <typename T, int V, bool RELU>
@@ -433,7 +456,17 @@ KFB_API hipError_t kfb_synthetic_images(int dtype, void* x, long n, float mean, 
 
 KFB_API hipError_t kfb_synthetic_labels(int* y, long n, int maxval, uint32_t seed,
                                         hipStream_t stream) {
-  hipLaunchKernelGGL(synthetic_labels_k, dim3(egrid(n)), dim3(256), 0, stream, y, n, maxval, seed);
+  hipLaunchKernelGGL(synthetic_labels_k, dim3(egrid(n)), dim3(256), 0, stream, y, n, maxval, seed,
+                     99u);
+  return hipGetLastError();
+}
+
+// Integers uniform in [0, maxval); ``salt`` separates tensors drawn with one
+// per-step seed (NCF's users, items and labels).
+KFB_API hipError_t kfb_synthetic_ints(int* y, long n, int maxval, uint32_t seed, uint32_t salt,
+                                      hipStream_t stream) {
+  hipLaunchKernelGGL(synthetic_labels_k, dim3(egrid(n)), dim3(256), 0, stream, y, n, maxval, seed,
+                     salt);
   return hipGetLastError();
 }
 
@@ -442,6 +475,24 @@ KFB_API hipError_t kfb_synthetic_uniform(int dtype, void* x, long n, float lo, f
   KFB_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL((synthetic_uniform_k<T>), dim3(egrid(n)), dim3(256), 0, stream, (T*)x, n,
                        lo, scale, seed, salt);
+  });
+  return hipGetLastError();
+}
+
+KFB_API hipError_t kfb_mul(int dtype, const void* a, const void* b, void* y, long n,
+                           hipStream_t stream) {
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((mul_k<T>), dim3(egrid(n)), dim3(256), 0, stream, (const T*)a,
+                       (const T*)b, (T*)y, n);
+  });
+  return hipGetLastError();
+}
+
+KFB_API hipError_t kfb_mul_bwd(int dtype, const void* a, const void* b, const void* dy, void* da,
+                               void* db, long n, hipStream_t stream) {
+  KFB_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((mul_bwd_k<T>), dim3(egrid(n)), dim3(256), 0, stream, (const T*)a,
+                       (const T*)b, (const T*)dy, (T*)da, (T*)db, n);
   });
   return hipGetLastError();
 }

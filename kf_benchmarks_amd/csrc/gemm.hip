@@ -136,7 +136,8 @@ template <typename T>
 __global__ void __launch_bounds__(256) slab_reduce_k(const float* __restrict__ slab, int nsplit,
                                                      int M, int N, int ldslab,
                                                      const float* __restrict__ bias, int relu,
-                                                     T* __restrict__ out, int ldc) {
+                                                     T* __restrict__ out, int ldc,
+                                                     int accumulate) {
   const int q4 = ldslab >> 2;
   const long i = blockIdx.x * 256L + threadIdx.x;
   if (i >= (long)M * q4) return;
@@ -146,14 +147,15 @@ __global__ void __launch_bounds__(256) slab_reduce_k(const float* __restrict__ s
   const float* s = slab + (long)m * ldslab + n;
   v4f acc = *(const v4f*)s;
   for (int k = 1; k < nsplit; ++k) acc += *(const v4f*)(s + k * plane);
+  T* c = out + (long)m * ldc + n;
   float o[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     float t = acc[r];
     if (bias && n + r < N) t += bias[n + r];
+    if (accumulate && n + r < N) t += (float)c[r];  // (wgrad: fp32 C += result)
     o[r] = relu ? fmaxf(t, 0.f) : t;
   }
-  T* c = out + (long)m * ldc + n;
   if (n + 3 < N && (ldc & 3) == 0) {
     Vec<T, 4> w;
 #pragma unroll
@@ -198,7 +200,7 @@ static hipError_t run(int mode, const Args& a0, int nsplit, hipStream_t s) {
   const bool pv = a.ldp % E == 0 && (pks ? a.M : a.K) % E == 0;
   const bool qv = a.ldq % E == 0 && (qks ? a.N : a.K) % E == 0;
   const int tiles = ((a.M + TILE - 1) / TILE) * ((a.N + TILE - 1) / TILE);
-  if (mode == 2) {  // wgrad: fp32 output, no split
+  if (mode == 2 && nsplit <= 1) {  // wgrad: fp32 output
     a.kper = a.K;
     launch<T, true, true, OUT_F32>(a, pv, qv, tiles, s);
     return hipGetLastError();
@@ -213,13 +215,19 @@ static hipError_t run(int mode, const Args& a0, int nsplit, hipStream_t s) {
   a.kper = ((nk + nsplit - 1) / nsplit) * Tr<T>::BK;
   nsplit = (a.K + a.kper - 1) / a.kper;
   if (mode == 0) launch<T, false, true, OUT_SLAB>(a, pv, qv, tiles * nsplit, s);
-  else launch<T, false, false, OUT_SLAB>(a, pv, qv, tiles * nsplit, s);
+  else if (mode == 1) launch<T, false, false, OUT_SLAB>(a, pv, qv, tiles * nsplit, s);
+  else launch<T, true, true, OUT_SLAB>(a, pv, qv, tiles * nsplit, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const long work = (long)a.M * (a.ldslab / 4);
-  hipLaunchKernelGGL(slab_reduce_k<T>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s,
-                     (const float*)a.slab, nsplit, a.M, a.N, a.ldslab, a.bias, a.relu, (T*)a.c,
-                     a.ldc);
+  if (mode == 2)  // the split wgrad's fp32 (+=) output
+    hipLaunchKernelGGL(slab_reduce_k<float>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
+                       s, (const float*)a.slab, nsplit, a.M, a.N, a.ldslab, nullptr, 0,
+                       (float*)a.c, a.ldc, a.accumulate);
+  else
+    hipLaunchKernelGGL(slab_reduce_k<T>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s,
+                       (const float*)a.slab, nsplit, a.M, a.N, a.ldslab, a.bias, a.relu, (T*)a.c,
+                       a.ldc, 0);
   return hipGetLastError();
 }
 
@@ -228,7 +236,7 @@ static hipError_t run(int mode, const Args& a0, int nsplit, hipStream_t s) {
 
 using namespace kfb;
 
-// Split count kfb_gemm will use for a forward / dgrad GEMM of this shape
+// Split count kfb_gemm will use for a GEMM of this output shape and reduction
 // (the caller sizes the slab workspace: nsplit * M * round_up(N, 4) floats).
 KFB_API int kfb_gemm_splits(int dtype, int M, int N, int K) {
   return dtype == F32 ? gm::choose_split<float>(M, N, K) : gm::choose_split<bf16>(M, N, K);
@@ -237,8 +245,10 @@ KFB_API int kfb_gemm_splits(int dtype, int M, int N, int K) {
 // mode 0: forward  C[M][N] = P[M][K] . Q[K][N]           (P KC, Q KS)  -> T
 // mode 1: dgrad    C[M][N] = P[M][K] . Q[N][K]^T         (P KC, Q KC)  -> T
 // mode 2: wgrad    C[M][N] = P[K][M]^T . Q[K][N]          (P KS, Q KS)  -> fp32 (+=)
-// T outputs get bias[n] (nullable) and an optional ReLU; modes 0/1 split K
-// into `slab` (>= nsplit * M * round_up(N, 4) floats) when nsplit > 1.
+// T outputs get bias[n] (nullable) and an optional ReLU; K is split into
+// `slab` (>= nsplit * M * round_up(N, 4) floats) when nsplit > 1 (wgrad: a
+// small output over a long batch, e.g. NCF's 256 x 256 layers at batch 2048,
+// which unsplit runs 4 workgroups down the whole batch).
 KFB_API hipError_t kfb_gemm(int dtype, int mode, const void* p, int ldp, const void* q, int ldq,
                             int M, int N, int K, void* c, int ldc, const float* bias, int relu,
                             int accumulate, float* slab, long slab_elems, int nsplit,
@@ -250,7 +260,7 @@ KFB_API hipError_t kfb_gemm(int dtype, int mode, const void* p, int ldp, const v
   const long qel = mode == 1 ? (long)N * ldq : (long)K * ldq;
   if (pel * esz >= (1L << 31) || qel * esz >= (1L << 31)) return hipErrorInvalidValue;
   const int ldslab = (N + 3) / 4 * 4;
-  if (mode != 2 && nsplit > 1 && (slab == nullptr || (long)nsplit * M * ldslab > slab_elems))
+  if (nsplit > 1 && (slab == nullptr || (long)nsplit * M * ldslab > slab_elems))
     return hipErrorInvalidValue;
   gm::Args a{p, q, M, N, K, ldp, ldq, (int)(pel * esz), (int)(qel * esz), c, ldc, slab,
              ldslab, K, bias, relu, accumulate};

@@ -65,7 +65,7 @@ class NeuMF(nn.Module):
         # kernels (ops.nn); the tables are [rows, dim] like the official model
         users, items = inputs[0], inputs[1]
         emb = F_ops.embedding
-        gmf = emb(users, self.mf_user.weight) * emb(items, self.mf_item.weight)
+        gmf = F_ops.mul(emb(users, self.mf_user.weight), emb(items, self.mf_item.weight))
         h = F_ops.concat_channels([emb(users, self.mlp_user.weight),
                                    emb(items, self.mlp_item.weight)])
         for lin in self.mlp:
@@ -95,17 +95,20 @@ class NcfModel(model_lib.ModuleModel):
         return [torch.int32, torch.int32, torch.int32]
 
     def get_synthetic_inputs(self, input_name, nclass, device="cpu", seed=0):
-        g = torch.Generator(device="cpu").manual_seed(seed)
-        bs = self.batch_size
-        users = torch.randint(0, NUM_USERS_20M, (bs,), generator=g, dtype=torch.int32)
-        items = torch.randint(0, NUM_ITEMS_20M, (bs,), generator=g, dtype=torch.int32)
-        labels = torch.randint(0, 2, (bs,), generator=g, dtype=torch.int32)
-        return users.to(device), items.to(device), labels.to(device)
+        # drawn on the device (one launch each; a launch tape re-samples them)
+        bs, ints = self.batch_size, F_ops.synthetic_ints
+        return (ints(bs, NUM_USERS_20M, device, seed, 21), ints(bs, NUM_ITEMS_20M, device, seed, 22),
+                ints(bs, 2, device, seed, 23))
 
     def loss_function(self, inputs, build_network_result):
         logits = build_network_result.logits.float()
-        # softmax over [1, logit] (kept as the official model does)
-        logits = F_ops.concat_channels([torch.ones_like(logits), logits])
+        # softmax over [1, logit] (kept as the official model does); the ones
+        # column is a persistent tensor (no fill kernel inside the step)
+        ones = getattr(self, "_ones", None)
+        if ones is None or ones.shape != logits.shape or ones.device != logits.device \
+                or ones.dtype != logits.dtype:
+            ones = self._ones = torch.ones_like(logits)
+        logits = F_ops.concat_channels([ones, logits])
         return F_ops.softmax_cross_entropy(logits, inputs[2])
 
     def accuracy_function(self, inputs, logits):

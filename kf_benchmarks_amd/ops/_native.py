@@ -94,6 +94,9 @@ _SIGS = {
     "kfb_augment_blocks": [],
     "kfb_synthetic_labels": [P, L, I, c_uint32, P],
     "kfb_synthetic_uniform": [I, P, L, F, F, c_uint32, c_uint32, P],
+    "kfb_synthetic_ints": [P, L, I, c_uint32, c_uint32, P],
+    "kfb_mul": [I, P, P, P, L, P],
+    "kfb_mul_bwd": [I, P, P, P, P, P, L, P],
     "kfb_add": [I, P, P, P, L, I, P],
     "kfb_gemm": [I, I, P, I, P, I, I, I, I, P, I, P, I, I, P, L, I, P],
     "kfb_gemm_splits": [I, I, I, I],

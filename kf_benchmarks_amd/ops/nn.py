@@ -699,6 +699,36 @@ def fanout(x, k: int, force: bool = False):
     return list(_FanOut.apply(x, k))
 
 
+class _Mul(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        a, b = a.contiguous(), b.contiguous()
+        y = torch.empty_like(a)
+        N.call("kfb_mul", N.dt(a), a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(),
+               N.stream(a.device))
+        ctx.save_for_backward(a, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        a, b = ctx.saved_tensors
+        dy = dy.contiguous()
+        da, db = torch.empty_like(a), torch.empty_like(b)
+        N.call("kfb_mul_bwd", N.dt(a), a.data_ptr(), b.data_ptr(), dy.data_ptr(), da.data_ptr(),
+               db.data_ptr(), a.numel(), N.stream(a.device))
+        return da, db
+
+
+def mul(a, b):
+    """Elementwise a * b of one shape and dtype (GPU: native forward and
+    backward, so a launch tape can record it)."""
+    if not _on_gpu(a):
+        return a * b
+    if a.shape != b.shape or a.dtype != b.dtype:
+        raise ValueError("mul: operands must have one shape and dtype")
+    return _Mul.apply(a, b)
+
+
 def add(a, b, relu: bool = False):
     if not _on_gpu(a):
         y = a + b
@@ -1025,6 +1055,10 @@ def _at(t, elems):
     return t.as_strided((1,), (1,), t.storage_offset() + elems)
 
 
+# KFB_SPLIT_WGRAD=0: affine weight gradients never split the batch reduction
+_SPLIT_WGRAD = os.environ.get("KFB_SPLIT_WGRAD", "1") != "0"
+
+
 def _gemm(mode, p, ldp, q, ldq, rows, cols, red, out, ldc, bias=None, relu=False,
           accumulate=False):
     """csrc/gemm.hip, out [rows][cols]: mode 0 out = p . q (q [red][cols]),
@@ -1050,7 +1084,7 @@ def _gemm(mode, p, ldp, q, ldq, rows, cols, red, out, ldc, bias=None, relu=False
         return
     dev = p.device
     nsplit, slab = 1, None
-    if mode != _GEMM_WGRAD:
+    if mode != _GEMM_WGRAD or _SPLIT_WGRAD:
         nsplit = N.query("kfb_gemm_splits", N.dt(p), rows, cols, red)
         if nsplit > 1:
             slab = torch.empty((nsplit * rows * ((cols + 3) // 4 * 4),), dtype=torch.float32,
@@ -1487,6 +1521,20 @@ def synthetic_uniform(shape, dtype, device, seed: int, salt: int, lo=0.0, hi=1.0
            float(hi - lo), N.dyn("input_seed", seed & 0xFFFFFFFF), int(salt) & 0xFFFFFFFF,
            N.stream(x.device))
     return x
+
+
+def synthetic_ints(n, maxval, device, seed: int, salt: int):
+    """int32 uniform in [0, maxval) made on the device; the per-step seed is a
+    launch-tape argument, ``salt`` a per-tensor constant."""
+    if torch.device(device).type != "cuda":
+        g = torch.Generator().manual_seed(seed + salt)
+        return torch.randint(0, maxval, (n,), generator=g, dtype=torch.int32)
+    if not 0 < maxval <= 1 << 24:
+        raise ValueError("synthetic_ints: maxval must be in (0, 2^24]")
+    y = torch.empty((n,), dtype=torch.int32, device=device)
+    N.call("kfb_synthetic_ints", y.data_ptr(), n, int(maxval),
+           N.dyn("input_seed", seed & 0xFFFFFFFF), int(salt) & 0xFFFFFFFF, N.stream(device))
+    return y
 
 
 def synthetic_labels(n, nclass, device, seed: int):

@@ -197,6 +197,36 @@ def test_fused_optimizer(cuda, kind):
     torch.testing.assert_close(b[1], a[1], rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_mul_forward_backward(cuda, dtype):
+    """Native elementwise product (NCF's GMF layer) vs the fp32 torch formula."""
+    a = torch.randn(513, 64, device=cuda).to(dtype).requires_grad_(True)
+    b = torch.randn(513, 64, device=cuda).to(dtype).requires_grad_(True)
+    dy = torch.randn(513, 64, device=cuda).to(dtype)
+    y = F.mul(a, b)
+    y.backward(dy)
+    af, bf, gf = a.detach().float(), b.detach().float(), dy.float()
+    tol = dict(rtol=1e-2, atol=1e-2) if dtype == torch.bfloat16 else dict(rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(y.float(), af * bf, **tol)
+    torch.testing.assert_close(a.grad.float(), gf * bf, **tol)
+    torch.testing.assert_close(b.grad.float(), gf * af, **tol)
+
+
+def test_synthetic_ints_and_uniform(cuda):
+    """Device-drawn integers / uniforms: in range, roughly uniform, the salt
+    separates tensors of one seed, the seed re-draws them."""
+    a = F.synthetic_ints(1 << 16, 138493, cuda, 5, 21)
+    b = F.synthetic_ints(1 << 16, 138493, cuda, 5, 22)
+    c = F.synthetic_ints(1 << 16, 138493, cuda, 6, 21)
+    assert a.dtype == torch.int32 and int(a.min()) >= 0 and int(a.max()) < 138493
+    assert abs(a.float().mean().item() / 138492 - 0.5) < 0.01
+    assert not torch.equal(a, b) and not torch.equal(a, c)
+    assert torch.equal(a, F.synthetic_ints(1 << 16, 138493, cuda, 5, 21))
+    u = F.synthetic_uniform((4096, 4), torch.float32, cuda, 3, 14, 1.0, 10.0)
+    assert float(u.min()) >= 1.0 and float(u.max()) < 10.0
+    assert abs(u.mean().item() - 5.5) < 0.1
+
+
 @pytest.mark.parametrize("kind", ["momentum", "adam"])
 def test_fused_optimizer_decay_mask(cuda, kind):
     """Weight decay on a subset of the variables (a model's L2 filter, e.g.
@@ -378,6 +408,9 @@ def _rel_err(got, ref):
     (128, 4096, 1001),    # logits: Cout % 8 != 0 (per-element loads / stores)
     (512, 9216, 4096),    # AlexNet fc6 at bs 512
     (37, 203, 77),        # ragged everything
+    (2048, 256, 256),     # NCF MLP at batch 2048: split-K weight gradient
+    (2048, 128, 64),
+    (4099, 203, 77),      # ragged split-K weight gradient
 ])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
 def test_linear_production_shapes(cuda, B, cin, cout, dt):
@@ -403,17 +436,19 @@ def test_linear_production_shapes(cuda, B, cin, cout, dt):
     assert _rel_err(bd.grad, dyf.sum(0)) < lim
 
 
-def test_linear_grad_sink_accumulates(cuda):
+@pytest.mark.parametrize("B", [64, 2048])
+def test_linear_grad_sink_accumulates(cuda, B):
     """A FlatParams-managed weight: dW is accumulated in place in the flat
-    gradient view (no autograd tensor returned) and the ready callback fires."""
+    gradient view (no autograd tensor returned) and the ready callback fires
+    (B=2048: through the split-K slab and its accumulating reduce)."""
     torch.manual_seed(3)
-    x = torch.randn(64, 256, device=cuda).to(torch.bfloat16)
+    x = torch.randn(B, 256, device=cuda).to(torch.bfloat16)
     w = torch.nn.Parameter(torch.randn(256, 128, device=cuda) / 16)
     sink = torch.full((256, 128), 0.5, device=cuda)
     w._kfb_grad_sink = sink
     fired = []
     w._kfb_ready_cb = lambda p: fired.append(p)
-    dy = torch.randn(64, 128, device=cuda).to(torch.bfloat16)
+    dy = torch.randn(B, 128, device=cuda).to(torch.bfloat16)
     y = F.linear(x, w, None, w_lp=w.detach().to(torch.bfloat16), relu=False)
     y.backward(dy)
     ref = x.float().t() @ dy.float() + 0.5

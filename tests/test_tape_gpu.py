@@ -503,30 +503,49 @@ def test_resnet50_s1_dual_tape_bitwise(cuda, _deterministic, monkeypatch):
     assert not _same(e1, t), _same(e1, t)[:8]
 
 
-@pytest.mark.parametrize("model,data_name,bs,kw", [
-    ("deepspeech2", "librispeech", 2, {}),
-    ("ncf", None, 256, dict(optimizer="adam", use_bf16=False))])
-def test_module_models_with_launch_tape(cuda, monkeypatch, model, data_name, bs, kw):
-    """The module models (DeepSpeech2, NCF: ModuleNetwork) accept the launch
-    tape's network hooks; their steps hold torch device ops (the per-step
-    synthetic inputs), so the recording is refused and the run stays eager
-    with the reason recorded (it used to raise AttributeError)."""
+def test_deepspeech2_with_launch_tape(cuda, monkeypatch):
+    """DeepSpeech2 (a ModuleNetwork) accepts the launch tape's network hooks;
+    its step holds torch device ops (sequence lengths, the CTC inputs), so the
+    recording is refused and the run stays eager with the reason recorded
+    (it used to raise AttributeError)."""
     from kf_benchmarks_amd import params as P
     from kf_benchmarks_amd.benchmark import BenchmarkCNN
     monkeypatch.delenv("KFB_TAPE_STRICT", raising=False)
-    args = dict(model=model, batch_size=bs, num_gpus=1, use_bf16=True, optimizer="momentum",
-                data_format="NHWC", variable_update="kungfu", launch_tape=True,
-                display_every=10 ** 9)
-    if data_name:
-        args["data_name"] = data_name
-    args.update(kw)
-    b = BenchmarkCNN(P.make_params(**args))
+    b = BenchmarkCNN(P.make_params(model="deepspeech2", batch_size=2, num_gpus=1, use_bf16=True,
+                                   optimizer="momentum", data_format="NHWC",
+                                   variable_update="kungfu", launch_tape=True,
+                                   display_every=10 ** 9, data_name="librispeech"))
     b.build()
     losses = [float(b.train_step(need_loss=True)[0]) for _ in range(4)]
     torch.cuda.synchronize()
     assert all(l == l for l in losses), losses  # finite
     assert getattr(b, "_tape", None) is None
     assert "recording failed" in (getattr(b, "_tape_reason", "") or "")
+
+
+def _run_ncf(tape, steps=6):
+    from kf_benchmarks_amd import params as P
+    from kf_benchmarks_amd.benchmark import BenchmarkCNN
+    b = BenchmarkCNN(P.make_params(model="ncf", batch_size=256, num_gpus=1, use_bf16=False,
+                                   optimizer="adam", variable_update="kungfu", launch_tape=tape,
+                                   display_every=10 ** 9, loss_type_to_report="base_loss"))
+    b.build()
+    losses = [float(b.train_step(need_loss=True)[0]) for _ in range(steps)]
+    torch.cuda.synchronize()
+    return b, torch.tensor(losses), b.flat.flat.detach().cpu().clone()
+
+
+def test_ncf_tape_matches_eager(cuda):
+    """NCF's step is all native (device-drawn users / items / labels, native
+    GMF product, a persistent ones column): it is taped, and the taped run
+    follows the eager one (the embedding gradients' scatter-adds are atomics,
+    so the check is a tolerance, not bitwise)."""
+    be, le, we = _run_ncf(False)
+    bt, lt, wt = _run_ncf(True)
+    assert getattr(bt, "_tape", None) is not None, getattr(bt, "_tape_reason", None)
+    assert bt._tape.replays == 3
+    torch.testing.assert_close(lt, le, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(wt, we, rtol=1e-3, atol=1e-5)
 
 
 def test_ssd300_masked_decay_tape(cuda, _deterministic, monkeypatch):
