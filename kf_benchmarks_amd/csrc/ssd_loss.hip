@@ -12,13 +12,14 @@
 //
 // Three launches instead of the ~20 (two full argsorts) of the tensor form:
 //   1. ssd_rows_k   - grid over all B*A rows: one online-softmax pass per row
+//                     (16 lanes per row)
 //                     gives lse[i] and v[i] = ce (+ smooth-L1 if positive);
 //   2. ssd_select_k - one 1024-lane workgroup per image: the keys
 //                     ce*(1-pos) sit in LDS (35 KB) and a 4-pass 8-bit radix
 //                     select finds the k-th largest; writes the per-anchor
 //                     weight w = pos+neg and the image loss;
 //   3. ssd_mean_k   - mean over images.
-// Backward (one pass over the rows, bf16/f32 logits in, same dtype out):
+// Backward (one pass over the elements, bf16/f32 logits in, same dtype out):
 //   dx[a][4+c] = g/(B n_b) * w[a] * (softmax(x[a])[c] - [c == label[a]])
 //   dx[a][j]   = g/(B n_b) * pos[a] * clamp(x[a][j] - gt[a][j], -1, 1)
 // Labels arrive as the model's float32 input column and are truncated like
@@ -41,20 +42,17 @@ __device__ __forceinline__ int ssd_label(float l, int C, bool* pos) {
   return li < 0 ? 0 : (li >= C ? C - 1 : li);
 }
 
-// Online log-sum-exp over the C class logits of one row.
-template <typename T>
-__device__ __forceinline__ float row_lse(const T* __restrict__ row, int C) {
-  float m = -INFINITY, s = 0.f;
-  for (int c = 0; c < C; ++c) {
-    const float v = (float)row[c];
-    if (v > m) {
-      s = s * __expf(m - v) + 1.f;
-      m = v;
-    } else {
-      s += __expf(v - m);
-    }
-  }
-  return m + __logf(s);
+// 16 lanes per row (16 rows per 256-thread workgroup): each lane keeps an
+// online (max, sum) over every 16th class logit, the pairs merge across the
+// group by shuffles, so a wave reads 4 consecutive rows' bytes together
+// (one thread per row strode the rows 4 + C elements apart: uncoalesced).
+constexpr int SSD_G = 16;
+
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+  const float mm = fmaxf(m, m2);
+  if (mm == -INFINITY) return;  // both empty
+  s = s * __expf(m - mm) + s2 * __expf(m2 - mm);
+  m = mm;
 }
 
 template <typename T>
@@ -63,19 +61,34 @@ ssd_rows_k(const T* __restrict__ x, const float* __restrict__ gt_loc,
            const float* __restrict__ label, long rows, int C, float* __restrict__ lse_out,
            float* __restrict__ v_out) {
   const int R = 4 + C;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < rows;
-       i += (long)gridDim.x * blockDim.x) {
+  const int g = threadIdx.x & (SSD_G - 1);
+  for (long i = (long)blockIdx.x * (256 / SSD_G) + threadIdx.x / SSD_G; i < rows;
+       i += (long)gridDim.x * (256 / SSD_G)) {
     const T* row = x + i * R;
+    float m = -INFINITY, sm = 0.f;
+    for (int c = g; c < C; c += SSD_G) {
+      const float v = (float)row[4 + c];
+      if (v > m) {
+        sm = sm * __expf(m - v) + 1.f;
+        m = v;
+      } else {
+        sm += __expf(v - m);
+      }
+    }
     bool pos;
     const int l = ssd_label(label[i], C, &pos);
-    const float lse = row_lse(row + 4, C);
-    float v = lse - (float)row[4 + l];
-    if (pos) {
+    float sl = 0.f;
+    if (pos && g < 4) sl = smooth_l1((float)row[g] - gt_loc[i * 4 + g]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v += smooth_l1((float)row[j] - gt_loc[i * 4 + j]);
+    for (int o = SSD_G / 2; o > 0; o >>= 1) {
+      lse_merge(m, sm, __shfl_xor(m, o, SSD_G), __shfl_xor(sm, o, SSD_G));
+      sl += __shfl_xor(sl, o, SSD_G);
     }
-    lse_out[i] = lse;
-    v_out[i] = v;
+    if (g == 0) {
+      const float lse = m + __logf(sm);
+      lse_out[i] = lse;
+      v_out[i] = lse - (float)row[4 + l] + sl;
+    }
   }
 }
 
@@ -192,35 +205,30 @@ __global__ void ssd_mean_k(const float* __restrict__ loss_img, int B, float* __r
   if (threadIdx.x == 0) out[0] = s / (float)B;
 }
 
+// One thread per logit element (coalesced: consecutive lanes, consecutive
+// elements); the per-anchor scalars come from L1 (host: B*A*(4+C) < 2^31).
 template <typename T>
 __global__ void __launch_bounds__(256)
 ssd_bwd_k(const T* __restrict__ x, const float* __restrict__ gt_loc,
           const float* __restrict__ label, const float* __restrict__ num_matched,
           const float* __restrict__ lse, const float* __restrict__ w, const float* __restrict__ g,
           int B, int A, int C, T* __restrict__ dx) {
-  const int R = 4 + C;
-  const long rows = (long)B * A;
+  const unsigned R = 4 + C;
+  const unsigned n = (unsigned)B * (unsigned)A * R;
   const float gs = g[0] / (float)B;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < rows;
-       i += (long)gridDim.x * blockDim.x) {
-    const int b = (int)(i / A);
-    const float scale = gs / num_matched[b];
-    const T* row = x + i * R;
-    T* drow = dx + i * R;
+  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const unsigned i = e / R;
+    const int c = (int)(e - i * R);
+    const float scale = gs / num_matched[i / (unsigned)A];
     bool pos;
     const int l = ssd_label(label[i], C, &pos);
-    const float wgt = w[i] * scale;
-    const float m = lse[i];
-    for (int c = 0; c < C; ++c) {
-      const float p = __expf((float)row[4 + c] - m);
-      drow[4 + c] = (T)(wgt * (p - (c == l ? 1.f : 0.f)));
-    }
-    const float ps = pos ? scale : 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float d = (float)row[j] - gt_loc[i * 4 + j];
-      drow[j] = (T)(ps * fminf(fmaxf(d, -1.f), 1.f));
-    }
+    const float xv = (float)x[e];
+    float d;
+    if (c >= 4)
+      d = w[i] * scale * (__expf(xv - lse[i]) - (c - 4 == l ? 1.f : 0.f));
+    else
+      d = (pos ? scale : 0.f) * fminf(fmaxf(xv - gt_loc[i * 4 + c], -1.f), 1.f);
+    dx[e] = (T)d;
   }
 }
 
@@ -246,7 +254,7 @@ KFB_API hipError_t kfb_ssd_loss_fwd(int dtype, const void* x, const float* gt_lo
   float* v = lse + rows;
   float* w = v + rows;
   KFB_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL((ssd_rows_k<T>), dim3(row_grid(rows)), dim3(256), 0, stream,
+    hipLaunchKernelGGL((ssd_rows_k<T>), dim3(row_grid(rows * SSD_G)), dim3(256), 0, stream,
                        (const T*)x, gt_loc, label, rows, C, lse, v);
   });
   hipLaunchKernelGGL(ssd_select_k, dim3(B), dim3(SSD_SEL_THREADS), 0, stream, v, label,
@@ -262,10 +270,12 @@ KFB_API hipError_t kfb_ssd_loss_bwd(int dtype, const void* x, const float* gt_lo
                                     void* dx, hipStream_t stream) {
   if (A < 1 || B < 1 || C < 1) return hipErrorInvalidValue;
   const long rows = (long)B * A;
+  if (rows * (4 + C) >= (1L << 31)) return hipErrorInvalidValue;
   const float* lse = work + B;
   const float* w = lse + 2 * rows;
   KFB_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL((ssd_bwd_k<T>), dim3(row_grid(rows)), dim3(256), 0, stream, (const T*)x,
+    hipLaunchKernelGGL((ssd_bwd_k<T>), dim3(row_grid(rows * (4 + C))), dim3(256), 0, stream,
+                       (const T*)x,
                        gt_loc, label, num_matched, lse, w, g, B, A, C, (T*)dx);
   });
   return hipGetLastError();

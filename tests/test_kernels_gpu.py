@@ -508,11 +508,12 @@ def test_embedding_lookup_and_grad(cuda, dim):
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("case", ["mixed", "all_negative", "many_matched"])
+@pytest.mark.parametrize("case", ["mixed", "all_negative", "many_matched", "few_classes"])
 def test_ssd_loss(cuda, dt, case):
-    """Fused SSD loss (csrc/ssd_loss.hip: per-row lse + per-image radix
-    select of the hard negatives) vs the stable-sort tensor form in fp32."""
-    B, A, C = 4, 8732, 81
+    """Fused SSD loss (csrc/ssd_loss.hip: per-row lse over 16 lanes + per-image
+    radix select of the hard negatives) vs the stable-sort tensor form in fp32
+    (few_classes: C < 16, so some lanes of a row hold no class)."""
+    B, A, C = 4, 8732, (5 if case == "few_classes" else 81)
     g = torch.Generator().manual_seed(7)
     logits = torch.randn(B, A, 4 + C, generator=g) * 2
     gt_loc = torch.randn(B, A, 4, generator=g)
@@ -520,7 +521,7 @@ def test_ssd_loss(cuda, dt, case):
         label = torch.zeros(B, A, 1)
         nm = torch.rand(B, generator=g) * 9 + 1
     else:
-        frac = 0.02 if case == "mixed" else 0.2
+        frac = 0.2 if case == "many_matched" else 0.02
         pos = torch.rand(B, A, 1, generator=g) < frac
         label = torch.where(pos, torch.randint(1, C, (B, A, 1), generator=g).float(),
                             torch.zeros(B, A, 1)) + 0.3  # truncation like .long()
