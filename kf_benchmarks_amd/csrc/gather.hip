@@ -174,6 +174,22 @@ __global__ void __launch_bounds__(256)
 heads_k(const T* __restrict__ src, T* __restrict__ dst, int nb, int A, int Bd, int R,
         long row0, int col0, long ob, int ld, int dir) {
   const long n = (long)nb * A * Bd * R;
+  if (n < (1L << 31) && row0 + (long)Bd * A <= (1L << 31) / ld) {
+    // 32-bit index math (every SSD300 head): unsigned divisions are a few
+    // instructions, the 64-bit ones a long software sequence per element
+    const unsigned n32 = (unsigned)n, uR = R, uBd = Bd, uA = A;
+    for (unsigned e = blockIdx.x * 256u + threadIdx.x; e < n32; e += gridDim.x * 256u) {
+      unsigned q = e / uR;
+      const unsigned r = e - q * uR;
+      unsigned q2 = q / uBd;
+      const unsigned j = q - q2 * uBd;
+      const unsigned b = q2 / uA, i = q2 - b * uA;
+      const long o = b * ob + (long)((unsigned)row0 + j * uA + i) * ld + col0 + r;
+      if (dir == 0) dst[o] = src[e];
+      else dst[e] = src[o];
+    }
+    return;
+  }
   for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
     const int r = (int)(e % R);
     long q = e / R;
