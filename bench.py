@@ -70,6 +70,10 @@ def main(argv=None):
                          "N > 1 it needs the native RCCL communicator, which a startup "
                          "self-test validates against torch's group; see comm.selftest in the "
                          "JSON).  -1 (default): on for GPU runs")
+    ap.add_argument("--job_timeout", type=float, default=1800.0,
+                    help="self-launched N > 1 runs: kfb-run stops the whole job after this many "
+                         "seconds (0: no limit); a stuck collective is caught earlier by the "
+                         "per-rank watchdog (KFB_COMM_TIMEOUT_S)")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
@@ -84,7 +88,20 @@ def main(argv=None):
         print("bench.py: --gpus=%d but the launcher started %d ranks" % (a.gpus, world_env),
               file=sys.stderr)
         return 2
+    try:
+        return _run(a)
+    except Exception as e:  # noqa: BLE001 - one diagnosable line, then a non-zero exit
+        if world_env > 1:
+            rank = comm.env_rank()
+            line = json.dumps({"status": "error", "rank": rank, "n_gpus": a.gpus,
+                               "reason": "%s: %s" % (type(e).__name__, str(e)[:500])})
+            print(line, file=sys.stdout if rank == 0 else sys.stderr)
+            sys.stdout.flush()
+        raise
 
+
+def _run(a):
+    from kf_benchmarks_amd.parallel import comm
     import torch
     from kf_benchmarks_amd import params as P
     from kf_benchmarks_amd.benchmark import BenchmarkCNN
@@ -140,9 +157,12 @@ def main(argv=None):
 
     bench.strategy.broadcast_initial_model(bench.optimizer.slot_tensors().values())
 
+    from kf_benchmarks_amd.parallel import watchdog
+    stall = _stall_point()
     t0 = time.time()
     for i in range(a.warmup):
         loss, _ = bench.train_step(need_loss=(i == a.warmup - 1))
+    watchdog.beat("warmup_sync", startup=True)
     sync()
     warm_loss = float(loss) if a.warmup > 0 else float("nan")
     if a.verbose and world.is_chief:
@@ -160,10 +180,13 @@ def main(argv=None):
     sync()
     start = time.perf_counter()
     host = 0.0
-    for _ in range(a.steps):
+    for i in range(a.steps):
+        if stall is not None and stall == (world.rank, i):
+            _stall(world.rank, i)
         h0 = time.perf_counter()
         loss, _ = bench.train_step()
         host += time.perf_counter() - h0
+    watchdog.beat("final_sync")
     sync()
     world.barrier(bdev)
     sync()
@@ -177,6 +200,7 @@ def main(argv=None):
 
     # replica consistency (outside the timed region): every rank's fp32
     # master-weight checksum; synchronous strategies must agree bit for bit
+    watchdog.beat("consistency")
     w = bench.strategy.flat.flat
     mine = tuple(float(v) for v in torch.stack([w.double().sum(),
                                                  w.double().square().sum()]).cpu())
@@ -189,26 +213,34 @@ def main(argv=None):
         exposed = reducer.pop_exposed_ms()
     t = torch.tensor([elapsed, (sum(exposed) / len(exposed)) if exposed else 0.0],
                      dtype=torch.float64, device=dev)
+    watchdog.beat("report")
     comm.all_reduce(t, op="max")
     elapsed = float(t[0].item())
     exposed_ms = float(t[1].item())
     taped_steps = getattr(getattr(bench, "_tape", None), "replays", 0) > 0
+    if taped_steps and reducer is not None:
+        # a replayed step re-issues the recorded collectives: count them there
+        per_step = sum(1 for nm in bench._tape.recorder.names if nm in _COLLECTIVES)
+    elif reducer is not None:
+        per_step = (reducer.launch_count - launches0) / a.steps
+    else:
+        per_step = 0
     comm_info = {
         "backend": world.device_backend,
         # native-communicator startup check (None: no native communicator)
         "selftest": getattr(bench, "comm_selftest", None),
+        # RCCL communicators of our own still alive (world + subgroups)
+        "native_comms_live": _native_comms_live(),
         "buckets": reducer.num_buckets if reducer is not None else 0,
-        # replayed steps skip the reducer's Python bookkeeping: not measured
-        "collectives_per_step": (None if taped_steps else
-                                 (reducer.launch_count - launches0) / a.steps
-                                 if reducer is not None else 0),
+        "collectives_per_step": per_step,
         "wire_dtype": a.wire_dtype,
         "bucket_size_mb": a.bucket_size_mb,
         "rccl_channels": os.environ.get("NCCL_MAX_NCHANNELS", "auto"),
         "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
-        # all-reduce time per step that backward did not hide (max over ranks)
+        # all-reduce time per step that backward did not hide (max over
+        # ranks; native timing events inside the step, taped or eager)
         "exposed_allreduce_ms": (round(exposed_ms, 3) if (reducer is not None and cuda
-                                                          and not taped_steps) else None),
+                                                          and exposed) else None),
     }
     n = world.size
     images = a.batch_size * n * a.steps
@@ -264,12 +296,41 @@ def main(argv=None):
         }
         print(json.dumps(out))
         sys.stdout.flush()
+    watchdog.beat("shutdown", startup=True)
     bench.strategy.close()  # collective: model stores / peers released on every rank
     close_input = getattr(getattr(bench, "input", None), "close", None)
     if close_input is not None:
         close_input()  # input producer threads stopped before interpreter exit
     world.shutdown()
     return 0
+
+
+# native entry points that issue one device collective each
+_COLLECTIVES = ("kfb_rccl_all_reduce", "kfb_rccl_reduce", "kfb_rccl_broadcast",
+                "kfb_rccl_all_gather", "kfb_rccl_reduce_scatter", "kfb_rccl_send",
+                "kfb_rccl_recv")
+
+
+def _native_comms_live():
+    from kf_benchmarks_amd.parallel import rccl
+    return rccl.live_count()
+
+
+def _stall_point():
+    """KFB_TEST_STALL=<rank>:<step> (failure-handling tests): that rank stops
+    making progress before that timed step, as a hung peer would."""
+    v = os.environ.get("KFB_TEST_STALL")
+    if not v:
+        return None
+    r, s = v.split(":")
+    return int(r), int(s)
+
+
+def _stall(rank, step):
+    print("bench.py: rank %d stalls before timed step %d (KFB_TEST_STALL)" % (rank, step),
+          file=sys.stderr)
+    sys.stderr.flush()
+    time.sleep(3600)
 
 
 def _self_launch(a, argv) -> int:
@@ -291,8 +352,10 @@ def _self_launch(a, argv) -> int:
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     logdir = tempfile.mkdtemp(prefix="kfb_bench_")
     args = list(sys.argv[1:] if argv is None else argv)
-    cmd = [launcher.launcher_binary(), "-np", str(a.gpus), "-chief-only", "-logdir", logdir,
-           "--", sys.executable, os.path.abspath(__file__)] + args
+    cmd = [launcher.launcher_binary(), "-np", str(a.gpus), "-chief-only", "-logdir", logdir]
+    if a.job_timeout and a.job_timeout > 0:
+        cmd += ["-timeout", "%g" % a.job_timeout]
+    cmd += ["--", sys.executable, os.path.abspath(__file__)] + args
     return subprocess.call(cmd, env=env)
 
 

@@ -32,6 +32,7 @@ from .models import model_config
 from .models.model import make_network
 from .ops import _native
 from .parallel import comm
+from .parallel import watchdog
 from .parallel.variable_mgr import make_strategy
 
 log_fn = cnn_util.log_fn
@@ -432,6 +433,7 @@ class BenchmarkCNN:
         self._built = True
 
     def _validate_comm(self):
+        p = self.params
         """Multi-rank runs on the native communicator: check it bitwise
         against torch's host group on this job's collective buffer sizes and
         dtypes (gradient buckets and their wire dtype, the whole model) before
@@ -442,11 +444,29 @@ class BenchmarkCNN:
         sizes = {1, self.flat.numel}
         dtypes = [torch.float32]
         r = getattr(self.strategy, "reducer", None)
+        groups = []
+        hier = getattr(r, "hierarchical", None) if r is not None else None
         if r is not None:
             sizes.update(e - s for s, e in r.buckets)
             if r.wire_dtype is not None:
                 dtypes.append(r.wire_dtype)
-        st = comm.validate_native(sorted(sizes), tuple(dtypes))
+            if hier is not None and hier.native is not None:
+                # the two-level reduction's own native communicators
+                g, lead = hier.native
+                groups.append(("hier", g, g.rank, g.size))
+                if lead is not None:
+                    groups.append(("leaders", lead, lead.rank, lead.size))
+        st = comm.validate_native(sorted(sizes), tuple(dtypes), groups=groups)
+        if st is not None and st.get("fallback") and hier is not None \
+                and hier.native is not None:
+            # the strategy's reducer was built on native subgroups: rebuild
+            # it on torch groups like the world's collectives (collective:
+            # every rank shares the verdict)
+            self.strategy.close()
+            r.remove()
+            self.strategy = make_strategy(p, self.world, self.flat, self.tower_mode,
+                                          self.num_gpus)
+            st["rebuilt_strategy"] = True
         if st is not None:
             log_fn("Native RCCL self-test: %s (%d checks%s)"
                    % ("passed" if st["ok"] else "FAILED", st["checked"],
@@ -614,6 +634,9 @@ class BenchmarkCNN:
 
     def train_step(self, need_loss=False, need_accuracy=False):
         """One full training step; returns (loss_tensor, accuracy_dict)."""
+        # multi-rank runs: the step must come back within KFB_COMM_TIMEOUT_S
+        # (first steps: autotuning and tape recording get longer)
+        watchdog.beat("step", self.global_step, startup=self.global_step < 4)
         if self.params.launch_tape and self._tape_reason is None:
             r = self._tape_step(need_loss, need_accuracy)
             if r is not None:
@@ -891,11 +914,13 @@ class BenchmarkCNN:
                 if p.save_model_secs and time.time() - last_ckpt_time >= p.save_model_secs:
                     last_ckpt_time = time.time()
             if eval_hook is not None and local_step >= 0:
+                watchdog.beat("eval", self.global_step, startup=True)
                 if eval_hook.maybe_eval(self.global_step):
                     done = True
             local_step += 1
             if local_step >= total_steps:
                 done = True
+        watchdog.beat("final_sync", self.global_step)
         step_train_times.extend(timer.collect())
         if self.device_type == "cuda":
             torch.cuda.synchronize(self.device)
@@ -912,6 +937,7 @@ class BenchmarkCNN:
         if self.benchmark_logger:
             self.benchmark_logger.log_metric("average_examples_per_sec", images_per_sec,
                                              global_step=num_steps)
+        watchdog.beat("finish", self.global_step, startup=True)
         if p.train_dir and self.world.is_chief and not forward_only:
             self.saver.save(p.train_dir, self.global_step)
         tracer.finish()
@@ -928,6 +954,7 @@ class BenchmarkCNN:
             self.world.barrier(self.device if self.device_type == "cuda" else None)
         if last_loss is None and loss is not None:
             last_loss = float(loss)
+        watchdog.pause()  # no collective after this point
         stats = {"num_workers": self.num_workers, "num_steps": num_steps,
                  "average_wall_time": elapsed / num_steps if num_steps > 0 else 0,
                  "images_per_sec": images_per_sec}

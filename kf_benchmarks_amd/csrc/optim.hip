@@ -53,6 +53,10 @@ opt_step_k(float* __restrict__ w, const float* __restrict__ g, float* __restrict
        i += (long)gridDim.x * blockDim.x) {
     float4 wv = reinterpret_cast<float4*>(w)[i];
     float4 gv = reinterpret_cast<const float4*>(g)[i];
+    // the L2 term is part of the gradient of the loss the step's forward
+    // computed, so it uses those weights, not the averaged ones (KungFu's
+    // averaging optimizers assign the average, then apply the gradients)
+    const float w0[4] = {wv.x, wv.y, wv.z, wv.w};
     if (mix) {
       const float4 pv = reinterpret_cast<const float4*>(a.mix)[i];
       wv = make_float4(a.mix_a * wv.x + a.mix_b * pv.x, a.mix_a * wv.y + a.mix_b * pv.y,
@@ -74,7 +78,7 @@ opt_step_k(float* __restrict__ w, const float* __restrict__ g, float* __restrict
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float gk = gg[k] * a.grad_scale;
-      if ((dm >> (8 * k)) & 0xffu) gk += a.weight_decay * ww[k];
+      if ((dm >> (8 * k)) & 0xffu) gk += a.weight_decay * w0[k];
       if (a.clip > 0.f) gk = fminf(fmaxf(gk, -a.clip), a.clip);
       if (KIND == SGD) {
         ww[k] -= a.lr * gk;

@@ -480,6 +480,73 @@ KFB_API hipError_t kfb_event_create_device(hipEvent_t* ev) {
 
 KFB_API hipError_t kfb_event_destroy(hipEvent_t ev) { return hipEventDestroy(ev); }
 
+// ---- interval timer: pairs of timing events in a ring ----------------------
+// The exposed-communication probe (parallel/bucket.py): mark 0 when the
+// backward's kernels are done, mark 1 when the compute stream may use the
+// reduced gradients.  Both marks are entry-point calls (the kfb_event_ prefix
+// keeps a replayed tape on the entry point), so every replayed step records
+// into the next slot and the host reads the intervals after the fact.
+struct EventTimer {
+  std::vector<hipEvent_t> a, b;
+  long w = 0;  // next slot to fill (mark 1 advances it)
+  long r = 0;  // first slot not yet read
+};
+
+KFB_API hipError_t kfb_event_timer_new(int slots, void** out) {
+  if (slots <= 0 || !out) return hipErrorInvalidValue;
+  EventTimer* t = new EventTimer;
+  t->a.resize(slots);
+  t->b.resize(slots);
+  for (int i = 0; i < slots; ++i) {
+    hipError_t e = hipEventCreate(&t->a[i]);
+    if (e == hipSuccess) e = hipEventCreate(&t->b[i]);
+    if (e != hipSuccess) return e;
+  }
+  *out = t;
+  return hipSuccess;
+}
+
+KFB_API hipError_t kfb_event_timer_mark(void* h, int which, hipStream_t s) {
+  EventTimer* t = (EventTimer*)h;
+  if (!t || (which != 0 && which != 1)) return hipErrorInvalidValue;
+  const size_t k = (size_t)(t->w % (long)t->a.size());
+  const hipError_t e = hipEventRecord(which == 0 ? t->a[k] : t->b[k], s);
+  if (which == 1) t->w += 1;
+  return e;
+}
+
+// Waits for the intervals recorded since the last read and writes their
+// lengths (ms) to out (at most max, the newest ones); returns how many.
+KFB_API int kfb_event_timer_read(void* h, float* out, int max) {
+  EventTimer* t = (EventTimer*)h;
+  if (!t || !out || max <= 0) return -1;
+  const long n = (long)t->a.size();
+  long r = t->r;
+  if (t->w - r > n) r = t->w - n;  // overwritten: keep the newest n
+  if (t->w - r > max) r = t->w - max;
+  int got = 0;
+  for (; r < t->w; ++r) {
+    const size_t k = (size_t)(r % n);
+    if (hipEventSynchronize(t->b[k]) != hipSuccess) return -1;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, t->a[k], t->b[k]) != hipSuccess) ms = 0.f;
+    out[got++] = ms > 0.f ? ms : 0.f;
+  }
+  t->r = t->w;
+  return got;
+}
+
+KFB_API int kfb_event_timer_free(void* h) {
+  EventTimer* t = (EventTimer*)h;
+  if (!t) return 0;
+  for (size_t i = 0; i < t->a.size(); ++i) {
+    hipEventDestroy(t->a[i]);
+    hipEventDestroy(t->b[i]);
+  }
+  delete t;
+  return 0;
+}
+
 // dst waits for everything enqueued on src so far (ev: scratch event).
 KFB_API hipError_t kfb_stream_wait(hipStream_t dst, hipStream_t src, hipEvent_t ev) {
   if (Op* op = cur_op()) {

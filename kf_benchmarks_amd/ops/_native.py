@@ -49,6 +49,10 @@ _SIGS = {
     "kfb_event_create_device": [P],
     "kfb_event_destroy": [P],
     "kfb_stream_wait": [P, P, P],
+    "kfb_event_timer_new": [I, P],
+    "kfb_event_timer_mark": [P, I, P],
+    "kfb_event_timer_read": [P, P, I],
+    "kfb_event_timer_free": [P],
     "kfb_memset": [P, I, ctypes.c_size_t, P],
     "kfb_memcpy_d2d": [P, P, ctypes.c_size_t, P],
     "kfb_tape_available": [],

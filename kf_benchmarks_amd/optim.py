@@ -237,10 +237,14 @@ class FusedOptimizer:
             if finish:
                 f.after_update()
             return
+        w_pre = None
         if msrc is not None and (mok is None or int(mok.reshape(-1)[0]) != 0):
             with torch.no_grad():
+                if weight_decay:
+                    # (the L2 gradient is of the forward's weights, pre-average)
+                    w_pre = w.clone()
                 w.mul_(ma).add_(msrc, alpha=mb)
-        self._step_torch(g, lr, grad_scale, weight_decay, clipv, mom, b1, b2, eps, lr_t)
+        self._step_torch(g, lr, grad_scale, weight_decay, clipv, mom, b1, b2, eps, lr_t, w_pre)
         if wout is not None:
             wout.copy_(w)
         f.after_update()
@@ -256,12 +260,13 @@ class FusedOptimizer:
         return {"lr_t": lr_t}
 
     @torch.no_grad()
-    def _step_torch(self, g, lr, grad_scale, wd, clip, mom, b1, b2, eps, lr_t):
+    def _step_torch(self, g, lr, grad_scale, wd, clip, mom, b1, b2, eps, lr_t, w_decay=None):
         w = self.flat.update_target
         gk = g * grad_scale
         if wd:
+            wd_src = w if w_decay is None else w_decay
             dm = self.decay_mask
-            gk = gk + (wd * w if dm is None else wd * w * dm.to(w.device, w.dtype))
+            gk = gk + (wd * wd_src if dm is None else wd * wd_src * dm.to(w.device, w.dtype))
         if clip > 0:
             gk = gk.clamp(-clip, clip)
         if self.kind == "sgd":

@@ -116,12 +116,16 @@ class BucketReducer:
         # has the previous step's reduction outstanding while it launches)
         self._wire = [None, None]
         self.launch_count = 0  # collectives issued (tests, all_reduce_benchmark)
-        # exposed-communication probe (bench.py): per step, an event when the
-        # backward's kernels are done (both streams) and one when the compute
-        # stream may use the reduced gradients; their distance is the
-        # all-reduce time backward did not hide
-        self.timing = False
-        self._timing_events = []
+        # exposed-communication probe (bench.py): per step, a native timing
+        # event when the backward's kernels are done (both streams) and one
+        # when the compute stream may use the reduced gradients; their
+        # distance is the all-reduce time backward did not hide.  Both are
+        # native calls, so a recorded launch tape replays them (each replay
+        # fills the next slot of the timer's ring).  KFB_COMM_PROBE=0: off.
+        self.timing = False  # (kept for callers; the probe runs whenever on)
+        self.probe = os.environ.get("KFB_COMM_PROBE", "1") != "0"
+        self._timer = None
+        self._timing_events = []  # CPU runs: none
         self._handles = []
         if overlap:
             for _, p, _, _ in segs:
@@ -240,9 +244,14 @@ class BucketReducer:
         self._active = False
 
     def close(self):
-        """Releases the reducer's own communicators (hierarchical subgroups)."""
+        """Releases the reducer's own communicators (hierarchical subgroups)
+        and the probe's events."""
         if self.hierarchical is not None:
             self.hierarchical.close()
+        if self._timer is not None:
+            from ..ops import _native as N
+            N.load().kfb_event_timer_free(self._timer)
+            self._timer = None
 
     def finish(self):
         """Launch whatever did not fire (unused params, overlap off) and make
@@ -250,7 +259,9 @@ class BucketReducer:
         if self.relaxed:
             self._finish_relaxed()
             return
-        ev = self._backward_done_event() if self.timing else None
+        probe = self.probe and self.flat.grad.is_cuda
+        if probe:
+            self._mark_backward_done()
         while self._next < len(self.buckets):
             self._launch(self._next)
             self._next += 1
@@ -259,38 +270,51 @@ class BucketReducer:
                 work.wait()
             if buf is not None and buf is not view:
                 _unwire(view, buf)
-        if ev is not None:
-            end = torch.cuda.Event(enable_timing=True)
-            end.record()
-            self._timing_events.append((ev, end))
+        if probe:
+            from ..ops import _native as N
+            dev = self.flat.grad.device
+            N.call("kfb_event_timer_mark", self._probe_timer(dev), 1, N.stream(dev))
         self._works = []
         self._active = False
 
-    def _backward_done_event(self):
-        g = self.flat.grad
-        if not g.is_cuda:
-            return None
-        from ..ops.conv_hip import wgrad_stream
-        side = wgrad_stream(g.device)
-        cur = torch.cuda.current_stream(g.device)
-        ev = torch.cuda.Event(enable_timing=True)
-        if side is not None and side != cur:
+    _PROBE_SLOTS = 4096
+
+    def _probe_timer(self, dev):
+        if self._timer is None:
+            import ctypes
             from ..ops import _native as N
-            N.stream_wait(side.cuda_stream, cur.cuda_stream)
-            ev.record(side)
-        else:
-            ev.record(cur)
-        return ev
+            h = ctypes.c_void_p()
+            err = N.load().kfb_event_timer_new(self._PROBE_SLOTS, ctypes.byref(h))
+            if err != 0:
+                raise N.NativeError("kfb_event_timer_new failed with hipError %d" % err)
+            self._timer = h.value
+        return self._timer
+
+    def _mark_backward_done(self):
+        """Mark 0: the side stream (weight gradients) catches up with the
+        compute stream, then records, so the event completes only once both
+        streams' backward kernels have."""
+        from ..ops import _native as N
+        from ..ops.conv_hip import wgrad_stream
+        g = self.flat.grad
+        side = wgrad_stream(g.device)
+        cur = N.stream(g.device)
+        s = cur
+        if side is not None and side.cuda_stream != cur:
+            N.stream_wait(side.cuda_stream, cur)
+            s = side.cuda_stream
+        N.call("kfb_event_timer_mark", self._probe_timer(g.device), 0, s)
 
     def pop_exposed_ms(self) -> List[float]:
-        """Exposed all-reduce milliseconds of every timed step since the last
-        call (synchronizes on the recorded events)."""
-        out = []
-        for a, b in self._timing_events:
-            b.synchronize()
-            out.append(max(a.elapsed_time(b), 0.0))
-        self._timing_events = []
-        return out
+        """Exposed all-reduce milliseconds of every step since the last call,
+        eager or replayed from a launch tape (synchronizes on the events)."""
+        if self._timer is None:
+            return []
+        import ctypes
+        from ..ops import _native as N
+        buf = (ctypes.c_float * self._PROBE_SLOTS)()
+        n = N.load().kfb_event_timer_read(self._timer, buf, self._PROBE_SLOTS)
+        return [float(buf[i]) for i in range(max(n, 0))]
 
     def reduce_now(self):
         """Synchronous all-reduce of the whole gradient (no backward hooks)."""

@@ -55,6 +55,8 @@ class World:
         all-reduce on the device, then a host wait."""
         if not self.has_pg:
             return
+        from . import watchdog
+        watchdog.beat("barrier")
         if self.native is not None and device is not None:
             self.native.barrier()
             return
@@ -88,6 +90,8 @@ class World:
             self.device_group = dist.new_group(list(range(self.size)), backend="nccl")
 
     def shutdown(self):
+        from . import watchdog
+        watchdog.stop()
         if self.native is not None:
             self.native.close()
             self.native = None
@@ -268,6 +272,12 @@ def init_world(device_type: str = "cuda", all_reduce_spec: Optional[str] = None,
         here = True
     world = World(rank, size, local_rank, dist.get_backend(), here, has_pg=True)
     world.device_index = device_index
+    if size > 1:
+        # from here on a stuck collective ends the job with a diagnosis
+        # (parallel/watchdog.py; KFB_COMM_TIMEOUT_S=0 turns it off)
+        from . import watchdog
+        if watchdog.start(rank):
+            watchdog.beat("startup", startup=True)
     if native:
         try:
             store = dist.distributed_c10d._get_default_store()
@@ -317,64 +327,187 @@ def reset_world():
 # fallback branch runs on a real communicator
 _SELFTEST_INJECT = os.environ.get("KFB_SELFTEST_INJECT") == "1"
 
+# largest buffer a self-test check moves (bigger job buffers are checked at
+# this size: the startup cost must not grow with the model).  Host buffers
+# (CPU rehearsals, where the candidate is a stand-in over gloo and the
+# pattern arithmetic runs on one core per rank) use the smaller cap.
+SELFTEST_CAP_BYTES = 64 << 20
+SELFTEST_CAP_BYTES_HOST = 8 << 20
+
+
+def _selftest_cap(device) -> int:
+    return SELFTEST_CAP_BYTES if (device is not None and torch.device(device).type == "cuda") \
+        else SELFTEST_CAP_BYTES_HOST
+
+
+_HASH = {}
+
+
+def _selftest_hash(n: int, seed: int, device):
+    """17 bits of an index hash (int32), identical on every rank; one per
+    (seed, device), grown to the largest size asked for and sliced."""
+    key = (seed, str(device))
+    h = _HASH.get(key)
+    if h is None or h.numel() < n:
+        i = torch.arange(n, device=device, dtype=torch.int64)
+        h = (i * 2654435761 + seed * 97) & 0xFFFFFFFF
+        h = ((h ^ (h >> 13)) * 1274126177) & 0xFFFFFFFF
+        # 16 hash bits and a sign bit, as int32
+        h = ((h >> 8) & 0x1FFFF).to(torch.int32)
+        _HASH[key] = h
+    return h[:n]
+
+
+def _selftest_base(n: int, lim: int, seed: int, device):
+    """(base, sign): an index-hashed integer in [-lim, lim] and a +-1 per
+    element (int32), identical on every rank."""
+    h = _selftest_hash(n, seed, device)
+    # (multiply-shift maps the 16 bits onto [0, 2 lim] without a division)
+    return (((h & 0xFFFF) * (2 * lim + 1)) >> 16) - lim, ((h >> 15) & 2) - 1
+
+
+def _member_weights(members: int, dt) -> Optional[list]:
+    """Per-member multipliers of the sign term: member + 1 (distinct
+    contributions) while every partial sum stays exact in ``dt``, else 1
+    for everyone; None when not even that fits (then the dtype is not
+    checked at this group size)."""
+    top = _EXACT.get(dt, 1 << 24)
+    if members * (members + 1) // 2 <= top:
+        return list(range(1, members + 1))
+    if members <= top:
+        return [1] * members
+    return None
+
+
+_EXACT = {torch.bfloat16: 256, torch.float16: 2048}
+
+
+def selftest_pattern(n: int, member: int, lim: int, seed: int, device,
+                     weights=None) -> torch.Tensor:
+    """Member ``member``'s test data: base(i) + sign(i) * w[member].
+    Element i differs across the buffer (misplaced data is caught) and
+    across members (a missing or doubled contribution is caught), and the
+    results of every collective have a closed form each rank evaluates on
+    its own device (:func:`selftest_expected`) - no buffer crosses the
+    host network."""
+    base, sign = _selftest_base(n, lim, seed, device)
+    w = weights[member] if weights is not None else member + 1
+    return base + sign * w
+
+
+def selftest_expected(kind: str, n: int, members: int, lim: int, seed: int, device,
+                      weights=None):
+    weights = weights if weights is not None else list(range(1, members + 1))
+    base, sign = _selftest_base(n, lim, seed, device)
+    if kind == "broadcast":  # member 0's data
+        return base + sign * weights[0]
+    if kind == "max":
+        return base + torch.where(sign > 0, sign * max(weights), sign * min(weights))
+    return base * members + sign * sum(weights)  # sum / reduce
+
+
+def _selftest_lim(dt, members: int, weights=None) -> int:
+    # every partial sum of ``members`` values stays an integer the dtype
+    # holds exactly (bf16: |x| <= 256, fp16: <= 2048), in any order
+    weights = weights if weights is not None else list(range(1, members + 1))
+    top = _EXACT.get(dt)
+    if top is None:
+        return 1024
+    return max(0, (top - sum(weights)) // members)
+
 
 def selftest_device_collectives(cand, sizes, dtypes=(torch.float32,), device=None,
-                                 seed: int = 0) -> dict:
-    """Checks a candidate device communicator ``cand`` (all_reduce /
-    broadcast returning works whose wait() orders the current stream, and
-    barrier) against torch's host-side group on the same buffers, bitwise:
-    for every buffer size and dtype a broadcast from rank 0 and a sum / max
-    all-reduce of small integer-valued data (exact in every dtype and any
-    summation order, so a correct collective matches bit for bit), then a
-    barrier.  Collective over all ranks; every rank returns the same verdict
-    {"ok", "checked", "failed"} (any rank's mismatch fails all)."""
+                                 seed: int = 0, groups=None) -> dict:
+    """Checks device communicators bitwise on device-generated data.
+
+    ``groups``: [(name, comm, member_index, members)] - the world
+    communicator and e.g. the hierarchical reduction's subgroups; default
+    the world's ``cand`` alone.  For every buffer size (capped at
+    SELFTEST_CAP_BYTES), dtype and group: broadcast from member 0, sum / max
+    all-reduce, and sum reduce to member 0 of integer data from
+    :func:`selftest_pattern`.  Each rank computes the expected results
+    itself from every member's pattern, so no buffer crosses the host
+    network; only the per-rank failure lists are exchanged (one small
+    ``all_gather_object``).  A check that raises is recorded as a failure
+    and the loop goes on, so every rank issues the same collectives and
+    reaches the verdict.  Collective over all ranks; every rank returns the
+    same verdict {"ok", "checked", "failed"}."""
     w = get_world()
     dev = device if device is not None else getattr(cand, "device", None)
+    if groups is None:
+        groups = [("world", cand, w.rank, w.size)]
     failed = []
     checked = 0
-    for n in sizes:
-        n = int(n)
-        for dt in dtypes:
-            lim = 16 if dt in (torch.bfloat16, torch.float16) else 1024
-            g = torch.Generator().manual_seed((seed * 1000003 + w.rank * 7919 + n) & 0x7FFFFFFF)
-            host = torch.randint(-lim, lim + 1, (n,), generator=g).to(dt)
-            for kind in ("broadcast", "sum", "max"):
-                ref = host.clone().float()
-                if kind == "broadcast":
-                    dist.broadcast(ref, 0)
-                else:
-                    dist.all_reduce(ref, op=_ROP[kind])
-                buf = host.to(dev) if dev is not None else host.clone()
-                work = cand.broadcast(buf, 0) if kind == "broadcast" else \
-                    cand.all_reduce(buf, kind)
-                if work is not None:
-                    work.wait()
-                got = buf.float().cpu()
-                if _SELFTEST_INJECT and kind == "sum" and n > 1 and w.rank == 0:
-                    got[0] += 1  # (test hook: a wrong sum on rank 0)
-                checked += 1
-                if not torch.equal(got, ref.to(dt).float()):
-                    failed.append("%s n=%d %s" % (kind, n, str(dt).replace("torch.", "")))
-    cand.barrier()
+    cap = _selftest_cap(dev)
+    # the hash once, at the largest size checked (the rest are slices)
+    _selftest_hash(max(1, min(max(int(n) for n in sizes), cap // 2)), seed, dev)
+    for gname, gc, me, members in groups:
+        if gc is None:
+            continue
+        seen = set()
+        for n in sizes:
+            for dt in dtypes:
+                esz = torch.tensor([], dtype=dt).element_size()
+                n_ = max(1, min(int(n), cap // esz))
+                if (n_, dt) in seen:
+                    continue  # (sizes above the cap collapse into one check)
+                seen.add((n_, dt))
+                wts = _member_weights(members, dt)
+                if wts is None:
+                    continue  # (more members than the dtype counts exactly)
+                lim = _selftest_lim(dt, members, wts)
+                base, sign = _selftest_base(n_, lim, seed, dev)
+                mine = (base + sign * wts[me]).to(dt)
+                expect = {"broadcast": (base + sign * wts[0]).to(dt),
+                          "max": (base + torch.where(sign > 0, sign * max(wts),
+                                                     sign * min(wts))).to(dt),
+                          "sum": (base * members + sign * sum(wts)).to(dt)}
+                expect["reduce"] = expect["sum"]
+                for kind in ("broadcast", "sum", "max", "reduce"):
+                    tag = "%s%s n=%d %s" % ("" if gname == "world" else gname + ":", kind, n_,
+                                            str(dt).replace("torch.", ""))
+                    checked += 1
+                    try:
+                        buf = mine.clone()
+                        if kind == "broadcast":
+                            work = gc.broadcast(buf, 0)
+                        elif kind == "reduce":
+                            work = gc.reduce(buf, 0, "sum")
+                        else:
+                            work = gc.all_reduce(buf, kind)
+                        if work is not None:
+                            work.wait()
+                        if kind == "reduce" and me != 0:
+                            continue  # (non-root buffers are unspecified)
+                        good = torch.equal(buf, expect[kind])
+                        if _SELFTEST_INJECT and kind == "sum" and n_ > 1 and w.rank == 0:
+                            good = False  # (test hook: a wrong sum on rank 0)
+                    except Exception as e:  # noqa: BLE001 - a raising collective fails the check
+                        good = False
+                        tag += " (raised %s)" % type(e).__name__
+                    if not good:
+                        failed.append(tag)
+    try:
+        cand.barrier()
+    except Exception as e:  # noqa: BLE001
+        failed.append("barrier (raised %s)" % type(e).__name__)
+    _HASH.clear()
     verdicts = all_gather_object(failed)
     bad = sorted({f for fl in verdicts for f in fl})
     return {"ok": not bad, "checked": checked, "failed": bad[:8]}
 
 
-def validate_native(sizes, dtypes=(torch.float32,)) -> Optional[dict]:
-    """KFB_NATIVE_COMM=auto: self-test the native communicator on the job's
-    buffer sizes and fall back to torch's ProcessGroupNCCL if it fails.
-    Returns the self-test record (None: no native communicator)."""
+def validate_native(sizes, dtypes=(torch.float32,), groups=None) -> Optional[dict]:
+    """KFB_NATIVE_COMM=auto: self-test the native communicators (the world's
+    and ``groups``' subgroups) on the job's buffer sizes and fall back to
+    torch's ProcessGroupNCCL if any fails.  Returns the self-test record
+    (None: no native communicator)."""
     w = get_world()
     if w.native is None or not w.has_pg:
         return None
     from . import rccl as _rccl
-    try:
-        st = selftest_device_collectives(w.native, sizes, dtypes)
-    except Exception as e:  # noqa: BLE001 - a raising collective is a failed test
-        st = {"ok": False, "checked": 0, "failed": ["raised: %s" % e]}
-        # (the other ranks' verdicts are unknown: agree on failure)
-        all_gather_object(["raised"])
+    all_groups = [("world", w.native, w.rank, w.size)] + list(groups or [])
+    st = selftest_device_collectives(w.native, sizes, dtypes, groups=all_groups)
     st["mode"] = _rccl.mode()
     if not st["ok"] and _rccl.mode() == "auto":
         w.fall_back_to_torch("self-test failed: %s" % ", ".join(st["failed"]))

@@ -373,7 +373,8 @@ class PairAveraging(Strategy):
     def __init__(self, params, world, flat, **kw):
         super().__init__(params, world, flat, **kw)
         self.rng = random.Random(params.kungfu_peer_seed * 7919 + world.rank)
-        self.prefetch = bool(getattr(params, "kungfu_pair_prefetch", True))
+        self.lockstep = bool(getattr(params, "kungfu_pair_lockstep", False))
+        self.prefetch = bool(getattr(params, "kungfu_pair_prefetch", True)) and not self.lockstep
         self.store = None
         self._peer_buf = None
         self._mix = None
@@ -408,6 +409,13 @@ class PairAveraging(Strategy):
         else:
             self.store.finish_pull()
             ok = None
+        if self.lockstep:
+            # every worker holds its peer's step-t model before anyone
+            # publishes step t+1's
+            w = self.flat.flat
+            if w.is_cuda:
+                torch.cuda.synchronize(w.device)
+            self.world.barrier(w.device if w.is_cuda else None)
         # w <- (w + w_peer) / 2 and the update in ONE pass, written straight
         # into the publish slot
         self._mix = (self._peer_buf, 0.5, 0.5, ok)
@@ -421,6 +429,10 @@ class PairAveraging(Strategy):
     def after_update(self, step):
         if self.store is not None:
             self.store.end_publish()
+            if self.lockstep:
+                self.store.flush()  # committed: the next pulls see it
+                w = self.flat.flat
+                self.world.barrier(w.device if w.is_cuda else None)
 
     def abort_update(self, step):
         self._mix = self._wout = None
@@ -437,6 +449,8 @@ class PairAveraging(Strategy):
     def tape_blocker(self):
         if self.world.size > 1 and not self.flat.flat.is_cuda:
             return "host-memory model store"
+        if self.lockstep:
+            return "lock-step PairAveraging synchronizes on the host"
         if self.store is not None and not self.store.device_check:
             return "peer headers not mappable for the device seqlock check"
         return None

@@ -51,6 +51,14 @@ class RcclError(RuntimeError):
     pass
 
 
+_LIVE = set()  # handles of this process's communicators not yet destroyed
+
+
+def live_count() -> int:
+    """Native communicators alive in this process (world + subgroups)."""
+    return len(_LIVE)
+
+
 def available() -> bool:
     try:
         return bool(N.load().kfb_rccl_available())
@@ -128,6 +136,9 @@ class NativeComm:
                     "ncclCommInitRank")
         self.h = h.value
         self.collectives = 0
+        _LIVE.add(self.h)
+        from . import watchdog
+        watchdog.add_comm(self.h)  # polled for async errors, aborted on a hang
 
     def _check(self, rc, what):
         if rc != 0:
@@ -194,14 +205,17 @@ class NativeComm:
 
     def check(self):
         rc = N.load().kfb_rccl_async_error(self.h)
-        if rc != 0:
+        if rc != 0 and rc != 1007:  # (1007: ncclInProgress)
             self._check(rc, "RCCL asynchronous error")
 
     def close(self, abort=False):
         if getattr(self, "h", None):
+            from . import watchdog
+            watchdog.remove_comm(self.h)
             try:
                 self.stream.synchronize()
             except RuntimeError:
                 abort = True
             N.load().kfb_rccl_destroy(self.h, int(abort))
+            _LIVE.discard(self.h)
             self.h = None

@@ -52,7 +52,9 @@ class Strategy:
         self.reducer: Optional[BucketReducer] = None
         if self.reduces_gradients and world.communicates:
             hier = None
-            if hierarchical and world.size > 1:
+            # (a forced 1-rank group builds it too: the GPU tests' real
+            # communicator path, tests/test_dist_gpu.py)
+            if hierarchical and (world.size > 1 or comm.force_pg()):
                 from .allreduce import Hierarchical
                 hier = Hierarchical(world.size, world.rank,
                                     str(getattr(params, "network_topology", "dgx1")))

@@ -220,6 +220,11 @@ D.DEFINE_boolean("kungfu_pair_prefetch", True,
                  "PairAveraging: pull the peer model at the start of the step, overlapping "
                  "forward/backward (the averaged model is one step older than KungFu's); "
                  "false pulls it at update time, as KungFu's apply_gradients does.")
+D.DEFINE_boolean("kungfu_pair_lockstep", False,
+                 "PairAveraging, deterministic mode (tests/oracles): pull at update time, "
+                 "every worker finishes its pull before any publishes, and every publish "
+                 "commits before the next step, so the averaged peer model is exactly the "
+                 "peer's model of the same step (costs two barriers per step).")
 D.DEFINE_boolean("synthetic_resample", True,
                  "Re-sample the synthetic batch on device every step, inside the timed step "
                  "(as the fork's graph does; --nosynthetic_resample reuses one batch like "

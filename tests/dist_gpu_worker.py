@@ -57,6 +57,10 @@ def main():
         loss, _ = bench.train_step(need_loss=True)
         losses.append(float(loss))
     torch.cuda.synchronize()
+    # exposed all-reduce per step from the reducer's native timing events
+    # (recorded into the launch tape too, so replayed steps report as well)
+    exposed = (bench.strategy.reducer.pop_exposed_ms()
+               if bench.strategy.reducer is not None else [])
     reduce_identity = None
     if os.environ.get("KFB_TEST_REDUCE_IDENTITY") and bench.strategy.reducer is not None:
         # one more synchronous all-reduce of the last gradient over the group:
@@ -91,7 +95,7 @@ def main():
            "nccl_pgs": nccl_pgs, "losses": losses, "w0": w0, "wsum": flat.double().sum().item(),
            "wabs": flat.double().abs().sum().item(), "head": flat[:64].cpu().tolist(),
            "tail": flat[-64:].cpu().tolist(), "rank": comm.get_world().rank,
-           "gsegs": gsegs, "trace": trace,
+           "gsegs": gsegs, "trace": trace, "exposed_ms": exposed,
            "segs": {name: flat[off:off + n].double().sum().item()
                     for name, _, off, n in bench.flat.segments()},
            "size": comm.get_world().size, "backend": comm.get_world().device_backend,

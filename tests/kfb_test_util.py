@@ -129,11 +129,26 @@ def manually_compute_losses(inputs, num_workers, params, aggregation, staged=Fal
     """Simulates ``num_workers`` workers on the analytic model.
 
     aggregation: 'sum' (parameter_server/replicated/... all-reduce SUM),
-    'mean' (kungfu sync_sgd), 'none' (independent).  Returns losses[w][step]
-    as reported with loss_type_to_report.  ``staged``: --staged_vars, the
-    loss and gradients of step t use the variables as they were before the
-    previous update (tcb/variable_mgr_util.py:236-393).
+    'mean' (kungfu sync_sgd), 'none' (independent), and KungFu's model
+    averaging optimizers (the wrappers of
+    tcb/benchmark_cnn.py:1196-1201):
+
+    * 'sma' (SynchronousAveragingOptimizer): every worker moves to
+      (1 - alpha) w + alpha * mean_r(w_r), then applies its own gradient;
+    * 'ada_sgd': 'sma' until --kungfu_ada_switch_step, 'mean' afterwards;
+    * 'pair' (PairAveragingOptimizer, lock-step): worker r averages with the
+      step-t model of a peer drawn by its own RNG (seed
+      kungfu_peer_seed * 7919 + r), w <- (w + w_peer) / 2, then applies its
+      own gradient.
+
+    In the averaging modes the gradient is of the loss the step's forward
+    computed, so its L2 term uses the forward's (pre-average) weights.
+    Returns losses[w][step] as reported with loss_type_to_report.
+    ``staged``: --staged_vars, the loss and gradients of step t use the
+    variables as they were before the previous update
+    (tcb/variable_mgr_util.py:236-393).
     """
+    import random
     bs = params.batch_size
     n_batches = inputs.shape[0] // bs
     x_all = inputs.astype(np.float64) / 127.5 - 1.0
@@ -149,6 +164,10 @@ def manually_compute_losses(inputs, num_workers, params, aggregation, staged=Fal
     acc = [[0.0, 0.0] for _ in range(num_workers)]
     losses = [[] for _ in range(num_workers)]
     RA, RB = list(A), list(B)  # staged reads
+    alpha = float(getattr(params, "kungfu_sma_alpha", 0.1))
+    switch = int(getattr(params, "kungfu_ada_switch_step", 100))
+    rngs = [random.Random(int(getattr(params, "kungfu_peer_seed", 0)) * 7919 + w)
+            for w in range(num_workers)]
     for step in range(params.num_batches):
         grads = []
         for w in range(num_workers):
@@ -159,13 +178,29 @@ def manually_compute_losses(inputs, num_workers, params, aggregation, staged=Fal
             total = base + wd * (a * a + b * b) / 2
             losses[w].append(base if params.loss_type_to_report == "base_loss" else total)
             grads.append((m * b, m * a, a, b))  # data gradient; wd added at update
-        if aggregation == "sum":
+        mode = aggregation
+        if mode == "ada_sgd":
+            mode = "sma" if step < switch else "mean"
+        mixA, mixB = list(A), list(B)  # the weights the update starts from
+        if mode == "sma":
+            avgA, avgB = sum(A) / num_workers, sum(B) / num_workers
+            mixA = [(1 - alpha) * a + alpha * avgA for a in A]
+            mixB = [(1 - alpha) * b + alpha * avgB for b in B]
+            agg = [(g[0], g[1]) for g in grads]
+        elif mode == "pair":
+            agg = [(g[0], g[1]) for g in grads]
+            for w in range(num_workers):
+                if num_workers > 1:
+                    q = rngs[w].randrange(num_workers - 1)
+                    q = q + 1 if q >= w else q
+                    mixA[w], mixB[w] = 0.5 * (A[w] + A[q]), 0.5 * (B[w] + B[q])
+        elif mode == "sum":
             # every worker's gradient carries its own wd * w term (the
             # reference oracle applies each worker's total-loss gradient,
             # tcb/test_util.py:365-443); replicas are identical in sum modes
             agg = [(sum(g[0] for g in grads) + (num_workers - 1) * wd * A[0],
                     sum(g[1] for g in grads) + (num_workers - 1) * wd * B[0])] * num_workers
-        elif aggregation == "mean":
+        elif mode == "mean":
             agg = [(sum(g[0] for g in grads) / num_workers,
                     sum(g[1] for g in grads) / num_workers)] * num_workers
         else:
@@ -175,6 +210,7 @@ def manually_compute_losses(inputs, num_workers, params, aggregation, staged=Fal
             ga = agg[w][0] + wd * wa
             gb = agg[w][1] + wd * wb
             RA[w], RB[w] = A[w], B[w]
+            A[w], B[w] = mixA[w], mixB[w]
             if params.optimizer == "sgd":
                 A[w] -= lr * ga
                 B[w] -= lr * gb

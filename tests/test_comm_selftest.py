@@ -46,7 +46,8 @@ def _run(n, kind, tmp_path, timeout=180):
 def test_selftest_passes_and_keeps_native(n, tmp_path):
     res = _run(n, "good", tmp_path)
     for r in res:
-        assert r["selftest"]["ok"] and r["selftest"]["checked"] == 3 * 2 * 3
+        # 3 sizes x 2 dtypes x (broadcast, sum, max, reduce)
+        assert r["selftest"]["ok"] and r["selftest"]["checked"] == 3 * 2 * 4
         assert r["validate"]["ok"] and "fallback" not in r["validate"]
         assert r["native_after"] and not r["closed"]
 
@@ -62,3 +63,15 @@ def test_selftest_failure_on_one_rank_falls_back_everywhere(n, tmp_path):
                                 "sum n=65536 bfloat16", "sum n=65536 float32"]
         assert not r["validate"]["ok"] and r["validate"]["fallback"]
         assert not r["native_after"] and r["closed"]
+
+
+def test_selftest_cost_bounded_on_vgg16_8_ranks(tmp_path):
+    """VGG-16's 138 M parameters (BASELINE #5): every distinct bucket size is
+    checked once, capped (64 MB on a GPU; 8 MB for these host stand-ins), on
+    data each rank generates itself; the whole startup check on 8 gloo ranks
+    stays within 10 s."""
+    res = _run(8, "vgg16", tmp_path, timeout=300)
+    for r in res:
+        assert r["selftest"]["ok"], r["selftest"]
+        assert max(r["sizes"]) > 100_000_000  # (the whole model is one size)
+        assert r["seconds"] <= 10.0, r["seconds"]

@@ -156,6 +156,11 @@ def test_one_rank_rccl_resnet50_overlap(cuda, tmp_path, native, tape):
     assert a["taped"] == (2 if tape else 0)
     launches = 3 * a["num_buckets"] if not tape else 3 * a["num_buckets"]  # eager+recorded
     assert a["num_buckets"] >= 4 and a["bucket_launches"] == launches
+    # the exposed-communication probe: one interval per step, replayed
+    # steps included (its marks are native calls inside the recorded step)
+    import math
+    assert len(a["exposed_ms"]) == steps, a["exposed_ms"]
+    assert all(math.isfinite(x) and 0.0 <= x < 1000.0 for x in a["exposed_ms"]), a["exposed_ms"]
     assert a["w0"] == b["w0"]
     import math
     for k in a["segs"]:
@@ -256,4 +261,32 @@ def test_bench_native_selftest_and_fallback(cuda, inject):
     else:
         assert st["ok"] and "fallback" not in st
         assert out["backend"] == "rccl" and out["config"]["launch_tape"] is True
+    assert out["weights_in_sync"] is True and out["value"] > 0
+    if not inject:
+        # the exposed-communication probe runs inside the taped step
+        c = out["comm"]
+        assert c["exposed_allreduce_ms"] is not None and c["exposed_allreduce_ms"] >= 0
+        assert c["collectives_per_step"] == c["buckets"] > 0
+        assert c["native_comms_live"] == 1  # the world communicator
+
+
+def test_bench_selftest_fallback_rebuilds_hierarchical(cuda):
+    """--hierarchical_copy on the native communicator builds its subgroup
+    communicators with the strategy; when the startup self-test fails (a
+    wrong sum injected), the fallback rebuilds the strategy on torch groups,
+    so NO native communicator is left (the subgroups used to keep
+    reducing on native RCCL after the self-test declared it bad)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, KFB_FORCE_PG="1", KFB_SELFTEST_INJECT="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "KFB_DIST_BACKEND", "KFB_NATIVE_COMM"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "2",
+           "--batch_size", "16", "--hierarchical_copy"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    st = out["comm"]["selftest"]
+    assert not st["ok"] and st["fallback"] and st.get("rebuilt_strategy") is True
+    # the subgroup was checked as well as the world
+    assert any(f.startswith("hier:") for f in st["failed"]), st["failed"]
+    assert out["backend"] == "nccl" and out["comm"]["native_comms_live"] == 0
     assert out["weights_in_sync"] is True and out["value"] > 0

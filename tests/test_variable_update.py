@@ -98,20 +98,63 @@ def test_two_workers(vu, kopt, agg, tmp_path):
         np.testing.assert_allclose(res[r]["losses"], expected[r], rtol=1e-5, atol=0)
 
 
-def test_two_workers_sma_keeps_models_close(tmp_path):
-    """kungfu sma: models are pulled toward the average every step, so the two
-    workers' variables end closer than with independent training."""
-    sma = run_workers(2, dict(variable_update="kungfu", kungfu_option="sma", num_batches=6,
-                              kungfu_sma_alpha=0.5), tmp_path)
-    ind = run_workers(2, dict(variable_update="independent", num_batches=6), tmp_path)
-    d_sma = np.abs(np.array(sma[0]["vars"]) - np.array(sma[1]["vars"])).sum()
-    d_ind = np.abs(np.array(ind[0]["vars"]) - np.array(ind[1]["vars"])).sum()
-    assert d_sma < d_ind
+@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("opt", ["sgd", "momentum"])
+def test_workers_sma_exact(n, opt, tmp_path):
+    """kungfu sma (SynchronousAveragingOptimizer): every step each worker
+    moves to (1 - alpha) w + alpha * mean_r(w_r), then applies its own
+    gradient - deterministic, so every worker's reported loss matches the
+    analytic oracle (tcb/benchmark_cnn_test.py:1236-1365 style)."""
+    kw = dict(variable_update="kungfu", kungfu_option="sma", num_batches=6,
+              kungfu_sma_alpha=0.3, optimizer=opt)
+    res = run_workers(n, kw, tmp_path)
+    params = tu.get_var_update_params(**kw)
+    expected = tu.manually_compute_losses(tu.get_fake_var_update_inputs(), n, params, "sma")
+    for r in range(n):
+        np.testing.assert_allclose(res[r]["losses"], expected[r], rtol=1e-5, atol=0)
+    # the averaging is real: the oracle's workers differ from independent ones
+    ind = tu.manually_compute_losses(tu.get_fake_var_update_inputs(), n, params, "none")
+    assert any(abs(a - b) > 1e-3 for a, b in zip(expected[1][1:], ind[1][1:]))
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_workers_ada_sgd_exact(n, tmp_path):
+    """kungfu ada_sgd: SMA for the first kungfu_ada_switch_step steps, then
+    synchronous SGD (mean gradient) on each worker's own weights."""
+    kw = dict(variable_update="kungfu", kungfu_option="ada_sgd", num_batches=7,
+              kungfu_sma_alpha=0.5, kungfu_ada_switch_step=3)
+    res = run_workers(n, kw, tmp_path)
+    params = tu.get_var_update_params(**kw)
+    expected = tu.manually_compute_losses(tu.get_fake_var_update_inputs(), n, params, "ada_sgd")
+    for r in range(n):
+        np.testing.assert_allclose(res[r]["losses"], expected[r], rtol=1e-5, atol=0)
+    # the switch matters: pure SMA and pure S-SGD both differ from it
+    for other in ("sma", "mean"):
+        o = tu.manually_compute_losses(tu.get_fake_var_update_inputs(), n, params, other)
+        assert any(abs(a - b) > 1e-6 for a, b in zip(expected[0], o[0])), other
+
+
+@pytest.mark.parametrize("n,seed", [(2, 0), (4, 0), (4, 5)])
+def test_workers_pair_averaging_exact(n, seed, tmp_path):
+    """kungfu async_sgd (PairAveragingOptimizer) in its lock-step mode (pull
+    at update time; all pulls before any publish; each publish committed
+    before the next step): worker r averages with the step-t model of the
+    peer its own RNG drew, w <- (w + w_peer) / 2, then applies its own
+    gradient - the oracle replays the same peer draws."""
+    kw = dict(variable_update="kungfu", kungfu_option="async_sgd", num_batches=6,
+              kungfu_pair_lockstep=True, kungfu_peer_seed=seed)
+    res = run_workers(n, kw, tmp_path)
+    params = tu.get_var_update_params(**kw)
+    expected = tu.manually_compute_losses(tu.get_fake_var_update_inputs(), n, params, "pair")
+    for r in range(n):
+        np.testing.assert_allclose(res[r]["losses"], expected[r], rtol=1e-5, atol=0)
 
 
 def test_two_workers_async_pair_averaging(tmp_path):
-    """kungfu async_sgd (PairAveraging): every worker trains and publishes;
-    models stay finite and the run completes without a global barrier per step."""
+    """kungfu async_sgd (PairAveraging), the default asynchronous mode: every
+    worker trains and publishes without a global barrier per step; models
+    stay finite and every step's loss lies between the independent and the
+    fully averaged (S-SGD) oracles' ranges."""
     res = run_workers(2, dict(variable_update="kungfu", kungfu_option="async_sgd",
                               num_batches=6), tmp_path)
     for r in res:
