@@ -206,6 +206,9 @@ def _run(a):
                                                  w.double().square().sum()]).cpu())
     sums = comm.all_gather_object(mine)
     in_sync = all(x == sums[0] for x in sums)
+    # how far the replicas drifted apart (0 for synchronous strategies; the
+    # model-averaging ones keep it small): spread of the weight sums
+    spread = max(x[0] for x in sums) - min(x[0] for x in sums)
 
     exposed = []
     if reducer is not None:
@@ -293,6 +296,7 @@ def _run(a):
             # when this approaches ms_per_step)
             "host_ms_per_step": round(1000.0 * host / a.steps, 3),
             "weights_in_sync": in_sync,
+            "replica_spread": spread,
         }
         print(json.dumps(out))
         sys.stdout.flush()

@@ -764,7 +764,7 @@ class BenchmarkCNN:
             return s * self.num_gpus
         if self.num_gpus > 1:
             return s
-        return s * (self.world.size if self.strategy.reduces_gradients else 1)
+        return s * (self.world.size if self.strategy.aggregates_gradients else 1)
 
     def _auto_loss_scale_check(self) -> bool:
         """Dynamic loss scaling (tcb/variable_mgr_util.py:51-139): halve the

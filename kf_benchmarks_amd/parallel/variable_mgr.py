@@ -66,6 +66,12 @@ class Strategy:
     def grad_scale(self) -> float:
         return self.tower_scale
 
+    @property
+    def aggregates_gradients(self) -> bool:
+        """Whether this step's applied gradient is a sum over workers (then
+        it carries every worker's L2 term; see BenchmarkCNN._l2_multiplier)."""
+        return self.reduces_gradients
+
     def broadcast_initial_model(self, slots=()):
         """Rank-0 broadcast of every variable (+ optimizer slots, BN stats):
         what horovod.broadcast_global_variables(0) / kungfu broadcast do at
@@ -263,6 +269,11 @@ class KungFuAdaSGD(Strategy):
     @property
     def grad_scale(self):
         return 1.0 / self.world.size if self._step >= self.switch_step else 1.0
+
+    @property
+    def aggregates_gradients(self):
+        # the averaging phase applies each worker's own gradient
+        return self._step >= self.switch_step
 
     def before_backward(self, step):
         self._step = step

@@ -52,6 +52,7 @@ def main():
             gsegs.append({name: g[off:off + n].double().sum().item()
                           for name, _, off, n in bench.flat.segments()})
         bench.strategy.after_backward = after_backward
+    torn = _inject_torn_snapshot(bench, comm.get_world().rank)
     losses = []
     for _ in range(steps):
         loss, _ = bench.train_step(need_loss=True)
@@ -113,9 +114,60 @@ def main():
         res["pa_publishes"] = bench.strategy.store.publishes
         res["pa_retries"] = bench.strategy.store.retries
         bench.strategy.close()  # collective: no peer is still reading our slots
+        res["pa_torn"] = bench.strategy.torn_snapshots
+        res["torn_check"] = torn
     with open(out, "w") as f:
         json.dump(res, f)
     comm.get_world().shutdown()
+
+
+def _inject_torn_snapshot(bench, rank):
+    """KFB_TEST_TORN_STEP=s (rank 0, PairAveraging): at step s the pull's
+    expected sequence word is off by one publish, as if the peer rewrote the
+    slot during the copy; the device seqlock check must reject the snapshot
+    and the fused update skip the averaging.  Records the update's inputs
+    and output at that step (filled in as the step runs)."""
+    import torch
+    s = int(os.environ.get("KFB_TEST_TORN_STEP", "-1"))
+    st = bench.strategy
+    out = {}
+    if s < 0 or rank != 0 or getattr(st, "store", None) is None:
+        return out
+    store = st.store
+    orig_pv = store.pull_values
+
+    def pull_values(peer):
+        v = orig_pv(peer)
+        if bench.global_step == s:
+            v = dict(v, pa_seq=v["pa_seq"] + 2)
+        return v
+    store.pull_values = pull_values
+    opt = bench.optimizer
+    orig_step = opt.step
+
+    def step(lr, grad_scale=1.0, weight_decay=0.0, clip=None, grad=None, mix=None, wout=None,
+             **k):
+        if bench.global_step != s:
+            return orig_step(lr, grad_scale, weight_decay, clip, grad, mix, wout, **k)
+        torch.cuda.synchronize()
+        w = bench.flat.flat.detach().clone()
+        g = bench.flat.grad.detach().clone()
+        peer = mix[0].detach().clone()
+        r = orig_step(lr, grad_scale, weight_decay, clip, grad, mix, wout, **k)
+        torch.cuda.synchronize()
+        post = bench.flat.flat.detach()
+        gk = g * grad_scale
+        nomix = w - lr * (gk + weight_decay * w)
+        avg = 0.5 * w + 0.5 * peer
+        withmix = avg - lr * (gk + weight_decay * w)
+        scale = float(post.abs().max())
+        out.update(err_nomix=float((post - nomix).abs().max()) / scale,
+                   err_mix=float((post - withmix).abs().max()) / scale,
+                   peer_differs=bool(float((peer - w).abs().max()) > 0),
+                   ok_flag=int(mix[3].item()) if mix[3] is not None else None)
+        return r
+    opt.step = step
+    return out
 
 
 if __name__ == "__main__":

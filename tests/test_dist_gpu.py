@@ -194,6 +194,24 @@ def test_two_ranks_pair_averaging_training(cuda, tmp_path):
         assert all(l == l and abs(l) < 1e3 for l in r["losses"])
 
 
+def test_pair_averaging_torn_snapshot_skips_averaging(cuda, tmp_path):
+    """PairAveraging's device-side torn-snapshot guard: rank 0's pull at
+    step 3 sees a sequence word that moved during the copy (injected); the
+    seqlock check kernel clears the flag, the fused update applies the plain
+    gradient step without the averaging, and the rejection is counted.  The
+    steps around it average normally (lock-step mode, 2 ranks, 1 GPU)."""
+    kw = dict(model="trivial", batch_size=16, num_gpus=1, use_bf16=True, optimizer="sgd",
+              data_format="NHWC", variable_update="kungfu", kungfu_option="async_sgd",
+              kungfu_pair_lockstep=True)
+    env = dict(KFB_TEST_TORN_STEP="3", KFB_TEST_GRAD_SEGS=None)
+    r0, r1 = _run(kw, 5, tmp_path, env_extra=env)
+    t = r0["torn_check"]
+    assert t["ok_flag"] == 0 and t["peer_differs"], t
+    assert t["err_nomix"] < 1e-6 < t["err_mix"], t
+    assert r0["pa_torn"] == 1 and r1["pa_torn"] == 0
+    assert r0["pa_publishes"] == r1["pa_publishes"] == 5
+
+
 @pytest.mark.parametrize("option", ["sma", "ada_sgd"])
 def test_one_rank_rccl_model_averaging_taped(cuda, tmp_path, option):
     """KungFu SMA / ada_sgd through the native 1-rank RCCL communicator from
