@@ -138,11 +138,6 @@ def _run(a):
                       datasets_repeat_cached_sample=bool(a.data_dir),
                       synthetic_resample=not a.reuse_synthetic)
     bench = BenchmarkCNN(p)
-    if cuda and os.environ.get("KFB_COMPUTE_PRIORITY", "0") == "1":
-        # compute stream at high priority (see BenchmarkCNN.run)
-        prio = torch.cuda.Stream(device=bench.device, priority=-1)
-        prio.wait_stream(torch.cuda.current_stream(bench.device))
-        torch.cuda.set_stream(prio)
     bench.build()
     world = comm.get_world()
     if world.size != a.gpus:

@@ -131,8 +131,10 @@ def validate_params_combinations(params):
             raise ValueError("Automatic loss scaling is not supported with staged_vars.")
     if p.debugger is not None and p.debugger != "cli" and ":" not in p.debugger:
         raise ValueError('--debugger must be "cli" or in the form host:port')
-    if p.hierarchical_copy and p.num_gpus <= 1 and comm.env_world_size() <= 1:
-        # (one process per GPU: the ranks of the world are the devices)
+    if p.hierarchical_copy and p.num_gpus <= 1 and comm.env_world_size() <= 1 \
+            and not comm.force_pg():
+        # (one process per GPU: the ranks of the world are the devices; a
+        # forced 1-rank group is the GPU tests' stand-in)
         raise ValueError("--hierarchical_copy requires --num_gpus to be greater than 1")
     if p.save_model_secs and p.save_model_steps:
         raise ValueError("At most one of --save_model_secs and --save_model_steps can be "
@@ -282,8 +284,10 @@ class BenchmarkCNN:
         # the compute GPU and the RCCL communicator's GPU come from ONE
         # function (comm.select_device_index), decided before the world exists
         env_size = comm.env_world_size()
+        # (KFB_FORCE_PG=1 with one rank: the GPU tests' single-tower stand-in
+        # for the mode, over a real 1-rank RCCL group)
         self.tower_mode = (os.environ.get("KFB_TOWER_GROUP") == "1" and self.num_gpus > 1
-                           and env_size == self.num_gpus)
+                           and (env_size == self.num_gpus or (env_size == 1 and comm.force_pg())))
         dev_index = None
         if self.device_type == "cuda":
             dev_index = comm.select_device_index(self.gpu_indices, self.num_gpus, self.tower_mode,
@@ -536,8 +540,6 @@ class BenchmarkCNN:
         p = self.params
         if self.device_type != "cuda" or p.kernel_impl != "hip":
             return "not a HIP device run"
-        if self.tower_mode:
-            return "tower processes average the reported loss on the host"
         if self.world.communicates:
             if self.world.native is None and self.strategy.steps_use_collectives():
                 return "device collectives go through torch.distributed (not recordable)"
@@ -614,6 +616,8 @@ class BenchmarkCNN:
             self.input.tape_post()
             log_fn("launch tape: recorded %d native calls (per-step arguments: %s)"
                    % (len(t.recorder), ", ".join(t.recorder.keys()) or "none"))
+            if need_loss and self.tower_mode:
+                loss = self._tower_mean(loss)
             return loss, acc
         p = self.params
         step = self.global_step
@@ -630,7 +634,17 @@ class BenchmarkCNN:
         loss = self._tape_loss
         if l2 is not None:
             loss = loss + len(self.devices) * p.weight_decay * l2
+        if need_loss and self.tower_mode:
+            loss = self._tower_mean(loss)
         return loss, None
+
+    def _tower_mean(self, loss):
+        """The reported loss of one worker is the mean over its towers (the
+        tower processes): a one-element all-reduce outside the recorded step,
+        issued by every tower at the same steps (the display schedule)."""
+        lt = loss.detach().reshape(1).float().clone()
+        comm.all_reduce(lt)
+        return lt[0] / self.world.size
 
     def train_step(self, need_loss=False, need_accuracy=False):
         """One full training step; returns (loss_tensor, accuracy_dict)."""
@@ -664,10 +678,7 @@ class BenchmarkCNN:
             # the reported total loss uses the weights of this step's forward
             loss = loss + len(self.devices) * p.weight_decay * self.l2_loss_value()
         if need_loss and self.tower_mode:
-            # the reported loss of one worker is the mean over its towers
-            lt = loss.detach().reshape(1).float().clone()
-            comm.all_reduce(lt)
-            loss = lt[0] / self.num_gpus
+            loss = self._tower_mean(loss)
         grad_scale = self.strategy.grad_scale
         if self.loss_scale:
             grad_scale /= self.loss_scale
@@ -702,11 +713,11 @@ class BenchmarkCNN:
         self.global_step += 1
         return loss, acc
 
-    # KFB_EARLY_UPDATE=1: the update of all but the stem's variables runs on
-    # the weight-gradient stream beside the stem's backward.  Off: both are
-    # HBM-bound (the update moves ~560 MB on ResNet-50), so the overlap saves
-    # nothing and the split costs 0.08 ms/step (profiles/r8_early_update_ab.txt)
-    _EARLY_UPDATE = os.environ.get("KFB_EARLY_UPDATE", "0") == "1"
+    # The update of all but the stem's variables on the weight-gradient stream
+    # beside the stem's backward: off.  Both are HBM-bound (the update moves
+    # ~560 MB on ResNet-50), so the overlap saves nothing and the split costs
+    # 0.08 ms/step (profiles/r8_early_update_ab.txt)
+    _EARLY_UPDATE = False
 
     def _early_update_args(self, step):
         """The optimizer arguments of this step's update if part of it may run
@@ -796,16 +807,8 @@ class BenchmarkCNN:
 
     # ------------------------------------------------------------------- run
     def run(self):
-        if self.device_type == "cuda" and os.environ.get("KFB_COMPUTE_PRIORITY", "0") == "1":
-            # the compute stream at high priority: the hardware dispatches its
-            # workgroups ahead of the weight-gradient side stream's, which then
-            # fills the CUs the dgrad chain leaves idle (A/B knob)
-            stream = torch.cuda.Stream(device=self.device, priority=-1)
-            stream.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(stream):
-                out = self._run()
-            torch.cuda.current_stream(self.device).wait_stream(stream)
-            return out
+        # (a high-priority compute stream, dispatching ahead of the
+        # weight-gradient side stream, measured neutral and is not used)
         return self._run()
 
     def _run(self):

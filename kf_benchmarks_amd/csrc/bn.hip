@@ -1258,14 +1258,9 @@ bn_pool3s2_k(const T* __restrict__ dz, const T* __restrict__ z, const uint8_t* _
 // bs256 stage 1: 4.3 -> 5.6 TB/s in isolation, +1% on the step); below that
 // the grid-stride passes run (isolated rates within +-5%, but the flat grids
 // cost ResNet-152 bs128 ~6% beside the weight-gradient stream).
-// KFB_BN_FLAT=0: never flat; KFB_BN_FLAT=2: flat at every size.
-static int bn_flat_mode() {
-  static const int m = [] {
-    const char* e = getenv("KFB_BN_FLAT");
-    return e ? atoi(e) : 1;
-  }();
-  return m;
-}
+// (mode 1 of the round-2 A/B: flat above the size threshold; 0 = never and
+// 2 = every size both lost)
+static int bn_flat_mode() { return 1; }
 
 static bool flat_ok(long nvec, int C, int V) {
   const int cv = C / V;
@@ -1310,46 +1305,28 @@ static void launch_bwd_apply(int gb, hipStream_t stream, const void* dy, const v
                        Cc);
 }
 
-// KFB_BN_FOLD_BWD (or kfb_bn_set_fold_bwd): the backward apply passes fold
-// their conv-epilogue partials (bn_bwd_apply_fold_k) instead of a finalize
-// launch - 1 (default): tensors up to KFB_BN_FOLD_MAXMB (32 MB), 2: every
-// size, 0: never.  On the large tensors the slice layout streams slower
+// kfb_bn_set_fold_bwd (tests): the backward apply passes fold their
+// conv-epilogue partials (bn_bwd_apply_fold_k) instead of a finalize launch -
+// 1 (default): tensors up to 32 MB, 2: every size, 0: never.  On the large tensors the slice layout streams slower
 // than the grid-stride / flat passes (every size: ResNet-50 bs256 +0.1
 // ms/step; up to 16 or 32 MB: -0.09 ms, profiles/r12_bn_fold_bwd.txt); on
 // the small ones the launch it removes waits for a dispatch slot beside the
 // weight-gradient stream (ResNet-152 bs32 2,515 -> 2,581-2,606 img/s).
-static int g_fold_bwd = -1;
+static int g_fold_bwd = 1;
 
 static bool fold_bwd_ok(int V, int nslab, int C, long rows) {
-  if (g_fold_bwd < 0) {
-    const char* e = getenv("KFB_BN_FOLD_BWD");
-    g_fold_bwd = e ? atoi(e) : 1;
-  }
-  static const long max_bytes = [] {
-    const char* e = getenv("KFB_BN_FOLD_MAXMB");
-    return (long)((e ? atof(e) : 32.0) * (1 << 20));
-  }();
+  constexpr long max_bytes = 32L << 20;  // (16 / 32 / 64 / 128 MB measured alike)
   return g_fold_bwd && V == 8 && nslab == FS_SLOTS && C % FS_C == 0 && rows > 0 &&
          (g_fold_bwd == 2 || rows * C * 2 <= max_bytes);
 }
 
-// KFB_BN_FOLD_R=0: the dual backward's second BN keeps its finalize launch
-// even when its partials could be folded (A/B switch)
-static int g_fold_r = -1;  // -1: from the environment
-static bool fold_r_on() {
-  if (g_fold_r < 0) {
-    const char* e = getenv("KFB_BN_FOLD_R");
-    g_fold_r = (e && atoi(e) == 0) ? 0 : 1;
-  }
-  return g_fold_r != 0;
-}
+// kfb_bn_set_fold_r(0) (tests): the dual backward's second BN keeps its
+// finalize launch even when its partials could be folded
+static int g_fold_r = 1;
+static bool fold_r_on() { return g_fold_r != 0; }
 
 static int fold_bwd_grid(long rows, int C) {
-  static const long target = [] {
-    const char* e = getenv("KFB_BN_FOLD_WGS");
-    const long v = e ? atol(e) : 1024;
-    return v < 64 ? 64L : v > 8192 ? 8192L : v;
-  }();
+  constexpr long target = 1024;  // workgroups (256-thread blocks measured slower)
   const int ns = C / FS_C;
   long nrb = target / ns;
   const long need = (rows + 63) / 64;  // two 32-row groups per iteration
@@ -1400,7 +1377,7 @@ hipError_t bn_finalize_grad_launch(const float* slots, int C, long rows, const f
 
 
 // test / A/B hook: 1 folds the dual backward's second-BN finalize into the
-// apply pass when its partials allow it (KFB_BN_FOLD_R)
+// apply pass when its partials allow it
 KFB_API void kfb_bn_set_fold_r(int on) { kfb::g_fold_r = on ? 1 : 0; }
 KFB_API int kfb_bn_get_fold_r() { return kfb::fold_r_on() ? 1 : 0; }
 

@@ -1531,7 +1531,7 @@ struct SkArgs {
   int* cnt;   // [Tsk] tickets, zero between launches
   int T, nk, Tdp;
   long L;     // Tsk * nk: K steps of the stream-K region
-  int probe;  // KFB_SK_PROBE=1 (timing probe only, wrong results): no fix-up
+  int probe;  // 1 (timing probe only, wrong results): no fix-up
 };
 
 // workgroup whose range holds step i of the stream-K region (P ranges of L)
@@ -1774,20 +1774,13 @@ struct WgArgs {
   FastDiv fd_ohw, fd_ow;  // WG_GENERIC: the per-step row -> (img, oh, ow)
 };
 
-#ifndef KFB_WG_BK
-#define KFB_WG_BK 32
-#endif
-constexpr int WG_BK = KFB_WG_BK;  // reduction rows per step (64 measured no faster)
+constexpr int WG_BK = 32;  // reduction rows per step (64 measured no faster)
 // waves per SIMD the wgrad register budget is sized for: 2 lets the 128x128
 // tiles use 134-142 VGPRs (3 workgroups per CU); 4 (<= 128 VGPRs) spills in
 // the main loop and measured 2.5x slower on the 1x1 wgrads
 // (profiles/r5_wgrad_occupancy_ab.txt)
-#ifndef KFB_WG_OCC
-#define KFB_WG_OCC 2
-#endif
-#ifndef KFB_WG_XCD
-#define KFB_WG_XCD 1
-#endif
+#define WG_OCC 2
+constexpr bool WG_XCD = true;  // XCD-aware workgroup order (r4_wgrad_xcd_ab.txt)
 
 // 256-byte rows (128 elements); 32-byte unit u (0..7) of row r stored at
 // u ^ f(r), f(r) = (r & 3) | ((r >> 3) & 1) << 2.
@@ -1811,7 +1804,7 @@ __device__ __forceinline__ v4s ds_read_tr(const T* p) {
 enum { WG_GENERIC = 0, WG_GATHER = 1, WG_PLAIN = 2 };
 
 template <typename T, int BMC, int BNK, int MODE>
-__global__ void __launch_bounds__(256, KFB_WG_OCC) wgrad_k(WgArgs a) {
+__global__ void __launch_bounds__(256, WG_OCC) wgrad_k(WgArgs a) {
   // BMC = output-channel tile (rows of dW), BNK = k tile (cols of dW); both 128 or 64.
   constexpr int TN = BMC / 32, TM = BNK / 32;
   constexpr int DC = WG_BK * BMC / 8 / 256;  // dy chunks per thread
@@ -1827,7 +1820,7 @@ __global__ void __launch_bounds__(256, KFB_WG_OCC) wgrad_k(WgArgs a) {
   // dy rows and overlapping x rows) get consecutive remapped ids, i.e. one
   // XCD and its L2; the hardware's round-robin order spread them over 8 L2s
   // (4-11% L2 hit rate on the 56x56 3x3 wgrad).
-  const int bid = KFB_WG_XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int bid = WG_XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   const int split = bid / tiles;
   const int tile = bid - split * tiles;
   const int c0 = (tile / ktiles) * BMC, k0 = (tile % ktiles) * BNK;
@@ -2069,7 +2062,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_glds_k(WgArgs a) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ctiles = (a.Ncol + BMC - 1) / BMC, ktiles = (a.Ktot + BNK - 1) / BNK;
   const int tiles = ctiles * ktiles;
-  const int bid = KFB_WG_XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int bid = WG_XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   const int split = bid / tiles;
   const int tile = bid - split * tiles;
   const int c0 = (tile / ktiles) * BMC, k0 = (tile % ktiles) * BNK;
@@ -2274,10 +2267,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce_grouped_k(const float* __res
 // order (no grouped atomic fold); for bitwise run-to-run comparisons
 static int g_deterministic = 0;
 
-static bool igemm_fast_disabled() {
-  static const bool off = getenv("KFB_IGEMM_NOFAST") != nullptr;  // A/B switch
-  return off;
-}
+static bool igemm_fast_disabled() { return false; }
 
 template <typename T>
 static void launch_glds_tall(const IgArgs& a, bool wide, hipStream_t s) {
@@ -2443,7 +2433,7 @@ static hipError_t launch_sk(const IgArgs& a, hipStream_t s) {
   const int Tsk = tiles < P ? tiles : (tiles % P == 0 ? 0 : P + tiles % P);
   sk.Tdp = tiles - Tsk;
   sk.L = (long)Tsk * sk.nk;
-  static const int probe = getenv("KFB_SK_PROBE") ? atoi(getenv("KFB_SK_PROBE")) : 0;
+  const int probe = 0;  // (1: timing probe without the fix-up; 2: + geometry print)
   sk.probe = probe;
   const int grid = (sk.Tdp > 0 || sk.L >= P) ? P : (int)sk.L;
   if (grid < 1) return hipSuccess;

@@ -568,14 +568,10 @@ static int g_s1_grid_force = 0;  // test hook: workgroups per launch (0 = one pe
 // SIMD leaves exposed - except the K = 64 data gradient: at one workgroup
 // its output stores go through the LDS staging (no room beside two rings),
 // 291 -> 279 us at 56x56, ResNet-50 -0.06 ms/step on 4 interleaved pairs
-// (profiles/r12_s1_staged_stores.txt); KFB_S1_WPC=1 forces one
+// (profiles/r12_s1_staged_stores.txt)
 static int s1_wpc(int K, bool dg) {
-  static const int force = [] {
-    const char* e = getenv("KFB_S1_WPC");
-    return e ? atoi(e) : 0;
-  }();
   const bool two = dg ? K == 256 : K <= 256;
-  return (force == 1 || !two) ? 1 : 2;
+  return two ? 2 : 1;
 }
 
 static int s1_grid(int tiles, int nsl, int wpc) {

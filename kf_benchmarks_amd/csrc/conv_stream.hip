@@ -664,7 +664,7 @@ hipError_t launch_conv_s3(int dtype, const IgArgs& a, hipStream_t stream) {
     else if (a.mcoef) mask = 3;
   }
   if (epi == s3::EPI_STATS && (a.bias || a.relu)) return hipErrorInvalidValue;
-#define KFB_S3_LAUNCH(T)                                                                      \
+#define S3_LAUNCH_CASES(T)                                                                      \
   switch (epi * 4 + mask) {                                                                   \
     case 0: hipLaunchKernelGGL((s3::conv_s3_k<T, 0, 0>), dim3(grid), dim3(256), 0, stream, a, g); break; \
     case 4: hipLaunchKernelGGL((s3::conv_s3_k<T, 1, 0>), dim3(grid), dim3(256), 0, stream, a, g); break; \
@@ -673,13 +673,13 @@ hipError_t launch_conv_s3(int dtype, const IgArgs& a, hipStream_t stream) {
     default: return hipErrorInvalidValue;                                                      \
   }
   if (dtype == BF16) {
-    KFB_S3_LAUNCH(bf16)
+    S3_LAUNCH_CASES(bf16)
   } else if (dtype == F16) {
-    KFB_S3_LAUNCH(f16)
+    S3_LAUNCH_CASES(f16)
   } else {
     return hipErrorInvalidValue;
   }
-#undef KFB_S3_LAUNCH
+#undef S3_LAUNCH_CASES
   return hipGetLastError();
 }
 

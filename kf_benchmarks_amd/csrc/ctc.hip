@@ -147,17 +147,29 @@ __global__ void __launch_bounds__(NT) ctc_k(Args a) {
 
 // dz = grad * gloss[b] (gloss: the upstream gradient of each sequence's loss)
 template <typename T>
+// dz = grad * gloss[b * gstride] * mul (gstride 0: one scalar gradient for
+// every sequence, e.g. the backward of the batch-mean loss)
 __global__ void __launch_bounds__(256) scale_k(const float* __restrict__ grad,
                                                const float* __restrict__ gloss, T* __restrict__ dz,
-                                               long ldt, long ldb, int T_, int B, int C) {
+                                               long ldt, long ldb, int T_, int B, int C,
+                                               int gstride, float mul) {
   const long n = (long)T_ * B * C;
   for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
     const int c = (int)(e % C);
     const long r = e / C;
     const int b = (int)(r % B), t = (int)(r / B);
     const long off = t * ldt + b * ldb + c;
-    dz[off] = (T)(grad[off] * gloss[b]);
+    dz[off] = (T)(grad[off] * (gloss[b * gstride] * mul));
   }
+}
+
+// Input lengths on the logits' time axis: out = in * num / den (integer
+// division, as the reference's length scaling), on the device so a
+// recorded step holds no host or torch arithmetic.
+__global__ void scale_lengths_k(const int* __restrict__ in, int* __restrict__ out, int n, int num,
+                                int den) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (int)(((long long)in[i] * num) / den);
 }
 
 }  // namespace ctc
@@ -192,6 +204,28 @@ KFB_API hipError_t kfb_ctc_grad_scale(int dtype, const float* grad, const float*
   if (blocks > 4096) blocks = 4096;
   KFB_DISPATCH_DTYPE(dtype, T_,
                      hipLaunchKernelGGL(ctc::scale_k<T_>, dim3((unsigned)blocks), dim3(256), 0,
-                                        stream, grad, gloss, (T_*)dz, ldt, ldb, T, B, C));
+                                        stream, grad, gloss, (T_*)dz, ldt, ldb, T, B, C, 1, 1.f));
+  return hipGetLastError();
+}
+
+// Backward of mean_b(loss_b): dz = grad * g[0] * inv_count.
+KFB_API hipError_t kfb_ctc_grad_scale_mean(int dtype, const float* grad, const float* g, void* dz,
+                                           long ldt, long ldb, int T, int B, int C,
+                                           float inv_count, hipStream_t stream) {
+  const long n = (long)T * B * C;
+  long blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  KFB_DISPATCH_DTYPE(dtype, T_,
+                     hipLaunchKernelGGL(ctc::scale_k<T_>, dim3((unsigned)blocks), dim3(256), 0,
+                                        stream, grad, g, (T_*)dz, ldt, ldb, T, B, C, 0,
+                                        inv_count));
+  return hipGetLastError();
+}
+
+KFB_API hipError_t kfb_ctc_scale_lengths(const int* in, int* out, int n, int num, int den,
+                                         hipStream_t stream) {
+  if (n <= 0 || den <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ctc::scale_lengths_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                     in, out, n, num, den);
   return hipGetLastError();
 }

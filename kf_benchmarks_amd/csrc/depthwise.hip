@@ -203,7 +203,7 @@ KFB_API hipError_t kfb_dw_wgrad(int dtype, const void* dy, const void* x, float*
   if (ppb < 1024) ppb = 1024;
   blocks_x = (M + ppb - 1) / ppb;
   const dim3 grid((unsigned)blocks_x, (unsigned)groups);
-#define KFB_DW_W(KM)                                                                        \
+#define DW_WGRAD_LAUNCH(KM)                                                                        \
   KFB_DISPATCH_DTYPE(dtype, T, {                                                            \
     if (vw == 4)                                                                            \
       hipLaunchKernelGGL((dw_wgrad_k<T, 4, KM>), grid, dim3(256), 0, stream, (const T*)dy,  \
@@ -216,12 +216,12 @@ KFB_API hipError_t kfb_dw_wgrad(int dtype, const void* dy, const void* x, float*
                          (const T*)x, dw, g, ppb);                                           \
   })
   if (KH * KW <= 9) {
-    KFB_DW_W(9);
+    DW_WGRAD_LAUNCH(9);
   } else if (KH * KW <= 25) {
-    KFB_DW_W(25);
+    DW_WGRAD_LAUNCH(25);
   } else {
-    KFB_DW_W(49);
+    DW_WGRAD_LAUNCH(49);
   }
-#undef KFB_DW_W
+#undef DW_WGRAD_LAUNCH
   return hipGetLastError();
 }

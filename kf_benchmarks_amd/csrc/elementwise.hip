@@ -370,8 +370,7 @@ KFB_API hipError_t kfb_act_bwd_bias(int dtype, const void* dy, const void* y, vo
   // Without a bias gradient the slab count is free: size the grid for the
   // whole tensor (callers pass nslab = 1 there, which left one workgroup per
   // channel chunk streaming every row, ~1.3 ms per NASNet ReLU backward).
-  static const bool one_slab = getenv("KFB_ACT_BWD_ONESLAB") != nullptr;  // A/B knob
-  if (!db && !one_slab) nslab = kfb_colsum_num_slabs(rows, C);
+  if (!db) nslab = kfb_colsum_num_slabs(rows, C);
   KFB_DISPATCH_DTYPE(dtype, T, {
     KFB_DISPATCH_VEC(V, VV, {
       const int cw = C < 256 * VV ? C : 256 * VV;

@@ -228,14 +228,14 @@ static int pgrid(long total) {
 
 using namespace kfb;
 
-#define KFB_POOL_GEO                                                                   \
+#define POOL_GEO_ARGS                                                                   \
   PoolGeo g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};                               \
   const int V = vec_width(C);
 
 KFB_API hipError_t kfb_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int N, int H,
                                    int W, int C, int OH, int OW, int kh, int kw, int sh, int sw,
                                    int pt, int pl, hipStream_t stream) {
-  KFB_POOL_GEO
+  POOL_GEO_ARGS
   if (kh * kw > 255) return hipErrorInvalidValue;
   KFB_DISPATCH_DTYPE(dtype, T, {
     KFB_DISPATCH_VEC(V, VV, {
@@ -250,7 +250,7 @@ KFB_API hipError_t kfb_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* i
 KFB_API hipError_t kfb_maxpool_bwd(int dtype, const void* dy, const uint8_t* idx, void* dx, int N,
                                    int H, int W, int C, int OH, int OW, int kh, int kw, int sh,
                                    int sw, int pt, int pl, hipStream_t stream) {
-  KFB_POOL_GEO
+  POOL_GEO_ARGS
   KFB_DISPATCH_DTYPE(dtype, T, {
     KFB_DISPATCH_VEC(V, VV, {
       const long total = (long)N * H * W * (C / VV);
@@ -264,7 +264,7 @@ KFB_API hipError_t kfb_maxpool_bwd(int dtype, const void* dy, const uint8_t* idx
 KFB_API hipError_t kfb_avgpool_fwd(int dtype, const void* x, void* y, int N, int H, int W, int C,
                                    int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl,
                                    hipStream_t stream) {
-  KFB_POOL_GEO
+  POOL_GEO_ARGS
   KFB_DISPATCH_DTYPE(dtype, T, {
     KFB_DISPATCH_VEC(V, VV, {
       const long total = (long)N * OH * OW * (C / VV);
@@ -278,7 +278,7 @@ KFB_API hipError_t kfb_avgpool_fwd(int dtype, const void* x, void* y, int N, int
 KFB_API hipError_t kfb_avgpool_bwd(int dtype, const void* dy, void* dx, int N, int H, int W, int C,
                                    int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl,
                                    hipStream_t stream) {
-  KFB_POOL_GEO
+  POOL_GEO_ARGS
   KFB_DISPATCH_DTYPE(dtype, T, {
     KFB_DISPATCH_VEC(V, VV, {
       const long total = (long)N * H * W * (C / VV);

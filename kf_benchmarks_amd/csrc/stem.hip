@@ -231,8 +231,7 @@ KFB_API hipError_t kfb_s2d_stem(int dtype, const void* x, void* x2, int N, int H
   if (C > 4 || KH > 8 || (W * C * esz) % 4 || W * C * esz > 4 * S2D_ROW_DW ||
       ((uintptr_t)x & 3))
     return hipErrorInvalidValue;
-  static const bool generic = getenv("KFB_S2D_GENERIC") != nullptr;  // A/B switch
-  if (C == 3 && esz == 2 && 3 * OW2 <= S2D3_Q && !generic) {
+  if (C == 3 && esz == 2 && 3 * OW2 <= S2D3_Q) {
     if (dtype == BF16)
       hipLaunchKernelGGL((s2d_stem3_k<bf16>), dim3(N * OH), dim3(256), 0, stream, (const bf16*)x,
                          (bf16*)x2, H, W, OH, OW2, KH, pt, pl);

@@ -209,11 +209,7 @@ static hipError_t replay_raw(const Raw& r) {
   }
 }
 
-// KFB_TAPE_BIND=0: replay every cross-stream wait as record + wait
-static const bool g_bind = [] {
-  const char* e = getenv("KFB_TAPE_BIND");
-  return !(e && atoi(e) == 0);
-}();
+static const bool g_bind = true;  // (off: every wait replayed as record + wait)
 
 // A cross-stream wait recorded right after a kernel launch on its source
 // stream (nothing else issued on that stream in between) is replayed by

@@ -31,23 +31,23 @@ from ..ops import nn as F
 from .layers import AffineLayer, BatchNormLayer, ConvLayer, DepthwiseConvLayer
 
 
-# Independent branches (ResNet projection shortcuts) on a side stream with
-# KFB_SIDE_BRANCHES=1.  Off by default: interleaved A/B on ResNet-50 bs256
-# measured 12150 (off) vs 12115 img/s (on) - the four projection branches are
-# short next to the stream synchronization they add.
-_SIDE_BRANCHES = os.environ.get("KFB_SIDE_BRANCHES", "0") == "1"
-# conv(defer_bn=True) returns the BN unapplied (KFB_DEFER_BN=0: always apply)
-_DEFER_BN = os.environ.get("KFB_DEFER_BN", "1") != "0"
-# KFB_POOL_LINKS=0: a pool consuming a BN output disables that BN's fused
-# backward (the pre-pool-link behaviour; A/B switch)
-_POOL_LINKS = os.environ.get("KFB_POOL_LINKS", "1") != "0"
-# KFB_CONCAT_LINKS=1: concat outputs get an accumulation-only link (their
-# consumers' gradients sum in the last conv's dgrad epilogue).  Off by default:
-# Inception-v3 drops 112 of 124 adds per 4 steps (-0.45 ms/step GPU time) but
-# the Python link bookkeeping (events, stream waits) costs host time in these
-# host-bound models: wall time unchanged on Inception-v3, -2% on GoogLeNet
+# Independent branches (ResNet projection shortcuts) on a side stream: off
+# (interleaved A/B on ResNet-50 bs256 measured 12150 (off) vs 12115 img/s (on)
+# - the four projection branches are short next to the stream
+# synchronization they add).
+_SIDE_BRANCHES = False
+# conv(defer_bn=True) returns the BN unapplied (tests/test_model_gpu.py
+# compares it against always applying)
+_DEFER_BN = True
+# a pool consuming a BN output keeps that BN's fused backward (pool links)
+_POOL_LINKS = True
+# Concat outputs with an accumulation-only link (their consumers' gradients
+# summed in the last conv's dgrad epilogue): off.  Inception-v3 drops 112 of
+# 124 adds per 4 steps (-0.45 ms/step GPU time) but the Python link
+# bookkeeping (events, stream waits) costs host time in these host-bound
+# models: wall time unchanged on Inception-v3, -2% on GoogLeNet
 # (profiles/r4_concat_links_ab.txt)
-_CONCAT_LINKS = os.environ.get("KFB_CONCAT_LINKS", "0") == "1"
+_CONCAT_LINKS = False
 _BRANCH_STREAMS = {}
 
 
@@ -402,7 +402,7 @@ class ConvNetBuilder:
         """A tensor read by several branches (a concat output; the fused stem
         BN+ReLU+max-pool output): an accumulation-only BNLink, so its
         consumers' gradients sum in the last conv's dgrad epilogue instead of
-        autograd's separate adds.  Concat outputs only with KFB_CONCAT_LINKS=1
+        autograd's separate adds.  Concat outputs only with _CONCAT_LINKS
         (measured neutral there); ``always`` for the stem (one 103 MB add per
         ResNet step)."""
         if (_CONCAT_LINKS or always) and y.is_cuda and getattr(y, "_kfb_bn_link", None) is None:

@@ -101,8 +101,9 @@ class _ConvBN(nn.Module):
 
     def forward(self, x):  # x NHWC [B, T, F, C]
         ph, pw = self.pad
-        y = F_ops.conv2d(x, self.weight, None, self.stride, (ph, ph, pw, pw))
-        y = torch.clamp(y, 0.0, 6.0)  # relu6 before BN, as the reference
+        y = F_ops.conv2d(x, self.weight, getattr(self, "weight_lp", None), self.stride,
+                         (ph, ph, pw, pw))
+        y = F_ops.activation(y, "relu6")  # relu6 before BN, as the reference
         return self.bn(y)
 
 
@@ -128,7 +129,8 @@ class _RNNLayer(nn.Module):
         self.wh = nn.Parameter(wh.to(device))
 
     def forward(self, x):  # [T, B, din] -> [T, B, dirs*H]
-        return rnn_ops.rnn_layer(x, self.wx, self.bx, self.wh, self.kind, self.dirs, self.hidden)
+        return rnn_ops.rnn_layer(x, self.wx, self.bx, self.wh, self.kind, self.dirs, self.hidden,
+                                 wx_lp=getattr(self.wx, "_kfb_lp", None))
 
 
 class DeepSpeech2(nn.Module):
@@ -165,7 +167,8 @@ class DeepSpeech2(nn.Module):
         for bn, rnn in zip(self.bns, self.rnns):
             x = rnn(bn(x))
         x = self.final_bn(x)
-        logits = F_ops.linear(x.reshape(T * B, -1), self.fc_weight, self.fc_bias)
+        logits = F_ops.linear(x.reshape(T * B, -1), self.fc_weight, self.fc_bias,
+                              w_lp=getattr(self.fc_weight, "_kfb_lp", None))
         # [B, T, C] view of the time-major logits
         return model_lib.BuildNetworkResult(logits=logits.view(T, B, -1).transpose(0, 1),
                                             extra_info=None)
@@ -220,9 +223,9 @@ class DeepSpeech2Model(model_lib.ModuleModel):
         logits = build_network_result.logits  # [B, T', nclass] (time-major storage)
         T = logits.shape[1]
         # sequence lengths scaled to the logits' time axis, as the reference
-        ctc_len = (inputs[2].reshape(-1).long() * T) // self.max_time_steps
-        losses = rnn_ops.ctc_loss(logits, inputs[1], ctc_len, inputs[3].reshape(-1))
-        return losses.mean()
+        # (on the device, inside the native loss)
+        return rnn_ops.ctc_loss_mean(logits, inputs[1], inputs[2], inputs[3], T,
+                                     self.max_time_steps)
 
     def accuracy_function(self, inputs, logits):
         return {"probs": torch.softmax(logits.float(), dim=-1), "labels": inputs[1]}

@@ -91,56 +91,31 @@ IG_ALGOS = {"classic": IG_CLASSIC, "glds": IG_GLDS, "classic_n64": IG_CLASSIC_N6
             "gbig448": IG_GBIG448}
 _IG_FORCE = IG_ALGOS.get(os.environ.get("KFB_IGEMM_ALGO", ""))
 _ig_tuned = {}
-_NO_SMALL = os.environ.get("KFB_IGEMM_NOSMALL", "0") == "1"  # A/B knob: drop IG_SMALL
-_NO_S3 = os.environ.get("KFB_IGEMM_NOS3", "0") == "1"  # A/B knob: drop IG_S3
-_NO_S1 = os.environ.get("KFB_IGEMM_NOS1", "0") == "1"  # A/B knob: drop IG_S1
-# A/B knob: drop IG_S7 (in-network 18.87 / 18.87 vs 19.31 / 19.35 ms/step without it,
-# gpurun_out/r10o, profiles/r10_round4_ab.txt)
-_NO_S7 = os.environ.get("KFB_IGEMM_NOS7", "0") == "1"
-_NO_GSHORT = os.environ.get("KFB_IGEMM_NOGSHORT", "0") == "1"  # A/B knob: drop IG_GSHORT*
-_GSHORT3 = os.environ.get("KFB_IGEMM_GSHORT3", "1") != "0"  # A/B knob: the 3-stage forms
-_NO_MULTI = os.environ.get("KFB_IGEMM_NOMULTI", "0") == "1"  # A/B knob: drop IG_*MULTI*
-_NO_BIG = os.environ.get("KFB_IGEMM_NOBIG", "0") == "1"  # A/B knob: drop IG_GBIG*
-_NO_224 = os.environ.get("KFB_IGEMM_NO224", "0") == "1"  # A/B knob: drop IG_GBIG224
-_SK = os.environ.get("KFB_IGEMM_SK", "0") == "1"  # offer IG_SK128 to the autotune
-# KFB_IGEMM_EARLY=1: offer the early-epilogue-operand kernels (IG_*_E) to the
-# autotune.  Off: at 3 workgroups per CU (their early operands stay live
-# through the K loop) they lost to the 4-workgroup one-stage kernel on every
-# ResNet-50 dgrad geometry, by 5-20% (profiles/r8_early_epilogue.txt)
-_EARLY_EPI = os.environ.get("KFB_IGEMM_EARLY", "0") == "1"
-# KFB_IGEMM_DB=1: offer IG_DB.  Off: 380-410 TF/s on every ResNet-50 shape (the
-# per-lane B-fragment loads touch 16 pixel rows per instruction; the LDS-staged
-# loaders read whole rows), 1.1-2x slower than the chosen kernels
-# (profiles/r8_direct_b.txt)
-_DB = os.environ.get("KFB_IGEMM_DB", "0") == "1"
-# KFB_IGEMM_MF32=1: offer the *_32 kernels.  Off: within -4..+1% of their 16x16x32
-# forms on every ResNet-50 shape (the MFMA issue rate is not what binds these
-# kernels; profiles/r8_mfma_forms.txt)
-_MF32 = os.environ.get("KFB_IGEMM_MF32", "0") == "1"
+# Offered to the autotune only where they won (the lost forms stay
+# selectable by name through KFB_IGEMM_ALGO, for the kernel tests):
+#  * IG_SK128 (stream-K): slower than the one-tile kernels on every ResNet-50
+#    bs256 geometry, neutral on the few-tile small-batch layers
+#    (profiles/r7_stream_k.txt);
+#  * IG_*_E (epilogue operands loaded before the K loop): 3 instead of 4
+#    workgroups per CU lost 5-20% on every dgrad geometry
+#    (profiles/r8_early_epilogue.txt);
+#  * IG_DB (pixel operand straight into B fragments): 380-410 TF/s, 1.1-2x
+#    slower than the chosen kernels (profiles/r8_direct_b.txt);
+#  * IG_*_32 (32x32x16 MFMA forms): within -4..+1% (profiles/r8_mfma_forms.txt).
 # largest K (= KH*KW*Cin) offered the multi-tile candidates (register-staged;
 # the LDS-DMA form gets twice that)
-_MULTI_K = int(os.environ.get("KFB_IGEMM_MULTI_K", "2304"))
-# KFB_SCATTER_ZFILL=0: strided-1x1 data gradients zero-fill their output with a
-# separate pass instead of zeroing the unsampled pixels in the epilogue
-_SCATTER_ZFILL = os.environ.get("KFB_SCATTER_ZFILL", "1") != "0"
-# KFB_PENDING_ADDEND=0: a non-last consumer of a BN-linked tensor deposits its
-# dgrad and the pending sum is a separate add (A/B switch)
-_PENDING_ADDEND = os.environ.get("KFB_PENDING_ADDEND", "1") != "0"
-# KFB_ACT_FUSE=1: the ReLU / bias backward of a conv without BN runs in the
-# consuming conv's dgrad epilogue instead of as its own pass (kfb_act_bwd_bias).
-# Off by default: on VGG-16 it removes 1.05 ms/step of act_bwd_bias but the
-# extra read of y slows the dgrad convs by 0.8 ms, and the separate pass
-# overlaps the weight-gradient side stream, so the step got 0.5 ms slower
-# (profiles/r4_act_fuse_ab.txt)
-_ACT_FUSE = os.environ.get("KFB_ACT_FUSE", "0") == "1"
+_MULTI_K = 2304
+# The ReLU / bias backward of a conv without BN in the consuming conv's dgrad
+# epilogue instead of its own pass: off (on VGG-16 it removes 1.05 ms/step of
+# act_bwd_bias but the extra read of y slows the dgrad convs by 0.8 ms and the
+# separate pass overlaps the weight-gradient side stream: 0.5 ms slower,
+# profiles/r4_act_fuse_ab.txt); tests/test_conv_gpu.py switches it on
+_ACT_FUSE = False
 N.register_optional("kfb_conv_stats_spread", [], N.c_int)
 N.register_optional("kfb_conv_wgrad", [N.I, N.P, N.P, N.P] + [N.I] * 12 + [N.I, N.I, N.P, N.L, N.P])
 N.register_optional("kfb_conv_wgrad_splits", [N.I] * 8, N.c_int)
 
 _WGRAD_TARGET_BLOCKS = int(os.environ.get("KFB_WGRAD_BLOCKS", "768"))
-# Split partial sums go to a plain-store fp32 slab + one reduce launch
-# (KFB_WGRAD_SLAB=0: fp32 atomics into dW, ~1.3 TB/s at the memory side).
-_WGRAD_SLAB = os.environ.get("KFB_WGRAD_SLAB", "1") != "0"
 
 
 def supported(x, w, stride, pads) -> bool:
@@ -157,8 +132,6 @@ def _pad8(n):
 
 
 STATS_SPREAD = 32  # must match IG_SPREAD in csrc/conv_igemm.hip (checked at load)
-# KFB_BN_SHIFT=0: uncentered statistics partials (A/B switch)
-_STATS_SHIFT = os.environ.get("KFB_BN_SHIFT", "1") != "0"
 
 
 class _StatsArena:
@@ -169,8 +142,6 @@ class _StatsArena:
         self.buf = {}
         self.off = {}
         self.need = {}
-
-    enabled = os.environ.get("KFB_STATS_ARENA", "1") != "0"
 
     def reset(self, device):
         key = str(torch.device(device))
@@ -192,7 +163,7 @@ class _StatsArena:
     def take(self, n, device):
         key = str(torch.device(device))
         n = (n + 63) // 64 * 64
-        buf = self.buf.get(key) if self.enabled else None
+        buf = self.buf.get(key)
         off = self.off.get(key, 0)
         self.off[key] = off + n
         self.need[key] = max(self.need.get(key, 0), off + n)
@@ -225,7 +196,7 @@ def stats_buffer(channels, device, shift=None):
     full = STATS_ARENA.take(2 * STATS_SPREAD * channels + 64, device)
     buf = full[:2 * STATS_SPREAD * channels]
     buf._kfb_counter = full[2 * STATS_SPREAD * channels:]
-    if shift is not None and _STATS_SHIFT:
+    if shift is not None:
         buf._kfb_shift = shift
     return buf
 
@@ -375,62 +346,44 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
     fast = N.load().kfb_conv_igemm_fast(C, KH, KW, trans)
     # (IG_TALL512 is never the fastest on the ResNet-50 shapes: force-only)
     cands = (IG_CLASSIC, IG_GLDS, IG_ONEBUF, IG_TALL256) if fast else (IG_CLASSIC,)
-    if fast and not _NO_SMALL:
-        cands += (IG_SMALL,)
-    if fast and not _NO_GSHORT:
-        cands += (IG_GSHORT64,) + ((IG_GSHORT128,) if ncol > 64 else ())
-        if _MF32:
-            cands += (IG_GSHORT64_32,) + ((IG_GSHORT128_32,) if ncol > 64 else ())
-        if _GSHORT3:
-            cands += (IG_GSHORT64_3,) + ((IG_GSHORT128_3,) if ncol > 64 else ())
-    if fast and not _NO_MULTI and mask is None and xbn is None and addend is None \
+    if fast:
+        cands += (IG_SMALL, IG_GSHORT64, IG_GSHORT64_3)
+        if ncol > 64:
+            cands += (IG_GSHORT128, IG_GSHORT128_3)
+    if fast and mask is None and xbn is None and addend is None \
             and KH * KW * C <= _MULTI_K and C % 64 == 0:
         # short-K layers: store-phase bound, the multi-tile overlap pays there
         cands += (IG_MULTI2, IG_MULTI4, IG_SMALL_MULTI4)
-    if fast and not _NO_MULTI and KH * KW * C <= 2 * _MULTI_K and C % 64 == 0:
+    if fast and KH * KW * C <= 2 * _MULTI_K and C % 64 == 0:
         cands += (IG_GMULTI64,) + ((IG_GMULTI128,) if ncol > 64 else ())
-    if fast and not _NO_BIG:
+    if fast:
         # big tiles only where they give most CUs a workgroup: 196 256x256
         # tiles on 256 CUs (the 14x14 3x3 convs at batch 256) still beat 784
         # 128x128 tiles on 512 slots (71 vs 79 us, profiles/r7_stream_k.txt)
         M = geo[0] * geo[4] * geo[5]
         if ncol >= 256 and ((M + 255) // 256) * ((ncol + 255) // 256) >= 192:
             cands += (IG_GBIG256,) + ((IG_G8P,) if C % 64 == 0 else ())
-            if not _NO_224 and ((M + 223) // 224) * ((ncol + 255) // 256) > \
+            if ((M + 223) // 224) * ((ncol + 255) // 256) > \
                     ((M + 255) // 256) * ((ncol + 255) // 256):
                 cands += (IG_GBIG224,)
-            if _MF32:
-                cands += (IG_GBIG256_32,)
         if 64 < ncol <= 256 and ((M + 511) // 512) * ((ncol + 127) // 128) >= 256:
             cands += (IG_GBIG512,)
-        if 64 < ncol <= 256 and not _NO_224 and ((M + 447) // 448) * ((ncol + 127) // 128) >= 256:
+        if 64 < ncol <= 256 and ((M + 447) // 448) * ((ncol + 127) // 128) >= 256:
             cands += (IG_GBIG448,)
-    if fast and _SK and C % 64 == 0 and ncol > 64:
-        # stream-K: measured slower than the one-tile kernels on every
-        # ResNet-50 bs256 geometry (per-item setup, pipeline refill and the
-        # fix-up tail cost more than the partial round it removes at
-        # K <= 4608, profiles/r7_stream_k.txt) and neutral on the few-tile
-        # small-batch layers (ResNet-152 bs32, ResNet-50 bs64); offered only
-        # with KFB_IGEMM_SK=1
-        cands += (IG_SK128,)
     if fast and C % 64 != 0:
         # 8-channel geometry: the generic loader competes with the FAST ones
         cands += (IG_GENERIC,)
-    if fast and _DB and C % 64 == 0:
-        cands += (IG_DB,)
-    if fast and _EARLY_EPI and (xbn is not None or addend is not None):
-        cands += (IG_ONEBUF_N64_E, IG_CLASSIC_N64_E)
-    if fast and not _NO_S3 and N.load().kfb_conv_s3_applicable(
+    if fast and N.load().kfb_conv_s3_applicable(
             C, ncol, KH, KW, geo[8], geo[9], geo[10], geo[11], geo[1], geo[2], geo[4], geo[5]) \
             and geo[13] == geo[4] and geo[14] == geo[5] and geo[15] == 1 and geo[16] == ncol:
         cands += (IG_S3,)
-    if fast and not _NO_S1 and mcoef is None and bact[0] is None and not (int(bact[1]) & 3) \
+    if fast and mcoef is None and bact[0] is None and not (int(bact[1]) & 3) \
             and (mask is None or (xbn is not None and mask.dtype == torch.uint8)) \
             and N.load().kfb_conv_s1_applicable(
             C, ncol, KH, KW, geo[8], geo[9], geo[10], geo[11], geo[1], geo[2], geo[4], geo[5]) \
             and geo[13] == geo[4] and geo[14] == geo[5] and geo[15] == 1 and geo[16] == ncol:
         cands += (IG_S1,)
-    if not _NO_S7 and xbn is None and addend is None and mask is None and bact[0] is None \
+    if xbn is None and addend is None and mask is None and bact[0] is None \
             and not (int(bact[1]) & 3) and not trans and N.load().kfb_conv_s7_applicable(
             C, ncol, KH, KW, geo[8], geo[9], geo[10], geo[11], geo[1], geo[2], geo[4], geo[5]) \
             and geo[13] == geo[4] and geo[14] == geo[5] and geo[15] == 1 and geo[16] == ncol:
@@ -486,12 +439,12 @@ def _igemm(x, wmat, y, N_, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, ncol, YH, YW
     return deferred
 
 
-# KFB_BN_RECOMPUTE=1: a residual BN's producing streaming 1x1 conv sums the
-# statistics without storing its output; the BN's apply pass recomputes it
-# (profiles/r12_bn_recompute.txt).  =<K> (K > 1): only for convs with at most
-# K input channels; 0: off (the conv stores y, the BN apply reads it back).
-_RC = os.environ.get("KFB_BN_RECOMPUTE", "0")
-_RECOMPUTE = True if _RC == "1" else (int(_RC) if _RC.isdigit() and int(_RC) > 1 else False)
+# A residual BN's producing streaming 1x1 conv sums the statistics without
+# storing its output; the BN's apply pass recomputes it (True; K > 1: only
+# for convs with at most K input channels).  Off: it did not win in the
+# network (profiles/r12_bn_recompute.txt); tests/test_bn_recompute_gpu.py
+# switches it on against the exact oracle.
+_RECOMPUTE = False
 
 
 def conv_fwd(x, wl, stride, pads, stats=None, bias=None, relu=False):
@@ -560,7 +513,7 @@ def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None, addend=None, wt=None,
         if ys is None:
             return None
         # stride 2 over an even grid: the epilogue zeroes the unsampled pixels
-        zfill = dx is None and _SCATTER_ZFILL and ys == 2 and H == 2 * OH and W == 2 * OW
+        zfill = dx is None and ys == 2 and H == 2 * OH and W == 2 * OW
         if dx is None:
             dx = (torch.empty if zfill else torch.zeros)((n, H, W, C), dtype=dy.dtype,
                                                          device=dy.device)
@@ -585,11 +538,12 @@ def conv_dgrad(dy, wl, x_shape, stride, pads, fuse=None, addend=None, wt=None,
 def _wgrad_launch(dy, x, dw, geo, target):
     n, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, cout = geo
     slab, slab_elems = None, 0
-    if _WGRAD_SLAB or (target >> 16) == 2:  # (the streaming wgrad always folds slabs)
-        splits = N.load().kfb_conv_wgrad_splits(n, OH, OW, KH, KW, C, cout, target)
-        if splits > 1 or (target >> 16) == 2:
-            slab_elems = splits * cout * KH * KW * C
-            slab = torch.empty((slab_elems,), dtype=torch.float32, device=x.device)
+    # split partial sums: a plain-store fp32 slab + one reduce launch (fp32
+    # atomics into dW ran at ~1.3 TB/s at the memory side)
+    splits = N.load().kfb_conv_wgrad_splits(n, OH, OW, KH, KW, C, cout, target)
+    if splits > 1 or (target >> 16) == 2:  # (the streaming wgrad always folds slabs)
+        slab_elems = splits * cout * KH * KW * C
+        slab = torch.empty((slab_elems,), dtype=torch.float32, device=x.device)
     N.call("kfb_conv_wgrad", N.dt(x), dy.data_ptr(), x.data_ptr(), dw.data_ptr(), n, H, W, C, OH,
            OW, KH, KW, sh, sw, pt, pl, cout, target,
            slab.data_ptr() if slab is not None else None, slab_elems, N.stream(x.device))
@@ -619,7 +573,7 @@ def _wgrad_candidates(geo):
     n, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, cout = geo
     if _WGRAD_ALGO == "s3":
         return (_WGRAD_S3,)
-    s3 = ((_WGRAD_S3,) if not _NO_S3 and N.load().kfb_conv_s3_applicable(
+    s3 = ((_WGRAD_S3,) if N.load().kfb_conv_s3_applicable(
         C, cout, KH, KW, sh, sw, pt, pl, H, W, OH, OW) else ())
     glds = tuple(t | _WGRAD_GLDS for t in _WGRAD_CANDIDATES) if cout > 64 else ()
     if _WGRAD_ALGO == "classic" or not glds:
@@ -735,17 +689,11 @@ _WGRAD_SIDE = os.environ.get("KFB_WGRAD_STREAM", "1") != "0"
 _SIDE_STREAMS = {}
 
 
-# weight gradients with more dY rows (pixels) than this run on the compute stream
-# after their dgrad instead of beside the dgrad chain (large-grid layers fill
-# the chip alone; two compute-bound kernels sharing it can be slower than
-# the two back to back)
-_WGRAD_SIDE_MAX = int(float(os.environ.get("KFB_WGRAD_SIDE_MAX", "1e18")))
 # A layer's side-stream weight gradient is enqueued before its data gradient
 # (both need only dy and x), so the side stream waits on the kernel that
 # produced dy rather than on the data gradient and the two run side by side
 # (ResNet-50 bs256: 18.36-18.41 vs 18.78-18.80 ms/step, 3 interleaved pairs,
-# profiles/r12_side_stream_order.txt); KFB_WGRAD_FIRST=0: after it
-_WGRAD_FIRST = os.environ.get("KFB_WGRAD_FIRST", "1") != "0"
+# profiles/r12_side_stream_order.txt)
 
 
 def wgrad_stream(device):
@@ -790,10 +738,10 @@ def join_wgrad_stream(device=None):
 
 
 N.register_optional("kfb_s2d_stem", [N.I, N.P, N.P] + [N.I] * 9 + [N.P])
-_STEM_S2D = os.environ.get("KFB_STEM_S2D", "1") != "0"
 # BN backward partials in the epilogue of strided-1x1 (scatter) dgrads whose
-# pending gradient is sparse on the same grid (A/B and test switch)
-_SCATTER_BN_FUSE = os.environ.get("KFB_SCATTER_BN_FUSE", "1") != "0"
+# pending gradient is sparse on the same grid (tests/test_model_gpu.py
+# switches it off for its oracle)
+_SCATTER_BN_FUSE = True
 
 
 def use_s2d(x, wl_shape, stride, needs_dx, pads) -> bool:
@@ -801,7 +749,7 @@ def use_s2d(x, wl_shape, stride, needs_dx, pads) -> bool:
     stem) and no input gradient: run it as a 64-channel stride-1 conv over a
     space-to-depth repack (csrc/stem.hip)."""
     cout, KH, KW, cin = wl_shape
-    if not (_STEM_S2D and not needs_dx and tuple(stride) == (2, 2) and cin <= 4
+    if not (not needs_dx and tuple(stride) == (2, 2) and cin <= 4
             and KH <= 8 and KW <= 8 and KH * KW >= 25 and cout % 8 == 0
             and hasattr(N.load(), "kfb_s2d_stem")):
         return False
@@ -813,7 +761,7 @@ def use_s2d(x, wl_shape, stride, needs_dx, pads) -> bool:
 
 # "pairs": the stem as an 8x4-tap stride-(2,1) conv over a padded pixel-pair
 # view of the image (csrc/stem.hip); "s2d": a 64-channel space-to-depth repack
-_STEM_MODE = os.environ.get("KFB_STEM_MODE", "pairs")
+_STEM_MODE = "pairs"
 N.register_optional("kfb_stem_pad", [N.I, N.P, N.P] + [N.I] * 8 + [N.P])
 N.register_optional("kfb_stem_weight", [N.I, N.P, N.P] + [N.I] * 4 + [N.P])
 N.register_optional("kfb_stem_weight_grad", [N.P, N.P] + [N.I] * 4 + [N.P])
@@ -964,7 +912,7 @@ class _Conv2d(torch.autograd.Function):
         w = ctx.w
         sink = getattr(w, "_kfb_grad_sink", None)
         if not (sink is not None and cout_p == ctx.meta[3] and wp.shape[-1] == cin
-                and _fuse_enabled()) or dy.numel() // dy.shape[-1] > _WGRAD_SIDE_MAX:
+                and _fuse_enabled()):
             return False
         side = wgrad_stream(dy.device)
         if side is None:
@@ -1003,8 +951,8 @@ class _Conv2d(torch.autograd.Function):
             dy = _pad_rkc(dy, 1, rows, cout, 1, cout_p).view(tuple(dy.shape[:-1]) + (cout_p,))
         dx = None
         # the side-stream weight gradient needs only dy and x: enqueued before
-        # the data gradient, it may start beside it (KFB_WGRAD_FIRST)
-        side_done = (_WGRAD_FIRST and ctx.needs_input_grad[1]
+        # the data gradient, it may start beside it
+        side_done = (ctx.needs_input_grad[1]
                      and _Conv2d._side_wgrad(ctx, dy, xp, wp, stride, pads, cin, cout_p))
         if ctx.x_needs_grad:
             link = ctx.link
@@ -1060,7 +1008,7 @@ class _Conv2d(torch.autograd.Function):
                     sparse = (stride[0] if not padded and stride[0] == stride[1]
                               and is_scatter_dgrad(wp.shape, stride, pads) else None)
                     g = None
-                    if not padded and link.pending is not None and _PENDING_ADDEND:
+                    if not padded and link.pending is not None:
                         # accumulate onto the pending gradient in the dgrad
                         # epilogue (one read of it) instead of a separate add
                         link.take_pending_stream()

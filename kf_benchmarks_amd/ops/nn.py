@@ -89,12 +89,12 @@ def _bn_cpu(x, gamma, beta, residual, rm, rv, decay, eps, relu, training):
     return y.to(x.dtype).contiguous()
 
 
-# KFB_MASK_RECOMPUTE=1: consumers' dgrad epilogues recompute a non-residual
-# BN's ReLU mask from x_bn instead of reading the BN output.  Off by default:
-# the output read is the conv input the following wgrad reads anyway, and
-# reading it first leaves it in the 256 MB last-level cache; interleaved A/B
-# on ResNet-50 bs256: 11667 img/s (read) vs 11567 (recompute).
-_MASK_RECOMPUTE = os.environ.get("KFB_MASK_RECOMPUTE", "0") == "1" and _conv.FUSE_BN
+# Consumers' dgrad epilogues could recompute a non-residual BN's ReLU mask
+# from x_bn instead of reading the BN output: off (the output read is the conv
+# input the following wgrad reads anyway, and reading it first leaves it in
+# the 256 MB last-level cache; ResNet-50 bs256: 11667 img/s read vs 11567
+# recompute)
+_MASK_RECOMPUTE = False
 
 
 class BNLink:
@@ -223,9 +223,9 @@ def _grad_ready(p):
         cb(p)
 
 
-# KFB_RELU_BITS=0: consumers' dgrad epilogues read the BN output itself for
-# the ReLU mask (16x the bytes of the bit mask)
-_RELU_BITS = os.environ.get("KFB_RELU_BITS", "1") != "0"
+# off (tests): consumers' dgrad epilogues read the BN output itself for the
+# ReLU mask (16x the bytes of the bit mask)
+_RELU_BITS = True
 
 
 def _relu_bits_buffer(x, rows, C):
@@ -412,11 +412,11 @@ class DeferredBN:
 _DUAL_ALIAS_RES = True
 # ... and takes bn_r's backward partials from its last consumer's streaming
 # 1x1 dgrad epilogue (kfb_conv_s1_dgrad_dual) instead of a pass over dy and
-# xr (KFB_S1_DUAL=0: that pass)
-_S1_DUAL = os.environ.get("KFB_S1_DUAL", "1") != "0"
+# xr (off: that pass)
+_S1_DUAL = True
 # ... and with a pre-masked dy runs both BN backwards with one apply pass
-# (kfb_bn_bwd_dual; KFB_DUAL_BN_BWD=0: two separate BN backwards)
-_DUAL_BWD_FUSE = os.environ.get("KFB_DUAL_BN_BWD", "1") != "0"
+# (kfb_bn_bwd_dual; off: two separate BN backwards)
+_DUAL_BWD_FUSE = True
 
 
 class _BatchNormTrainDual(torch.autograd.Function):
@@ -845,8 +845,9 @@ N.register_optional("kfb_bn_relu_maxpool_bwd", [N.I, N.P, N.P, N.P, N.P, N.P] + 
 # consumers' dgrad epilogue (sum dz', sum dz' (z - beta), rescaled by
 # 1 / (gamma * invstd)) instead of its own pass over x.  Default since round
 # 4: 18.93 / 18.75 / 18.72 vs 19.09 / 19.06 / 18.82 ms/step interleaved
-# (gpurun_out/r10t, profiles/r10_round4_ab.txt); KFB_POOL_LINK=0 turns it off.
-_POOL_LINK = os.environ.get("KFB_POOL_LINK", "1") == "1"
+# (gpurun_out/r10t, profiles/r10_round4_ab.txt); tests/test_model_gpu.py compares
+# it with the link off.
+_POOL_LINK = True
 
 
 # Called once at the top of the stem BN+ReLU+max-pool backward (the point
@@ -1055,8 +1056,8 @@ def _at(t, elems):
     return t.as_strided((1,), (1,), t.storage_offset() + elems)
 
 
-# KFB_SPLIT_WGRAD=0: affine weight gradients never split the batch reduction
-_SPLIT_WGRAD = os.environ.get("KFB_SPLIT_WGRAD", "1") != "0"
+# off: affine weight gradients never split the batch reduction
+_SPLIT_WGRAD = True
 
 
 def _gemm(mode, p, ldp, q, ldq, rows, cols, red, out, ldc, bias=None, relu=False,
@@ -1094,8 +1095,8 @@ def _gemm(mode, p, ldp, q, ldq, rows, cols, red, out, ldc, bias=None, relu=False
            slab.numel() if slab is not None else 0, nsplit, N.stream(dev))
 
 
-# KFB_LINEAR_WGRAD_SIDE=0: affine weight gradients on the compute stream
-_LINEAR_WGRAD_SIDE = os.environ.get("KFB_LINEAR_WGRAD_SIDE", "1") != "0"
+# off: affine weight gradients on the compute stream
+_LINEAR_WGRAD_SIDE = True
 
 
 class _Linear(torch.autograd.Function):

@@ -220,6 +220,73 @@ class _CTC(torch.autograd.Function):
         return dz, None, None, None
 
 
+N.register_optional("kfb_ctc_grad_scale_mean", [N.I, N.P, N.P, N.P, N.L, N.L, N.I, N.I, N.I,
+                                                N.F, N.P])
+N.register_optional("kfb_ctc_scale_lengths", [N.P, N.P, N.I, N.I, N.I, N.P])
+
+
+class _CTCMean(torch.autograd.Function):
+    """mean_b CTC(logits_b) with the input lengths scaled to the logits' time
+    axis (ilen * len_num // len_den, the reference's length arithmetic,
+    tcb/models/experimental/deepspeech.py:407-414) - every piece a native
+    call: the length scaling, the loss + gradient kernel, the batch mean and
+    the mean's backward, so the step that holds it can be taped."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, ilen, llen, len_num, len_den):
+        B, T, C = logits.shape
+        dev = logits.device
+        Lmax = labels.shape[1]
+        smax = 2 * Lmax + 1
+        if smax > N.query("kfb_ctc_max_states"):
+            raise N.NativeError("CTC label length %d exceeds the kernel's state buffer" % Lmax)
+        if logits.stride(2) != 1:
+            logits = logits.contiguous()
+        sb, st, _ = logits.stride()
+        for t in (labels, ilen, llen):
+            if t.dtype != torch.int32 or not t.is_contiguous():
+                raise N.NativeError("ctc_loss_mean takes contiguous int32 labels / lengths")
+        sl = torch.empty((B,), dtype=torch.int32, device=dev)
+        N.call("kfb_ctc_scale_lengths", ilen.data_ptr(), sl.data_ptr(), B, int(len_num),
+               int(len_den), N.stream(dev))
+        lp = torch.empty((T * B * C,), dtype=torch.float32, device=dev)
+        alpha = torch.empty((B * T * smax,), dtype=torch.float32, device=dev)
+        loss = torch.empty((B,), dtype=torch.float32, device=dev)
+        grad = torch.empty_strided(logits.shape, logits.stride(), dtype=torch.float32,
+                                   device=dev)
+        N.call("kfb_ctc_loss", N.dt(logits), logits.data_ptr(), st, sb, labels.data_ptr(),
+               sl.data_ptr(), llen.data_ptr(), T, B, C, Lmax, lp.data_ptr(), alpha.data_ptr(),
+               smax, loss.data_ptr(), grad.data_ptr(), N.stream(dev))
+        mean = torch.empty((), dtype=torch.float32, device=dev)
+        N.call("kfb_mean_f32", loss.data_ptr(), B, mean.data_ptr(), N.stream(dev))
+        ctx.save_for_backward(grad)
+        ctx.dtype = logits.dtype
+        return mean
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        B, T, C = grad.shape
+        sb, st, _ = grad.stride()
+        if g.dtype != torch.float32 or not g.is_contiguous():
+            raise N.NativeError("ctc_loss_mean: fp32 loss gradient expected")
+        dz = torch.empty_strided(grad.shape, grad.stride(), dtype=ctx.dtype, device=grad.device)
+        N.call("kfb_ctc_grad_scale_mean", N.dt(dz), grad.data_ptr(), g.data_ptr(),
+               dz.data_ptr(), st, sb, T, B, C, 1.0 / B, N.stream(grad.device))
+        return dz, None, None, None, None, None
+
+
+def ctc_loss_mean(logits, labels, ilen, llen, len_num=1, len_den=1):
+    """Batch-mean CTC loss (fp32 scalar) of logits [B, T, C] (blank = C-1)
+    with input lengths ilen * len_num // len_den; infeasible sequences give
+    0.  On the GPU every op is native (recordable in a launch tape)."""
+    if not logits.is_cuda:
+        ilen_s = (ilen.reshape(-1).long() * len_num) // len_den
+        return ctc_loss_reference(logits, labels, ilen_s, llen.reshape(-1)).mean()
+    return _CTCMean.apply(logits, labels.contiguous(), ilen.reshape(-1).contiguous(),
+                          llen.reshape(-1).contiguous(), len_num, len_den)
+
+
 def ctc_loss(logits, labels, ilen, llen):
     """Per-sequence CTC losses [B] of logits [B, T, C] (blank = C-1);
     infeasible sequences (label longer than the input allows) give 0."""

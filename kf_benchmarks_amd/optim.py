@@ -66,6 +66,10 @@ class FlatParams:
 
     def _attach_lp_views(self):
         index = {id(p): (o, p) for p, o in zip(self.params, self.offsets)}
+        # every parameter knows its compute copy (module models pass it to
+        # the ops instead of casting the fp32 master every step)
+        for p, o in zip(self.params, self.offsets):
+            p._kfb_lp = self.lp[o:o + p.numel()].view(p.shape)
         for layer in self.net.ordered_layers():
             for attr, lp_attr in (("weight", "weight_lp"), ("weights", "weights_lp")):
                 p = getattr(layer, attr, None)

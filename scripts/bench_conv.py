@@ -70,10 +70,14 @@ def main():
     only = {int(i) for i in a.shapes.split(",")} if a.shapes else None
     dev = torch.device("cuda", 0)
     dt = torch.bfloat16
-    tot = {"hip": [0.0, 0.0, 0.0], "miopen": [0.0, 0.0, 0.0]}
+    tot = {"hip": [0.0, 0.0, 0.0], "miopen": [0.0, 0.0, 0.0], "sol": [0.0, 0.0, 0.0]}
     rows = []
-    print("%-28s %8s | %9s %7s | %9s %7s | %9s %7s" % ("shape", "pass", "hip_us", "TF/s",
-                                                        "miopen_us", "TF/s", "", ""))
+    if a.sol:
+        print("%-28s %8s | %9s %7s | %-24s %6s | %s" % ("shape", "pass", "hip_us", "TF/s",
+                                                         "sol_us (bound)", "%sol", "blaslt_us"))
+    else:
+        print("%-28s %8s | %9s %7s | %9s %7s | %s" % ("shape", "pass", "hip_us", "TF/s",
+                                                       "miopen_us", "TF/s", "hip/miopen"))
     for si, (H, cin, cout, k, s, cnt) in enumerate(RESNET50):
         if only is not None and si not in only:
             continue
@@ -127,22 +131,30 @@ def main():
                     name, pas, th, flops / th / 1e6, sol,
                     "mem" if bytes_[pas] / 6e12 > flops / 2.5e15 else "mfma", 100 * sol / th, tm))
                 tot["hip"][i] += th * cnt
-                tot["miopen"][i] += sol * cnt
+                tot["sol"][i] += sol * cnt
+                rows.append({"shape": name, "pass": pas, "hip_us": th, "sol_us": sol,
+                             "blaslt_us": tm, "count": cnt})
                 continue
             tm = timeit(mi[pas], a.iters) if not a.hip_only else float("nan")
             tot["hip"][i] += th * cnt
             tot["miopen"][i] += tm * cnt
             name = "%dx%d %d->%d k%d s%d" % (H, H, cin, cout, k, s)
-            print("%-28s %8s | %9.1f %7.1f | %9.1f %7.1f" % (name, pas, th, flops / th / 1e6,
-                                                            tm, flops / tm / 1e6))
+            print("%-28s %8s | %9.1f %7.1f | %9.1f %7.1f | %5.2f%s" % (
+                name, pas, th, flops / th / 1e6, tm, flops / tm / 1e6, th / tm,
+                "  MIOPEN FASTER" if tm < th else ""))
             rows.append({"shape": name, "pass": pas, "hip_us": th, "miopen_us": tm,
                          "count": cnt, "tflops_hip": flops / th / 1e6,
                          "tflops_miopen": flops / tm / 1e6})
     for key in (("hip", "sol") if a.sol else ("hip", "miopen")):
-        lab, key = key, "miopen" if key == "sol" else key
         f, d, wg = tot[key]
         print("%-8s ResNet-50 conv time per step: fwd %.2f ms  dgrad %.2f ms  wgrad %.2f ms  "
-              "total %.2f ms" % (lab, f / 1e3, d / 1e3, wg / 1e3, (f + d + wg) / 1e3))
+              "total %.2f ms" % (key, f / 1e3, d / 1e3, wg / 1e3, (f + d + wg) / 1e3))
+    if not a.sol and not a.hip_only:
+        slower = [r for r in rows if r["miopen_us"] < r["hip_us"]]
+        print("layers where MIOpen is faster: %d of %d" % (len(slower), len(rows)))
+        for r in slower:
+            print("  %-28s %6s hip %8.1f us  miopen %8.1f us  (x%d per step)"
+                  % (r["shape"], r["pass"], r["hip_us"], r["miopen_us"], r["count"]))
     if a.json:
         with open(a.json, "w") as fh:
             json.dump({"rows": rows, "totals_us": tot}, fh, indent=1)

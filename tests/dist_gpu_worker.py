@@ -101,6 +101,7 @@ def main():
                     for name, _, off, n in bench.flat.segments()},
            "size": comm.get_world().size, "backend": comm.get_world().device_backend,
            "taped": getattr(getattr(bench, "_tape", None), "replays", 0),
+           "tower_mode": bench.tower_mode,
            "bucket_launches": (bench.strategy.reducer.launch_count
                                if bench.strategy.reducer is not None else 0),
            "num_buckets": (bench.strategy.reducer.num_buckets

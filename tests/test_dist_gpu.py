@@ -194,6 +194,27 @@ def test_two_ranks_pair_averaging_training(cuda, tmp_path):
         assert all(l == l and abs(l) < 1e3 for l in r["losses"])
 
 
+@pytest.mark.parametrize("vu", ["replicated", "parameter_server"])
+def test_tower_mode_taped_over_rccl(cuda, tmp_path, vu):
+    """--num_gpus=N runs as N tower processes (KFB_TOWER_GROUP); the
+    reported loss is the mean over the towers, a one-element all-reduce
+    issued outside the recorded step, so tower mode tapes like any
+    native-communicator run.  Here the single-tower stand-in
+    over a real 1-rank RCCL group (KFB_FORCE_PG=1): taped and eager runs
+    agree."""
+    kw = dict(model="resnet50", batch_size=8, num_gpus=2, use_bf16=True, optimizer="momentum",
+              data_format="NHWC", variable_update=vu, bucket_size_mb=4.0)
+    env = dict(_RCCL, KFB_NATIVE_COMM="1", KFB_TOWER_GROUP="1", KFB_TEST_GRAD_SEGS=None)
+    (a,) = _run(dict(kw, launch_tape=True), 6, tmp_path, n=1,
+                env_extra=dict(env, KFB_TAPE_STRICT="1"), tag="taped")
+    (b,) = _run(dict(kw, launch_tape=False), 6, tmp_path, n=1, env_extra=env, tag="eager")
+    assert a["backend"] == "rccl" and a["tower_mode"] is True
+    assert a["taped"] == 3, a["taped"]  # 2 eager, 1 recorded, 3 replayed
+    assert a["w0"] == b["w0"]
+    for la, lb in zip(a["losses"], b["losses"]):
+        assert la == la and abs(la - lb) <= 0.05 * max(1.0, abs(lb)), (a["losses"], b["losses"])
+
+
 def test_pair_averaging_torn_snapshot_skips_averaging(cuda, tmp_path):
     """PairAveraging's device-side torn-snapshot guard: rank 0's pull at
     step 3 sees a sequence word that moved during the copy (injected); the

@@ -173,6 +173,33 @@ def test_ctc_gpu(cuda, dt):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_ctc_loss_mean_gpu(cuda, dt):
+    """The DeepSpeech2 loss as one native op: input lengths scaled on the
+    device (ilen * T // max_time, the reference's arithmetic), CTC, batch
+    mean and the mean's backward; vs torch's ctc_loss on the same scaled
+    lengths (fp32 reference)."""
+    torch.manual_seed(1)
+    B, T, C, L, TMAX = 5, 48, 29, 10, 3494
+    z = torch.randn(T, B, C) * 2
+    labels = torch.randint(0, C - 1, (B, L), dtype=torch.int32)
+    ilen = torch.tensor([[3494], [2000], [3494], [700], [80]], dtype=torch.int32)
+    llen = torch.tensor([[10], [7], [1], [10], [5]], dtype=torch.int32)
+    za = z.to(cuda, dt).requires_grad_(True)
+    la = R.ctc_loss_mean(za.transpose(0, 1), labels.to(cuda), ilen.to(cuda), llen.to(cuda), T,
+                         TMAX)
+    la.backward(torch.tensor(1.5, device=cuda))
+    zb = z.to(dt).float().requires_grad_(True)
+    sl = (ilen.reshape(-1).long() * T) // TMAX
+    lb = R.ctc_loss_reference(zb.transpose(0, 1), labels, sl, llen.reshape(-1)).mean()
+    (lb * 1.5).backward()
+    assert la.dim() == 0 and la.dtype == torch.float32
+    torch.testing.assert_close(la.cpu(), lb.detach(), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(za.grad.float().cpu(), zb.grad, rtol=2e-2 if dt != torch.float32
+                               else 1e-4, atol=1e-2 if dt != torch.float32 else 1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_permute01_gpu(cuda, dt):
     x = torch.randn(7, 5, 3, 24)
     y = R.permute01(x.to(cuda, dt).requires_grad_(True))
