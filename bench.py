@@ -244,12 +244,14 @@ def _run(a):
     images = a.batch_size * n * a.steps
     value = images / elapsed
     if world.is_chief:
-        headline = a.model == "resnet50" and not a.data_dir
+        headline = a.model == "resnet50" and not a.data_dir and a.kernel_impl == "hip"
         base = BASELINE_IMG_PER_SEC.get(n) if headline else None
         out = {
             "metric": ("images/sec (whole node) ResNet-50 synthetic at 1/2/4/8 MI355X"
-                       if headline else "images/sec (whole node) %s %s"
-                       % (a.model, "real data" if a.data_dir else "synthetic")),
+                       if headline else "images/sec (whole node) %s %s%s"
+                       % (a.model, "real data" if a.data_dir else "synthetic",
+                          "" if a.kernel_impl == "hip"
+                          else " (convs on PyTorch/MIOpen: reference bar only)")),
             "value": round(value, 2),
             "unit": "images/sec",
             "n_gpus": n,

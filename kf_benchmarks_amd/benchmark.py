@@ -176,9 +176,10 @@ def validate_params_combinations(params):
         raise ValueError("Only one of --eval and --forward_only may be specified")
     if p.variable_consistency == "relaxed" and p.variable_update != "replicated":
         raise ValueError("variable_consistency=relaxed requires variable_update=replicated")
-    if p.kernel_impl != "hip":
-        # (ops take impl="torch" only as a test oracle, never from the CLI)
-        raise ValueError("--kernel_impl must be hip (the only GPU path)")
+    if p.kernel_impl not in ("hip", "torch"):
+        # torch: the convolutions on stock PyTorch / MIOpen, everything else
+        # on our kernels - the same-node reference bar, never a headline
+        raise ValueError("--kernel_impl must be hip or torch")
 
 
 class _EventTimer:

@@ -206,20 +206,22 @@ __global__ void ssd_mean_k(const float* __restrict__ loss_img, int B, float* __r
 }
 
 // One thread per logit element (coalesced: consecutive lanes, consecutive
-// elements); the per-anchor scalars come from L1 (host: B*A*(4+C) < 2^31).
-template <typename T>
+// elements); the per-anchor scalars come from L1.  I: the element index type
+// - 32-bit (cheaper divisions) while B*A*(4+C) < 2^31, 64-bit beyond (large
+// per-GPU batches, e.g. ~2,900+ images at 81 classes).
+template <typename T, typename I>
 __global__ void __launch_bounds__(256)
 ssd_bwd_k(const T* __restrict__ x, const float* __restrict__ gt_loc,
           const float* __restrict__ label, const float* __restrict__ num_matched,
           const float* __restrict__ lse, const float* __restrict__ w, const float* __restrict__ g,
           int B, int A, int C, T* __restrict__ dx) {
-  const unsigned R = 4 + C;
-  const unsigned n = (unsigned)B * (unsigned)A * R;
+  const I R = 4 + C;
+  const I n = (I)B * (I)A * R;
   const float gs = g[0] / (float)B;
-  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-    const unsigned i = e / R;
+  for (I e = (I)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (I)gridDim.x * blockDim.x) {
+    const I i = e / R;
     const int c = (int)(e - i * R);
-    const float scale = gs / num_matched[i / (unsigned)A];
+    const float scale = gs / num_matched[i / (I)A];
     bool pos;
     const int l = ssd_label(label[i], C, &pos);
     const float xv = (float)x[e];
@@ -270,13 +272,18 @@ KFB_API hipError_t kfb_ssd_loss_bwd(int dtype, const void* x, const float* gt_lo
                                     void* dx, hipStream_t stream) {
   if (A < 1 || B < 1 || C < 1) return hipErrorInvalidValue;
   const long rows = (long)B * A;
-  if (rows * (4 + C) >= (1L << 31)) return hipErrorInvalidValue;
+  const bool narrow = rows * (4 + C) < (1L << 31);
   const float* lse = work + B;
   const float* w = lse + 2 * rows;
   KFB_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL((ssd_bwd_k<T>), dim3(row_grid(rows * (4 + C))), dim3(256), 0, stream,
-                       (const T*)x,
-                       gt_loc, label, num_matched, lse, w, g, B, A, C, (T*)dx);
+    if (narrow)
+      hipLaunchKernelGGL((ssd_bwd_k<T, unsigned>), dim3(row_grid(rows * (4 + C))), dim3(256), 0,
+                         stream, (const T*)x, gt_loc, label, num_matched, lse, w, g, B, A, C,
+                         (T*)dx);
+    else
+      hipLaunchKernelGGL((ssd_bwd_k<T, unsigned long long>), dim3(row_grid(rows * (4 + C))),
+                         dim3(256), 0, stream, (const T*)x, gt_loc, label, num_matched, lse, w,
+                         g, B, A, C, (T*)dx);
   });
   return hipGetLastError();
 }

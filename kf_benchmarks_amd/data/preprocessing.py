@@ -204,7 +204,7 @@ def adjust_hue(img, delta):
     return _hsv_to_rgb((h + delta) % 1.0, s, v)
 
 
-_NATIVE_COLOR = os.environ.get("KFB_NATIVE_COLOR", "1") != "0"
+_NATIVE_COLOR = True  # (False: the numpy colour distortion, the tests' reference)
 
 
 def distort_color(image, batch_position, rng: np.random.Generator, distort_color_in_yiq=False):
@@ -257,9 +257,9 @@ def train_image(image_buffer, height, width, bbox, batch_position, resize_method
     return image
 
 
-# KFB_JPEG_DRAFT=0: decode every JPEG at full size (the DCT-domain 1/2-1/8
-# scaling below changes the pixels slightly; the crop keeps >= the output size)
-_JPEG_DRAFT = os.environ.get("KFB_JPEG_DRAFT", "1") != "0"
+# False: decode every JPEG at full size (the DCT-domain 1/2-1/8 scaling below
+# changes the pixels slightly; the crop keeps >= the output size)
+_JPEG_DRAFT = True
 AUG_PARAMS = 8  # per-image parameter row of the device augmentation (csrc/augment.hip)
 
 
@@ -270,7 +270,7 @@ def train_image_u8(image_buffer, height, width, bbox, batch_position, resize_met
     [height, width, 3], and the image's augmentation parameters
     (flip, brightness, saturation, hue, contrast, order, distort, 0), drawn
     from ``rng`` in train_image's order so both paths see the same randoms.
-    The JPEG is opened once; with ``draft`` (default KFB_JPEG_DRAFT) libjpeg
+    The JPEG is opened once; with ``draft`` (default _JPEG_DRAFT) libjpeg
     decodes at the largest 1/2^k scale that keeps the crop >= the output."""
     im = Image.open(io.BytesIO(image_buffer))
     W0, H0 = im.size
@@ -887,11 +887,11 @@ def get_preprocessor(bench, subset):
                fuse_decode_and_crop=params.fuse_decode_and_crop)
 
 
-# KFB_NATIVE_PIPE=0: with device augmentation, decode/crop/resize on Python
-# threads over PIL instead of the native pipeline
-_NATIVE_PIPE = os.environ.get("KFB_NATIVE_PIPE", "1") != "0"
-# KFB_DEVICE_AUGMENT=0: the whole train preprocessing on the host threads
-_DEVICE_AUGMENT = os.environ.get("KFB_DEVICE_AUGMENT", "1") != "0"
+# False: with device augmentation, decode/crop/resize on Python threads over
+# PIL instead of the native pipeline
+_NATIVE_PIPE = True
+# False: the whole train preprocessing on the host threads
+_DEVICE_AUGMENT = True
 
 
 def make_batch_iterator(bench, subset="train"):

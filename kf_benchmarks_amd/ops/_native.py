@@ -273,8 +273,9 @@ def _pair_event(dst, src, device_only=False):
     return ev
 
 
-# KFB_DEVICE_EVENTS=0: every cross-stream wait records with the system-scope fence
-_DEVICE_EVENTS = os.environ.get("KFB_DEVICE_EVENTS", "1") != "0"
+# compute-to-compute waits skip the system-scope fence (False: every
+# cross-stream wait records with it)
+_DEVICE_EVENTS = True
 
 
 def stream_wait(dst_stream: int, src_stream: int, device_only: bool = False):

@@ -287,7 +287,8 @@ def _igemm_call(algo, x, wmat, y, geo, stats=None, mask=None, xbn=None, mean=Non
            N.ptr(bias), int(relu), algo, N.ptr(stats_shift(stats)), *fin, N.stream(x.device))
 
 
-_TUNE_LOG = os.environ.get("KFB_AUTOTUNE_LOG", "0") == "1"  # print every timed choice
+# KFB_AUTOTUNE_LOG=1 prints every timed choice (tests/test_conv_gpu.py)
+_TUNE_LOG = os.environ.get("KFB_AUTOTUNE_LOG", "0") == "1"
 _ALGO_NAMES = {}
 
 

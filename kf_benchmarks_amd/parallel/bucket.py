@@ -121,9 +121,9 @@ class BucketReducer:
         # when the compute stream may use the reduced gradients; their
         # distance is the all-reduce time backward did not hide.  Both are
         # native calls, so a recorded launch tape replays them (each replay
-        # fills the next slot of the timer's ring).  KFB_COMM_PROBE=0: off.
-        self.timing = False  # (kept for callers; the probe runs whenever on)
-        self.probe = os.environ.get("KFB_COMM_PROBE", "1") != "0"
+        # fills the next slot of the timer's ring); two event records per step.
+        self.timing = False  # (kept for callers; the probe always runs)
+        self.probe = True
         self._timer = None
         self._timing_events = []  # CPU runs: none
         self._handles = []

@@ -132,8 +132,8 @@ def force_pg() -> bool:
 def _pg_options(backend: str):
     """RCCL communicator options: the collective stream gets high priority
     so bucket all-reduces are scheduled ahead of the compute kernels queued
-    beside them (SURVEY 2.4 / 7.4 #3).  KFB_RCCL_LOW_PRIORITY=1 opts out."""
-    if backend != "nccl" or os.environ.get("KFB_RCCL_LOW_PRIORITY") == "1":
+    beside them (SURVEY 2.4 / 7.4 #3)."""
+    if backend != "nccl":
         return None
     try:
         opts = dist.ProcessGroupNCCL.Options()

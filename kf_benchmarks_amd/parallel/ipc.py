@@ -87,6 +87,11 @@ def wrap(addr: int, numel: int, dtype: torch.dtype, device: torch.device) -> tor
             "data": (int(addr), False), "version": 2}
     with torch.cuda.device(device):
         t = torch.as_tensor(_Arr(), device=device)
+    if t.data_ptr() != int(addr) or t.device != torch.device(device):
+        # a copy (or another device's tensor) would silently break the
+        # sharing: writes must land in the peer's allocation
+        raise RuntimeError("ipc.wrap: tensor at 0x%x on %s is not a view of the mapping at 0x%x "
+                           "on %s" % (t.data_ptr(), t.device, int(addr), device))
     return t
 
 

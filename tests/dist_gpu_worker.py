@@ -110,6 +110,13 @@ def main():
     if state is not None:  # asynchronous parameter server
         comm.get_world().barrier()
         res["ps_global_step"] = state.global_step
+        # every rank reads the SAME shared model (rank 0's device memory,
+        # mapped into the others): equal checksums mean the applies landed
+        # in one model, not in per-rank copies
+        torch.cuda.synchronize()
+        res["ps_shared_sum"] = [float(t.double().sum()) for t in state.shared]
+        res["ps_shared_views"] = [t.data_ptr() for t in state.shared]
+        comm.get_world().barrier()
         bench.strategy.close()
     elif getattr(bench.strategy, "store", None) is not None:  # PairAveraging
         res["pa_publishes"] = bench.strategy.store.publishes

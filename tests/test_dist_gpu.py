@@ -88,6 +88,10 @@ def test_two_ranks_async_parameter_server(cuda, tmp_path):
     r0, r1 = _run(kw, 3, tmp_path)
     assert r0["ps_global_step"] == r1["ps_global_step"] == 6
     assert r0["w0"] == r1["w0"]
+    # rank 1's applies landed in rank 0's shared model: both ranks read the
+    # same bytes (ipc.wrap raises if the mapping came back as a copy)
+    assert r0["ps_shared_sum"] == r1["ps_shared_sum"]
+    assert all(s == s for s in r0["ps_shared_sum"])
     for r in (r0, r1):
         assert r["wsum"] != r["w0"] and r["wsum"] == r["wsum"]
         assert all(l == l and abs(l) < 1e3 for l in r["losses"])

@@ -538,6 +538,48 @@ def test_ssd_loss(cuda, dt, case):
     torch.testing.assert_close(a.grad.float().cpu(), b.grad, **t)
 
 
+def test_ssd_loss_bwd_past_2g_elements(cuda):
+    """The SSD loss backward at B*A*(4+C) >= 2^31 elements (~2,900 images of
+    8732 anchors x 85 logits) runs its 64-bit-index form (it used
+    to refuse that size): its first and last images equal a small call over
+    those images bitwise (32-bit form, same arithmetic)."""
+    from kf_benchmarks_amd.ops import _native as N
+    A, C = 8732, 81
+    B = (1 << 31) // (A * (4 + C)) + 2
+    assert B * A * (4 + C) >= (1 << 31)
+    dev = torch.device(cuda)
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn((B, A, 4 + C), generator=g, device=dev, dtype=torch.bfloat16)
+    gt = torch.randn((B, A, 4), generator=g, device=dev)
+    label = torch.randint(0, C, (B, A), generator=g, device=dev).float() + 0.3
+    nm = torch.rand((B,), generator=g, device=dev) * 50 + 1
+    lse = torch.randn((B, A), generator=g, device=dev)
+    w = torch.rand((B, A), generator=g, device=dev)
+
+    def work_of(imgs):
+        n = len(imgs)
+        wk = torch.zeros(n + 3 * n * A, device=dev)
+        wk[n:n + n * A] = lse[imgs].reshape(-1)
+        wk[n + 2 * n * A:] = w[imgs].reshape(-1)
+        return wk
+
+    def bwd(xx, gg, ll, nn_, wk, b):
+        dx = torch.empty_like(xx)
+        gs = torch.full((1,), float(b), device=dev)  # g / B = 1 in every call
+        N.call("kfb_ssd_loss_bwd", N.dt(xx), xx.data_ptr(), gg.data_ptr(), ll.data_ptr(),
+               nn_.data_ptr(), wk.data_ptr(), gs.data_ptr(), b, A, C, dx.data_ptr(),
+               N.stream(dev))
+        return dx
+
+    big = bwd(x, gt, label, nm, work_of(list(range(B))), B)
+    for imgs in ([0, 1], [B - 2, B - 1]):
+        small = bwd(x[imgs].contiguous(), gt[imgs].contiguous(), label[imgs].contiguous(),
+                    nm[imgs].contiguous(), work_of(imgs), 2)
+        assert torch.equal(big[imgs], small), imgs
+    del big, x
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("dt", DT)
 def test_ssd_heads(cuda, dt):
     """Anchor-major SSD logits from NHWC heads (kfb_ssd_heads) vs the
