@@ -297,7 +297,10 @@ def _run(a):
         }
         print(json.dumps(out))
         sys.stdout.flush()
-    watchdog.beat("shutdown", startup=True)
+    # the result line is out: no second JSON line may follow it (a launcher
+    # tearing down a peer that fails after this point is not this job's
+    # failure); shutdown hangs are bounded by the launcher's own timeout
+    watchdog.stop()
     bench.strategy.close()  # collective: model stores / peers released on every rank
     close_input = getattr(getattr(bench, "input", None), "close", None)
     if close_input is not None:
