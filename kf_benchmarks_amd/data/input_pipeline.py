@@ -21,23 +21,43 @@ import numpy as np
 import torch
 
 
+def _mix32(*vals) -> int:
+    """A 31-bit seed from integers (splitmix64 rounds): the synthetic streams
+    of different (seed, rank, step) are independent, where consecutive
+    integers would share draws (the label seed of one step used to be the
+    image seed of the next, and ranks were 1000 steps apart)."""
+    m = (1 << 64) - 1
+    x = 0x9E3779B97F4A7C15
+    for v in vals:
+        x = (x ^ (int(v) & m)) & m
+        x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & m
+        x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & m
+        x ^= x >> 31
+    return x & 0x7FFFFFFE  # (even: the op draws labels from seed + 1)
+
+
 class SyntheticInput:
     def __init__(self, bench, subset="train"):
         self.bench = bench
         model = bench.model
         nclass = bench.dataset.num_classes
         self.resample = bench.params.synthetic_resample
-        self.seed = bench.params.tf_random_seed + 1000 * bench.task_index
+        self.base = (bench.params.tf_random_seed, bench.task_index)
         self.step = 0
         self.inputs = tuple(model.get_synthetic_inputs("input", nclass, bench.device,
-                                                       self.seed))
+                                                       self.seed_at(0)))
+
+    def seed_at(self, step: int) -> int:
+        """The images' seed of ``step`` (labels: + 1) on this rank."""
+        return _mix32(*self.base, step)
 
     def next(self):
         if self.resample:
             self.step += 1
             model = self.bench.model
             self.inputs = tuple(model.get_synthetic_inputs(
-                "input", self.bench.dataset.num_classes, self.bench.device, self.seed + self.step))
+                "input", self.bench.dataset.num_classes, self.bench.device,
+                self.seed_at(self.step)))
         return self.inputs
 
     # launch tape: a replayed step re-samples the batch with the seeds an
@@ -47,7 +67,7 @@ class SyntheticInput:
             self.step += 1
 
     def tape_values(self):
-        s = self.seed + self.step
+        s = self.seed_at(self.step)
         return {"input_seed": s & 0xFFFFFFFF, "input_seed_labels": (s + 1) & 0xFFFFFFFF}
 
     def tape_post(self):

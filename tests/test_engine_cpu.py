@@ -163,3 +163,15 @@ def test_failed_update_releases_strategy(tmp_path):
         fcntl.flock(f2, fcntl.LOCK_EX | fcntl.LOCK_NB)  # would raise if still held
         fcntl.flock(f2, fcntl.LOCK_UN)
     st._lock_f.close()
+
+
+def test_synthetic_seed_streams_are_independent():
+    """Synthetic batches: every (rank, step) gets its own mixed seed; a
+    step's label seed (seed + 1) is never another step's or rank's image
+    seed (it used to be the next step's, and ranks were 1000 steps apart)."""
+    from kf_benchmarks_amd.data.input_pipeline import _mix32
+    seeds = {(r, s): _mix32(1234, r, s) for r in range(8) for s in range(2000)}
+    vals = list(seeds.values())
+    assert len(set(vals)) == len(vals)
+    assert all(v % 2 == 0 and 0 <= v < 2 ** 31 for v in vals)
+    assert not (set(vals) & {v + 1 for v in vals})
