@@ -801,6 +801,7 @@ class BenchmarkCNN:
         return False
 
     def forward_only_step(self):
+        watchdog.beat("forward", self.global_step, startup=self.global_step < 4)
         inputs = tuple(self.input.next())
         with torch.no_grad():
             res = self.net.forward_inputs(inputs, phase_train=False)

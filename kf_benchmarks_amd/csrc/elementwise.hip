@@ -157,38 +157,44 @@ synthetic_images_k(T* __restrict__ x, long n, float mean, float std, uint32_t se
   }
 }
 
-// 8 values per thread (one 16-byte store): both Box-Muller outputs of each
-// draw are used, rejected independently (|z| <= 2), with 32-bit indexing
-// and a per-thread hoisted seed hash - ~10x the per-element kernel above,
-// cheap enough to re-sample the synthetic batch every training step.
+// 8 values per thread (one 16-byte store), 32-bit indexing and a per-thread
+// hoisted seed hash, cheap enough to re-sample the synthetic batch every
+// training step (inside the timed step).  The truncated normal (|z| <= 2) is
+// drawn by inversion instead of Box-Muller rejection: z = sqrt(2) *
+// erfinv(erf(sqrt(2)) * (2u - 1)) maps one uniform to one value with no
+// data-dependent loop (with rejection nearly every wave ran 2-3 rounds of
+// log + sqrt + sincos for its few rejected lanes).  erfinv: single-precision
+// polynomial in w = -log(1 - x^2) (Giles' central branch; |x| <= erf(sqrt 2)
+// keeps w <= 2.42, inside the branch's w < 5 range).
 __device__ __forceinline__ float u01h(uint32_t sh, uint32_t i) {
   const uint32_t h = hash_u32(i ^ sh);
   return ((h >> 8) + 0.5f) * (1.0f / 16777216.0f);
 }
 
+__device__ __forceinline__ float trunc_normal2(float u) {
+  const float x = 0.954499736f * (2.f * u - 1.f);  // erf(sqrt(2)) * (2u - 1)
+  float w = -__logf((1.f - x) * (1.f + x)) - 2.5f;
+  float p = 2.81022636e-08f;
+  p = fmaf(p, w, 3.43273939e-07f);
+  p = fmaf(p, w, -3.5233877e-06f);
+  p = fmaf(p, w, -4.39150654e-06f);
+  p = fmaf(p, w, 0.00021858087f);
+  p = fmaf(p, w, -0.00125372503f);
+  p = fmaf(p, w, -0.00417768164f);
+  p = fmaf(p, w, 0.246640727f);
+  p = fmaf(p, w, 1.50140941f);
+  const float z = 1.41421356f * p * x;
+  return fminf(fmaxf(z, -2.f), 2.f);  // (rounding at the ends)
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256)
 synthetic_images8_k(T* __restrict__ x, unsigned n8, float mean, float std, uint32_t seed) {
+  const uint32_t sh = hash_u32(seed + 0x9e3779b9U);
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += gridDim.x * blockDim.x) {
     Vec<T, 8> o;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      float z0 = 0.f, z1 = 0.f;
-      bool ok0 = false, ok1 = false;
-      for (uint32_t k = 0; k < 8 && !(ok0 && ok1); ++k) {
-        const uint32_t sh1 = hash_u32(seed + 0x9e3779b9U * (2 * k + 1));
-        const uint32_t sh2 = hash_u32(seed + 0x9e3779b9U * (2 * k + 2));
-        const uint32_t j = i * 4 + p;
-        const float r = sqrtf(-2.f * __logf(u01h(sh1, j)));
-        float sn, cs;
-        __sincosf(6.28318530718f * u01h(sh2, j), &sn, &cs);
-        const float a = r * cs, b = r * sn;
-        if (!ok0 && fabsf(a) <= 2.f) { z0 = a; ok0 = true; }
-        if (!ok1 && fabsf(b) <= 2.f) { z1 = b; ok1 = true; }
-      }
-      o.v[2 * p] = from_f32<T>(mean + std * z0);
-      o.v[2 * p + 1] = from_f32<T>(mean + std * z1);
-    }
+    for (int k = 0; k < 8; ++k) o.v[k] = from_f32<T>(mean + std * trunc_normal2(u01h(sh, i * 8 + k)));
     *reinterpret_cast<Vec<T, 8>*>(x + (long)i * 8) = o;
   }
 }

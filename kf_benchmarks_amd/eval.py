@@ -32,7 +32,9 @@ def eval_once(bench, input_source, num_batches, global_step, summary_writer=None
     top1 = top5 = 0.0
     batch = bench.batch_size
     loop_start = start = time.time()
+    from .parallel import watchdog
     for step in range(num_batches):
+        watchdog.beat("eval", step, startup=step < 2)
         inputs = tuple(input_source.next())
         with torch.no_grad():
             res = bench.net.forward_inputs(inputs, phase_train=False)

@@ -175,6 +175,26 @@ def test_synthetic_inputs(cuda):
     assert lab.min().item() >= 0 and lab.max().item() < 1000
 
 
+def test_synthetic_images_truncated_normal_bf16(cuda):
+    """The per-step synthetic batch (bf16, 8 values per thread, drawn by
+    inverting the truncated normal's CDF): mean 127, std 60 * 0.87963 (the
+    std of a normal truncated at +-2), every value within +-2 std, and the
+    histogram matches the truncated normal's CDF."""
+    img = F.synthetic_images((64, 64, 64, 3), torch.bfloat16, cuda, 11).float().cpu()
+    z = (img.reshape(-1) - 127.0) / 60.0
+    assert abs(z.mean().item()) < 5e-3
+    assert abs(z.std().item() - 0.87963) < 5e-3
+    assert z.min().item() >= -2.0 - 1e-2 and z.max().item() <= 2.0 + 1e-2
+    from math import erf, sqrt
+    norm = erf(sqrt(2.0))
+    for t in (-1.5, -0.5, 0.0, 0.7, 1.9):
+        want = 0.5 + 0.5 * erf(t / sqrt(2.0)) / norm
+        assert abs((z <= t).float().mean().item() - want) < 1.2e-2, t  # (bf16 bins)
+    again = F.synthetic_images((64, 64, 64, 3), torch.bfloat16, cuda, 11).float().cpu()
+    other = F.synthetic_images((64, 64, 64, 3), torch.bfloat16, cuda, 12).float().cpu()
+    assert torch.equal(img, again) and not torch.equal(img, other)
+
+
 @pytest.mark.parametrize("kind", ["sgd", "momentum", "rmsprop", "adam"])
 def test_fused_optimizer(cuda, kind):
     from kf_benchmarks_amd import optim
