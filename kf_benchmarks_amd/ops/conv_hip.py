@@ -292,7 +292,7 @@ _TUNE_LOG = os.environ.get("KFB_AUTOTUNE_LOG", "0") == "1"
 _ALGO_NAMES = {}
 
 
-def _time_candidates(cands, run, rounds=2, reps=3, label=None):
+def _time_candidates(cands, run, rounds=2, reps=3, label=None, slack=0.0, cost=None):
     """The fastest candidate: each is warmed once, then timed ``reps``
     back-to-back calls per round over ``rounds`` interleaved rounds (min
     per candidate).  The device is synchronized first so no other stream's
@@ -313,6 +313,12 @@ def _time_candidates(cands, run, rounds=2, reps=3, label=None):
             ev1.synchronize()
             best_t[c] = min(best_t[c], ev0.elapsed_time(ev1))
     best = min(best_t, key=best_t.get)
+    if slack > 0 and cost is not None:
+        # the cheapest candidate (e.g. fewest weight-gradient splits: fewer
+        # slab bytes and reduce work beside the compute stream) among those
+        # within ``slack`` of the fastest isolated time
+        near = [c for c in cands if best_t[c] <= best_t[best] * (1.0 + slack)]
+        best = min(near, key=lambda c: (cost(c), best_t[c]))
     if _TUNE_LOG and label is not None:
         if not _ALGO_NAMES:
             _ALGO_NAMES.update({v: k for k, v in IG_ALGOS.items()})
@@ -555,7 +561,10 @@ def _wgrad_launch(dy, x, dw, geo, target):
 # the candidate workgroup targets on the real operands and caches the best.
 # KFB_CONV_AUTOTUNE=0 pins _WGRAD_TARGET_BLOCKS.
 _AUTOTUNE = os.environ.get("KFB_CONV_AUTOTUNE", "1") != "0" and "KFB_WGRAD_BLOCKS" not in os.environ
-_WGRAD_CANDIDATES = (384, 512, 768, 1024)
+_WGRAD_CANDIDATES = tuple(c for c in (384, 512, 768, 1024)
+                          if c <= int(os.environ.get("KFB_AB_WGRAD_MAX", "1024")))
+# (A/B under test: prefer the smallest grid within this fraction of the best)
+_WGRAD_SLACK = float(os.environ.get("KFB_AB_WGRAD_SLACK", "0"))
 # bit 16 of a candidate selects the LDS-DMA wgrad kernel (wgrad_glds_k: 128-wide
 # output-channel tiles, operands < 2 GiB); KFB_WGRAD_ALGO=classic|glds pins one.
 # (Its 2-stage ring of 64-row steps was measured against a 4-stage ring of
@@ -593,7 +602,8 @@ def _tune_wgrad(dy, x, dw, geo):
         return _WGRAD_TARGET_BLOCKS
     scratch = torch.zeros_like(dw)
     best = _time_candidates(_wgrad_candidates(geo), lambda t: _wgrad_launch(dy, x, scratch, geo, t),
-                            label="wgrad %s" % (geo,))
+                            label="wgrad %s" % (geo,), slack=_WGRAD_SLACK,
+                            cost=lambda t: t & 0xFFFF)
     _wgrad_tuned[key] = best
     return best
 

@@ -23,4 +23,10 @@ step() {
 step ds2_bs16 400 python bench.py --model deepspeech2 --batch_size 16 --steps 5 --warmup 4
 step rccl_1rank 300 env KFB_FORCE_PG=1 python bench.py --steps 20 --warmup 6
 bash scripts/gpu_miopen_bar.sh "$TAG" || exit $?
+# probe: can two ranks share the box's one GPU over our native RCCL
+# communicator (the N > 1 native + tape path)?  RCCL may refuse duplicate
+# devices; the watchdog bounds any hang (KFB_COMM_TIMEOUT_S)
+step rccl_2rank_1gpu 300 env HIP_VISIBLE_DEVICES=0 KFB_COMM_TIMEOUT_S=90 python -m torch.distributed.run \
+    --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 \
+    --steps 10 --warmup 5 --batch_size 64
 echo done

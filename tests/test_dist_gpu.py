@@ -130,7 +130,10 @@ def test_one_rank_rccl_is_identity(cuda, tmp_path, native):
     assert a["bucket_launches"] == 4 * a["num_buckets"] > 0
     assert b["bucket_launches"] == 0
     assert a["reduce_identity"] is True
-    assert a["w0"] == b["w0"] and a["losses"][0] == b["losses"][0]
+    # (the first loss to fp32 rounding: the 150528-deep FC forward is a
+    # split-K GEMM whose partial sums land in either order)
+    assert a["w0"] == b["w0"]
+    assert abs(a["losses"][0] - b["losses"][0]) <= 1e-6 * abs(b["losses"][0])
     for la, lb in zip(a["losses"], b["losses"]):
         assert abs(la - lb) <= 1e-4 * max(1.0, abs(lb)), (a["losses"], b["losses"])
 
