@@ -561,6 +561,7 @@ def _wgrad_launch(dy, x, dw, geo, target):
 # the candidate workgroup targets on the real operands and caches the best.
 # KFB_CONV_AUTOTUNE=0 pins _WGRAD_TARGET_BLOCKS.
 _AUTOTUNE = os.environ.get("KFB_CONV_AUTOTUNE", "1") != "0" and "KFB_WGRAD_BLOCKS" not in os.environ
+_AUTOTUNE_WGRAD = _AUTOTUNE  # (separately switchable by the tests)
 _WGRAD_CANDIDATES = tuple(c for c in (384, 512, 768, 1024)
                           if c <= int(os.environ.get("KFB_AB_WGRAD_MAX", "1024")))
 # (A/B under test: prefer the smallest grid within this fraction of the best)
@@ -623,7 +624,7 @@ def conv_wgrad(dy, x, w_shape, stride, pads, out=None):
     else:
         dw = torch.zeros((cout, KH, KW, C), dtype=torch.float32, device=x.device)
     geo = (n, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, cout)
-    target = _tune_wgrad(dy, x, dw, geo) if _AUTOTUNE else _WGRAD_TARGET_BLOCKS
+    target = _tune_wgrad(dy, x, dw, geo) if _AUTOTUNE_WGRAD else _WGRAD_TARGET_BLOCKS
     _wgrad_launch(dy, x, dw, geo, target)
     return dw
 
