@@ -211,8 +211,23 @@ class DeepSpeech2Model(model_lib.ModuleModel):
                 [self.batch_size, 1]]
 
     def get_synthetic_inputs(self, input_name, nclass, device="cpu", seed=0):
-        g = torch.Generator(device="cpu").manual_seed(seed)
         shapes = self.get_input_shapes("train")
+        if torch.device(device).type == "cuda":
+            # drawn on the device (one launch each, the seed a launch-tape
+            # argument, so a replayed step re-samples them); the constant
+            # sequence lengths are persistent tensors (no fill per step)
+            B, L = shapes[1]
+            feats = F_ops.synthetic_uniform(tuple(shapes[0]), self.data_type, device, seed, 31)
+            labels = F_ops.synthetic_ints(B * L, 28, device, seed, 32).view(B, L)
+            key = (str(device), B)
+            lens = getattr(self, "_lens", None)
+            if lens is None or lens[0] != key:
+                lens = self._lens = (key, torch.full(shapes[2], self.max_time_steps,
+                                                     dtype=torch.int32, device=device),
+                                     torch.full(shapes[3], self.max_label_length,
+                                                dtype=torch.int32, device=device))
+            return feats, labels, lens[1], lens[2]
+        g = torch.Generator(device="cpu").manual_seed(seed)
         feats = torch.rand(shapes[0], generator=g).to(device, self.data_type)
         labels = torch.randint(0, 28, shapes[1], generator=g, dtype=torch.int32).to(device)
         ilen = torch.full(shapes[2], self.max_time_steps, dtype=torch.int32, device=device)

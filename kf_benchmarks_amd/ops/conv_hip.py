@@ -105,6 +105,13 @@ _ig_tuned = {}
 # largest K (= KH*KW*Cin) offered the multi-tile candidates (register-staged;
 # the LDS-DMA form gets twice that)
 _MULTI_K = 2304
+# the streaming 3x3 kernels (IG_S3, the s3 weight gradient) off: the
+# bitwise tape oracles run without them (tests/test_tape_gpu.py)
+_NO_S3 = False
+# the streaming 1x1 / stem kernels off (tests: their A/B against the
+# one-tile kernels, e.g. tests/test_tape_gpu.py)
+_NO_S1 = False
+_NO_S7 = False
 # The ReLU / bias backward of a conv without BN in the consuming conv's dgrad
 # epilogue instead of its own pass: off (on VGG-16 it removes 1.05 ms/step of
 # act_bwd_bias but the extra read of y slows the dgrad convs by 0.8 ms and the
@@ -380,17 +387,17 @@ def _igemm_algo(x, wmat, y, geo, fused=(None, None, None, None, None, None), bac
     if fast and C % 64 != 0:
         # 8-channel geometry: the generic loader competes with the FAST ones
         cands += (IG_GENERIC,)
-    if fast and N.load().kfb_conv_s3_applicable(
+    if fast and not _NO_S3 and N.load().kfb_conv_s3_applicable(
             C, ncol, KH, KW, geo[8], geo[9], geo[10], geo[11], geo[1], geo[2], geo[4], geo[5]) \
             and geo[13] == geo[4] and geo[14] == geo[5] and geo[15] == 1 and geo[16] == ncol:
         cands += (IG_S3,)
-    if fast and mcoef is None and bact[0] is None and not (int(bact[1]) & 3) \
+    if fast and not _NO_S1 and mcoef is None and bact[0] is None and not (int(bact[1]) & 3) \
             and (mask is None or (xbn is not None and mask.dtype == torch.uint8)) \
             and N.load().kfb_conv_s1_applicable(
             C, ncol, KH, KW, geo[8], geo[9], geo[10], geo[11], geo[1], geo[2], geo[4], geo[5]) \
             and geo[13] == geo[4] and geo[14] == geo[5] and geo[15] == 1 and geo[16] == ncol:
         cands += (IG_S1,)
-    if xbn is None and addend is None and mask is None and bact[0] is None \
+    if not _NO_S7 and xbn is None and addend is None and mask is None and bact[0] is None \
             and not (int(bact[1]) & 3) and not trans and N.load().kfb_conv_s7_applicable(
             C, ncol, KH, KW, geo[8], geo[9], geo[10], geo[11], geo[1], geo[2], geo[4], geo[5]) \
             and geo[13] == geo[4] and geo[14] == geo[5] and geo[15] == 1 and geo[16] == ncol:
@@ -584,7 +591,7 @@ def _wgrad_candidates(geo):
     n, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl, cout = geo
     if _WGRAD_ALGO == "s3":
         return (_WGRAD_S3,)
-    s3 = ((_WGRAD_S3,) if N.load().kfb_conv_s3_applicable(
+    s3 = ((_WGRAD_S3,) if not _NO_S3 and N.load().kfb_conv_s3_applicable(
         C, cout, KH, KW, sh, sw, pt, pl, H, W, OH, OW) else ())
     glds = tuple(t | _WGRAD_GLDS for t in _WGRAD_CANDIDATES) if cout > 64 else ()
     if _WGRAD_ALGO == "classic" or not glds:

@@ -231,3 +231,22 @@ def test_stream_and_autotune_knobs_keep_the_gradients(cuda, monkeypatch, knob, o
     vals = sorted(cos.values())
     worst = sorted(cos.items(), key=lambda kv: kv[1])[:6]
     assert vals[len(vals) // 2] > 0.99 and vals[0] > 0.95, (vals[0], vals[len(vals) // 2], worst)
+
+
+@pytest.mark.parametrize("algo", ["glds", "classic", "onebuf", "glds_n64", "gshort64",
+                                  "tall256"])
+def test_forced_conv_kernel_in_network_keeps_the_gradients(cuda, monkeypatch, algo):
+    """Every conv of ResNet-50 (fwd and dgrad with their fused BN epilogues)
+    on one forced igemm kernel (the streaming kernels' geometries included):
+    the autotune may pick any offered kernel on any layer, so each must give
+    the network's gradients, BN gamma / beta included, not only pass the
+    single-layer epilogue tests."""
+    from kf_benchmarks_amd.ops import conv_hip
+    loss_ref, ref = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
+    monkeypatch.setattr(conv_hip, "_IG_FORCE", conv_hip.IG_ALGOS[algo])
+    loss_f, got = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
+    assert abs(loss_f - loss_ref) < 5e-3 * abs(loss_ref), (loss_f, loss_ref)
+    cos = {k: _cos(got[k], r) for k, r in ref.items() if r.norm() > 0}
+    vals = sorted(cos.values())
+    worst = sorted(cos.items(), key=lambda kv: kv[1])[:6]
+    assert vals[len(vals) // 2] > 0.99 and vals[0] > 0.95, (vals[0], vals[len(vals) // 2], worst)
