@@ -204,12 +204,3 @@ KFB_API int kfb_rccl_recv(void* comm, void* buf, size_t count, int dtype, int pe
 
 KFB_API int kfb_rccl_group_start() { return api().ok ? rc(api().group_start()) : 999; }
 KFB_API int kfb_rccl_group_end() { return api().ok ? rc(api().group_end()) : 999; }
-
-// A high-priority stream for the collectives (scheduled ahead of the
-// compute kernels queued beside them).
-KFB_API hipError_t kfb_stream_create_priority(int high, hipStream_t* s) {
-  int lo = 0, hi = 0;
-  hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
-  if (e != hipSuccess) return e;
-  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, high ? hi : lo);
-}

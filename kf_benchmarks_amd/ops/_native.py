@@ -246,6 +246,8 @@ def stream(device=None) -> int:
         elif isinstance(device, int):
             idx = device
         else:
+            if isinstance(device, str):
+                device = torch.device(device)
             idx = device.index if device.index is not None else torch.cuda.current_device()
         return _RAW_STREAM(idx)
     return torch.cuda.current_stream(device).cuda_stream

@@ -117,26 +117,14 @@ def is_parameter_server(alg: str) -> bool:
     return alg in PS_ALGS
 
 
-_SIDE = {}
-
-
 def _side_stream(buf):
-    """(context, stream) for a chained collective: a side stream that waits
-    for the producer, so stage-to-stage waits never block the compute
-    stream (async collectives of one group are NOT ordered by gloo, and on
-    RCCL a wait on the caller's stream would serialize it behind the comm)."""
-    import torch
-    if not buf.is_cuda:
-        return _null()
-    st = _SIDE.get(buf.device)
-    if st is None:
-        st = _SIDE[buf.device] = torch.cuda.Stream(buf.device)
-    # the native (recordable) wait, not torch's Stream.wait_stream: a launch
-    # tape replays this edge, so the chained collective never reads a bucket
-    # before backward has written it
-    from ..ops import _native as N
-    N.stream_wait(st.cuda_stream, N.stream(buf.device))
-    return torch.cuda.stream(st)
+    """Context of a chained collective's stages.  Device buffers: the
+    caller's stream itself - the bucket reducer issues from the weight-
+    gradient side stream, which already follows the producers, and one
+    stream orders the stages (a further stream waiting on it cost 7-11
+    ms/step, profiles/r13_comm_stream_ab.txt).  Host (gloo) buffers: no
+    stream; the stages are ordered by host waits."""
+    return _null()
 
 
 def launch_collective(comm, buf, alg: str, bucket_index: int, world_size: int, op: str = "sum",
@@ -146,8 +134,8 @@ def launch_collective(comm, buf, alg: str, bucket_index: int, world_size: int, o
 
     Multi-stage chains (parameter-server reduce -> broadcast, and the
     hierarchical reduce -> leader all-reduce -> broadcast) order their stages
-    with ``Work.wait()``: on RCCL that is a stream wait on the side stream
-    (the host and the compute stream run on), on gloo - the CPU test
+    with ``Work.wait()``: on the native communicator the stages share the
+    issuing stream (the wait is a no-op), on gloo - the CPU test
     backend, whose async ops are not ordered - it is a host wait inside the
     backward hook.  The chains are verified over gloo at 2-8 ranks
     (tests/test_variable_update.py, tests/test_scale_rehearsal.py) and over
@@ -170,9 +158,9 @@ def launch_collective(comm, buf, alg: str, bucket_index: int, world_size: int, o
 class Hierarchical:
     """Two-level all-reduce over torch.distributed subgroups.  Built
     collectively (every rank constructs it, same order).  The three stages
-    run on a side stream that first waits for the producer stream
-    (:func:`_side_stream`), so the caller's stream is only blocked by the
-    final wait."""
+    run in order on the issuing stream (the bucket reducer's weight-gradient
+    side stream, :func:`_side_stream`), so the compute stream is only
+    blocked by the final wait."""
 
     def __init__(self, world_size: int, rank: int, topology: str = "dgx1"):
         import torch.distributed as dist

@@ -5,14 +5,18 @@ RCCL unique id and publishes it in the job's TCP store (the rendezvous of
 ``torch.distributed``'s env:// init, which here only carries host-side
 traffic over gloo); every rank then calls ``ncclCommInitRank`` on its GPU.
 
-Collectives run on a dedicated high-priority stream: the stream first
-waits for the caller's current stream (the gradients are ready there), the
-collective is enqueued, and :meth:`Work.wait` makes the then-current stream
-wait for the comm stream.  All three steps are native calls
-(``kfb_stream_wait``, ``kfb_rccl_*``), so a recorded launch tape replays
-them with the rest of the step.  Replaces the reference's NCCL / Horovod /
-KungFu device collectives (tcb/allreduce.py:297-299, tcb/benchmark_cnn.py:
-3122-3130, 2094-2100); SURVEY section 7.1.
+Collectives run on the caller's current stream, as RCCL's own API does:
+the bucket reducer issues them from the weight-gradient side stream, which
+has already caught up with the compute stream, so the collective follows
+both producers without a stream of its own; :meth:`Work.wait` makes the
+then-current stream wait for the issuing one.  Both are native calls
+(``kfb_rccl_*``, ``kfb_stream_wait``), so a recorded launch tape replays
+them with the rest of the step.  (A dedicated collective stream - one more
+stream waiting on the side stream - cost 28.5 vs 17.6 ms/step at one rank
+at either priority, 24.3 at ordinary priority; profiles/r13_comm_stream_ab.txt.)
+Replaces the reference's NCCL / Horovod / KungFu device collectives
+(tcb/allreduce.py:297-299, tcb/benchmark_cnn.py:3122-3130, 2094-2100);
+SURVEY section 7.1.
 """
 
 from __future__ import annotations
@@ -95,19 +99,21 @@ def subgroup(world_native: "NativeComm", ranks, store, tag: str):
 
 
 class Work:
-    """Completion handle of the collectives enqueued so far on a comm stream."""
+    """Completion handle of a collective: the stream it was issued on."""
 
-    __slots__ = ("comm", "device")
+    __slots__ = ("stream_h", "device")
 
-    def __init__(self, comm, device):
-        self.comm, self.device = comm, device
+    def __init__(self, stream_h, device):
+        self.stream_h, self.device = stream_h, device
 
     def wait(self):
         """The caller's current stream waits for the collective (no host wait)."""
-        N.stream_wait(N.stream(self.device), self.comm.stream_h)
+        cur = N.stream(self.device)
+        if cur != self.stream_h:
+            N.stream_wait(cur, self.stream_h)
 
     def synchronize(self):
-        self.comm.stream.synchronize()
+        torch.cuda.synchronize(self.device)
 
 
 class NativeComm:
@@ -127,10 +133,6 @@ class NativeComm:
         else:
             raw = store.get(key)
             ctypes.memmove(uid, raw, 128)
-        # a high-priority stream: the collectives are scheduled ahead of the
-        # compute kernels queued beside them
-        self.stream = torch.cuda.Stream(self.device, priority=-1)
-        self.stream_h = self.stream.cuda_stream
         h = ctypes.c_void_p()
         self._check(lib.kfb_rccl_init(size, uid, rank, device_index, ctypes.byref(h)),
                     "ncclCommInitRank")
@@ -145,52 +147,49 @@ class NativeComm:
             msg = N.load().kfb_rccl_error_string(rc)
             raise RcclError("%s failed: %s (%d)" % (what, msg.decode() if msg else "?", rc))
 
-    def _enter(self, t: torch.Tensor):
+    def _enter(self, t: torch.Tensor) -> int:
+        """The stream to issue on: the caller's current one."""
         if not t.is_cuda or not t.is_contiguous():
             raise RcclError("native collectives take contiguous device tensors")
         if t.dtype not in _DT:
             raise RcclError("dtype %s not supported by the native communicator" % t.dtype)
-        N.stream_wait(self.stream_h, N.stream(t.device))  # inputs are ready
-        t.record_stream(self.stream)
         self.collectives += 1
+        return N.stream(t.device)
 
     def all_reduce(self, t, op="sum"):
-        self._enter(t)
+        s = self._enter(t)
         N.call("kfb_rccl_all_reduce", self.h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype],
-               _OPS[op], self.stream_h)
-        return Work(self, t.device)
+               _OPS[op], s)
+        return Work(s, t.device)
 
     def reduce(self, t, dst=0, op="sum"):
-        self._enter(t)
+        s = self._enter(t)
         N.call("kfb_rccl_reduce", self.h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype],
-               _OPS[op], int(dst), self.stream_h)
-        return Work(self, t.device)
+               _OPS[op], int(dst), s)
+        return Work(s, t.device)
 
     def broadcast(self, t, src=0):
-        self._enter(t)
+        s = self._enter(t)
         N.call("kfb_rccl_broadcast", self.h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype],
-               int(src), self.stream_h)
-        return Work(self, t.device)
+               int(src), s)
+        return Work(s, t.device)
 
     def all_gather(self, out, t):
         """out [size * t.numel()] receives every rank's t, rank-major."""
-        self._enter(t)
-        out.record_stream(self.stream)
+        s = self._enter(t)
         N.call("kfb_rccl_all_gather", self.h, t.data_ptr(), out.data_ptr(), t.numel(),
-               _DT[t.dtype], self.stream_h)
-        return Work(self, t.device)
+               _DT[t.dtype], s)
+        return Work(s, t.device)
 
     def send(self, t, peer):
-        self._enter(t)
-        N.call("kfb_rccl_send", self.h, t.data_ptr(), t.numel(), _DT[t.dtype], int(peer),
-               self.stream_h)
-        return Work(self, t.device)
+        s = self._enter(t)
+        N.call("kfb_rccl_send", self.h, t.data_ptr(), t.numel(), _DT[t.dtype], int(peer), s)
+        return Work(s, t.device)
 
     def recv(self, t, peer):
-        self._enter(t)
-        N.call("kfb_rccl_recv", self.h, t.data_ptr(), t.numel(), _DT[t.dtype], int(peer),
-               self.stream_h)
-        return Work(self, t.device)
+        s = self._enter(t)
+        N.call("kfb_rccl_recv", self.h, t.data_ptr(), t.numel(), _DT[t.dtype], int(peer), s)
+        return Work(s, t.device)
 
     def group_start(self):
         N.call("kfb_rccl_group_start")
@@ -213,7 +212,7 @@ class NativeComm:
             from . import watchdog
             watchdog.remove_comm(self.h)
             try:
-                self.stream.synchronize()
+                torch.cuda.synchronize(self.device)
             except RuntimeError:
                 abort = True
             N.load().kfb_rccl_destroy(self.h, int(abort))

@@ -97,6 +97,27 @@ def main():
             "dgrad": lambda: conv_hip.conv_dgrad(dy, wp, xp.shape, (s, s), pads),
             "wgrad": lambda: conv_hip.conv_wgrad(dy, xp, wp.shape, (s, s), pads),
         }
+        if k == 7 and s == 2 and cin <= 4:
+            # the stem as the network runs it (ops/conv_hip.py _Conv2d, "pairs"):
+            # the padded pixel-pair view and the pair weight are built per call
+            # and timed with the conv; no data gradient (the input's)
+            def stem_fwd():
+                xv = conv_hip.stem_pairs_input(x, w.shape, pads)
+                w2 = conv_hip.stem_pairs_weight(w)
+                return conv_hip.conv_fwd(xv, w2, (2, 1), (0, 0, 0, 0))
+
+            xv0 = conv_hip.stem_pairs_input(x, w.shape, pads)
+            w20 = conv_hip.stem_pairs_weight(w)
+            dwo = torch.zeros((cout, k, k, cin), dtype=torch.float32, device=dev)
+
+            def stem_wgrad():
+                scratch = torch.zeros((cout, 8, 4, 8), dtype=torch.float32, device=dev)
+                conv_hip.conv_wgrad(dy, xv0, w20.shape, (2, 1), (0, 0, 0, 0), out=scratch)
+                conv_hip.N.call("kfb_stem_weight_grad", scratch.data_ptr(), dwo.data_ptr(), cout,
+                                k, k, cin, conv_hip.N.stream(dev))
+                return dwo
+
+            hip = {"fwd": stem_fwd, "wgrad": stem_wgrad}
         xc = x.permute(0, 3, 1, 2)
         wc = w.permute(0, 3, 1, 2)
         dyc = dy.permute(0, 3, 1, 2)

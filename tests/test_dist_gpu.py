@@ -99,8 +99,8 @@ def test_two_ranks_async_parameter_server(cuda, tmp_path):
 
 # RCCL proper: a 1-rank "nccl" process group (KFB_FORCE_PG=1).  RCCL refuses
 # two ranks on one device, so on the 1-GPU box the real communicator runs at
-# size 1: same bucket hooks, same async all-reduce on RCCL's high-priority
-# stream, same broadcast; the result must match the run without any group.
+# size 1: same bucket hooks, same async all-reduce issued from the weight-
+# gradient side stream, same broadcast; the result must match the run without any group.
 _RCCL = dict(KFB_FORCE_PG="1", KFB_DIST_BACKEND=None, WORLD_SIZE=None, RANK=None,
              LOCAL_RANK=None)
 _NOCOMM = dict(KFB_DIST_BACKEND=None, WORLD_SIZE=None, RANK=None, LOCAL_RANK=None)

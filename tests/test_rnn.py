@@ -216,6 +216,7 @@ def test_deepspeech2_small_gpu_matches_cpu(cuda, rnn_type):
     from kf_benchmarks_amd.models.model import make_network
     d = datasets.create_dataset(None, "librispeech")
     losses, grads = [], []
+    cpu_inp = None
     for dev in ("cpu", cuda):
         m = model_config.get_model_config("deepspeech2", d, P.make_params(model="deepspeech2"))
         m.max_time_steps, m.max_label_length, m.rnn_hidden_size = 120, 20, 32
@@ -223,7 +224,11 @@ def test_deepspeech2_small_gpu_matches_cpu(cuda, rnn_type):
         m.set_batch_size(4)
         torch.manual_seed(0)
         net = make_network(m, d.num_classes, str(dev), torch.float32)
-        inp = m.get_synthetic_inputs("x", d.num_classes, str(dev), 0)
+        # the same inputs on both (the device draws its own synthetic stream)
+        if cpu_inp is None:
+            inp = cpu_inp = m.get_synthetic_inputs("x", d.num_classes, "cpu", 0)
+        else:
+            inp = tuple(t.to(dev) for t in cpu_inp)
         res = net.forward_inputs(inp)
         loss = m.loss_function(inp, res)
         loss.backward()
