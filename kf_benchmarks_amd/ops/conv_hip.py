@@ -569,10 +569,13 @@ def _wgrad_launch(dy, x, dw, geo, target):
 # KFB_CONV_AUTOTUNE=0 pins _WGRAD_TARGET_BLOCKS.
 _AUTOTUNE = os.environ.get("KFB_CONV_AUTOTUNE", "1") != "0" and "KFB_WGRAD_BLOCKS" not in os.environ
 _AUTOTUNE_WGRAD = _AUTOTUNE  # (separately switchable by the tests)
-_WGRAD_CANDIDATES = tuple(c for c in (384, 512, 768, 1024)
-                          if c <= int(os.environ.get("KFB_AB_WGRAD_MAX", "1024")))
-# (A/B under test: prefer the smallest grid within this fraction of the best)
-_WGRAD_SLACK = float(os.environ.get("KFB_AB_WGRAD_SLACK", "0"))
+_WGRAD_CANDIDATES = (384, 512, 768, 1024)
+# The autotune takes the smallest grid (fewest split-K slabs: fewer slab
+# bytes and reduce work beside the compute stream) within this fraction of
+# the fastest isolated time: in the network, 0.3 beat the fastest-isolated
+# choice by 0.13 ms/step on interleaved runs, 0.15 by 0.08, 0.5 by 0.07,
+# and capping the grid at 512 lost 0.25 (profiles/r13_wgrad_grid_ab.txt)
+_WGRAD_SLACK = 0.3
 # bit 16 of a candidate selects the LDS-DMA wgrad kernel (wgrad_glds_k: 128-wide
 # output-channel tiles, operands < 2 GiB); KFB_WGRAD_ALGO=classic|glds pins one.
 # (Its 2-stage ring of 64-row steps was measured against a 4-stage ring of

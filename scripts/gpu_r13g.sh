@@ -3,6 +3,7 @@
 # on the caller's stream, exposed-time probe off) against torch's group, and
 # the DeepSpeech2 GPU tests fixed after r13f.  Each GPU step under its own
 # time limit; fault / abort / timeout stops the script.
+# (The KFB_AB_* switches were temporary and were removed after this A/B.)
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"
