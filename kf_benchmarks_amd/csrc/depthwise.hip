@@ -10,10 +10,9 @@
 //   fwd   : y[n,oh,ow,c]  = sum_{a,b} x[n, oh*s-pt+a, ow*s-pl+b, c] * w[a,b,c]
 //   dgrad : dx[n,h,w,c]   = sum_{a,b: (h+pt-a)%s==0 ...} dy[n,(h+pt-a)/s,(w+pl-b)/s,c] * w[a,b,c]
 //   wgrad : dw[a,b,c]    += sum_{n,oh,ow} dy[n,oh,ow,c] * x[n, oh*s-pt+a, ow*s-pl+b, c]
-// wgrad: a workgroup owns one V-channel group and a slice of output pixels;
-// its 256 lanes each accumulate KH*KW*V partial sums in registers over a
-// strided subset of the slice, reduce through LDS and add the block's sum
-// into the fp32 filter gradient with one atomic per element.
+// wgrad: see dw_wgrad_k (lanes along the NHWC vector index, taps x V
+// partial sums per lane, one LDS reduction and one atomic per element and
+// workgroup).
 #include "common.h"
 
 namespace kfb {
@@ -93,61 +92,109 @@ dw_dgrad_k(const T* __restrict__ dy, const T* __restrict__ w, T* __restrict__ dx
   }
 }
 
-// KMAX taps accumulated per lane in registers (7x7 max).
-template <typename T, int V, int KMAX>
+// Filter gradient.  Lanes run along the NHWC vector index (pixel-major,
+// channel group minor), so a wave's dy / x loads are contiguous runs: with
+// cv = C/V channel groups, a workgroup holds cvb = min(cv, 256) groups
+// (blockIdx.y picks the chunk) times P = 256/cvb pixel lanes, and every
+// thread keeps its channel group while it walks its slice of pixels with
+// stride P.  A workgroup covers ROWS filter rows of at most RW taps each
+// (blockIdx.z picks the row group: 3x3 filters in one, 5x5 / 7x7 one row per
+// group, so the accumulators stay at <= 7 x 8 registers and there are
+// enough workgroups).  The P pixel lanes of a group are summed through LDS
+// one tap at a time and the workgroup adds its sum into the fp32 filter
+// gradient (one atomic per element and workgroup).  (The per-pixel-lane
+// layout it replaces loaded one 8-byte piece per lane from a different cache
+// line: MobileNet-v2's filter gradients took 5.3 of its 14.8 ms step,
+// profiles/r13_depthwise.txt.)
+template <typename T, int V, int ROWS, int RW>
 __global__ void __launch_bounds__(256)
 dw_wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ dw, DwGeo g,
-           int pix_per_block) {
-  __shared__ float red[256 / 64][KMAX * V];
+           int cvb, int P, int ppb, FastDiv fow, FastDiv foh) {
+  __shared__ float red[256 * V];
   const int cv = g.C / V;
-  const int cg = blockIdx.y;  // channel group
+  const int tid = threadIdx.x;
+  const int gl = tid % cvb, q = tid / cvb;
+  const int cg = blockIdx.y * cvb + gl;
+  const bool active = q < P && cg < cv;
   const int c = cg * V;
-  const long M = (long)g.N * g.OH * g.OW;
-  const long p0 = (long)blockIdx.x * pix_per_block;
-  const long p1 = p0 + pix_per_block < M ? p0 + pix_per_block : M;
-  const int taps = g.KH * g.KW;
-  float acc[KMAX][V];
+  const int row0 = blockIdx.z * ROWS;
+  const int M = g.N * g.OH * g.OW;
+  const int p0 = blockIdx.x * ppb;
+  const int p1 = p0 + ppb < M ? p0 + ppb : M;
+  float acc[ROWS * RW][V];
 #pragma unroll
-  for (int t = 0; t < KMAX; ++t)
+  for (int t = 0; t < ROWS * RW; ++t)
 #pragma unroll
     for (int k = 0; k < V; ++k) acc[t][k] = 0.f;
-  for (long p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
-    const int ow = (int)(p % g.OW);
-    const long q = p / g.OW;
-    const int oh = (int)(q % g.OH);
-    const int n = (int)(q / g.OH);
-    float dv[V];
-    load_vec<T, V>(dy + p * g.C + c, dv);
-    const int h0 = oh * g.sh - g.pt, w0 = ow * g.sw - g.pl;
+  if (active) {
+    for (int p = p0 + q; p < p1; p += P) {
+      const int r = fow.div(p);
+      const int ow = p - r * g.OW;
+      const int n = foh.div(r);
+      const int oh = r - n * g.OH;
+      float dv[V];
+      load_vec<T, V>(dy + (long)p * g.C + c, dv);
+      const int h0 = oh * g.sh - g.pt + row0, w0 = ow * g.sw - g.pl;
+      const T* xn = x + (long)n * g.H * g.W * g.C + c;
 #pragma unroll
-    for (int t = 0; t < KMAX; ++t) {
-      const int a = t / g.KW, b = t - a * g.KW;
-      const int h = h0 + a, ww = w0 + b;
-      if (t < taps && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W) {
-        float xv[V];
-        load_vec<T, V>(x + (((long)n * g.H + h) * g.W + ww) * g.C + c, xv);
+      for (int a = 0; a < ROWS; ++a) {
+        const int h = h0 + a;
+        if (row0 + a >= g.KH || (unsigned)h >= (unsigned)g.H) continue;
 #pragma unroll
-        for (int k = 0; k < V; ++k) acc[t][k] = fmaf(dv[k], xv[k], acc[t][k]);
+        for (int b = 0; b < RW; ++b) {
+          const int ww = w0 + b;
+          if (b < g.KW && (unsigned)ww < (unsigned)g.W) {
+            float xv[V];
+            load_vec<T, V>(xn + ((long)h * g.W + ww) * g.C, xv);
+#pragma unroll
+            for (int k = 0; k < V; ++k) acc[a * RW + b][k] = fmaf(dv[k], xv[k], acc[a * RW + b][k]);
+          }
+        }
       }
     }
   }
-  // wave reduce, then across the 4 waves through LDS
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // per tap: the P pixel lanes of each channel group through LDS
 #pragma unroll
-  for (int t = 0; t < KMAX; ++t) {
+  for (int t = 0; t < ROWS * RW; ++t) {
+    const int a = t / RW, b = t - a * RW;
+    if (row0 + a < g.KH && b < g.KW) {  // uniform over the block
+      if (active) {
 #pragma unroll
-    for (int k = 0; k < V; ++k) {
-      const float s = wave_sum(acc[t][k]);
-      if (lane == 0) red[wid][t * V + k] = s;
+        for (int k = 0; k < V; ++k) red[tid * V + k] = acc[t][k];
+      }
+      __syncthreads();
+      float* dwt = dw + (long)((row0 + a) * g.KW + b) * g.C;
+      for (int e = tid; e < cvb * V; e += 256) {
+        const int gl2 = e / V, k = e - gl2 * V;
+        const int cg2 = blockIdx.y * cvb + gl2;
+        if (cg2 < cv) {
+          float s = 0.f;
+          for (int qq = 0; qq < P; ++qq) s += red[(qq * cvb + gl2) * V + k];
+          if (s != 0.f) atomicAdd(dwt + cg2 * V + k, s);
+        }
+      }
+      __syncthreads();
     }
   }
-  __syncthreads();
-  for (int e = threadIdx.x; e < taps * V; e += blockDim.x) {
-    const float s = red[0][e] + red[1][e] + red[2][e] + red[3][e];
-    const int t = e / V, k = e - t * V;
-    if (s != 0.f) atomicAdd(dw + t * g.C + c + k, s);
-  }
-  (void)cv;
+}
+
+// V channels per lane (<= 8: ROWS * RW * V accumulators <= 72)
+template <typename T, int ROWS, int RW>
+static void launch_dw_wgrad(int vw, dim3 grid, hipStream_t stream, const void* dy, const void* x,
+                            float* dw, const DwGeo& g, int cvb, int P, int ppb, FastDiv fow,
+                            FastDiv foh) {
+  if (vw == 8)
+    hipLaunchKernelGGL((dw_wgrad_k<T, 8, ROWS, RW>), grid, dim3(256), 0, stream, (const T*)dy,
+                       (const T*)x, dw, g, cvb, P, ppb, fow, foh);
+  else if (vw == 4)
+    hipLaunchKernelGGL((dw_wgrad_k<T, 4, ROWS, RW>), grid, dim3(256), 0, stream, (const T*)dy,
+                       (const T*)x, dw, g, cvb, P, ppb, fow, foh);
+  else if (vw == 2)
+    hipLaunchKernelGGL((dw_wgrad_k<T, 2, ROWS, RW>), grid, dim3(256), 0, stream, (const T*)dy,
+                       (const T*)x, dw, g, cvb, P, ppb, fow, foh);
+  else
+    hipLaunchKernelGGL((dw_wgrad_k<T, 1, ROWS, RW>), grid, dim3(256), 0, stream, (const T*)dy,
+                       (const T*)x, dw, g, cvb, P, ppb, fow, foh);
 }
 
 inline DwGeo geo(int N, int H, int W, int C, int OH, int OW, int KH, int KW, int sh, int sw,
@@ -193,34 +240,44 @@ KFB_API hipError_t kfb_dw_wgrad(int dtype, const void* dy, const void* x, float*
                                 int W, int C, int OH, int OW, int KH, int KW, int sh, int sw,
                                 int pt, int pl, hipStream_t stream) {
   const DwGeo g = geo(N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl);
-  if (KH * KW > 49) return hipErrorInvalidValue;
   const long M = (long)N * OH * OW;
-  const int vw = C % 4 == 0 ? 4 : (C % 2 == 0 ? 2 : 1);  // 4 channels: KMAX*V registers
-  // ~ 2048 blocks in total across channel groups, at least 1024 pixels each
-  const int groups = C / vw;
-  long blocks_x = (2048 + groups - 1) / groups;
-  int ppb = (int)((M + blocks_x - 1) / blocks_x);
-  if (ppb < 1024) ppb = 1024;
-  blocks_x = (M + ppb - 1) / ppb;
-  const dim3 grid((unsigned)blocks_x, (unsigned)groups);
-#define DW_WGRAD_LAUNCH(KM)                                                                        \
-  KFB_DISPATCH_DTYPE(dtype, T, {                                                            \
-    if (vw == 4)                                                                            \
-      hipLaunchKernelGGL((dw_wgrad_k<T, 4, KM>), grid, dim3(256), 0, stream, (const T*)dy,  \
-                         (const T*)x, dw, g, ppb);                                           \
-    else if (vw == 2)                                                                       \
-      hipLaunchKernelGGL((dw_wgrad_k<T, 2, KM>), grid, dim3(256), 0, stream, (const T*)dy,  \
-                         (const T*)x, dw, g, ppb);                                           \
-    else                                                                                    \
-      hipLaunchKernelGGL((dw_wgrad_k<T, 1, KM>), grid, dim3(256), 0, stream, (const T*)dy,  \
-                         (const T*)x, dw, g, ppb);                                           \
+  if (KW > 7 || KH < 1 || M >= (1L << 31) - 256 || M <= 0) return hipErrorInvalidValue;
+  const int vw = vec_width(C);
+  const int cv = C / vw;
+  const int cvb = cv < 256 ? cv : 256;
+  const int P = 256 / cvb;
+  const int chunks = (cv + cvb - 1) / cvb;
+  const bool small = KH <= 3 && KW <= 3;   // one row group of 3 x 3 taps
+  const int zg = small ? 1 : KH;           // else one filter row per group
+  const int tapsz = small ? 9 : KW;        // taps per workgroup (upper bound)
+  // ~2048 workgroups with >= 8 pixel iterations per lane, and <= ~2M atomics
+  // per launch (each workgroup adds tapsz * cvb * V) but >= 64 workgroups
+  constexpr long kMinIters = 8, kBlocks = 2048, kAtomics = 2L << 20;
+  long bx = (M + kMinIters * P - 1) / (kMinIters * P);
+  long cap = kBlocks / ((long)chunks * zg);
+  const long acap = kAtomics / ((long)tapsz * C * zg);
+  if (acap < cap) cap = acap;
+  if (cap < 64) cap = 64;
+  if (bx > cap) bx = cap;
+  if (bx < 1) bx = 1;
+  long ppb = (M + bx - 1) / bx;
+  ppb = (ppb + P - 1) / P * P;
+  bx = (M + ppb - 1) / ppb;
+  const dim3 grid((unsigned)bx, (unsigned)chunks, (unsigned)zg);
+  const FastDiv fow(OW), foh(OH);
+#define DW_WGRAD_LAUNCH(ROWS, RW)                                                        \
+  KFB_DISPATCH_DTYPE(dtype, T, {                                                         \
+    launch_dw_wgrad<T, ROWS, RW>(vw, grid, stream, dy, x, dw, g, cvb, P, (int)ppb, fow,  \
+                                 foh);                                                   \
   })
-  if (KH * KW <= 9) {
-    DW_WGRAD_LAUNCH(9);
-  } else if (KH * KW <= 25) {
-    DW_WGRAD_LAUNCH(25);
+  if (small) {
+    DW_WGRAD_LAUNCH(3, 3);
+  } else if (KW <= 3) {
+    DW_WGRAD_LAUNCH(1, 3);
+  } else if (KW <= 5) {
+    DW_WGRAD_LAUNCH(1, 5);
   } else {
-    DW_WGRAD_LAUNCH(49);
+    DW_WGRAD_LAUNCH(1, 7);
   }
 #undef DW_WGRAD_LAUNCH
   return hipGetLastError();
