@@ -243,21 +243,37 @@ __device__ __forceinline__ float bwd_fma(float g, float a, float x, float b, flo
 }
 
 // ReLU bit mask of one 8-channel vector of a 2-byte output: bit k of byte
-// mb[i] = (stored y[8i + k] > 0), from the value as rounded to T, so it equals
-// the test a consumer would make on y itself.  A conv dgrad epilogue reads
+// mb[i] = act_pass(stored y[8i + k]), from the value as rounded to T, so it
+// equals the test a consumer would make on y itself.  A conv dgrad epilogue reads
 // this byte (1/16 of y's bytes) instead of y (IgArgs::maskbits).
-template <typename T, int V>
+// ACT: the activation after the BN - 1 ReLU, 2 ReLU6 (MobileNet-v2's
+// min(max(y, 0), 6), tcb/models/mobilenet_conv_blocks.py); act_pass is its
+// gradient gate on the stored output y (the gradient passes where 0 < y, and
+// for ReLU6 y < 6).
+template <int ACT>
+__device__ __forceinline__ float act_apply(float o) {
+  o = fmaxf(o, 0.f);
+  if constexpr (ACT == 2) o = fminf(o, 6.f);
+  return o;
+}
+template <int ACT>
+__device__ __forceinline__ bool act_pass(float y) {
+  if constexpr (ACT == 2) return y > 0.f && y < 6.f;
+  return y > 0.f;
+}
+
+template <typename T, int V, int ACT = 1>
 __device__ __forceinline__ void relu_bits(uint8_t* __restrict__ mb, unsigned i, const float (&v)[V]) {
   if constexpr (V == 8 && sizeof(T) == 2) {
     if (!mb) return;
     unsigned b = 0;
 #pragma unroll
-    for (int k = 0; k < V; ++k) b |= ((float)(T)v[k] > 0.f ? 1u : 0u) << k;
+    for (int k = 0; k < V; ++k) b |= (act_pass<ACT>((float)(T)v[k]) ? 1u : 0u) << k;
     mb[i] = (uint8_t)b;
   }
 }
 
-template <typename T, int V, bool RES, bool RELU, int U = 0>
+template <typename T, int V, bool RES, int RELU, int U = 0>
 __global__ void __launch_bounds__(256)
 bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y, long nvec, int C,
            const float* __restrict__ scale, const float* __restrict__ shift,
@@ -272,7 +288,7 @@ bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y
     for (int k = 0; k < V; ++k) {
       float o = __builtin_fmaf(v[k], sc[k], sf[k]);
       if (RES) o += rr[k];
-      if (RELU) o = fmaxf(o, 0.f);
+      if (RELU) o = act_apply<RELU>(o);
       v[k] = o;
     }
   };
@@ -297,7 +313,7 @@ bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y
       if (i < n) {
         apply(v[u], rr[u], sc, sf);
         store_vec<T, V>(y + (long)i * V, v[u]);
-        if (RELU) relu_bits<T, V>(mb, i, v[u]);
+        if (RELU) relu_bits<T, V, RELU>(mb, i, v[u]);
       }
     }
     return;
@@ -321,8 +337,8 @@ bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y
       store_vec<T, V>(y + (long)i * V, v0);
       store_vec<T, V>(y + (long)(i + stride) * V, v1);
       if (RELU) {
-        relu_bits<T, V>(mb, i, v0);
-        relu_bits<T, V>(mb, i + stride, v1);
+        relu_bits<T, V, RELU>(mb, i, v0);
+        relu_bits<T, V, RELU>(mb, i + stride, v1);
       }
     }
     if (i < n) {
@@ -331,7 +347,7 @@ bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y
       if (RES) load_vec<T, V>(res + (long)i * V, r0);
       apply(v0, r0, sc, sf);
       store_vec<T, V>(y + (long)i * V, v0);
-      if (RELU) relu_bits<T, V>(mb, i, v0);
+      if (RELU) relu_bits<T, V, RELU>(mb, i, v0);
     }
     return;
   }
@@ -345,7 +361,7 @@ bn_apply_k(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y
     coef_load<V>(shift, c, sf);
     apply(v, rr, sc, sf);
     store_vec<T, V>(y + e, v);
-    if (RELU) relu_bits<T, V>(mb, i, v);
+    if (RELU) relu_bits<T, V, RELU>(mb, i, v);
   }
 }
 
@@ -448,7 +464,7 @@ bn_apply2_k(const T* __restrict__ x, const T* __restrict__ xr, T* __restrict__ y
 }
 
 // ---------------------------------------------------------------- backward
-template <typename T, int V, bool MASK>
+template <typename T, int V, int MASK>
 __global__ void __launch_bounds__(BN_THREADS)
 bn_partial_grad_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __restrict__ x,
                   const float* __restrict__ mean, long rows, int C, int cw, int tpr, int rpi,
@@ -471,7 +487,7 @@ bn_partial_grad_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __
     auto row_acc = [&](const float (&g0)[V], const float (&xv)[V], const float (&yv)[V]) {
 #pragma unroll
       for (int i = 0; i < V; ++i) {
-        const float g = (!MASK || yv[i] > 0.f) ? g0[i] : 0.f;
+        const float g = (!MASK || act_pass<MASK>(yv[i])) ? g0[i] : 0.f;
         s[i] += g;
         q[i] += g * (xv[i] - m[i]);
       }
@@ -537,7 +553,7 @@ bn_finalize_grad_k(const float* __restrict__ pdy, const float* __restrict__ pdyx
   coefC[c] = (float)(-A * s1 / n - (double)mean[c] * B);
 }
 
-template <typename T, int V, bool MASK, bool DRES, int U = 0>
+template <typename T, int V, int MASK, bool DRES, int U = 0>
 __global__ void __launch_bounds__(256)
 bn_bwd_apply_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __restrict__ x,
                T* __restrict__ dx, T* __restrict__ dres, long nvec, int C,
@@ -569,7 +585,7 @@ bn_bwd_apply_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __res
       if (i < n) {
         if (MASK) {
 #pragma unroll
-          for (int k = 0; k < V; ++k) g[u][k] = yv[u][k] > 0.f ? g[u][k] : 0.f;
+          for (int k = 0; k < V; ++k) g[u][k] = act_pass<MASK>(yv[u][k]) ? g[u][k] : 0.f;
         }
         if (DRES) store_vec<T, V>(dres + (long)i * V, g[u]);
         float o[V];
@@ -595,10 +611,10 @@ bn_bwd_apply_k(const T* __restrict__ dy, const T* __restrict__ y, const T* __res
       load_vec<T, V>(y + (long)ia * V, y0);
       if (two) load_vec<T, V>(y + (long)ib * V, y1);
 #pragma unroll
-      for (int k = 0; k < V; ++k) g0[k] = y0[k] > 0.f ? g0[k] : 0.f;
+      for (int k = 0; k < V; ++k) g0[k] = act_pass<MASK>(y0[k]) ? g0[k] : 0.f;
       if (two) {
 #pragma unroll
-        for (int k = 0; k < V; ++k) g1[k] = y1[k] > 0.f ? g1[k] : 0.f;
+        for (int k = 0; k < V; ++k) g1[k] = act_pass<MASK>(y1[k]) ? g1[k] : 0.f;
       }
     }
     if (DRES) {
@@ -1291,7 +1307,7 @@ static long choose_slabs(long rows, int rpi, int nchunk) {
   return s;
 }
 
-template <typename T, int V, bool M, bool R>
+template <typename T, int V, int M, bool R>
 static void launch_bwd_apply(int gb, hipStream_t stream, const void* dy, const void* y,
                              const void* x, void* dx, void* dres, long nvec, int C,
                              const float* A, const float* B, const float* Cc) {
@@ -1335,7 +1351,7 @@ static int fold_bwd_grid(long rows, int C) {
   return (int)(nrb * ns);
 }
 
-template <typename T, int V, bool RES, bool RELU>
+template <typename T, int V, bool RES, int RELU>
 static void launch_apply(hipStream_t stream, const void* x, const void* res, void* y, long nvec,
                          int C, const float* scale, const float* shift, uint8_t* mb = nullptr) {
   if (flat_ok(nvec, C, V))
@@ -1421,11 +1437,12 @@ KFB_API hipError_t kfb_bn_fwd_train(int dtype, const void* x, const void* res, v
                            save_mean, save_invstd, scale, shift, kshift);
       const long nvec = rows * C / VV;
       if (res) {
-        if (relu) launch_apply<T, VV, true, true>(stream, x, res, y, nvec, C, scale, shift, mbits);
-        else launch_apply<T, VV, true, false>(stream, x, res, y, nvec, C, scale, shift);
+        if (relu) launch_apply<T, VV, true, 1>(stream, x, res, y, nvec, C, scale, shift, mbits);
+        else launch_apply<T, VV, true, 0>(stream, x, res, y, nvec, C, scale, shift);
       } else {
-        if (relu) launch_apply<T, VV, false, true>(stream, x, nullptr, y, nvec, C, scale, shift, mbits);
-        else launch_apply<T, VV, false, false>(stream, x, nullptr, y, nvec, C, scale, shift);
+        if (relu == 2) launch_apply<T, VV, false, 2>(stream, x, nullptr, y, nvec, C, scale, shift, mbits);
+        else if (relu) launch_apply<T, VV, false, 1>(stream, x, nullptr, y, nvec, C, scale, shift, mbits);
+        else launch_apply<T, VV, false, 0>(stream, x, nullptr, y, nvec, C, scale, shift);
       }
     });
   });
@@ -1491,18 +1508,20 @@ KFB_API hipError_t kfb_bn_fwd_infer(int dtype, const void* x, const void* res, v
     KFB_DISPATCH_VEC(V, VV, {
       const long nvec = rows * C / VV;
       if (res) {
-        if (relu) launch_apply<T, VV, true, true>(stream, x, res, y, nvec, C, scale, shift);
-        else launch_apply<T, VV, true, false>(stream, x, res, y, nvec, C, scale, shift);
+        if (relu) launch_apply<T, VV, true, 1>(stream, x, res, y, nvec, C, scale, shift);
+        else launch_apply<T, VV, true, 0>(stream, x, res, y, nvec, C, scale, shift);
       } else {
-        if (relu) launch_apply<T, VV, false, true>(stream, x, nullptr, y, nvec, C, scale, shift);
-        else launch_apply<T, VV, false, false>(stream, x, nullptr, y, nvec, C, scale, shift);
+        if (relu == 2) launch_apply<T, VV, false, 2>(stream, x, nullptr, y, nvec, C, scale, shift);
+        else if (relu) launch_apply<T, VV, false, 1>(stream, x, nullptr, y, nvec, C, scale, shift);
+        else launch_apply<T, VV, false, 0>(stream, x, nullptr, y, nvec, C, scale, shift);
       }
     });
   });
   return hipGetLastError();
 }
 
-// Backward. y (forward output) supplies the ReLU mask when relu != 0.
+// Backward. y (forward output) supplies the ReLU mask when relu != 0
+// (relu 2: ReLU6, no residual).
 // dres (may be null) receives the gradient of the residual input.
 // dgamma/dbeta are written (accumulate=0) or added to (accumulate=1).
 KFB_API hipError_t kfb_bn_bwd(int dtype, const void* dy, const void* y, const void* x, void* dx,
@@ -1522,12 +1541,16 @@ KFB_API hipError_t kfb_bn_bwd(int dtype, const void* dy, const void* y, const vo
       dim3 grid(nslab, g.nchunk);
       const size_t lds = 2 * (size_t)g.rpi * g.tpr * VV * sizeof(float);
       if (have_partials) {
-      } else if (relu)
-        hipLaunchKernelGGL((bn_partial_grad_k<T, VV, true>), grid, dim3(BN_THREADS), lds, stream,
+      } else if (relu == 2)
+        hipLaunchKernelGGL((bn_partial_grad_k<T, VV, 2>), grid, dim3(BN_THREADS), lds, stream,
+                           (const T*)dy, (const T*)y, (const T*)x, save_mean, rows, C, g.cw,
+                           g.tpr, g.rpi, slab_rows, pdy, pdyx);
+      else if (relu)
+        hipLaunchKernelGGL((bn_partial_grad_k<T, VV, 1>), grid, dim3(BN_THREADS), lds, stream,
                            (const T*)dy, (const T*)y, (const T*)x, save_mean, rows, C, g.cw,
                            g.tpr, g.rpi, slab_rows, pdy, pdyx);
       else
-        hipLaunchKernelGGL((bn_partial_grad_k<T, VV, false>), grid, dim3(BN_THREADS), lds,
+        hipLaunchKernelGGL((bn_partial_grad_k<T, VV, 0>), grid, dim3(BN_THREADS), lds,
                            stream, (const T*)dy, (const T*)y, (const T*)x, save_mean, rows, C,
                            g.cw, g.tpr, g.rpi, slab_rows, pdy, pdyx);
       const long nvec = rows * C / VV;
@@ -1552,12 +1575,14 @@ KFB_API hipError_t kfb_bn_bwd(int dtype, const void* dy, const void* y, const vo
                            pdy, pdyx, nslab, C, rows, gamma, save_mean, save_invstd, dgamma, dbeta,
                            coefA, coefB, coefC, accumulate, 0);
       const int gb = stream_grid(nvec);
-      if (relu) {
-        if (dres) launch_bwd_apply<T, VV, true, true>(gb, stream, dy, y, x, dx, dres, nvec, C, coefA, coefB, coefC);
-        else launch_bwd_apply<T, VV, true, false>(gb, stream, dy, y, x, dx, dres, nvec, C, coefA, coefB, coefC);
+      if (relu == 2) {  // (ReLU6: never with a residual add)
+        launch_bwd_apply<T, VV, 2, false>(gb, stream, dy, y, x, dx, dres, nvec, C, coefA, coefB, coefC);
+      } else if (relu) {
+        if (dres) launch_bwd_apply<T, VV, 1, true>(gb, stream, dy, y, x, dx, dres, nvec, C, coefA, coefB, coefC);
+        else launch_bwd_apply<T, VV, 1, false>(gb, stream, dy, y, x, dx, dres, nvec, C, coefA, coefB, coefC);
       } else {
-        if (dres) launch_bwd_apply<T, VV, false, true>(gb, stream, dy, y, x, dx, dres, nvec, C, coefA, coefB, coefC);
-        else launch_bwd_apply<T, VV, false, false>(gb, stream, dy, y, x, dx, dres, nvec, C, coefA, coefB, coefC);
+        if (dres) launch_bwd_apply<T, VV, 0, true>(gb, stream, dy, y, x, dx, dres, nvec, C, coefA, coefB, coefC);
+        else launch_bwd_apply<T, VV, 0, false>(gb, stream, dy, y, x, dx, dres, nvec, C, coefA, coefB, coefC);
       }
     });
   });

@@ -233,11 +233,12 @@ class ConvNetBuilder:
                 self.top_layer, self.top_size = y, num_out_channels
                 return y
         if use_batch_norm:
+            act = 0 if self.meta else F.bn_act_code(activation, y, residual)
             with self.scope(name):
                 self.top_layer, self.top_size = y, num_out_channels
-                y = self._batch_norm(y, relu=relu, residual=residual, stats=stats,
-                                     **self.batch_norm_config)
-            if activation not in ("relu", None, "linear"):
+                y = self._batch_norm(y, relu=act if act else relu, residual=residual,
+                                     stats=stats, **self.batch_norm_config)
+            if activation not in ("relu", None, "linear") and act != 2:
                 y = F.activation(y, activation)
         else:
             if not fuse_bact:
@@ -273,9 +274,11 @@ class ConvNetBuilder:
                                     None if self.meta else layer.weight_lp,
                                     (d_height, d_width), pads, self.impl)
         if use_batch_norm:
+            act = 0 if self.meta else F.bn_act_code(activation, y)
             with self.scope(name):
-                y = self._batch_norm(y, relu=activation == "relu", **self.batch_norm_config)
-            if activation not in ("relu", None, "linear"):
+                y = self._batch_norm(y, relu=act if act else activation == "relu",
+                                     **self.batch_norm_config)
+            if activation not in ("relu", None, "linear") and act != 2:
                 y = F.activation(y, activation)
         elif activation not in (None, "linear"):
             y = F.activation(y, activation)

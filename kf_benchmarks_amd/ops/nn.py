@@ -84,9 +84,29 @@ def _bn_cpu(x, gamma, beta, residual, rm, rv, decay, eps, relu, training):
     y = y.permute(0, 2, 3, 1)
     if residual is not None:
         y = y + residual.float()
-    if relu:
+    if relu == 2:
+        y = y.clamp(0.0, 6.0)
+    elif relu:
         y = torch.relu(y)
     return y.to(x.dtype).contiguous()
+
+
+def bn_act_code(activation, x, residual=None) -> int:
+    """The ``relu`` code a BN applies itself for ``activation``: 1 ReLU, 2
+    ReLU6 (MobileNet-v2) where the GPU apply pass can also write the bit
+    mask its consumers' dgrad epilogues gate with (2-byte dtype, C % 8 == 0,
+    no residual; csrc/bn.hip act_apply / act_pass), else 0 (the caller
+    applies the activation as its own pass)."""
+    if activation == "relu":
+        return 1
+    if activation == "relu6" and residual is None and x.is_cuda and x.element_size() == 2 \
+            and x.shape[-1] % 8 == 0 and _RELU_BITS and _conv.FUSE_BN and _RELU6_IN_BN:
+        return 2
+    return 0
+
+
+# ReLU6 applied by the BN it follows (bn_act_code); off: a separate act pass
+_RELU6_IN_BN = True
 
 
 # Consumers' dgrad epilogues could recompute a non-residual BN's ReLU mask
@@ -267,13 +287,15 @@ class _BatchNormTrain(torch.autograd.Function):
         st = fin[6] if fin is not None else torch.empty((2, C), dtype=torch.float32, device=dev)
         y = torch.empty_like(x)
         res = residual.contiguous() if residual is not None else None
-        rec = relu and residual is None and _MASK_RECOMPUTE
+        rec = relu == 1 and residual is None and _MASK_RECOMPUTE
         mbits = _relu_bits_buffer(x, rows, C) if relu and not rec else None
         # x never stored by its producing conv (conv_hip.conv_fwd, statistics
         # only): the apply pass recomputes it from the conv's input and
         # weights and stores it on the way (csrc/conv_s1.hip EPI_APPLY)
         rc = getattr(x, "_kfb_recompute", None) if stats is not None else None
         if rc is not None:
+            if relu == 2:
+                raise RuntimeError("BN recompute path with ReLU6 is not supported")
             global RECOMPUTED
             RECOMPUTED += 1
             xin, wl = rc
@@ -299,6 +321,8 @@ class _BatchNormTrain(torch.autograd.Function):
         ctx.gamma, ctx.beta = gamma, beta
         link = BNLink(x, st[0], relu, coef if rec else None)
         link.mbits = mbits
+        if relu == 2 and mbits is None:
+            link.other = True  # consumers may only gate ReLU6 with its bit mask
         link.gfin = (gamma, st, beta)
         y._kfb_bn_link = link
         ctx.link = link

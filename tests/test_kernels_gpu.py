@@ -68,6 +68,81 @@ def test_batch_norm_train(cuda, dt, shape, relu, res):
         assert (ra.grad.float().cpu() - rb.grad).abs().gt(0.05).float().mean() < 1e-5
 
 
+@pytest.mark.parametrize("shape", [(4, 7, 7, 64), (2, 5, 6, 24), (3, 4, 4, 2048),
+                                   (128, 64, 64, 256)])  # last: >= 256 MB, the flat passes
+def test_batch_norm_relu6(cuda, shape):
+    """BN + ReLU6 in one apply pass (MobileNet-v2; csrc/bn.hip act_apply /
+    act_pass): y = min(max(bn(x), 0), 6), its bit mask, and the backward
+    gated by 0 < y < 6 on the stored output - against an fp32 reference that
+    uses the kernel's own output for the gate (bf16 rounding puts values
+    within an ulp of 6 on either side)."""
+    torch.manual_seed(0)
+    dt = torch.bfloat16
+    C = shape[-1]
+    x = (torch.randn(shape) * 2 + 0.5).to(dt).float()
+    g0 = torch.rand(C) + 0.5
+    b0 = torch.randn(C) * 2 + 4  # a good share of the outputs above 6
+    xa = x.to(cuda, dt).requires_grad_(True)
+    ga = g0.clone().to(cuda).requires_grad_(True)
+    ba = b0.clone().to(cuda).requires_grad_(True)
+    rma, rva = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    ya = F.batch_norm(xa, ga, ba, rma, rva, 0.9, 1e-5, True, 2, None)
+    xf = x.view(-1, C)
+    mean, var = xf.mean(0), xf.var(0, unbiased=False)
+    xhat = (xf - mean) / torch.sqrt(var + 1e-5)
+    yref = (xhat * g0 + b0).clamp(0.0, 6.0).view(shape)
+    y = ya.detach().float().cpu()
+    torch.testing.assert_close(y, yref, rtol=2e-2, atol=4e-2)
+    assert (y >= 6).float().mean() > 0.05 and (y <= 0).float().mean() > 0.01
+    gate = (y > 0) & (y < 6)
+    mb = ya._kfb_bn_link.mbits
+    assert mb is not None
+    bits = torch.stack([(mb.cpu() >> k) & 1 for k in range(8)], -1).view(shape).bool()
+    assert torch.equal(bits, gate)
+    dy = torch.randn(shape).to(dt).float()
+    ya.backward(dy.to(cuda, dt))
+    n = xf.shape[0]
+    dyp = (dy * gate).view(-1, C)
+    dbeta = dyp.sum(0)
+    dgamma = (dyp * xhat).sum(0)
+    dx = (g0 / torch.sqrt(var + 1e-5)) * (dyp - dbeta / n - xhat * dgamma / n)
+    torch.testing.assert_close(xa.grad.float().cpu(), dx.view(shape), rtol=8e-2, atol=8e-2)
+    torch.testing.assert_close(ba.grad.cpu(), dbeta, rtol=1e-2, atol=0.5)
+    torch.testing.assert_close(ga.grad.cpu(), dgamma, rtol=1e-2, atol=0.5)
+
+
+def test_mobilenet_relu6_in_bn_matches_separate_pass(cuda, monkeypatch):
+    """MobileNet-v2 (bf16, 64 px, batch 4): with ReLU6 applied by the BN
+    (default) the loss is bitwise the separate-pass loss (clamping commutes
+    with rounding) and the gradients agree to fp32 summation order."""
+    from kf_benchmarks_amd import datasets, params as P
+    from kf_benchmarks_amd.models import model_config
+    from kf_benchmarks_amd.models.model import make_network
+    from kf_benchmarks_amd.ops import nn as nn_ops
+
+    def run():
+        d = datasets.create_dataset(None, "imagenet")
+        m = model_config.get_model_config("mobilenet", d, P.make_params(model="mobilenet"))
+        m.image_size = 64
+        torch.manual_seed(0)
+        net = make_network(m, d.num_classes, str(cuda), torch.bfloat16)
+        g = torch.Generator().manual_seed(3)
+        x = torch.randn(4, 64, 64, 3, generator=g).to(cuda, torch.bfloat16)
+        lab = torch.randint(0, d.num_classes - 1, (4,), generator=g).to(cuda)
+        loss = m.loss_function((x, lab), net(x))
+        loss.backward()
+        return float(loss), [p.grad.float().cpu().reshape(-1) for _, p in net.trainable_variables()
+                             if p.grad is not None]
+
+    la, ga = run()
+    monkeypatch.setattr(nn_ops, "_RELU6_IN_BN", False)
+    lb, gb = run()
+    assert la == lb, (la, lb)
+    cos = sorted(float(torch.nn.functional.cosine_similarity(a, b, dim=0))
+                 for a, b in zip(ga, gb) if b.norm() > 0)
+    assert cos[0] > 0.99 and cos[len(cos) // 2] > 0.999, cos[:5]
+
+
 @pytest.mark.parametrize("dt", DT)
 def test_batch_norm_infer(cuda, dt):
     C = 32
