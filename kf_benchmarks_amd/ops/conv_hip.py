@@ -574,7 +574,8 @@ _WGRAD_CANDIDATES = (384, 512, 768, 1024)
 # bytes and reduce work beside the compute stream) within this fraction of
 # the fastest isolated time: in the network, 0.3 beat the fastest-isolated
 # choice by 0.13 ms/step on interleaved runs, 0.15 by 0.08, 0.5 by 0.07,
-# and capping the grid at 512 lost 0.25 (profiles/r13_wgrad_grid_ab.txt)
+# and capping the grid at 512 lost 0.25; a 256 grid offered as well lost
+# 0.06, slack 0.4 0.06 (profiles/r13_wgrad_grid_ab.txt)
 _WGRAD_SLACK = 0.3
 # bit 16 of a candidate selects the LDS-DMA wgrad kernel (wgrad_glds_k: 128-wide
 # output-channel tiles, operands < 2 GiB); KFB_WGRAD_ALGO=classic|glds pins one.
