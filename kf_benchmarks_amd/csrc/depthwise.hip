@@ -97,10 +97,10 @@ dw_dgrad_k(const T* __restrict__ dy, const T* __restrict__ w, T* __restrict__ dx
 // cv = C/V channel groups, a workgroup holds cvb = min(cv, 256) groups
 // (blockIdx.y picks the chunk) times P = 256/cvb pixel lanes, and every
 // thread keeps its channel group while it walks its slice of pixels with
-// stride P.  A workgroup covers ROWS filter rows of at most RW taps each
-// (blockIdx.z picks the row group: 3x3 filters in one, 5x5 / 7x7 one row per
-// group, so the accumulators stay at <= 7 x 8 registers and there are
-// enough workgroups).  The P pixel lanes of a group are summed through LDS
+// stride P.  A workgroup covers ROWS filter rows x RW filter columns
+// (blockIdx.z picks the group: 3x3 filters in one, larger ones one row of
+// <= 7 columns per group, so the accumulators stay at <= 7 x 8 registers
+// and there are enough workgroups).  The P pixel lanes of a group are summed through LDS
 // one tap at a time and the workgroup adds its sum into the fp32 filter
 // gradient (one atomic per element and workgroup).  (The per-pixel-lane
 // layout it replaces loaded one 8-byte piece per lane from a different cache
@@ -109,7 +109,7 @@ dw_dgrad_k(const T* __restrict__ dy, const T* __restrict__ w, T* __restrict__ dx
 template <typename T, int V, int ROWS, int RW>
 __global__ void __launch_bounds__(256)
 dw_wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ dw, DwGeo g,
-           int cvb, int P, int ppb, FastDiv fow, FastDiv foh) {
+           int cvb, int P, int ppb, int ncg, FastDiv fow, FastDiv foh) {
   __shared__ float red[256 * V];
   const int cv = g.C / V;
   const int tid = threadIdx.x;
@@ -117,7 +117,8 @@ dw_wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict_
   const int cg = blockIdx.y * cvb + gl;
   const bool active = q < P && cg < cv;
   const int c = cg * V;
-  const int row0 = blockIdx.z * ROWS;
+  const int row0 = (int)(blockIdx.z / ncg) * ROWS;      // ncg column groups per row group
+  const int col0 = (int)(blockIdx.z % ncg) * RW;
   const int M = g.N * g.OH * g.OW;
   const int p0 = blockIdx.x * ppb;
   const int p1 = p0 + ppb < M ? p0 + ppb : M;
@@ -134,7 +135,7 @@ dw_wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict_
       const int oh = r - n * g.OH;
       float dv[V];
       load_vec<T, V>(dy + (long)p * g.C + c, dv);
-      const int h0 = oh * g.sh - g.pt + row0, w0 = ow * g.sw - g.pl;
+      const int h0 = oh * g.sh - g.pt + row0, w0 = ow * g.sw - g.pl + col0;
       const T* xn = x + (long)n * g.H * g.W * g.C + c;
 #pragma unroll
       for (int a = 0; a < ROWS; ++a) {
@@ -143,7 +144,7 @@ dw_wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict_
 #pragma unroll
         for (int b = 0; b < RW; ++b) {
           const int ww = w0 + b;
-          if (b < g.KW && (unsigned)ww < (unsigned)g.W) {
+          if (col0 + b < g.KW && (unsigned)ww < (unsigned)g.W) {
             float xv[V];
             load_vec<T, V>(xn + ((long)h * g.W + ww) * g.C, xv);
 #pragma unroll
@@ -157,13 +158,13 @@ dw_wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict_
 #pragma unroll
   for (int t = 0; t < ROWS * RW; ++t) {
     const int a = t / RW, b = t - a * RW;
-    if (row0 + a < g.KH && b < g.KW) {  // uniform over the block
+    if (row0 + a < g.KH && col0 + b < g.KW) {  // uniform over the block
       if (active) {
 #pragma unroll
         for (int k = 0; k < V; ++k) red[tid * V + k] = acc[t][k];
       }
       __syncthreads();
-      float* dwt = dw + (long)((row0 + a) * g.KW + b) * g.C;
+      float* dwt = dw + (long)((row0 + a) * g.KW + col0 + b) * g.C;
       for (int e = tid; e < cvb * V; e += 256) {
         const int gl2 = e / V, k = e - gl2 * V;
         const int cg2 = blockIdx.y * cvb + gl2;
@@ -181,20 +182,20 @@ dw_wgrad_k(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict_
 // V channels per lane (<= 8: ROWS * RW * V accumulators <= 72)
 template <typename T, int ROWS, int RW>
 static void launch_dw_wgrad(int vw, dim3 grid, hipStream_t stream, const void* dy, const void* x,
-                            float* dw, const DwGeo& g, int cvb, int P, int ppb, FastDiv fow,
-                            FastDiv foh) {
+                            float* dw, const DwGeo& g, int cvb, int P, int ppb, int ncg,
+                            FastDiv fow, FastDiv foh) {
   if (vw == 8)
     hipLaunchKernelGGL((dw_wgrad_k<T, 8, ROWS, RW>), grid, dim3(256), 0, stream, (const T*)dy,
-                       (const T*)x, dw, g, cvb, P, ppb, fow, foh);
+                       (const T*)x, dw, g, cvb, P, ppb, ncg, fow, foh);
   else if (vw == 4)
     hipLaunchKernelGGL((dw_wgrad_k<T, 4, ROWS, RW>), grid, dim3(256), 0, stream, (const T*)dy,
-                       (const T*)x, dw, g, cvb, P, ppb, fow, foh);
+                       (const T*)x, dw, g, cvb, P, ppb, ncg, fow, foh);
   else if (vw == 2)
     hipLaunchKernelGGL((dw_wgrad_k<T, 2, ROWS, RW>), grid, dim3(256), 0, stream, (const T*)dy,
-                       (const T*)x, dw, g, cvb, P, ppb, fow, foh);
+                       (const T*)x, dw, g, cvb, P, ppb, ncg, fow, foh);
   else
     hipLaunchKernelGGL((dw_wgrad_k<T, 1, ROWS, RW>), grid, dim3(256), 0, stream, (const T*)dy,
-                       (const T*)x, dw, g, cvb, P, ppb, fow, foh);
+                       (const T*)x, dw, g, cvb, P, ppb, ncg, fow, foh);
 }
 
 inline DwGeo geo(int N, int H, int W, int C, int OH, int OW, int KH, int KW, int sh, int sw,
@@ -241,15 +242,17 @@ KFB_API hipError_t kfb_dw_wgrad(int dtype, const void* dy, const void* x, float*
                                 int pt, int pl, hipStream_t stream) {
   const DwGeo g = geo(N, H, W, C, OH, OW, KH, KW, sh, sw, pt, pl);
   const long M = (long)N * OH * OW;
-  if (KW > 7 || KH < 1 || M >= (1L << 31) - 256 || M <= 0) return hipErrorInvalidValue;
+  if (KW < 1 || KH < 1 || M >= (1L << 31) - 256 || M <= 0) return hipErrorInvalidValue;
   const int vw = vec_width(C);
   const int cv = C / vw;
   const int cvb = cv < 256 ? cv : 256;
   const int P = 256 / cvb;
   const int chunks = (cv + cvb - 1) / cvb;
-  const bool small = KH <= 3 && KW <= 3;   // one row group of 3 x 3 taps
-  const int zg = small ? 1 : KH;           // else one filter row per group
-  const int tapsz = small ? 9 : KW;        // taps per workgroup (upper bound)
+  const bool small = KH <= 3 && KW <= 3;       // one group of 3 x 3 taps
+  const int rw = small || KW <= 3 ? 3 : KW <= 5 ? 5 : 7;
+  const int ncg = small ? 1 : (KW + rw - 1) / rw;  // column groups per filter row
+  const int zg = small ? 1 : KH * ncg;             // else one row x rw columns per group
+  const int tapsz = small ? 9 : rw;                // taps per workgroup (upper bound)
   // ~2048 workgroups with >= 8 pixel iterations per lane, and <= ~2M atomics
   // per launch (each workgroup adds tapsz * cvb * V) but >= 64 workgroups
   constexpr long kMinIters = 8, kBlocks = 2048, kAtomics = 2L << 20;
@@ -265,16 +268,16 @@ KFB_API hipError_t kfb_dw_wgrad(int dtype, const void* dy, const void* x, float*
   bx = (M + ppb - 1) / ppb;
   const dim3 grid((unsigned)bx, (unsigned)chunks, (unsigned)zg);
   const FastDiv fow(OW), foh(OH);
-#define DW_WGRAD_LAUNCH(ROWS, RW)                                                        \
-  KFB_DISPATCH_DTYPE(dtype, T, {                                                         \
-    launch_dw_wgrad<T, ROWS, RW>(vw, grid, stream, dy, x, dw, g, cvb, P, (int)ppb, fow,  \
-                                 foh);                                                   \
+#define DW_WGRAD_LAUNCH(ROWS, RW)                                                              \
+  KFB_DISPATCH_DTYPE(dtype, T, {                                                               \
+    launch_dw_wgrad<T, ROWS, RW>(vw, grid, stream, dy, x, dw, g, cvb, P, (int)ppb, ncg, fow,   \
+                                 foh);                                                         \
   })
   if (small) {
     DW_WGRAD_LAUNCH(3, 3);
-  } else if (KW <= 3) {
+  } else if (rw == 3) {
     DW_WGRAD_LAUNCH(1, 3);
-  } else if (KW <= 5) {
+  } else if (rw == 5) {
     DW_WGRAD_LAUNCH(1, 5);
   } else {
     DW_WGRAD_LAUNCH(1, 7);

@@ -239,7 +239,8 @@ DW_SHAPES = [(2, 14, 14, 32, 3, 1), (2, 15, 15, 24, 3, 2), (2, 9, 9, 16, 5, 1),
              # filter gradient: > 256 channel groups (two chunks, the second
              # partial), 256 % groups != 0 (idle lanes), many workgroups
              (2, 7, 7, 2560, 3, 1), (4, 28, 28, 144, 3, 1), (16, 56, 56, 32, 3, 2),
-             (2, 12, 12, 44, 5, 1), (2, 12, 12, 40, 7, 1)]
+             (2, 12, 12, 44, 5, 1), (2, 12, 12, 40, 7, 1),
+             (2, 12, 12, 16, 9, 1)]  # 9 columns: two column groups per filter row
 
 
 @pytest.mark.parametrize("shape", DW_SHAPES, ids=[str(s) for s in DW_SHAPES])
