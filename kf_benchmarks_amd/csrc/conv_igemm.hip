@@ -2744,6 +2744,7 @@ KFB_API hipError_t kfb_conv_igemm(int dtype, const void* x, const void* w, void*
 KFB_API int kfb_conv_stats_spread() { return IG_SPREAD; }
 
 KFB_API void kfb_set_deterministic(int on) { g_deterministic = on ? 1 : 0; }
+KFB_API int kfb_get_deterministic() { return g_deterministic; }
 
 // Number of reduction splits kfb_conv_wgrad uses for this geometry (the
 // slab workspace needs splits * Ncol * KH*KW*C floats).

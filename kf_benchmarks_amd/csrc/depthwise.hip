@@ -236,6 +236,8 @@ KFB_API hipError_t kfb_dw_dgrad(int dtype, const void* dy, const void* w, void* 
   return hipGetLastError();
 }
 
+KFB_API int kfb_get_deterministic();  // (conv_igemm.hip) fixed-order weight-gradient sums
+
 // dw: fp32 [KH][KW][C], accumulated into (caller zeroes or passes the gradient sink).
 KFB_API hipError_t kfb_dw_wgrad(int dtype, const void* dy, const void* x, float* dw, int N, int H,
                                 int W, int C, int OH, int OW, int KH, int KW, int sh, int sw,
@@ -262,7 +264,7 @@ KFB_API hipError_t kfb_dw_wgrad(int dtype, const void* dy, const void* x, float*
   if (acap < cap) cap = acap;
   if (cap < 64) cap = 64;
   if (bx > cap) bx = cap;
-  if (bx < 1) bx = 1;
+  if (bx < 1 || kfb_get_deterministic()) bx = 1;  // deterministic: one atomic per element
   long ppb = (M + bx - 1) / bx;
   ppb = (ppb + P - 1) / P * P;
   bx = (M + ppb - 1) / ppb;

@@ -146,6 +146,10 @@ FUSED_SHAPES = [
     (4, 2, 2, 512, 2048, 1, 1, 1, "SAME"),           # M=16
     (2, 13, 13, 64, 128, 1, 1, 2, "SAME"),           # scatter (addend only)
     (2, 20, 20, 128, 192, 3, 3, 1, "SAME_RESNET"),   # M = 800: 256-row tiles + remainder
+    # MobileNet-v2 projection / expansion widths (ReLU6 bit masks since round 6):
+    # dX channels not a multiple of 64
+    (2, 14, 14, 144, 24, 1, 1, 1, "SAME"),
+    (2, 9, 9, 96, 40, 3, 3, 1, "SAME_RESNET"),
 ]
 
 
@@ -216,6 +220,45 @@ def test_dgrad_fused_epilogue(cuda, shape, with_addend, ig_algo, mask_src):
         tol = 4e-3 * (r.abs() * (1 + (xb.float() - mean).abs())).sum((0, 1, 2)).max().item()
         torch.testing.assert_close(p[0], s1, rtol=1e-2, atol=tol)
         torch.testing.assert_close(p[1], s2, rtol=1e-2, atol=tol)
+
+
+@pytest.mark.parametrize("cin,cout", [(144, 24), (96, 24), (576, 96), (960, 160), (32, 16)])
+@pytest.mark.parametrize("algo", ["auto", "s1"])
+def test_dgrad_bits_mobilenet_widths(cuda, monkeypatch, cin, cout, algo):
+    """The 1x1 dgrad with the producer BN's bit mask, pending gradient and
+    partial sums at MobileNet-v2 widths (dX channels 32-960, not multiples of
+    64), autotuned or on the streaming 1x1 kernel where it applies."""
+    from kf_benchmarks_amd.ops import conv_hip
+    if algo == "s1":
+        if not conv_hip.N.load().kfb_conv_s1_applicable(cout, cin, 1, 1, 1, 1, 0, 0, 28, 28, 28, 28):
+            pytest.skip("streaming 1x1 kernel does not apply")
+        monkeypatch.setattr(conv_hip, "_IG_FORCE", conv_hip.IG_S1)
+    g = torch.Generator().manual_seed(7)
+    dt = torch.bfloat16
+    n, H, W = 4, 28, 28
+    x = torch.relu(torch.randn(n, H, W, cin, generator=g)).clamp(max=6.0).to(dt)
+    x[torch.rand(x.shape, generator=g) < 0.2] = 6.0  # clamped outputs: gate closed
+    w = (torch.randn(cout, 1, 1, cin, generator=g) / cin ** 0.5).to(dt)
+    dy = torch.randn(n, H, W, cout, generator=g).to(dt)
+    xb = torch.randn(n, H, W, cin, generator=g).to(dt)
+    mean = torch.randn(cin, generator=g)
+    add = torch.randn(n, H, W, cin, generator=g).to(dt)
+    gate = (x.float() > 0) & (x.float() < 6)
+    b = gate.reshape(-1, 8).to(torch.int32)
+    bits = (b * (1 << torch.arange(8, dtype=torch.int32))).sum(1).to(torch.uint8)
+    ref = (dy.float().reshape(-1, cout) @ w.float().reshape(cout, cin)).reshape(n, H, W, cin)
+    ref = (ref + add.float()) * gate
+    parts = conv_hip.stats_buffer(cin, cuda).zero_()
+    dx = conv_hip.conv_dgrad(dy.to(cuda), w.to(cuda), x.shape, (1, 1), (0, 0, 0, 0),
+                             (parts, bits.to(cuda), xb.to(cuda), mean.to(cuda)),
+                             addend=add.to(cuda))
+    torch.testing.assert_close(dx.float().cpu(), ref, rtol=3e-2, atol=3e-2)
+    p = parts.view(2, conv_hip.STATS_SPREAD, cin).sum(1).cpu()
+    r = dx.float().cpu()
+    tol = 4e-3 * (r.abs() * (1 + (xb.float() - mean).abs())).sum((0, 1, 2)).max().item()
+    torch.testing.assert_close(p[0], r.sum((0, 1, 2)), rtol=1e-2, atol=tol)
+    torch.testing.assert_close(p[1], (r * (xb.float() - mean)).sum((0, 1, 2)), rtol=1e-2,
+                               atol=tol)
 
 
 @pytest.mark.parametrize("shape", FUSED_SHAPES[:4], ids=[str(s) for s in FUSED_SHAPES[:4]])

@@ -138,9 +138,17 @@ def test_mobilenet_relu6_in_bn_matches_separate_pass(cuda, monkeypatch):
     monkeypatch.setattr(nn_ops, "_RELU6_IN_BN", False)
     lb, gb = run()
     assert la == lb, (la, lb)
-    cos = sorted(float(torch.nn.functional.cosine_similarity(a, b, dim=0))
-                 for a, b in zip(ga, gb) if b.norm() > 0)
-    assert cos[0] > 0.99 and cos[len(cos) // 2] > 0.999, cos[:5]
+    # the two backwards differ in fp32 summation order only (BN partial sums
+    # in the consumer's dgrad epilogue vs a separate pass), so every gradient
+    # tensor agrees to ~1e-3 of its own norm or, for the near-cancelling ones
+    # (a BN beta whose true gradient is ~0), of the typical gradient norm
+    norms = sorted(float(b.norm()) for b in gb)
+    floor = 1e-3 * norms[len(norms) // 2]
+    bad = [(i, float((a - b).norm()), float(b.norm())) for i, (a, b) in enumerate(zip(ga, gb))
+           if float((a - b).norm()) > 2e-2 * float(b.norm()) + floor]
+    assert not bad, bad[:8]
+    allc = float(torch.nn.functional.cosine_similarity(torch.cat(ga), torch.cat(gb), dim=0))
+    assert allc > 0.9999, allc
 
 
 @pytest.mark.parametrize("dt", DT)
