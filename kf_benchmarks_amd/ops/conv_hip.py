@@ -167,6 +167,20 @@ class _StatsArena:
             buf[:min(self.off.get(key, buf.numel()), buf.numel())].zero_()
         self.off[key] = 0
 
+    def snapshot(self):
+        """The current buffers (a launch tape keeps them alive: its replays
+        write them through raw pointers)."""
+        return dict(self.buf)
+
+    def forget_new(self, before):
+        """Drop buffers allocated since ``before`` (a snapshot): ones made
+        while a launch tape was recording live in the tape's private memory
+        pool and must not outlive it."""
+        for key, b in list(self.buf.items()):
+            if before.get(key) is not b:
+                del self.buf[key]
+                self.off.pop(key, None)
+
     def take(self, n, device):
         key = str(torch.device(device))
         n = (n + 63) // 64 * 64

@@ -322,6 +322,12 @@ class StepTape:
             _flag("Stream.wait_event")
             return orig_we(s, ev)
 
+        # the per-step statistics arena (conv_hip.STATS_ARENA) is global: the
+        # tape keeps the buffers its replays write alive, and a buffer the
+        # arena grows into while recording (from this tape's pool) is dropped
+        # from the arena when the tape closes
+        from . import conv_hip
+        self._arena_before = conv_hip.STATS_ARENA.snapshot()
         torch._C._cuda_beginAllocateToPool(dev, self.pool.id)
         torch.Tensor.record_stream = record_stream
         torch.cuda.Stream.wait_stream, torch.cuda.Stream.wait_event = wait_stream, wait_event
@@ -332,6 +338,9 @@ class StepTape:
                     out = step()
             else:
                 out = step()
+        except BaseException:
+            self._release_arena()
+            raise
         finally:
             N._TAPE = None
             torch.Tensor.record_stream = orig_rs
@@ -339,11 +348,14 @@ class StepTape:
             torch._C._cuda_endAllocateToPool(dev, self.pool.id)
         torch.cuda.synchronize(self.device)
         del keep
+        self._arena_keep = conv_hip.STATS_ARENA.snapshot()
         if waits:
+            self._release_arena()
             rec.close()
             raise TapeError("torch stream waits inside the recorded step (not replayable): %s"
                             % sorted(set(waits)), outputs=out)
         if probe is not None and probe.ops:
+            self._release_arena()
             rec.close()
             raise TapeError("torch device ops inside the recorded step (not replayable): %s"
                             % sorted(set(probe.ops)), outputs=out)
@@ -356,9 +368,24 @@ class StepTape:
         self.replays += 1
         return self.outputs
 
+    def _release_arena(self):
+        before = getattr(self, "_arena_before", None)
+        if before is not None:
+            from . import conv_hip
+            conv_hip.STATS_ARENA.forget_new(before)
+            self._arena_before = None
+        self._arena_keep = None
+
     def close(self):
         if self.recorder is not None:
             self.recorder.close()
             self.recorder = None
+        self._release_arena()
         self.outputs = None
         self.pool = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass

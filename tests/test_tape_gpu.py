@@ -581,3 +581,33 @@ def test_ssd300_masked_decay_tape(cuda, _deterministic, monkeypatch):
           % (spread_l, spread_w, dl, dw))
     assert dl <= 4 * spread_l + 1e-3 * float(le1.abs().max()), (dl, spread_l)
     assert dw <= 4 * spread_w + 1e-6, (dw, spread_w)
+
+
+def test_tape_close_drops_arena_grown_in_its_pool(cuda):
+    """A statistics-arena buffer allocated while a tape records lives in the
+    tape's private memory pool: closing the tape drops it from the (global)
+    arena, so later eager steps do not write into a released pool (seen as
+    corrupted BN partial sums in a network run after a taped test); a buffer
+    that existed before the recording is kept alive by the tape and stays."""
+    from kf_benchmarks_amd.ops import conv_hip
+    from kf_benchmarks_amd.ops.tape import StepTape
+    arena = conv_hip.STATS_ARENA
+    key = str(torch.device(cuda))
+    saved = arena.snapshot()
+    try:
+        arena.buf.pop(key, None)
+        tape = StepTape(cuda)
+        tape.record(lambda: arena.reset(cuda), check_torch_ops=False)
+        grown = arena.buf.get(key)
+        assert grown is not None
+        tape.close()
+        assert arena.buf.get(key) is not grown
+        arena.reset(cuda)  # outside any pool
+        kept = arena.buf[key]
+        tape = StepTape(cuda)
+        tape.record(lambda: arena.reset(cuda), check_torch_ops=False)
+        tape.close()
+        assert arena.buf.get(key) is kept
+    finally:
+        arena.buf.clear()
+        arena.buf.update(saved)
