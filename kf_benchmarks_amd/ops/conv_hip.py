@@ -160,11 +160,12 @@ class _StatsArena:
             self.buf[key] = buf = torch.zeros((max(need, 1 << 16),), dtype=torch.float32,
                                               device=device)
         elif buf.is_cuda:
-            # only the part handed out last step can be dirty (native memset:
-            # part of a recorded launch tape)
-            N.zero_(buf[:min(self.off.get(key, buf.numel()), buf.numel())])
+            # the whole buffer (a few MB; native memset: part of a recorded
+            # launch tape): a step of another network in this process, or a
+            # tape's replays, may have used more of it than the last step
+            N.zero_(buf)
         else:
-            buf[:min(self.off.get(key, buf.numel()), buf.numel())].zero_()
+            buf.zero_()
         self.off[key] = 0
 
     def snapshot(self):
