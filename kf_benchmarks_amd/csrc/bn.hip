@@ -14,8 +14,6 @@
 // so a launch has >= 1024 workgroups on 256 CUs for the ResNet shapes.
 #include "common.h"
 
-#include <cstdlib>
-
 namespace kfb {
 
 constexpr int BN_THREADS = 512;
@@ -1282,7 +1280,9 @@ static bool flat_ok(long nvec, int C, int V) {
   const int cv = C / V;
   const int mode = bn_flat_mode();
   const long bytes = nvec * 16;
-  return mode > 0 && (mode == 2 || bytes >= (256L << 20)) && cv > 0 && (cv & (cv - 1)) == 0 &&
+  // tensors from 64 MB up (was 256 MB: -0.09 and -0.16 ms/step on interleaved ResNet-50 runs,
+  // 16 MB no better; profiles/r13_bn_launch_ab.txt)
+  return mode > 0 && (mode == 2 || bytes >= (64L << 20)) && cv > 0 && (cv & (cv - 1)) == 0 &&
          256 % cv == 0 && nvec < (1L << 31) - 256L * 8;
 }
 

@@ -30,7 +30,9 @@ def _pair(x, dev, dt):
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("shape", [(4, 7, 7, 64), (2, 5, 6, 24), (3, 4, 4, 2048), (2, 3, 3, 20),
                                    # > 4 x the capped grid: the unrolled streaming loop + tail
-                                   (81, 32, 32, 256)])
+                                   (81, 32, 32, 256),
+                                   # >= 64 MB: the flat passes
+                                   (64, 64, 64, 256)])
 @pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
 def test_batch_norm_train(cuda, dt, shape, relu, res):
     torch.manual_seed(0)
