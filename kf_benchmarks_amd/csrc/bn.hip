@@ -1323,7 +1323,7 @@ static void launch_bwd_apply(int gb, hipStream_t stream, const void* dy, const v
 
 // kfb_bn_set_fold_bwd (tests): the backward apply passes fold their
 // conv-epilogue partials (bn_bwd_apply_fold_k) instead of a finalize launch -
-// 1 (default): tensors up to 32 MB, 2: every size, 0: never.  On the large tensors the slice layout streams slower
+// 1 (default): tensors up to 64 MB, 2: every size, 0: never.  On the large tensors the slice layout streams slower
 // than the grid-stride / flat passes (every size: ResNet-50 bs256 +0.1
 // ms/step; up to 16 or 32 MB: -0.09 ms, profiles/r12_bn_fold_bwd.txt); on
 // the small ones the launch it removes waits for a dispatch slot beside the
@@ -1331,7 +1331,10 @@ static void launch_bwd_apply(int gb, hipStream_t stream, const void* dy, const v
 static int g_fold_bwd = 1;
 
 static bool fold_bwd_ok(int V, int nslab, int C, long rows) {
-  constexpr long max_bytes = 32L << 20;  // (16 / 32 / 64 / 128 MB measured alike)
+  // up to 64 MB, where the flat passes take over (32 MB: +0.04 ms/step on
+  // interleaved runs, profiles/r13_bn_launch_ab.txt; 16 / 32 / 64 / 128 MB
+  // measured alike with the flat passes from 256 MB)
+  constexpr long max_bytes = 64L << 20;
   return g_fold_bwd && V == 8 && nslab == FS_SLOTS && C % FS_C == 0 && rows > 0 &&
          (g_fold_bwd == 2 || rows * C * 2 <= max_bytes);
 }
